@@ -1,0 +1,322 @@
+#!/usr/bin/env python3
+"""Benchmark: int4 group-32 weight-only linear GB/s + tokens/s, Llama-3-8B shapes, M = 1 decode.
+
+One "step" = one decoded token through every int4 linear of a Llama-3-8B-shaped stack
+(32 layers x {wqkv 6144x4096, wo 4096x4096, w1 14336x4096, w3 14336x4096, w2 4096x14336}
++ output 128256x4096): 161 launches of the gfx950 int4 GEMV, 4.70 GB of packed weights and
+scales per token (> 256 MiB Infinity Cache, so every byte comes from HBM). Weights are
+random-init nn.Linear-distributed bf16, quantized with the Int4WeightOnlyConfig(group_size=32)
+math and packed by the HIP pack kernel; activations are synthetic N(0,1) bf16; everything is
+resident in HBM before timing. The step is captured once in a HIP graph and replayed.
+
+N GPUs (torchrun, one rank per GPU): every linear is column-sharded (rank r owns output rows
+[r N/P, (r+1) N/P)) and its output is all-gathered over RCCL after each GEMV (north star,
+SURVEY §8e). Total work is fixed as P grows ("strong" scaling); value counts the whole model's
+bytes once per step.
+
+Reported (one JSON line, rank 0):
+  value        = algorithmic bytes per step x steps / wall time  (GB/s, whole job)
+  tokens_per_s = steps / wall time
+  roofline     = the GEMV kernel: sum of algorithmic bytes / sum of kernel durations, measured
+                 live with HIP events written by each kernel's dispatch (tao_profile_*), against
+                 the MI355X HBM3E peak of 8 TB/s
+  cpu_baseline = the reference's CPU "dequant path" (dequantize -> F.linear, bf16) restated in
+                 oracle/, timed on this host's cores over a bounded sample (rank 0, N = 1)
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "torchao-fork_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E, spec (MI355X_MICROARCH.md chip table)
+
+LLAMA3_8B = dict(dim=4096, n_layer=32, n_head=32, n_kv_head=8, head_dim=128,
+                 intermediate=14336, vocab=128256)
+
+
+def llama_linears(cfg):
+    """(name, N, K) of every nn.Linear quantize_ touches in gpt-fast's Llama (model.py)."""
+    d, hd = cfg["dim"], cfg["head_dim"]
+    qkv = (cfg["n_head"] + 2 * cfg["n_kv_head"]) * hd
+    out = []
+    for layer in range(cfg["n_layer"]):
+        out += [
+            (f"layers.{layer}.attention.wqkv", qkv, d),
+            (f"layers.{layer}.attention.wo", d, d),
+            (f"layers.{layer}.feed_forward.w1", cfg["intermediate"], d),
+            (f"layers.{layer}.feed_forward.w3", cfg["intermediate"], d),
+            (f"layers.{layer}.feed_forward.w2", d, cfg["intermediate"]),
+        ]
+    out.append(("output", cfg["vocab"], d))
+    return out
+
+
+def int4_alg_bytes(N, K, g, M=1):
+    """N*K/2 + (K/g)*N*4 + M*K*2 + M*N*2 (no bias)."""
+    return N * K // 2 + (K // g) * N * 4 + M * K * 2 + M * N * 2
+
+
+def make_int4_weight(N, K, g, seed, device):
+    """Random nn.Linear-init bf16 weight -> tinygemm qparams -> gfx950 packed (HIP pack kernel)."""
+    from torchao.quantization.quant_primitives import (
+        MappingType,
+        _choose_qparams_affine_tinygemm,
+        _quantize_affine_tinygemm,
+    )
+
+    gen = torch.Generator(device=device).manual_seed(seed)
+    bound = 1.0 / (K ** 0.5)
+    w = (torch.rand(N, K, generator=gen, device=device) * 2 - 1).mul_(bound).to(torch.bfloat16)
+    s, z = _choose_qparams_affine_tinygemm(
+        w, MappingType.ASYMMETRIC, (1, g), torch.int32, 0, 15, 1e-6,
+        zero_point_dtype=torch.bfloat16)
+    q = _quantize_affine_tinygemm(w, (1, g), s, z, torch.int32, 0, 15)
+    del w
+    packed = torch.ops.torchao.int4_pack(q)
+    del q
+    sz = torch.stack([s, z], dim=-1).contiguous()
+    return packed, sz
+
+
+def cpu_baseline(cfg, g, budget_s=12.0):
+    """The reference CPU dequant path (oracle restatement) on one layer's five linears, M = 1."""
+    from oracle import oracle
+
+    cores = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(cores)
+    layer = [lin for lin in llama_linears(cfg) if lin[0].startswith("layers.0.")]
+    mats = []
+    for i, (_, N, K) in enumerate(layer):
+        w = oracle.make_linear_weight(N, K, seed=i)
+        s, z = oracle.int4_qparams(w, g)
+        q = oracle.int4_quantize(w, s, z, g)
+        x = oracle.make_activation(1, K, seed=100 + i)
+        mats.append((x, q, s, z, N, K))
+    sample_bytes = sum(int4_alg_bytes(N, K, g) for (_, _, _, _, N, K) in mats)
+    for (x, q, s, z, _, _) in mats:  # warm up
+        oracle.int4_linear(x, q, s, z, g)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        for (x, q, s, z, _, _) in mats:
+            oracle.int4_linear(x, q, s, z, g)
+        reps += 1
+        if time.perf_counter() - t0 > budget_s or reps >= 200:
+            break
+    dt = time.perf_counter() - t0
+    # PyTorch's own CPU int4 GEMM (what the reference's Int4CPULayout dispatches to), same sample
+    tg = None
+    try:
+        packs = [oracle.int4_tinygemm_cpu_pack(q, s, z) + (x,) for (x, q, s, z, _, _) in mats]
+        for p, sz, x in packs:
+            oracle.int4_tinygemm_cpu(x, p, sz, g)
+        r2, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < 2.0:
+            for p, sz, x in packs:
+                oracle.int4_tinygemm_cpu(x, p, sz, g)
+            r2 += 1
+        tg = sample_bytes * r2 / (time.perf_counter() - t1) / 1e9
+    except Exception as e:  # pragma: no cover - depends on the host's torch build
+        tg = f"unavailable: {type(e).__name__}"
+    return {
+        "value": round(sample_bytes * reps / dt / 1e9, 3),
+        "unit": "GB/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": (f"reference CPU dequant path (dequantize -> F.linear bf16, oracle/oracle.py) on "
+                   f"layer 0's 5 int4 g{g} linears at M=1, {reps} reps in {dt:.1f}s"),
+        "ms_per_token_extrapolated": round(dt / reps * 1e3 * cfg["n_layer"], 1),
+        "aten_weight_int4pack_mm_for_cpu_GBps": round(tg, 3) if isinstance(tg, float) else tg,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--group-size", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=device)
+
+    import torchao
+    from torchao import _lib
+
+    _lib.lib()  # fail loudly if the native library is missing
+    cfg, g, P = LLAMA3_8B, args.group_size, world
+    lins = llama_linears(cfg)
+
+    # ---- build the sharded weights, inputs and outputs (all resident in HBM) ----
+    plan, bytes_per_step = [], 0
+    xs = {K: torch.randn(1, K, device=device, dtype=torch.bfloat16) for K in {K for _, _, K in lins}}
+    for i, (name, N, K) in enumerate(lins):
+        assert N % P == 0, (name, N, P)
+        n_loc = N // P
+        packed, sz = make_int4_weight(n_loc, K, g, seed=1000 * i + rank, device=device)
+        y_loc = torch.empty(1, n_loc, device=device, dtype=torch.bfloat16)
+        y_full = torch.empty(1, N, device=device, dtype=torch.bfloat16) if P > 1 else y_loc
+        plan.append((name, n_loc, K, packed, sz, y_loc, y_full))
+        bytes_per_step += int4_alg_bytes(N, K, g)
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.Stream(device)
+    lib = _lib.lib()
+
+    def step(do_gemv=True, do_comm=True):
+        sp = torch.cuda.current_stream(device).cuda_stream
+        for (_, n_loc, K, packed, sz, y_loc, y_full) in plan:
+            if do_gemv:
+                rc = lib.tao_int4wo_linear_bf16(xs[K].data_ptr(), packed.data_ptr(), sz.data_ptr(),
+                                                None, y_loc.data_ptr(), 1, n_loc, K, g, sp)
+                if rc:
+                    raise RuntimeError(lib.tao_last_error().decode())
+            if P > 1 and do_comm:
+                dist.all_gather_into_tensor(y_full, y_loc)
+
+    def capture(**kw):
+        graph = torch.cuda.CUDAGraph()
+        stream.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(stream):
+            step(**kw)  # warm-up outside capture (RCCL communicators, allocator)
+            with torch.cuda.graph(graph, stream=stream):
+                step(**kw)
+        torch.cuda.current_stream(device).wait_stream(stream)
+        torch.cuda.synchronize()
+        return graph
+
+    graph = None
+    if not args.no_graph:
+        try:
+            graph = capture()
+        except Exception as e:  # graph capture of collectives is runtime dependent
+            print(f"[bench] graph capture failed ({e}); timing eager launches", file=sys.stderr)
+            graph = None
+    run = graph.replay if graph is not None else step
+
+    def barrier():
+        if P > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        run()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if P > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- roofline: per-kernel durations of one eager step, HIP events from the dispatch ----
+    with _lib.KernelTimer(len(plan)) as timer:
+        step(do_comm=False)
+    torch.cuda.synchronize()
+    durs = timer.durations_ms
+    assert len(durs) == len(plan)
+    gemv_bytes = [int4_alg_bytes(n_loc, K, g) for (_, n_loc, K, *_r) in plan]
+    achieved = sum(gemv_bytes) / (sum(durs) * 1e-3) / 1e9
+    per_shape = {}
+    for (name, n_loc, K, *_r), d, b in zip(plan, durs, gemv_bytes):
+        key = f"{n_loc}x{K}"
+        e = per_shape.setdefault(key, {"launches": 0, "us": 0.0, "bytes": b})
+        e["launches"] += 1
+        e["us"] += d * 1e3
+    for key, e in per_shape.items():
+        e["us"] = round(e["us"] / e["launches"], 3)
+        e["GBps"] = round(e["bytes"] / (e["us"] * 1e-6) / 1e9, 1)
+
+    comm_ms = None
+    if P > 1:
+        gcomm = capture(do_gemv=False) if graph is not None else None
+        fn = gcomm.replay if gcomm is not None else (lambda: step(do_gemv=False))
+        for _ in range(2):
+            fn()
+        barrier()
+        tc = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        barrier()
+        comm_ms = (time.perf_counter() - tc) / args.steps * 1e3
+
+    cpu = None
+    if rank == 0 and P == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, g)
+
+    if rank == 0:
+        ms = elapsed / args.steps * 1e3
+        rec = {
+            "metric": "int4 WO linear GB/s + tokens/s vs CPU dequant path, Llama-3-8B shapes M=1",
+            "value": round(bytes_per_step * args.steps / elapsed / 1e9, 2),
+            "unit": "GB/s",
+            "tokens_per_s": round(args.steps / elapsed, 2),
+            "n_gpus": P,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init nn.Linear weights quantized int4 g32; N(0,1) bf16 activations)",
+            "config": {
+                "workload": "Llama-3-8B int4 g32 weight-only linears, M=1 decode: 32 layers x "
+                            "{wqkv 6144x4096, wo 4096x4096, w1/w3 14336x4096, w2 4096x14336} + "
+                            "output 128256x4096 (161 GEMV launches/step)",
+                "model": "Llama-3-8B (linears only)",
+                "global_batch": 1,
+                "seq_len": 1,
+                "group_size": g,
+                "bytes_per_step": bytes_per_step,
+                "parallelism": f"colwise-tp{P} + RCCL all-gather" if P > 1 else "single-gpu",
+                "hip_graph": graph is not None,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "int4wo_gemv_kernel",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": None,
+                "launches": len(durs),
+                "kernel_ms_per_step": round(sum(durs), 4),
+                "per_shape": per_shape,
+            },
+            "cpu_baseline": cpu,
+        }
+        if comm_ms is not None:
+            rec["allgather_ms_per_step"] = round(comm_ms, 4)
+        if cpu is not None:
+            rec["speedup_vs_cpu_baseline"] = round(rec["value"] / cpu["value"], 1)
+        print(json.dumps(rec), flush=True)
+
+    if P > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

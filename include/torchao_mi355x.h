@@ -1,0 +1,145 @@
+/*
+ * torchao_mi355x.h — C-ABI of the MI355X (gfx950) weight-only quantized linear path.
+ *
+ * This is the drop-in boundary. Every entry point takes plain device pointers, sizes and a
+ * hipStream_t passed as `void*` (NULL = the legacy default stream); no torch types appear here.
+ * Each function replaces one call site of the reference (torchao 0.13.0, cited file:line) —
+ * the aten/torchao op that the reference's Python layout `impl` functions invoke.
+ *
+ * Conventions (mirroring the reference op conventions):
+ *   - inputs are borrowed, contiguous, row-major; outputs are caller-allocated;
+ *   - no entry point allocates, synchronises or copies host<->device, so every call is
+ *     hipGraph-capturable (reference compiles decode with mode="reduce-overhead",
+ *     torchao/_models/llama/generate.py:865-872);
+ *   - bf16 tensors are passed as uint16_t bit patterns;
+ *   - return value is TAO_OK (0) or a TAO_ERR_* code; tao_last_error() gives the message for the
+ *     calling thread (the reference raises RuntimeError via TORCH_CHECK with the same meaning).
+ *
+ * int4 weight layout ("gfx950 row-stream layout"):
+ *   packed : uint32 [N][K/8]; dword d of row n holds k = 8d..8d+7 with
+ *            bits 4i..4i+3 = q[n][8d+2i], bits 16+4i..16+4i+3 = q[n][8d+2i+1]   (i = 0..3)
+ *   sz     : bf16 [N][K/group][2] = (scale, zero) interleaved per (row, group)
+ *   dequant: w = (q - 8) * scale + zero        (tinygemm float-zero domain)
+ */
+#ifndef TORCHAO_MI355X_H_
+#define TORCHAO_MI355X_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  TAO_OK = 0,
+  TAO_ERR_INVALID_ARGUMENT = 1, /* shape / alignment / group-size check failed   */
+  TAO_ERR_UNSUPPORTED = 2,      /* valid request this build does not implement     */
+  TAO_ERR_HIP = 3               /* a HIP runtime call or kernel launch failed      */
+};
+
+/* ---- library ------------------------------------------------------------------------------ */
+
+/* Version string of this library ("torchao-mi355x <ver> gfx950"). */
+const char* tao_version(void);
+/* Message describing the last failed call on this thread ("" if none). */
+const char* tao_last_error(void);
+/* Number of hipDevices visible (0 if no GPU / runtime unavailable). Never fails. */
+int tao_device_count(void);
+
+/* Per-kernel timing for benchmarks (not used on the inference path). Between begin and end,
+ * the calling thread's next `capacity` kernel launches carry a start/stop hipEvent pair written
+ * by the kernel's own dispatch packet (hipExtLaunchKernelGGL) — the interval rocprofv3 reports
+ * as the kernel duration. end() synchronises on the events and writes one duration (ms) per
+ * recorded launch, in launch order; *count receives how many. Do not open a session while
+ * capturing a hipGraph. */
+int tao_profile_begin(int capacity);
+int tao_profile_end(float* durations_ms, int capacity, int* count);
+
+/* ---- int4 weight-only (tinygemm-equivalent) ----------------------------------------------- */
+
+/* y[M][N] = x[M][K] @ dequant(packed, sz)^T (+ bias[N]), bf16 in/out, fp32 accumulate.
+ * Replaces aten._weight_int4pack_mm(x, packed, qGroupSize, qScaleAndZeros) called at
+ * torchao/dtypes/uintx/tensor_core_tiled_layout.py:104 (plus the bias add at :112-113).
+ * group_size in {32,64,128,256}; K % group_size == 0; M >= 0 (M == 0 is a no-op).
+ * x, y: 16-B aligned rows. bias may be NULL. */
+int tao_int4wo_linear_bf16(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
+                           const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K,
+                           int64_t group_size, void* stream);
+
+/* packed[N][K/8] <- q[N][K] (int32 values 0..15).
+ * Replaces aten._convert_weight_to_int4pack(u8, inner_k_tiles) at
+ * torchao/dtypes/uintx/tensor_core_tiled_layout.py:279 (device kernel). K % 8 == 0. */
+int tao_int4_pack(const int32_t* q, uint32_t* packed, int64_t N, int64_t K, void* stream);
+
+/* packed[N][K/8] <- u8[N][K/2] where u8 = q[:, 0::2] << 4 | q[:, 1::2]
+ * (the operand the reference builds at tensor_core_tiled_layout.py:276). */
+int tao_int4_pack_u8(const uint8_t* q_u8, uint32_t* packed, int64_t N, int64_t K,
+                     void* stream);
+
+/* q[N][K] (int32 0..15) <- packed. Exact inverse of tao_int4_pack.
+ * Replaces the identity-matmul recovery in get_plain (tensor_core_tiled_layout.py:465-517). */
+int tao_int4_unpack(const uint32_t* packed, int32_t* q, int64_t N, int64_t K, void* stream);
+
+/* w[N][K] bf16 <- dequant(packed, sz).
+ * mode 0: bf16((q-8)*s) then bf16(+z) — the two roundings of _dequantize_affine_tinygemm
+ *         (torchao/quantization/quant_primitives.py:1019-1023), bit-exact to AQT.dequantize();
+ * mode 1: one rounding of fma(q-8, s, z) — the semantics of the reference dequant kernel
+ *         (torchao/csrc/cuda/tensor_core_tiled_layout/tensor_core_tiled_layout.cu:184-190). */
+int tao_int4_dequant(const uint32_t* packed, const uint16_t* sz, uint16_t* w, int64_t N,
+                     int64_t K, int64_t group_size, int mode, void* stream);
+
+/* Host (CPU) versions of pack / unpack for weights that are quantized on the CPU before being
+ * moved to the GPU (quantize_ on a CPU model). Plain C++; identical bytes to the device kernels. */
+int tao_int4_pack_host(const int32_t* q, uint32_t* packed, int64_t N, int64_t K);
+int tao_int4_unpack_host(const uint32_t* packed, int32_t* q, int64_t N, int64_t K);
+
+/* ---- reference tile-format compat (torchao::*_tensor_core_tiled_layout) ------------------- */
+
+/* out[N][K] int32 <- tile-format packed_w [N/8][K/(ikt*16)][32][ikt/2] (int32).
+ * Replaces torchao::unpack_tensor_core_tiled_layout (torchao/ops.py:255-296,
+ * tensor_core_tiled_layout.cu:320-368). inner_k_tiles in {2,4,8}. */
+int tao_unpack_tensor_core_tiled_layout(const int32_t* packed_w, int32_t* out, int64_t N,
+                                        int64_t K, int64_t inner_k_tiles, void* stream);
+
+/* out[N][K] bf16 <- fma(q-8, s, z) with scales_and_zeros [K/g][N][2] bf16 (tinygemm packing,
+ * torchao/quantization/utils.py:395-409). Replaces torchao::dequantize_tensor_core_tiled_layout
+ * (torchao/ops.py:299-377, tensor_core_tiled_layout.cu:223-316). */
+int tao_dequantize_tensor_core_tiled_layout(const int32_t* packed_w,
+                                            const uint16_t* scales_and_zeros, uint16_t* out,
+                                            int64_t N, int64_t K, int64_t group_size,
+                                            int64_t inner_k_tiles, void* stream);
+
+/* Tile-format packer (the inverse of the unpack above): packed_w <- q[N][K] int32.
+ * Equivalent of aten._convert_weight_to_int4pack's output format as described by the reference
+ * unpack kernel (tensor_core_tiled_layout.cu:131-215). N % 8 == 0, K % (ikt*16) == 0. */
+int tao_pack_tensor_core_tiled_layout(const int32_t* q, int32_t* packed_w, int64_t N, int64_t K,
+                                      int64_t inner_k_tiles, void* stream);
+
+/* ---- int8 weight-only ---------------------------------------------------------------------- */
+
+/* y[M][N] = bf16( bf16(x @ w^T) * scale[n] ) (+ bias), w int8 [N][K], scale bf16 [N].
+ * Replaces torch.mm(x, w.t().to(bf16)) * scale at torchao/dtypes/uintx/plain_layout.py:256-266. */
+int tao_int8wo_linear_bf16(const uint16_t* x, const int8_t* w, const uint16_t* scale,
+                           const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K,
+                           void* stream);
+
+/* ---- int8 dynamic activation x int8 weight -------------------------------------------------- */
+
+/* Per-token symmetric reduced-range int8 quantization of x [M][K] bf16:
+ *   s[m] = max(bf16(amax(|x[m]|) / 127), bf16(1e-5)); q = clamp(rne(bf16(x * bf16(1/s))), -127, 127)
+ * Replaces _int8_symm_per_token_reduced_range_quant (torchao/quantization/quant_api.py:1258-1273). */
+int tao_int8_quant_per_token(const uint16_t* x, int8_t* q, uint16_t* scale, int64_t M,
+                             int64_t K, void* stream);
+
+/* y[M][N] = bf16( bf16( bf16(xq @ wq^T) * xs[m] ) * ws[n] ) (+ bias), exact int32 accumulation.
+ * Replaces int_scaled_matmul + the weight-scale epilogue at
+ * torchao/dtypes/uintx/plain_layout.py:294-315 and torchao/kernel/intmm.py:108-143. */
+int tao_int8_scaled_mm_bf16(const int8_t* xq, const uint16_t* xs, const int8_t* wq,
+                            const uint16_t* ws, const uint16_t* bias, uint16_t* y, int64_t M,
+                            int64_t N, int64_t K, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TORCHAO_MI355X_H_ */

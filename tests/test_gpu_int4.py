@@ -1,0 +1,216 @@
+"""GPU parity of the int4 path (pack / unpack / dequant / linear) against the CPU oracle.
+
+Every op here runs through the C-ABI library (torchao.ops -> torchao._lib -> include/*.h).
+Bars: integer/byte work bit-exact; bf16 outputs within the north-star tolerance of 1e-2
+relative L2 against the reference CPU dequant -> F.linear path (oracle.int4_linear), and much
+tighter against an fp32 accumulation of the same dequantised weights.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import bf16, golden_files, golden_ms, load_golden, unpack_u8_nibbles
+from oracle import oracle
+
+import torchao
+from torchao import _lib
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL_REF = 1e-2  # north_star: within 1e-2 relative on bf16 vs the reference dequant path
+TOL_FP32 = 4e-3  # vs fp32 accumulation of the identical dequantised weights
+
+
+def _qparams(N, K, g, seed=0):
+    w = oracle.make_linear_weight(N, K, seed=seed)
+    s, z = oracle.int4_qparams(w, g)
+    q = oracle.int4_quantize(w, s, z, g)
+    return w, q, s, z
+
+
+def _gpu_weight(q, s, z):
+    packed = torch.ops.torchao.int4_pack(q.to(DEV))
+    sz = torch.stack([s, z], dim=-1).contiguous().to(DEV)
+    return packed, sz
+
+
+def test_native_library_is_loaded_on_gpu():
+    assert _lib.is_available(), _lib.load_error()
+    assert _lib.lib().tao_device_count() >= 1
+    assert "gfx950" in torch.cuda.get_device_properties(0).gcnArchName
+
+
+@pytest.mark.parametrize("N,K", [(64, 256), (37, 352), (4096, 4096), (1000, 11008)])
+def test_pack_unpack_bit_exact(N, K):
+    rng = np.random.default_rng(N + K)
+    q = rng.integers(0, 16, size=(N, K), dtype=np.int32)
+    packed = torch.ops.torchao.int4_pack(torch.from_numpy(q).to(DEV))
+    np.testing.assert_array_equal(packed.cpu().numpy().view(np.uint32), oracle.pack_row_stream(q))
+    np.testing.assert_array_equal(torch.ops.torchao.int4_unpack(packed).cpu().numpy(), q)
+    # the u8 entry (reference's (q[2i] << 4 | q[2i+1]) operand) packs identically
+    qt = torch.from_numpy(q)
+    u8 = ((qt[:, 0::2] << 4) | qt[:, 1::2]).to(torch.uint8).to(DEV)
+    assert torch.equal(torch.ops.torchao.int4_pack_u8(u8), packed)
+
+
+@pytest.mark.parametrize("fname", golden_files("int4_"))
+def test_dequant_bit_exact_vs_reference(fname):
+    rec = load_golden(fname)
+    g = int(rec["g"])
+    q = unpack_u8_nibbles(rec["q_u8"])
+    s, z = bf16(rec["s"]), bf16(rec["z"])
+    packed, sz = _gpu_weight(q, s, z)
+    w0 = torch.ops.torchao.int4_dequantize(packed, sz, g, 0).cpu()
+    assert torch.equal(w0, oracle.int4_dequantize(q, s, z, g))
+    if "w_dequant" in rec.files:
+        assert torch.equal(w0, bf16(rec["w_dequant"]))  # reference AQT.dequantize(), bit exact
+    w1 = torch.ops.torchao.int4_dequantize(packed, sz, g, 1).cpu()
+    sz_tiny = torch.stack([s, z], -1).transpose(0, 1)
+    assert torch.equal(w1, oracle.dequant_tile_fma(q, sz_tiny, g))
+
+
+@pytest.mark.parametrize("fname", golden_files("int4_"))
+def test_linear_vs_reference_fixtures(fname):
+    rec = load_golden(fname)
+    g = int(rec["g"])
+    q = unpack_u8_nibbles(rec["q_u8"])
+    s, z, bias = bf16(rec["s"]), bf16(rec["z"]), bf16(rec["bias"])
+    packed, sz = _gpu_weight(q, s, z)
+    for M in golden_ms(rec):
+        x = bf16(rec[f"x_M{M}"])
+        y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, bias.to(DEV)).cpu()
+        assert y.shape == (M, int(rec["N"])) and y.dtype == torch.bfloat16
+        assert oracle.rel_l2(y, bf16(rec[f"y_dequant_M{M}"])) < TOL_REF
+        assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, g, bias)) < TOL_FP32
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 5, 7, 8, 9, 16, 17, 33, 64, 128])
+@pytest.mark.parametrize("g", [32, 128])
+def test_linear_all_m_paths(M, g):
+    N, K = 192, 1024
+    w, q, s, z = _qparams(N, K, g, seed=M)
+    x = oracle.make_activation(M, K, seed=M)
+    packed, sz = _gpu_weight(q, s, z)
+    y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, None).cpu()
+    assert oracle.rel_l2(y, oracle.int4_linear(x, q, s, z, g)) < TOL_REF
+    assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, g)) < TOL_FP32
+
+
+@pytest.mark.parametrize(
+    "N,K,g",
+    [(4096, 4096, 32), (6144, 4096, 32), (14336, 4096, 32), (4096, 14336, 32),
+     (11008, 4096, 32), (4096, 11008, 32), (8192, 28672, 64), (4096, 4096, 256)],
+)
+def test_llama_shapes_m1(N, K, g):
+    w, q, s, z = _qparams(N, K, g, seed=N ^ K)
+    x = oracle.make_activation(1, K, seed=5)
+    packed, sz = _gpu_weight(q, s, z)
+    y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, None).cpu()
+    assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, g)) < TOL_FP32
+    assert oracle.rel_l2(y, oracle.int4_linear(x, q, s, z, g)) < TOL_REF
+
+
+def test_linearity_and_determinism_full_size():
+    """Size-independent properties at 14336 x 4096: run-to-run bit identity and
+    additivity y(x1 + x2) ~ y(x1) + y(x2) (up to bf16 output rounding)."""
+    N, K, g = 14336, 4096, 32
+    w, q, s, z = _qparams(N, K, g, seed=11)
+    packed, sz = _gpu_weight(q, s, z)
+    x1 = oracle.make_activation(1, K, seed=21).to(DEV)
+    x2 = oracle.make_activation(1, K, seed=22).to(DEV)
+    f = lambda x: torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None).float()
+    a = f(x1)
+    assert torch.equal(a, f(x1))
+    lhs = f((x1.float() + x2.float()).to(torch.bfloat16))
+    rel = (lhs - (a + f(x2))).norm() / lhs.norm()
+    assert rel < 1e-2
+
+
+def test_empty_and_bias_and_batched_shapes():
+    N, K, g = 64, 256, 32
+    w, q, s, z = _qparams(N, K, g)
+    packed, sz = _gpu_weight(q, s, z)
+    x0 = torch.empty(0, K, dtype=torch.bfloat16, device=DEV)
+    assert torch.ops.torchao.int4_weight_only_linear(x0, packed, sz, g, None).shape == (0, N)
+    x = oracle.make_activation(6, K, seed=9)
+    bias = (torch.randn(N) * 0.5).to(torch.bfloat16)
+    y3 = torch.ops.torchao.int4_weight_only_linear(
+        x.reshape(2, 3, K).to(DEV), packed, sz, g, bias.to(DEV)
+    )
+    assert y3.shape == (2, 3, N)
+    ref = oracle.int4_linear(x, q, s, z, g, bias).reshape(2, 3, N)
+    assert oracle.rel_l2(y3.cpu(), ref) < TOL_REF
+
+
+def test_bad_arguments_raise():
+    packed = torch.zeros(8, 12, dtype=torch.int32, device=DEV)  # K = 96
+    sz = torch.zeros(8, 2, 2, dtype=torch.bfloat16, device=DEV)
+    x = torch.zeros(1, 96, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(Exception):
+        torch.ops.torchao.int4_weight_only_linear(x, packed, sz, 48, None)
+    with pytest.raises(Exception):
+        torch.ops.torchao.int4_weight_only_linear(x[:, :64], packed, sz, 32, None)
+
+
+@pytest.mark.parametrize("ikt", [2, 4, 8])
+@pytest.mark.parametrize("g", [32, 64, 128, 256])
+def test_tile_format_compat_ops(ikt, g):
+    N, K = 256, 1024
+    w, q, s, z = _qparams(N, K, g, seed=ikt)
+    tile = torch.from_numpy(oracle.pack_tile(q.numpy(), ikt)).to(DEV)
+    assert torch.equal(torch.ops.torchao.pack_tensor_core_tiled_layout(q.to(DEV), ikt), tile)
+    assert torch.equal(torchao.ops.unpack_tensor_core_tiled_layout(tile, ikt).cpu(), q)
+    sz_tiny = torch.stack([s, z], -1).transpose(0, 1).contiguous()
+    d = torchao.ops.dequantize_tensor_core_tiled_layout(tile, sz_tiny.to(DEV), g, ikt).cpu()
+    assert torch.equal(d, oracle.dequant_tile_fma(q, sz_tiny, g))
+    # reference test_ops.py:339-402 bar: dequant close to the python dequant
+    assert (d.float() - oracle.int4_dequantize(q, s, z, g).float()).abs().max() < 0.1
+
+
+def test_hip_graph_capture_and_replay():
+    N, K, g = 4096, 4096, 32
+    w, q, s, z = _qparams(N, K, g, seed=2)
+    packed, sz = _gpu_weight(q, s, z)
+    x = oracle.make_activation(1, K, seed=3).to(DEV)
+    y_eager = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)
+    graph = torch.cuda.CUDAGraph()
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)  # warm up
+        with torch.cuda.graph(graph, stream=stream):
+            y_graph = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)
+    torch.cuda.current_stream().wait_stream(stream)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(y_graph, y_eager)
+
+
+def test_quantize_api_end_to_end_on_gpu():
+    from torchao.quantization import Int4WeightOnlyConfig, quantize_
+
+    K, N = 1024, 512
+    m = torch.nn.Sequential(torch.nn.Linear(K, N), torch.nn.Linear(N, 256)).to(torch.bfloat16)
+    ref_w = [m[0].weight.detach().clone(), m[1].weight.detach().clone()]
+    m = m.to(DEV)
+    quantize_(m, Int4WeightOnlyConfig(group_size=32))
+    x = oracle.make_activation(4, K, seed=4)
+    y = m(x.to(DEV)).cpu()
+    # oracle: quantize the same weights on CPU, dequant path layer by layer
+    h = x
+    for i, lin in enumerate(m):
+        s, z = oracle.int4_qparams(ref_w[i], 32)
+        q = oracle.int4_quantize(ref_w[i], s, z, 32)
+        h = oracle.int4_linear(h, q, s, z, 32, lin.bias.detach().cpu())
+    assert oracle.rel_l2(y, h) < TOL_REF
+    # weights quantized on the GPU carry the same (q, s, z) as the CPU oracle
+    q0, s0, z0 = m[0].weight.tensor_impl.get_plain()
+    s_ref, z_ref = oracle.int4_qparams(ref_w[0], 32)
+    assert torch.equal(s0.cpu(), s_ref) and torch.equal(z0.cpu(), z_ref)
+    assert torch.equal(q0.cpu(), oracle.int4_quantize(ref_w[0], s_ref, z_ref, 32))
+    # moving a CPU-quantized weight to the GPU keeps working (layout is device independent)
+    lin = torch.nn.Linear(K, N, dtype=torch.bfloat16)
+    quantize_(lin, Int4WeightOnlyConfig(group_size=64))
+    lin = lin.to(DEV)
+    assert lin(x.to(DEV)).shape == (4, N)

@@ -1,0 +1,100 @@
+"""GPU parity of the int8 weight-only and int8 dynamic-activation paths against the oracle."""
+
+import pytest
+import torch
+
+from conftest import bf16, golden_files, golden_ms, load_golden
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL_REF = 1e-2
+
+
+@pytest.mark.parametrize("fname", golden_files("int8wo_"))
+def test_int8wo_vs_reference_fixtures(fname):
+    rec = load_golden(fname)
+    q = torch.from_numpy(rec["q"])
+    s, bias = bf16(rec["s"]), bf16(rec["bias"])
+    for M in golden_ms(rec):
+        x = bf16(rec[f"x_M{M}"])
+        y = torch.ops.torchao.int8_weight_only_linear(
+            x.to(DEV), q.to(DEV), s.to(DEV), bias.to(DEV)
+        ).cpu()
+        assert oracle.rel_l2(y, bf16(rec[f"y_M{M}"])) < TOL_REF
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 6, 8, 9, 16, 40, 128])
+def test_int8wo_all_m_paths(M):
+    N, K = 320, 2048
+    w = oracle.make_linear_weight(N, K, seed=M)
+    s = oracle.int8_weight_qparams(w)
+    q = oracle.int8_weight_quantize(w, s)
+    x = oracle.make_activation(M, K, seed=M + 1)
+    y = torch.ops.torchao.int8_weight_only_linear(x.to(DEV), q.to(DEV), s.to(DEV), None).cpu()
+    ref = oracle.int8wo_linear(x, q, s)
+    assert oracle.rel_l2(y, ref) < TOL_REF
+    exact = (x.double() @ q.double().t()) * s.double()
+    assert oracle.rel_l2(y, exact) < 4e-3
+
+
+@pytest.mark.parametrize("M,K", [(1, 4096), (7, 1024), (128, 4096), (33, 14336), (64, 16)])
+def test_int8_act_quant_bit_exact(M, K):
+    x = oracle.make_activation(M, K, seed=K + M) * 3
+    x[0] = 0.0
+    if M > 2:
+        x[2, 1] = 1000.0
+    q, s = torch.ops.torchao.int8_quantize_per_token(x.to(DEV))
+    q_ref, s_ref = oracle.int8_act_quant(x)
+    assert torch.equal(s.cpu(), s_ref)
+    assert torch.equal(q.cpu(), q_ref)
+
+
+@pytest.mark.parametrize("fname", golden_files("int8dyn_"))
+def test_int8dyn_vs_reference_fixtures(fname):
+    rec = load_golden(fname)
+    wq = torch.from_numpy(rec["wq"])
+    ws, bias = bf16(rec["ws"]), bf16(rec["bias"])
+    for M in golden_ms(rec):
+        x = bf16(rec[f"x_M{M}"])
+        q, s = torch.ops.torchao.int8_quantize_per_token(x.to(DEV))
+        assert torch.equal(q.cpu(), torch.from_numpy(rec[f"xq_M{M}"]))
+        assert torch.equal(s.cpu().reshape(-1), bf16(rec[f"xs_M{M}"]))
+        y = torch.ops.torchao.int8_scaled_mm(q, s, wq.to(DEV), ws.to(DEV), bias.to(DEV)).cpu()
+        assert oracle.rel_l2(y, bf16(rec[f"y_M{M}"])) < TOL_REF
+        # exact integer products + the reference epilogue order: bit exact to the reference
+        assert torch.equal(y, bf16(rec[f"y_M{M}"]))
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 4096, 4096), (16, 512, 1024), (200, 320, 2048), (1, 256, 256)])
+def test_int8_scaled_mm_exact_epilogue(M, N, K):
+    w = oracle.make_linear_weight(N, K, seed=N)
+    wq, ws = oracle.int8_dyn_weight(w)
+    x = oracle.make_activation(M, K, seed=M)
+    xq, xs = oracle.int8_act_quant(x)
+    y = torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), None).cpu()
+    assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="cpu"))
+    assert oracle.rel_l2(y, oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="fp32")) < TOL_REF
+
+
+def test_int8_configs_end_to_end():
+    from torchao.quantization import (
+        Int8DynamicActivationInt8WeightConfig,
+        Int8WeightOnlyConfig,
+        quantize_,
+    )
+
+    K, N = 1024, 256
+    base = torch.nn.Linear(K, N).to(torch.bfloat16)
+    x = oracle.make_activation(64, K, seed=1)
+    for cfg in (Int8WeightOnlyConfig(), Int8DynamicActivationInt8WeightConfig()):
+        m = torch.nn.Linear(K, N).to(torch.bfloat16)
+        m.load_state_dict(base.state_dict())
+        m = m.to(DEV)
+        quantize_(m, cfg)
+        y = m(x.to(DEV)).cpu()
+        ref = torch.nn.functional.linear(x.float(), base.weight.float(), base.bias.float())
+        # quantization error dominates here: SQNR bar of the reference integration tests
+        # (test_integration.py:978-1004 use >= 40 dB for int8wo; dynamic int8 is looser)
+        sqnr = 20 * torch.log10(ref.norm() / (ref - y.float()).norm())
+        assert sqnr > (35 if isinstance(cfg, Int8WeightOnlyConfig) else 25), (cfg, float(sqnr))

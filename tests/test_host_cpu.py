@@ -1,0 +1,318 @@
+"""CPU tests of the product's host side: the C-ABI contract, quantization host logic (pinned to
+the reference fixtures), the AffineQuantizedTensor / layout plug-in API, and op registration.
+No GPU compute is invoked here."""
+
+import ctypes
+import io
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, bf16, golden_files, load_golden, unpack_u8_nibbles
+from oracle import oracle
+
+import torchao
+from torchao import _lib
+from torchao.dtypes import (
+    AffineQuantizedTensor,
+    PlainLayout,
+    TensorCoreTiledAQTTensorImpl,
+    TensorCoreTiledLayout,
+    register_aqt_quantized_linear_dispatch,
+    deregister_aqt_quantized_linear_dispatch,
+)
+from torchao.quantization import (
+    Int4WeightOnlyConfig,
+    Int8DynamicActivationInt8WeightConfig,
+    Int8WeightOnlyConfig,
+    LinearActivationQuantizedTensor,
+    quantize_,
+)
+from torchao.quantization.quant_primitives import (
+    MappingType,
+    _choose_qparams_affine_tinygemm,
+    _dequantize_affine_tinygemm,
+    _quantize_affine_tinygemm,
+)
+
+HEADER = os.path.join(ROOT, "include", "torchao_mi355x.h")
+
+
+# ---------------------------------------------------------------------------------------------
+# C-ABI contract
+# ---------------------------------------------------------------------------------------------
+def _declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(tao_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    assert _lib.is_available(), _lib.load_error()
+    declared = _declared_functions()
+    assert len(declared) >= 15
+    assert declared == _lib.exported_symbols(), "header and ctypes bindings disagree"
+    raw = ctypes.CDLL(_lib.library_path())
+    for name in declared:
+        assert hasattr(raw, name), f"{name} declared in include/ but not exported"
+
+
+def test_library_metadata_and_error_reporting():
+    lib = _lib.lib()
+    assert b"gfx950" in lib.tao_version()
+    assert lib.tao_device_count() >= 0
+    # argument validation happens before any device work: a bad group size must fail loudly
+    rc = lib.tao_int4wo_linear_bf16(None, None, None, None, None, 1, 8, 96, 48, None)
+    assert rc == 1 and b"qGroupSize" in lib.tao_last_error()
+    with pytest.raises(RuntimeError, match="qGroupSize"):
+        _lib.call("tao_int4wo_linear_bf16", None, None, None, None, None, 1, 8, 96, 48, None)
+
+
+def test_gfx950_code_object_embedded():
+    blob = open(_lib.library_path(), "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_host_pack_matches_layout_spec():
+    rng = np.random.default_rng(1)
+    q = rng.integers(0, 16, size=(37, 96), dtype=np.int32)
+    packed = torch.ops.torchao.int4_pack(torch.from_numpy(q))
+    np.testing.assert_array_equal(packed.numpy().view(np.uint32), oracle.pack_row_stream(q))
+    back = torch.ops.torchao.int4_unpack(packed)
+    np.testing.assert_array_equal(back.numpy(), q)
+
+
+def test_host_pack_rejects_out_of_range():
+    q = torch.zeros(2, 16, dtype=torch.int32)
+    q[1, 3] = 16
+    with pytest.raises(RuntimeError, match=r"out of \[0,15\]"):
+        torch.ops.torchao.int4_pack(q)
+
+
+# ---------------------------------------------------------------------------------------------
+# quantization host logic against the reference fixtures
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("fname", golden_files("int4_"))
+def test_product_int4_primitives_bit_exact(fname):
+    rec = load_golden(fname)
+    g = int(rec["g"])
+    w = bf16(rec["w"])
+    bs = (1, g)
+    s, z = _choose_qparams_affine_tinygemm(
+        w, MappingType.ASYMMETRIC, bs, torch.int32, 0, 15, 1e-6, zero_point_dtype=torch.bfloat16
+    )
+    q = _quantize_affine_tinygemm(w, bs, s, z, torch.int32, 0, 15)
+    assert torch.equal(s, bf16(rec["s"])) and torch.equal(z, bf16(rec["z"]))
+    assert torch.equal(q, unpack_u8_nibbles(rec["q_u8"]))
+    if "w_dequant" in rec.files:
+        dq = _dequantize_affine_tinygemm(q, bs, s, z, torch.int32, 0, 15, output_dtype=torch.bfloat16)
+        assert torch.equal(dq, bf16(rec["w_dequant"]))
+
+
+@pytest.mark.parametrize("fname", golden_files("int4_"))
+def test_quantize_int4_on_cpu_model_packs_reference_qparams(fname):
+    rec = load_golden(fname)
+    N, K, g = int(rec["N"]), int(rec["K"]), int(rec["g"])
+    lin = torch.nn.Linear(K, N, bias=True, dtype=torch.bfloat16)
+    with torch.no_grad():
+        lin.weight.copy_(bf16(rec["w"]))
+    quantize_(lin, Int4WeightOnlyConfig(group_size=g))
+    w = lin.weight
+    assert isinstance(w, AffineQuantizedTensor)
+    assert isinstance(w._layout, TensorCoreTiledLayout)
+    assert isinstance(w.tensor_impl, TensorCoreTiledAQTTensorImpl)
+    assert w.shape == (N, K) and w.dtype == torch.bfloat16 and w.block_size == (1, g)
+    impl = w.tensor_impl
+    assert impl.packed_weight.shape == (N, K // 8) and impl.packed_weight.dtype == torch.int32
+    assert impl.scale_and_zero.shape == (N, K // g, 2)
+    q, s, z = impl.get_plain()
+    assert torch.equal(q, unpack_u8_nibbles(rec["q_u8"]))
+    assert torch.equal(s, bf16(rec["s"])) and torch.equal(z, bf16(rec["z"]))
+    np.testing.assert_array_equal(
+        impl.packed_weight.numpy().view(np.uint32), oracle.pack_row_stream(q.numpy())
+    )
+    if "w_dequant" in rec.files:
+        assert torch.equal(w.dequantize(), bf16(rec["w_dequant"]))
+    assert "AffineQuantizedTensor" in repr(lin)
+
+
+@pytest.mark.parametrize("fname", golden_files("int8wo_"))
+def test_quantize_int8wo_matches_reference(fname):
+    rec = load_golden(fname)
+    N, K = int(rec["N"]), int(rec["K"])
+    lin = torch.nn.Linear(K, N, dtype=torch.bfloat16)
+    with torch.no_grad():
+        lin.weight.copy_(bf16(rec["w"]))
+    quantize_(lin, Int8WeightOnlyConfig())
+    q, s, zp = lin.weight.tensor_impl.get_plain()
+    assert torch.equal(q, torch.from_numpy(rec["q"]))
+    assert torch.equal(s.reshape(-1), bf16(rec["s"]))
+    assert torch.equal(lin.weight.dequantize(), bf16(rec["w_dequant"]))
+
+
+@pytest.mark.parametrize("fname", golden_files("int8dyn_"))
+def test_quantize_int8dyn_weight_and_cpu_act_quant(fname):
+    from torchao.quantization.quant_api import _int8_symm_per_token_reduced_range_quant
+
+    rec = load_golden(fname)
+    N, K = int(rec["N"]), int(rec["K"])
+    lin = torch.nn.Linear(K, N, dtype=torch.bfloat16)
+    with torch.no_grad():
+        lin.weight.copy_(bf16(rec["w"]))
+    quantize_(lin, Int8DynamicActivationInt8WeightConfig())
+    assert isinstance(lin.weight, LinearActivationQuantizedTensor)
+    wq, ws, _ = lin.weight.original_weight_tensor.tensor_impl.get_plain()
+    assert torch.equal(wq, torch.from_numpy(rec["wq"]))
+    assert torch.equal(ws.reshape(-1), bf16(rec["ws"]))
+    M = min(int(k[3:]) for k in rec.files if k.startswith("x_M"))
+    xa = _int8_symm_per_token_reduced_range_quant(bf16(rec[f"x_M{M}"]))
+    xq, xs, _ = xa.tensor_impl.get_plain()
+    assert torch.equal(xq, torch.from_numpy(rec[f"xq_M{M}"]))
+    assert torch.equal(xs.reshape(-1), bf16(rec[f"xs_M{M}"]))
+
+
+def test_int4_skips_incompatible_group_size():
+    lin = torch.nn.Linear(96, 8, dtype=torch.bfloat16)
+    quantize_(lin, Int4WeightOnlyConfig(group_size=64))  # 96 % 64 != 0 -> left alone
+    assert type(lin.weight) is torch.nn.Parameter and not isinstance(lin.weight.data, AffineQuantizedTensor)
+
+
+def test_filter_fn_and_nested_modules():
+    m = torch.nn.Sequential(
+        torch.nn.Linear(64, 64), torch.nn.Sequential(torch.nn.Linear(64, 32), torch.nn.ReLU())
+    ).to(torch.bfloat16)
+    quantize_(m, Int4WeightOnlyConfig(group_size=32), filter_fn=lambda mod, fqn: fqn == "1.0")
+    assert not isinstance(m[0].weight, AffineQuantizedTensor)
+    assert isinstance(m[1][0].weight, AffineQuantizedTensor)
+
+
+# ---------------------------------------------------------------------------------------------
+# tensor subclass mechanics
+# ---------------------------------------------------------------------------------------------
+def _int4_linear(N=64, K=256, g=32):
+    lin = torch.nn.Linear(K, N, dtype=torch.bfloat16)
+    with torch.no_grad():
+        lin.weight.copy_(oracle.make_linear_weight(N, K, seed=3))
+    quantize_(lin, Int4WeightOnlyConfig(group_size=g))
+    return lin
+
+
+def test_int4_slice_rows_and_groups():
+    lin = _int4_linear()
+    w = lin.weight
+    full = w.dequantize()
+    rows = w[8:24]
+    assert rows.shape == (16, 256)
+    assert torch.equal(rows.dequantize(), full[8:24])
+    cols = aten_slice(w, 1, 64, 192)
+    assert cols.shape == (64, 128)
+    assert torch.equal(cols.dequantize(), full[:, 64:192])
+
+
+def aten_slice(t, dim, start, end):
+    return torch.ops.aten.slice.Tensor(t, dim, start, end, 1)
+
+
+def test_int4_transpose_detach_clone():
+    lin = _int4_linear()
+    w = lin.weight
+    wt = w.t()
+    assert wt.shape == (256, 64) and wt.tensor_impl.transposed
+    assert wt.t().shape == (64, 256)
+    c = w.detach().clone()
+    assert torch.equal(c.tensor_impl.packed_weight, w.tensor_impl.packed_weight)
+    assert c.tensor_impl.packed_weight.data_ptr() != w.tensor_impl.packed_weight.data_ptr()
+
+
+def test_state_dict_roundtrip_weights_only():
+    lin = _int4_linear()
+    buf = io.BytesIO()
+    torch.save(lin.state_dict(), buf)
+    buf.seek(0)
+    sd = torch.load(buf, weights_only=True)
+    lin2 = torch.nn.Linear(256, 64, dtype=torch.bfloat16)
+    quantize_(lin2, Int4WeightOnlyConfig(group_size=32))
+    lin2.load_state_dict(sd, assign=True)
+    assert torch.equal(lin2.weight.dequantize(), lin.weight.dequantize())
+
+
+def test_copy_between_same_layout():
+    a = _int4_linear()
+    b = _int4_linear()
+    with torch.no_grad():
+        b.weight.tensor_impl.packed_weight.zero_()
+        b.weight.copy_(a.weight)
+    assert torch.equal(b.weight.dequantize(), a.weight.dequantize())
+
+
+def test_custom_dispatch_plugin_takes_precedence():
+    lin = _int4_linear()
+    calls = []
+
+    def check(x, w, b):
+        return isinstance(w, AffineQuantizedTensor) and x.shape[-1] == 256
+
+    def impl(x, w, b):
+        calls.append(1)
+        return torch.zeros(*x.shape[:-1], w.shape[0], dtype=x.dtype)
+
+    register_aqt_quantized_linear_dispatch(check, impl)
+    # move the new entry to the front (dict order = precedence)
+    from torchao.dtypes import affine_quantized_tensor_ops as ops_mod
+
+    table = ops_mod._AQT_QLINEAR_DISPATCH_TABLE
+    items = list(table.items())
+    table.clear()
+    table[check] = impl
+    table.update({k: v for k, v in items if k is not check})
+    try:
+        y = lin(torch.randn(2, 256, dtype=torch.bfloat16))
+        assert calls == [1] and torch.count_nonzero(y) == 0
+    finally:
+        deregister_aqt_quantized_linear_dispatch(check)
+
+
+def test_cpu_linear_fails_loudly_no_silent_fallback():
+    """The int4 op has no CPU kernel: a CPU call must raise, never compute elsewhere."""
+    lin = _int4_linear()
+    with pytest.raises((NotImplementedError, RuntimeError)):
+        lin(torch.randn(1, 256, dtype=torch.bfloat16))
+
+
+# ---------------------------------------------------------------------------------------------
+# op registration (schemas + fake impls, used by torch.compile)
+# ---------------------------------------------------------------------------------------------
+def test_fake_impls_shapes():
+    from torch._subclasses.fake_tensor import FakeTensorMode
+
+    with FakeTensorMode():
+        x = torch.empty(3, 5, 4096, dtype=torch.bfloat16, device="cuda")
+        pw = torch.empty(512, 512, dtype=torch.int32, device="cuda")
+        sz = torch.empty(512, 128, 2, dtype=torch.bfloat16, device="cuda")
+        y = torch.ops.torchao.int4_weight_only_linear(x, pw, sz, 32, None)
+        assert y.shape == (3, 5, 512) and y.dtype == torch.bfloat16
+        tile = torch.empty(64, 32, 32, 4, dtype=torch.int32, device="cuda")
+        assert torch.ops.torchao.unpack_tensor_core_tiled_layout(tile, 8).shape == (512, 4096)
+        sz_t = torch.empty(128, 512, 2, dtype=torch.bfloat16, device="cuda")
+        d = torch.ops.torchao.dequantize_tensor_core_tiled_layout(tile, sz_t, 32, 8)
+        assert d.shape == (512, 4096) and d.dtype == torch.bfloat16
+        q, s = torch.ops.torchao.int8_quantize_per_token(x)
+        assert q.dtype == torch.int8 and s.shape == (3, 5, 1)
+        w8 = torch.empty(512, 4096, dtype=torch.int8, device="cuda")
+        ws = torch.empty(512, dtype=torch.bfloat16, device="cuda")
+        assert torch.ops.torchao.int8_scaled_mm(q, s, w8, ws, None).shape == (3, 5, 512)
+        assert torch.ops.torchao.int8_weight_only_linear(x, w8, ws, None).shape == (3, 5, 512)
+
+
+def test_fake_impl_rejects_bad_group_size():
+    from torch._subclasses.fake_tensor import FakeTensorMode
+
+    with FakeTensorMode():
+        x = torch.empty(1, 4096, dtype=torch.bfloat16, device="cuda")
+        pw = torch.empty(512, 512, dtype=torch.int32, device="cuda")
+        sz = torch.empty(512, 64, 2, dtype=torch.bfloat16, device="cuda")
+        with pytest.raises(Exception, match="qGroupSize"):
+            torch.ops.torchao.int4_weight_only_linear(x, pw, sz, 48, None)

@@ -1,0 +1,152 @@
+// Library-level C-ABI entry points (version, error state, device count) and the host-side
+// int4 packers. Kernel entry points live next to their kernels (int4_*.hip, int8_*.hip).
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+#include "tao_common.h"
+
+namespace tao {
+
+static thread_local char g_err[512] = {0};
+
+int set_error(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+void clear_error() { g_err[0] = 0; }
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(TAO_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+  return TAO_OK;
+}
+
+// ---- per-kernel timing sessions --------------------------------------------------------------
+struct ProfileSession {
+  bool active = false;
+  std::vector<hipEvent_t> start, stop;
+  size_t used = 0;
+};
+static thread_local ProfileSession g_prof;
+
+bool profile_slot(hipEvent_t* a, hipEvent_t* b) {
+  if (!g_prof.active || g_prof.used >= g_prof.start.size()) return false;
+  *a = g_prof.start[g_prof.used];
+  *b = g_prof.stop[g_prof.used];
+  ++g_prof.used;
+  return true;
+}
+
+static void profile_release() {
+  for (hipEvent_t e : g_prof.start) (void)hipEventDestroy(e);
+  for (hipEvent_t e : g_prof.stop) (void)hipEventDestroy(e);
+  g_prof.start.clear();
+  g_prof.stop.clear();
+  g_prof.used = 0;
+  g_prof.active = false;
+}
+
+}  // namespace tao
+
+extern "C" {
+
+const char* tao_version(void) { return "torchao-mi355x 0.1.0 gfx950"; }
+
+const char* tao_last_error(void) { return tao::g_err; }
+
+int tao_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+int tao_profile_begin(int capacity) {
+  TAO_CHECK_ARG(capacity > 0 && capacity <= (1 << 20), "profile: capacity out of range");
+  tao::profile_release();
+  tao::g_prof.start.resize(capacity, nullptr);
+  tao::g_prof.stop.resize(capacity, nullptr);
+  for (int i = 0; i < capacity; ++i) {
+    if (hipEventCreate(&tao::g_prof.start[i]) != hipSuccess ||
+        hipEventCreate(&tao::g_prof.stop[i]) != hipSuccess) {
+      tao::profile_release();
+      return tao::set_error(TAO_ERR_HIP, "profile: hipEventCreate failed");
+    }
+  }
+  tao::g_prof.active = true;
+  return TAO_OK;
+}
+
+int tao_profile_end(float* durations_ms, int capacity, int* count) {
+  TAO_CHECK_ARG(count != nullptr, "profile: null count");
+  *count = 0;
+  if (!tao::g_prof.active) return tao::set_error(TAO_ERR_INVALID_ARGUMENT, "profile: no session");
+  const int n = (int)tao::g_prof.used;
+  int rc = TAO_OK;
+  for (int i = 0; i < n && i < capacity; ++i) {
+    float ms = 0.f;
+    if (hipEventSynchronize(tao::g_prof.stop[i]) != hipSuccess ||
+        hipEventElapsedTime(&ms, tao::g_prof.start[i], tao::g_prof.stop[i]) != hipSuccess) {
+      rc = tao::set_error(TAO_ERR_HIP, "profile: event timing failed for launch %d", i);
+      break;
+    }
+    durations_ms[i] = ms;
+    *count = i + 1;
+  }
+  tao::profile_release();
+  return rc;
+}
+
+// Host packer: identical bytes to int4_pack_kernel (int4_pack.hip). Used when quantize_ runs on
+// a CPU-resident model (the reference quantizes on whatever device the weight lives on,
+// torchao/quantization/quant_api.py:173-222).
+int tao_int4_pack_host(const int32_t* q, uint32_t* packed, int64_t N, int64_t K) {
+  TAO_CHECK_ARG(N >= 0 && K >= 0 && K % 8 == 0, "int4 pack: need K %% 8 == 0 (K=%lld)",
+                (long long)K);
+  TAO_CHECK_ARG(q != nullptr || N * K == 0, "int4 pack: null q");
+  const int64_t KD = K / 8;
+  for (int64_t n = 0; n < N; ++n) {
+    const int32_t* row = q + n * K;
+    for (int64_t d = 0; d < KD; ++d) {
+      uint32_t w = 0;
+      for (int i = 0; i < 4; ++i) {
+        int32_t a = row[8 * d + 2 * i], b = row[8 * d + 2 * i + 1];
+        if ((uint32_t)a > 15u || (uint32_t)b > 15u)
+          return tao::set_error(TAO_ERR_INVALID_ARGUMENT,
+                                "int4 pack: value out of [0,15] at row %lld", (long long)n);
+        w |= (uint32_t)a << (4 * i);
+        w |= (uint32_t)b << (16 + 4 * i);
+      }
+      packed[n * KD + d] = w;
+    }
+  }
+  return TAO_OK;
+}
+
+int tao_int4_unpack_host(const uint32_t* packed, int32_t* q, int64_t N, int64_t K) {
+  TAO_CHECK_ARG(N >= 0 && K >= 0 && K % 8 == 0, "int4 unpack: need K %% 8 == 0 (K=%lld)",
+                (long long)K);
+  const int64_t KD = K / 8;
+  for (int64_t n = 0; n < N; ++n) {
+    for (int64_t d = 0; d < KD; ++d) {
+      uint32_t w = packed[n * KD + d];
+      int32_t* out = q + n * K + 8 * d;
+      for (int i = 0; i < 4; ++i) {
+        out[2 * i] = (w >> (4 * i)) & 0xF;
+        out[2 * i + 1] = (w >> (16 + 4 * i)) & 0xF;
+      }
+    }
+  }
+  return TAO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,146 @@
+// int8 per-channel weight-only linear, skinny-M (decode) path:
+//   y[m][n] = bf16( bf16( sum_k x[m][k] * w[n][k] ) * scale[n] ) (+ bias[n])
+// Replaces torch.mm(x, w.t().to(bf16)) * scale at torchao/dtypes/uintx/plain_layout.py:256-266,
+// which materialises a bf16 copy of W (2x the bytes) before a library GEMM; here W is read once.
+//
+// Same decomposition as int4_gemv.hip: a slice is 1024 k of one row = 64 lanes x 16 B (int8);
+// a wave owns RPW rows; Wk waves split K inside a workgroup; LDS combines the waves.
+// Per lane: bytes are biased to unsigned (xor 0x80), converted with v_cvt_f32_ubyte{0..3} and
+// FMA'd against x in f32; the bias is removed once per chunk as 128 * sum(x).
+#include "tao_common.h"
+#include "tao_reduce.h"
+
+namespace tao {
+namespace {
+
+template <int MT, int RPW>
+__global__ __launch_bounds__(512) void int8wo_gemv_kernel(
+    const uint16_t* __restrict__ x, const uint4* __restrict__ w,
+    const uint16_t* __restrict__ scale, const uint16_t* __restrict__ bias,
+    uint16_t* __restrict__ y, int M, int N, int K, int Wk, int G, int S) {
+  constexpr int V = RPW * MT;
+  extern __shared__ float red[];  // [G][Wk][V]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wk = wave % Wk;
+  const int rg = wave / Wk;
+  const int row0 = (blockIdx.x * G + rg) * RPW;
+  const int nchunk = K >> 4;  // 16-k (16-B) chunks per row
+
+  float acc[RPW][MT];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[r][m] = 0.f;
+
+  for (int s = wk; s < S; s += Wk) {
+    const int c = s * 64 + lane;
+    const bool cval = c < nchunk;
+    const int cc = cval ? c : nchunk - 1;
+
+    uint4 wv[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int n = row0 + r;
+      const int nn = n < N ? n : N - 1;
+      wv[r] = ld_nt_u4(w + (size_t)nn * nchunk + cc);
+    }
+    float xf[MT][16];
+    float sx128[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int mm = m < M ? m : M - 1;
+      const uint4* xp = reinterpret_cast<const uint4*>(x + (size_t)mm * K + (size_t)cc * 16);
+      const uint4 a = xp[0], b = xp[1];
+      const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t di = cval ? d[i] : 0u;
+        xf[m][2 * i] = bf16lo_to_f32(di);
+        xf[m][2 * i + 1] = bf16hi_to_f32(di);
+        t = dot2_bf16(di, 0x3F803F80u, t);
+      }
+      sx128[m] = 128.f * t;
+    }
+
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const uint32_t wd[4] = {wv[r].x ^ 0x80808080u, wv[r].y ^ 0x80808080u,
+                              wv[r].z ^ 0x80808080u, wv[r].w ^ 0x80808080u};
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          d = fmaf(xf[m][4 * j + 0], (float)(wd[j] & 0xFF), d);
+          d = fmaf(xf[m][4 * j + 1], (float)((wd[j] >> 8) & 0xFF), d);
+          d = fmaf(xf[m][4 * j + 2], (float)((wd[j] >> 16) & 0xFF), d);
+          d = fmaf(xf[m][4 * j + 3], (float)(wd[j] >> 24), d);
+        }
+        acc[r][m] += d - sx128[m];
+      }
+    }
+  }
+
+  float v[V];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) v[r * MT + m] = acc[r][m];
+  wave_reduce_scatter<V>(v, lane);
+
+  constexpr int T = Log2<V>::value;
+  const bool owner = (lane & ((64 >> T) - 1)) == 0;
+  const int idx = lane >> (6 - T);
+  float total = v[0];
+  bool writer = owner;
+  int widx = idx;
+  if (Wk > 1) {
+    if (owner) red[(rg * Wk + wk) * V + idx] = v[0];
+    __syncthreads();
+    writer = (wk == 0) && (lane < V);
+    widx = lane;
+    if (writer) {
+      total = 0.f;
+      for (int kk = 0; kk < Wk; ++kk) total += red[(rg * Wk + kk) * V + widx];
+    }
+  }
+  if (writer) {
+    const int r = widx / MT, m = widx % MT;
+    const int n = row0 + r;
+    if (n < N && m < M) {
+      // bf16 mm output, then bf16 * scale, then + bias: the reference's three roundings.
+      float o = round_bf16(round_bf16(total) * bf16_to_f32(scale[n]));
+      if (bias != nullptr) o = round_bf16(o + bf16_to_f32(bias[n]));
+      y[(size_t)m * N + n] = f32_to_bf16(o);
+    }
+  }
+}
+
+template <int MT, int RPW>
+int launch_gemv(const uint16_t* x, const int8_t* w, const uint16_t* scale, const uint16_t* bias,
+                uint16_t* y, int M, int N, int K, hipStream_t stream) {
+  const int nchunk = K / 16;
+  const int S = (nchunk + 63) / 64;
+  const int Wk = S < 8 ? S : 8;
+  const int G = (8 / Wk) > 0 ? 8 / Wk : 1;
+  const int rows_per_wg = G * RPW;
+  const int grid = (N + rows_per_wg - 1) / rows_per_wg;
+  const size_t lds = (size_t)G * Wk * RPW * MT * sizeof(float);
+  launch((int8wo_gemv_kernel<MT, RPW>), dim3(grid), dim3(64 * Wk * G), lds, stream,
+                     x, reinterpret_cast<const uint4*>(w), scale, bias, y, M, N, K, Wk, G, S);
+  return check_launch("int8wo_gemv_kernel");
+}
+
+}  // namespace
+
+int int8wo_gemv(const uint16_t* x, const int8_t* w, const uint16_t* scale, const uint16_t* bias,
+                uint16_t* y, int64_t M, int64_t N, int64_t K, hipStream_t stream) {
+  if (M <= 1) return launch_gemv<1, 4>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream);
+  if (M <= 2) return launch_gemv<2, 4>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream);
+  if (M <= 4) return launch_gemv<4, 2>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream);
+  return launch_gemv<8, 2>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream);
+}
+
+}  // namespace tao

@@ -1,0 +1,88 @@
+// Shared helpers for the gfx950 kernels behind include/torchao_mi355x.h.
+// Internal header: not part of the C-ABI.
+#pragma once
+
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/torchao_mi355x.h"
+
+namespace tao {
+
+// ---- error reporting (defined in capi.cpp) ------------------------------------------------
+int set_error(int code, const char* fmt, ...);
+void clear_error();
+
+#define TAO_CHECK_ARG(cond, ...)                                             \
+  do {                                                                       \
+    if (!(cond)) return ::tao::set_error(TAO_ERR_INVALID_ARGUMENT, __VA_ARGS__); \
+  } while (0)
+
+#define TAO_CHECK_ALIGN(ptr, bytes, name)                                            \
+  TAO_CHECK_ARG((reinterpret_cast<uintptr_t>(ptr) % (bytes)) == 0,                   \
+                "%s must be %d-byte aligned (got %p)", name, (int)(bytes), (const void*)(ptr))
+
+// Check the launch of the kernel just enqueued (no synchronisation: capture-safe).
+int check_launch(const char* what);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- optional per-kernel timing (tao_profile_begin / tao_profile_end, capi.cpp) ---------------
+// While a profile session is open on this thread, each launch gets a start/stop hipEvent pair
+// recorded by the kernel's own dispatch packet (hipExtLaunchKernelGGL): the same interval
+// rocprofv3 reports as the kernel's duration. Outside a session launches are plain.
+bool profile_slot(hipEvent_t* start, hipEvent_t* stop);
+
+// Enqueue a kernel (callers then check_launch(name)).
+template <typename K, typename... Args>
+void launch(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t stream, Args... args) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (profile_slot(&a, &b))
+    hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, stream, a, b, 0, args...);
+  else
+    hipLaunchKernelGGL(kernel, grid, block, lds, stream, args...);
+}
+
+// ---- device numerics --------------------------------------------------------------------
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+__device__ __forceinline__ float bf16lo_to_f32(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16hi_to_f32(uint32_t w) {
+  return __uint_as_float(w & 0xFFFF0000u);
+}
+
+// Round-to-nearest-even f32 -> bf16 (v_cvt_pk_bf16_f32 on gfx950; keeps NaN a NaN).
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
+}
+__device__ __forceinline__ float round_bf16(float f) { return bf16_to_f32(f32_to_bf16(f)); }
+
+// acc + a.lo*b.lo + a.hi*b.hi on bf16 pairs (v_dot2c_f32_bf16).
+__device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float acc) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a),
+                                         __builtin_bit_cast(bf16x2_t, b), acc, false);
+}
+
+// Two nibbles (bits 4i and 16+4i) -> bf16 pair (128+q_lo, 128+q_hi): the exact "magic number"
+// conversion (0x4300 = 128.0 in bf16, q fills the low mantissa bits).
+__device__ __forceinline__ uint32_t nib_pair_bf16(uint32_t w, int i) {
+  return ((w >> (4 * i)) & 0x000F000Fu) | 0x43004300u;
+}
+
+template <typename T>
+__device__ __forceinline__ T ld_nt(const T* p) {
+  return __builtin_nontemporal_load(p);
+}
+
+__device__ __forceinline__ uint4 ld_nt_u4(const uint4* p) {
+  // Non-temporal 16-B load of streamed-once weights (MI355X_MICROARCH "nt-weights").
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+constexpr int kWave = 64;
+
+}  // namespace tao

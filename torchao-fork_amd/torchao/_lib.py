@@ -1,0 +1,132 @@
+"""ctypes binding of the gfx950 C-ABI library (``include/torchao_mi355x.h``).
+
+The reference loads its native ops as ``torchao/_C*.so`` through ``torch.ops.load_library``
+(torchao/__init__.py:26-32). Here the native code is a plain C-ABI shared library with no torch
+types in its signatures; this module binds it with ctypes and ``torchao.ops`` registers the
+``torch.ops.torchao.*`` operators on top of it.
+
+The product path never falls back to anything else: if the library is missing or was built
+without a GPU-usable runtime, every op that needs it raises ``RuntimeError``.
+"""
+
+import ctypes
+import os
+from typing import Optional
+
+_LIB_NAME = "libtorchao_mi355x.so"
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), _LIB_NAME)
+
+_lib: Optional[ctypes.CDLL] = None
+_load_error: Optional[str] = None
+
+_i64 = ctypes.c_int64
+_p = ctypes.c_void_p
+_int = ctypes.c_int
+
+# name -> argtypes (restype is c_int unless listed in _RESTYPES)
+_SIGNATURES = {
+    "tao_version": [],
+    "tao_last_error": [],
+    "tao_device_count": [],
+    "tao_profile_begin": [_int],
+    "tao_profile_end": [_p, _int, _p],
+    "tao_int4wo_linear_bf16": [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p],
+    "tao_int4_pack": [_p, _p, _i64, _i64, _p],
+    "tao_int4_pack_u8": [_p, _p, _i64, _i64, _p],
+    "tao_int4_unpack": [_p, _p, _i64, _i64, _p],
+    "tao_int4_dequant": [_p, _p, _p, _i64, _i64, _i64, _int, _p],
+    "tao_int4_pack_host": [_p, _p, _i64, _i64],
+    "tao_int4_unpack_host": [_p, _p, _i64, _i64],
+    "tao_unpack_tensor_core_tiled_layout": [_p, _p, _i64, _i64, _i64, _p],
+    "tao_dequantize_tensor_core_tiled_layout": [_p, _p, _p, _i64, _i64, _i64, _i64, _p],
+    "tao_pack_tensor_core_tiled_layout": [_p, _p, _i64, _i64, _i64, _p],
+    "tao_int8wo_linear_bf16": [_p, _p, _p, _p, _p, _i64, _i64, _i64, _p],
+    "tao_int8_quant_per_token": [_p, _p, _p, _i64, _i64, _p],
+    "tao_int8_scaled_mm_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p],
+}
+_RESTYPES = {"tao_version": ctypes.c_char_p, "tao_last_error": ctypes.c_char_p}
+
+
+def library_path() -> str:
+    return _LIB_PATH
+
+
+def exported_symbols():
+    """Names the header declares (the C-ABI contract checked by the CPU tests)."""
+    return sorted(_SIGNATURES)
+
+
+def _load() -> Optional[ctypes.CDLL]:
+    global _lib, _load_error
+    if _lib is not None or _load_error is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        _load_error = (
+            f"{_LIB_NAME} not found at {_LIB_PATH}; build it with "
+            "`make -C torchao-fork_amd/csrc` (or __graft_entry__.build())"
+        )
+        return None
+    try:
+        # torch must be imported first so the HIP runtime it bundles (same soname,
+        # libamdhip64.so.7) is the one this library binds to.
+        import torch  # noqa: F401
+
+        lib = ctypes.CDLL(_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    except OSError as e:  # pragma: no cover - environment specific
+        _load_error = f"failed to load {_LIB_PATH}: {e}"
+        return None
+    for name, argtypes in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    _lib = lib
+    return _lib
+
+
+def is_available() -> bool:
+    return _load() is not None
+
+
+def load_error() -> Optional[str]:
+    _load()
+    return _load_error
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded library; raises RuntimeError (never falls back) when it is missing."""
+    handle = _load()
+    if handle is None:
+        raise RuntimeError(f"torchao MI355X native library unavailable: {_load_error}")
+    return handle
+
+
+class KernelTimer:
+    """``with KernelTimer(n) as t: <launch kernels>`` -> ``t.durations_ms`` (one per launch).
+
+    Uses tao_profile_begin/end: HIP events written by each kernel's own dispatch packet, so the
+    numbers are kernel execution times (what rocprofv3 reports), without launch gaps."""
+
+    def __init__(self, capacity: int):
+        self.capacity = capacity
+        self.durations_ms = []
+
+    def __enter__(self):
+        call("tao_profile_begin", self.capacity)
+        return self
+
+    def __exit__(self, *exc):
+        buf = (ctypes.c_float * self.capacity)()
+        n = ctypes.c_int(0)
+        call("tao_profile_end", ctypes.cast(buf, ctypes.c_void_p), self.capacity,
+             ctypes.cast(ctypes.pointer(n), ctypes.c_void_p))
+        self.durations_ms = [float(buf[i]) for i in range(n.value)]
+        return False
+
+
+def call(name: str, *args) -> None:
+    """Invoke a C-ABI entry point and turn a non-zero status into RuntimeError."""
+    handle = lib()
+    rc = getattr(handle, name)(*args)
+    if rc != 0:
+        msg = handle.tao_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (status {rc}): {msg}")

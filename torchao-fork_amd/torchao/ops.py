@@ -1,0 +1,431 @@
+"""``torch.ops.torchao`` operators of the MI355X weight-only quantized linear path.
+
+Follows the reference's registration pattern (torchao/ops.py:12-21 ``Library("torchao",
+"FRAGMENT")`` + ``lib.define`` schemas, :73-77 ``register_fake`` meta impls using
+``torch._check``). The device impls are registered for the ``CUDA`` dispatch key (which is HIP
+on ROCm, as in tensor_core_tiled_layout.cu:370-374) and call the gfx950 C-ABI library
+(``include/torchao_mi355x.h``) on the current stream: no allocation besides the output (caching
+allocator), no host synchronisation, so every op is hipGraph-capturable.
+
+Operators:
+  * ``unpack_tensor_core_tiled_layout`` / ``dequantize_tensor_core_tiled_layout`` — the
+    reference schemas (ops.py:16-21), on the reference tile format.
+  * ``pack_tensor_core_tiled_layout`` — inverse of the unpack (the tile format that
+    ``aten._convert_weight_to_int4pack`` produces), for checkpoint interchange.
+  * ``int4_pack`` / ``int4_unpack`` / ``int4_dequantize`` / ``int4_weight_only_linear`` — the
+    gfx950 row-stream int4 layout; ``int4_weight_only_linear`` replaces
+    ``aten._weight_int4pack_mm`` (tensor_core_tiled_layout.py:104).
+  * ``int8_weight_only_linear`` — replaces mm + scale (plain_layout.py:256-266).
+  * ``int8_quantize_per_token`` / ``int8_scaled_mm`` — replace the activation quant
+    (quant_api.py:1258-1273) and ``int_scaled_matmul`` + weight scale (plain_layout.py:294-315).
+"""
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from torchao import _lib
+
+lib = torch.library.Library("torchao", "FRAGMENT")
+lib.define("unpack_tensor_core_tiled_layout(Tensor packed_w, int inner_k_tiles) -> Tensor")
+lib.define(
+    "dequantize_tensor_core_tiled_layout(Tensor packed_w, Tensor scales_and_zeros, "
+    "int group_size, int inner_k_tiles) -> Tensor"
+)
+lib.define("pack_tensor_core_tiled_layout(Tensor int_data, int inner_k_tiles) -> Tensor")
+lib.define("int4_pack(Tensor int_data) -> Tensor")
+lib.define("int4_pack_u8(Tensor int_data_u8) -> Tensor")
+lib.define("int4_unpack(Tensor packed_w) -> Tensor")
+lib.define(
+    "int4_dequantize(Tensor packed_w, Tensor scales_and_zeros, int group_size, int mode=0) "
+    "-> Tensor"
+)
+lib.define(
+    "int4_weight_only_linear(Tensor x, Tensor packed_w, Tensor scales_and_zeros, "
+    "int group_size, Tensor? bias=None) -> Tensor"
+)
+lib.define(
+    "int8_weight_only_linear(Tensor x, Tensor w_int8, Tensor scale, Tensor? bias=None) -> Tensor"
+)
+lib.define("int8_quantize_per_token(Tensor x) -> (Tensor, Tensor)")
+lib.define(
+    "int8_scaled_mm(Tensor x_int8, Tensor x_scale, Tensor w_int8, Tensor w_scale, "
+    "Tensor? bias=None) -> Tensor"
+)
+
+_GROUP_SIZES = (32, 64, 128, 256)
+
+
+def _ptr(t: Optional[Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(t: Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _require_contig(t: Tensor, name: str):
+    torch._check(t.is_contiguous(), lambda: f"{name} must be contiguous")
+
+
+# ---------------------------------------------------------------------------------------------
+# reference tile format (torchao/ops.py:255-377)
+# ---------------------------------------------------------------------------------------------
+def _check_tile(packed_w: Tensor, inner_k_tiles: int):
+    torch._check(
+        packed_w.dim() == 4, lambda: f"packed weight should be a 4d tensor, got {packed_w.dim()}D"
+    )
+    torch._check(
+        packed_w.dtype is torch.int32, lambda: f"weight must be INT32, got {packed_w.dtype}"
+    )
+    torch._check(inner_k_tiles in (2, 4, 8), lambda: "inner_k_tiles must be 2, 4, or 8")
+    torch._check(packed_w.size(2) == 32, lambda: "packed weight must have 32 at dim 2")
+    torch._check(
+        packed_w.size(3) == inner_k_tiles // 2,
+        lambda: "packed weight must have inner_k_tiles/2 at dim 3",
+    )
+    return packed_w.size(0) * 8, packed_w.size(1) * inner_k_tiles * 16
+
+
+def _check_tile_sz(sz: Tensor, group_size: int, N: int, K: int):
+    torch._check(sz.dtype is torch.bfloat16, lambda: "scales_and_zeros must be bfloat16")
+    torch._check(sz.dim() == 3, lambda: f"scales_and_zeros must be 3D, got {sz.dim()}")
+    torch._check(group_size in _GROUP_SIZES, lambda: "qGroupSize must be 32, 64, 128, or 256")
+    torch._check(
+        sz.size(0) == K // group_size, lambda: "scales_and_zeros must have K // qGroupSize at dim 0"
+    )
+    torch._check(sz.size(1) == N, lambda: "scales_and_zeros must have N at dim 1")
+    torch._check(sz.size(2) == 2, lambda: "scales_and_zeros must have 2 at dim 2")
+
+
+@torch.library.register_fake("torchao::unpack_tensor_core_tiled_layout")
+def _(packed_w: Tensor, inner_k_tiles: int) -> Tensor:
+    N, K = _check_tile(packed_w, inner_k_tiles)
+    return packed_w.new_empty((N, K), dtype=torch.int32)
+
+
+def _unpack_tile_cuda(packed_w: Tensor, inner_k_tiles: int) -> Tensor:
+    N, K = _check_tile(packed_w, inner_k_tiles)
+    _require_contig(packed_w, "packed_w")
+    out = torch.empty((N, K), dtype=torch.int32, device=packed_w.device)
+    with torch.cuda.device(packed_w.device):
+        _lib.call("tao_unpack_tensor_core_tiled_layout", _ptr(packed_w), _ptr(out), N, K,
+                  inner_k_tiles, _stream(packed_w))
+    return out
+
+
+@torch.library.register_fake("torchao::dequantize_tensor_core_tiled_layout")
+def _(packed_w: Tensor, scales_and_zeros: Tensor, group_size: int, inner_k_tiles: int) -> Tensor:
+    N, K = _check_tile(packed_w, inner_k_tiles)
+    _check_tile_sz(scales_and_zeros, group_size, N, K)
+    return packed_w.new_empty((N, K), dtype=torch.bfloat16)
+
+
+def _dequant_tile_cuda(packed_w, scales_and_zeros, group_size, inner_k_tiles):
+    N, K = _check_tile(packed_w, inner_k_tiles)
+    _check_tile_sz(scales_and_zeros, group_size, N, K)
+    _require_contig(packed_w, "packed_w")
+    _require_contig(scales_and_zeros, "scales_and_zeros")
+    out = torch.empty((N, K), dtype=torch.bfloat16, device=packed_w.device)
+    with torch.cuda.device(packed_w.device):
+        _lib.call("tao_dequantize_tensor_core_tiled_layout", _ptr(packed_w),
+                  _ptr(scales_and_zeros), _ptr(out), N, K, group_size, inner_k_tiles,
+                  _stream(packed_w))
+    return out
+
+
+def _check_pack_tile(int_data: Tensor, inner_k_tiles: int):
+    torch._check(int_data.dim() == 2 and int_data.dtype is torch.int32,
+                 lambda: "int_data must be a 2D int32 tensor")
+    torch._check(inner_k_tiles in (2, 4, 8), lambda: "inner_k_tiles must be 2, 4, or 8")
+    N, K = int_data.shape
+    torch._check(N % 8 == 0, lambda: f"N ({N}) must be a multiple of 8")
+    torch._check(K % (inner_k_tiles * 16) == 0,
+                 lambda: f"K ({K}) must be a multiple of {inner_k_tiles * 16}")
+    return N, K
+
+
+@torch.library.register_fake("torchao::pack_tensor_core_tiled_layout")
+def _(int_data: Tensor, inner_k_tiles: int) -> Tensor:
+    N, K = _check_pack_tile(int_data, inner_k_tiles)
+    return int_data.new_empty(
+        (N // 8, K // (inner_k_tiles * 16), 32, inner_k_tiles // 2), dtype=torch.int32
+    )
+
+
+def _pack_tile_cuda(int_data: Tensor, inner_k_tiles: int) -> Tensor:
+    N, K = _check_pack_tile(int_data, inner_k_tiles)
+    _require_contig(int_data, "int_data")
+    out = torch.empty((N // 8, K // (inner_k_tiles * 16), 32, inner_k_tiles // 2),
+                      dtype=torch.int32, device=int_data.device)
+    with torch.cuda.device(int_data.device):
+        _lib.call("tao_pack_tensor_core_tiled_layout", _ptr(int_data), _ptr(out), N, K,
+                  inner_k_tiles, _stream(int_data))
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# gfx950 row-stream int4 layout
+# ---------------------------------------------------------------------------------------------
+def _check_int4_plain(int_data: Tensor):
+    torch._check(int_data.dim() == 2, lambda: "int4_pack expects a 2D [N, K] tensor")
+    torch._check(int_data.dtype is torch.int32, lambda: "int4_pack expects int32 values 0..15")
+    torch._check(int_data.size(1) % 8 == 0, lambda: "int4_pack: K must be a multiple of 8")
+
+
+@torch.library.register_fake("torchao::int4_pack")
+def _(int_data: Tensor) -> Tensor:
+    _check_int4_plain(int_data)
+    return int_data.new_empty((int_data.size(0), int_data.size(1) // 8), dtype=torch.int32)
+
+
+def _int4_pack_cuda(int_data: Tensor) -> Tensor:
+    _check_int4_plain(int_data)
+    int_data = int_data.contiguous()
+    N, K = int_data.shape
+    out = torch.empty((N, K // 8), dtype=torch.int32, device=int_data.device)
+    with torch.cuda.device(int_data.device):
+        _lib.call("tao_int4_pack", _ptr(int_data), _ptr(out), N, K, _stream(int_data))
+    return out
+
+
+def _int4_pack_cpu(int_data: Tensor) -> Tensor:
+    _check_int4_plain(int_data)
+    int_data = int_data.contiguous()
+    N, K = int_data.shape
+    out = torch.empty((N, K // 8), dtype=torch.int32)
+    _lib.call("tao_int4_pack_host", _ptr(int_data), _ptr(out), N, K)
+    return out
+
+
+@torch.library.register_fake("torchao::int4_pack_u8")
+def _(int_data_u8: Tensor) -> Tensor:
+    torch._check(int_data_u8.dim() == 2 and int_data_u8.dtype is torch.uint8,
+                 lambda: "int4_pack_u8 expects a 2D uint8 [N, K/2] tensor")
+    return int_data_u8.new_empty((int_data_u8.size(0), int_data_u8.size(1) // 4), dtype=torch.int32)
+
+
+def _int4_pack_u8_cuda(int_data_u8: Tensor) -> Tensor:
+    torch._check(int_data_u8.dim() == 2 and int_data_u8.dtype is torch.uint8,
+                 lambda: "int4_pack_u8 expects a 2D uint8 [N, K/2] tensor")
+    int_data_u8 = int_data_u8.contiguous()
+    N, K = int_data_u8.size(0), int_data_u8.size(1) * 2
+    out = torch.empty((N, K // 8), dtype=torch.int32, device=int_data_u8.device)
+    with torch.cuda.device(int_data_u8.device):
+        _lib.call("tao_int4_pack_u8", _ptr(int_data_u8), _ptr(out), N, K, _stream(int_data_u8))
+    return out
+
+
+@torch.library.register_fake("torchao::int4_unpack")
+def _(packed_w: Tensor) -> Tensor:
+    torch._check(packed_w.dim() == 2 and packed_w.dtype is torch.int32,
+                 lambda: "int4_unpack expects a 2D int32 [N, K/8] tensor")
+    return packed_w.new_empty((packed_w.size(0), packed_w.size(1) * 8), dtype=torch.int32)
+
+
+def _int4_unpack_cuda(packed_w: Tensor) -> Tensor:
+    _require_contig(packed_w, "packed_w")
+    N, K = packed_w.size(0), packed_w.size(1) * 8
+    out = torch.empty((N, K), dtype=torch.int32, device=packed_w.device)
+    with torch.cuda.device(packed_w.device):
+        _lib.call("tao_int4_unpack", _ptr(packed_w), _ptr(out), N, K, _stream(packed_w))
+    return out
+
+
+def _int4_unpack_cpu(packed_w: Tensor) -> Tensor:
+    packed_w = packed_w.contiguous()
+    N, K = packed_w.size(0), packed_w.size(1) * 8
+    out = torch.empty((N, K), dtype=torch.int32)
+    _lib.call("tao_int4_unpack_host", _ptr(packed_w), _ptr(out), N, K)
+    return out
+
+
+def _check_int4_weight(packed_w: Tensor, sz: Tensor, group_size: int):
+    torch._check(packed_w.dim() == 2 and packed_w.dtype is torch.int32,
+                 lambda: "packed weight must be a 2D int32 [N, K/8] tensor")
+    N, K = packed_w.size(0), packed_w.size(1) * 8
+    torch._check(group_size in _GROUP_SIZES, lambda: "qGroupSize must be 32, 64, 128, or 256")
+    torch._check(K % group_size == 0, lambda: f"K ({K}) must be divisible by qGroupSize")
+    torch._check(sz.dtype is torch.bfloat16, lambda: "scales_and_zeros must be bfloat16")
+    torch._check(
+        tuple(sz.shape) == (N, K // group_size, 2),
+        lambda: f"scales_and_zeros must be [N, K/g, 2] = {(N, K // group_size, 2)}, got {tuple(sz.shape)}",
+    )
+    return N, K
+
+
+@torch.library.register_fake("torchao::int4_dequantize")
+def _(packed_w: Tensor, scales_and_zeros: Tensor, group_size: int, mode: int = 0) -> Tensor:
+    N, K = _check_int4_weight(packed_w, scales_and_zeros, group_size)
+    return packed_w.new_empty((N, K), dtype=torch.bfloat16)
+
+
+def _int4_dequant_cuda(packed_w, scales_and_zeros, group_size, mode=0):
+    N, K = _check_int4_weight(packed_w, scales_and_zeros, group_size)
+    _require_contig(packed_w, "packed_w")
+    _require_contig(scales_and_zeros, "scales_and_zeros")
+    out = torch.empty((N, K), dtype=torch.bfloat16, device=packed_w.device)
+    with torch.cuda.device(packed_w.device):
+        _lib.call("tao_int4_dequant", _ptr(packed_w), _ptr(scales_and_zeros), _ptr(out), N, K,
+                  group_size, int(mode), _stream(packed_w))
+    return out
+
+
+def _linear_out_shape(x: Tensor, N: int):
+    return (*x.shape[:-1], N)
+
+
+@torch.library.register_fake("torchao::int4_weight_only_linear")
+def _(x, packed_w, scales_and_zeros, group_size, bias=None):
+    N, K = _check_int4_weight(packed_w, scales_and_zeros, group_size)
+    torch._check(x.dtype is torch.bfloat16, lambda: "int4 weight-only linear needs bf16 input")
+    torch._check(x.size(-1) == K, lambda: f"x last dim {x.size(-1)} != K {K}")
+    return x.new_empty(_linear_out_shape(x, N))
+
+
+def _int4_linear_cuda(x, packed_w, scales_and_zeros, group_size, bias=None):
+    N, K = _check_int4_weight(packed_w, scales_and_zeros, group_size)
+    torch._check(x.dtype is torch.bfloat16, lambda: "int4 weight-only linear needs bf16 input")
+    torch._check(x.size(-1) == K, lambda: f"x last dim {x.size(-1)} != K {K}")
+    x2 = x.reshape(-1, K)
+    if not x2.is_contiguous() or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    M = x2.size(0)
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    if bias is not None:
+        bias = bias.to(torch.bfloat16).contiguous()
+    _require_contig(packed_w, "packed_w")
+    _require_contig(scales_and_zeros, "scales_and_zeros")
+    with torch.cuda.device(x.device):
+        _lib.call("tao_int4wo_linear_bf16", _ptr(x2), _ptr(packed_w), _ptr(scales_and_zeros),
+                  _ptr(bias), _ptr(y), M, N, K, group_size, _stream(x))
+    return y.reshape(_linear_out_shape(x, N))
+
+
+# ---------------------------------------------------------------------------------------------
+# int8 weight-only and dynamic activation
+# ---------------------------------------------------------------------------------------------
+def _check_int8_weight(w: Tensor, scale: Tensor):
+    torch._check(w.dim() == 2 and w.dtype is torch.int8, lambda: "w must be a 2D int8 tensor")
+    torch._check(scale.numel() == w.size(0), lambda: "scale must have N elements")
+    return w.shape
+
+
+@torch.library.register_fake("torchao::int8_weight_only_linear")
+def _(x, w_int8, scale, bias=None):
+    N, K = _check_int8_weight(w_int8, scale)
+    torch._check(x.size(-1) == K, lambda: f"x last dim {x.size(-1)} != K {K}")
+    return x.new_empty(_linear_out_shape(x, N))
+
+
+def _int8wo_linear_cuda(x, w_int8, scale, bias=None):
+    N, K = _check_int8_weight(w_int8, scale)
+    torch._check(x.dtype is torch.bfloat16, lambda: "int8 weight-only linear (HIP) needs bf16 x")
+    torch._check(x.size(-1) == K, lambda: f"x last dim {x.size(-1)} != K {K}")
+    x2 = x.reshape(-1, K)
+    if not x2.is_contiguous() or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    M = x2.size(0)
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    w_int8 = w_int8.contiguous()
+    scale = scale.reshape(-1).to(torch.bfloat16).contiguous()
+    if bias is not None:
+        bias = bias.to(torch.bfloat16).contiguous()
+    with torch.cuda.device(x.device):
+        _lib.call("tao_int8wo_linear_bf16", _ptr(x2), _ptr(w_int8), _ptr(scale), _ptr(bias),
+                  _ptr(y), M, N, K, _stream(x))
+    return y.reshape(_linear_out_shape(x, N))
+
+
+@torch.library.register_fake("torchao::int8_quantize_per_token")
+def _(x):
+    return (
+        x.new_empty(x.shape, dtype=torch.int8),
+        x.new_empty((*x.shape[:-1], 1), dtype=torch.bfloat16),
+    )
+
+
+def _int8_quant_cuda(x: Tensor) -> Tuple[Tensor, Tensor]:
+    torch._check(x.dtype is torch.bfloat16, lambda: "int8 per-token quant (HIP) needs bf16 x")
+    K = x.size(-1)
+    x2 = x.reshape(-1, K)
+    if not x2.is_contiguous() or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    M = x2.size(0)
+    q = torch.empty((M, K), dtype=torch.int8, device=x.device)
+    s = torch.empty((M, 1), dtype=torch.bfloat16, device=x.device)
+    with torch.cuda.device(x.device):
+        _lib.call("tao_int8_quant_per_token", _ptr(x2), _ptr(q), _ptr(s), M, K, _stream(x))
+    return q.reshape(x.shape), s.reshape(*x.shape[:-1], 1)
+
+
+@torch.library.register_fake("torchao::int8_scaled_mm")
+def _(x_int8, x_scale, w_int8, w_scale, bias=None):
+    N, K = _check_int8_weight(w_int8, w_scale)
+    return x_int8.new_empty(_linear_out_shape(x_int8, N), dtype=torch.bfloat16)
+
+
+def _int8_scaled_mm_cuda(x_int8, x_scale, w_int8, w_scale, bias=None):
+    N, K = _check_int8_weight(w_int8, w_scale)
+    torch._check(x_int8.dtype is torch.int8, lambda: "x_int8 must be int8")
+    torch._check(x_int8.size(-1) == K, lambda: f"x last dim {x_int8.size(-1)} != K {K}")
+    x2 = x_int8.reshape(-1, K).contiguous()
+    M = x2.size(0)
+    xs = x_scale.reshape(-1).to(torch.bfloat16).contiguous()
+    torch._check(xs.numel() == M, lambda: "x_scale must have one entry per row")
+    ws = w_scale.reshape(-1).to(torch.bfloat16).contiguous()
+    w_int8 = w_int8.contiguous()
+    if bias is not None:
+        bias = bias.to(torch.bfloat16).contiguous()
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=x_int8.device)
+    with torch.cuda.device(x_int8.device):
+        _lib.call("tao_int8_scaled_mm_bf16", _ptr(x2), _ptr(xs), _ptr(w_int8), _ptr(ws),
+                  _ptr(bias), _ptr(y), M, N, K, _stream(x_int8))
+    return y.reshape(_linear_out_shape(x_int8, N))
+
+
+# ---- register device impls ------------------------------------------------------------------
+for _name, _fn in [
+    ("unpack_tensor_core_tiled_layout", _unpack_tile_cuda),
+    ("dequantize_tensor_core_tiled_layout", _dequant_tile_cuda),
+    ("pack_tensor_core_tiled_layout", _pack_tile_cuda),
+    ("int4_pack", _int4_pack_cuda),
+    ("int4_pack_u8", _int4_pack_u8_cuda),
+    ("int4_unpack", _int4_unpack_cuda),
+    ("int4_dequantize", _int4_dequant_cuda),
+    ("int4_weight_only_linear", _int4_linear_cuda),
+    ("int8_weight_only_linear", _int8wo_linear_cuda),
+    ("int8_quantize_per_token", _int8_quant_cuda),
+    ("int8_scaled_mm", _int8_scaled_mm_cuda),
+]:
+    lib.impl(_name, _fn, "CUDA")
+# Host packers (C++ in the same library) so quantize_ works on CPU-resident models.
+lib.impl("int4_pack", _int4_pack_cpu, "CPU")
+lib.impl("int4_unpack", _int4_unpack_cpu, "CPU")
+
+
+# ---- Python-level wrappers with the reference names (ops.py:255-377) ------------------------
+def unpack_tensor_core_tiled_layout(packed_w: Tensor, inner_k_tiles: int) -> Tensor:
+    """Tile-format int4 weight [N/8][K/(ikt*16)][32][ikt/2] -> int32 [N, K]."""
+    return torch.ops.torchao.unpack_tensor_core_tiled_layout.default(packed_w, inner_k_tiles)
+
+
+def dequantize_tensor_core_tiled_layout(
+    packed_w: Tensor, scales_and_zeros: Tensor, group_size: int, inner_k_tiles: int
+) -> Tensor:
+    """Tile-format int4 weight + [K/g, N, 2] scales/zeros -> bf16 [N, K]."""
+    return torch.ops.torchao.dequantize_tensor_core_tiled_layout.default(
+        packed_w, scales_and_zeros, group_size, inner_k_tiles
+    )
+
+
+def pack_tensor_core_tiled_layout(int_data: Tensor, inner_k_tiles: int) -> Tensor:
+    return torch.ops.torchao.pack_tensor_core_tiled_layout.default(int_data, inner_k_tiles)
+
+
+def int4_weight_only_linear(x, packed_w, scales_and_zeros, group_size, bias=None):
+    return torch.ops.torchao.int4_weight_only_linear.default(
+        x, packed_w, scales_and_zeros, group_size, bias
+    )
