@@ -66,6 +66,13 @@ int tao_int4wo_linear_bf16(const uint16_t* x, const uint32_t* packed, const uint
                            const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K,
                            int64_t group_size, void* stream);
 
+/* Tuning hook (benchmarks / autotuning sweeps): override the M == 1 int4 GEMV launch shape,
+ * process-wide. rows_per_wave in {1,2,4,8}; waves_k = waves splitting K inside a workgroup
+ * (1..8); row_groups = row groups per workgroup; waves_k * row_groups <= 8; occupancy in {4,8}
+ * = minimum waves per SIMD the register budget targets (rows_per_wave 4 only).
+ * 0 for any field keeps the built-in choice; all zeros restores the defaults. */
+int tao_tune_int4_gemv(int rows_per_wave, int waves_k, int row_groups, int occupancy);
+
 /* packed[N][K/8] <- q[N][K] (int32 values 0..15).
  * Replaces aten._convert_weight_to_int4pack(u8, inner_k_tiles) at
  * torchao/dtypes/uintx/tensor_core_tiled_layout.py:279 (device kernel). K % 8 == 0. */

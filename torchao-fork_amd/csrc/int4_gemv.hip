@@ -14,21 +14,25 @@
 //     every 32-k chunk lies in exactly one quantisation group because g in {32..256};
 //   * cross-lane: reduce-scatter over the RPW*M partials (V/2 + V/4 + ... shuffles), then a
 //     butterfly over the remaining lanes; cross-wave: LDS, one wave finishes and writes y.
+#include <atomic>
+
 #include "tao_common.h"
 #include "tao_reduce.h"
 
 namespace tao {
 namespace {
 
-template <int MT, int RPW>
-__global__ __launch_bounds__(512) void int4wo_gemv_kernel(
+// WPE: minimum waves per SIMD the register allocation must allow (8 -> <= 64 VGPRs, so four
+// 512-thread workgroups fit on a CU and mid-size grids run in a single resident round).
+template <int MT, int RPW, int WPE>
+__global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     const uint16_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
     const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K, int gshift,
     int Wk, int G, int S) {
   constexpr int V = RPW * MT;
   extern __shared__ float red[];  // [G][Wk][V]
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int wk = wave % Wk;
   const int rg = wave / Wk;
   const int row0 = (blockIdx.x * G + rg) * RPW;
@@ -55,53 +59,45 @@ __global__ __launch_bounds__(512) void int4wo_gemv_kernel(
       wv[r] = ld_nt_u4(wq + (size_t)nn * nchunk + cc);
       szv[r] = ld_nt(sz + (size_t)nn * ngroups + (cc >> gshift));
     }
-    uint4 xv[MT][4];
+    // Lanes past K contribute nothing: zero their (s, z) so the chunk term vanishes.
+    float sc[RPW], zp[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const bool ok = cval && (row0 + r) < N;
+      const uint32_t v = ok ? szv[r] : 0u;
+      sc[r] = bf16lo_to_f32(v);
+      zp[r] = bf16hi_to_f32(v);
+    }
+
+    // x is streamed one row of M at a time: 16 live VGPRs whatever M is.
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const int mm = m < M ? m : M - 1;
       const uint4* xp = reinterpret_cast<const uint4*>(x + (size_t)mm * K + (size_t)cc * 32);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) xv[m][j] = xp[j];
-    }
-    // Lanes past K contribute nothing: zero their (s, z) so the chunk term vanishes.
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-      const bool ok = cval && (row0 + r) < N;
-      szv[r] = ok ? szv[r] : 0u;
-    }
-
-    float sx[MT], sx136[MT];
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      float t = 0.f;
+      uint32_t xd[4][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        t = dot2_bf16(xv[m][j].x, 0x3F803F80u, t);
-        t = dot2_bf16(xv[m][j].y, 0x3F803F80u, t);
-        t = dot2_bf16(xv[m][j].z, 0x3F803F80u, t);
-        t = dot2_bf16(xv[m][j].w, 0x3F803F80u, t);
+        const uint4 t4 = xp[j];
+        xd[j][0] = t4.x;
+        xd[j][1] = t4.y;
+        xd[j][2] = t4.z;
+        xd[j][3] = t4.w;
       }
-      sx[m] = t;
-      sx136[m] = 136.f * t;
-    }
-
+      float sx = 0.f;
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-      const float sc = bf16lo_to_f32(szv[r]);
-      const float zp = bf16hi_to_f32(szv[r]);
-      const uint32_t wd[4] = {wv[r].x, wv[r].y, wv[r].z, wv[r].w};
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const uint32_t xd[4][4] = {{xv[m][0].x, xv[m][0].y, xv[m][0].z, xv[m][0].w},
-                                   {xv[m][1].x, xv[m][1].y, xv[m][1].z, xv[m][1].w},
-                                   {xv[m][2].x, xv[m][2].y, xv[m][2].z, xv[m][2].w},
-                                   {xv[m][3].x, xv[m][3].y, xv[m][3].z, xv[m][3].w}};
+        for (int i = 0; i < 4; ++i) sx = dot2_bf16(xd[j][i], 0x3F803F80u, sx);
+      const float sx136 = 136.f * sx;
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        const uint32_t wd[4] = {wv[r].x, wv[r].y, wv[r].z, wv[r].w};
         float d = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i) d = dot2_bf16(xd[j][i], nib_pair_bf16(wd[j], i), d);
-        acc[r][m] = fmaf(sc, d - sx136[m], fmaf(zp, sx[m], acc[r][m]));
+        acc[r][m] = fmaf(sc[r], d - sx136, fmaf(zp[r], sx, acc[r][m]));
       }
     }
   }
@@ -151,23 +147,37 @@ int gshift_of(int64_t g) {
   }
 }
 
-template <int MT, int RPW>
+// Launch shape: Wk waves split K inside a workgroup (each loops over its slices), G row
+// groups of RPW rows per workgroup; <= 8 waves (512 threads) per workgroup.
+struct GemvShape {
+  int wk, g;
+};
+
+GemvShape default_shape(int S) {
+  const int wk = S < 8 ? S : 8;
+  const int g = (8 / wk) > 0 ? 8 / wk : 1;
+  return {wk, g};
+}
+
+template <int MT, int RPW, int WPE>
 int launch_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
                 const uint16_t* bias, uint16_t* y, int M, int N, int K, int gshift,
-                hipStream_t stream) {
+                GemvShape sh, hipStream_t stream) {
   const int nchunk = K / 32;
   const int S = (nchunk + 63) / 64;
-  const int Wk = S < 8 ? S : 8;
-  const int G = (8 / Wk) > 0 ? 8 / Wk : 1;
-  const int rows_per_wg = G * RPW;
+  const int wk = sh.wk < S ? sh.wk : S;
+  const int rows_per_wg = sh.g * RPW;
   const int grid = (N + rows_per_wg - 1) / rows_per_wg;
-  const int threads = 64 * Wk * G;
-  const size_t lds = (size_t)G * Wk * RPW * MT * sizeof(float);
-  launch((int4wo_gemv_kernel<MT, RPW>), dim3(grid), dim3(threads), lds, stream, x,
-                     reinterpret_cast<const uint4*>(packed),
-                     reinterpret_cast<const uint32_t*>(sz), bias, y, M, N, K, gshift, Wk, G, S);
+  const int threads = 64 * wk * sh.g;
+  const size_t lds = (size_t)sh.g * wk * RPW * MT * sizeof(float);
+  launch((int4wo_gemv_kernel<MT, RPW, WPE>), dim3(grid), dim3(threads), lds, stream, x,
+         reinterpret_cast<const uint4*>(packed), reinterpret_cast<const uint32_t*>(sz), bias, y,
+         M, N, K, gshift, wk, sh.g, S);
   return check_launch("int4wo_gemv_kernel");
 }
+
+// Process-wide override of the M == 1 launch shape (tao_tune_int4_gemv; 0 = heuristic).
+std::atomic<int> g_tune_rpw{0}, g_tune_wk{0}, g_tune_g{0}, g_tune_occ{0};
 
 }  // namespace
 
@@ -176,10 +186,39 @@ int int4wo_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
                 const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K,
                 int64_t group_size, hipStream_t stream) {
   const int gs = gshift_of(group_size);
-  if (M <= 1) return launch_gemv<1, 4>(x, packed, sz, bias, y, (int)M, (int)N, (int)K, gs, stream);
-  if (M <= 2) return launch_gemv<2, 4>(x, packed, sz, bias, y, (int)M, (int)N, (int)K, gs, stream);
-  if (M <= 4) return launch_gemv<4, 4>(x, packed, sz, bias, y, (int)M, (int)N, (int)K, gs, stream);
-  return launch_gemv<8, 2>(x, packed, sz, bias, y, (int)M, (int)N, (int)K, gs, stream);
+  const int S = (int)((K / 32 + 63) / 64);
+  GemvShape sh = default_shape(S);
+  const int iM = (int)M, iN = (int)N, iK = (int)K;
+  if (M <= 1) {
+    // Measured on MI355X (experiments/sweep_gemv.py, profiles/r1_sweep_gemv.jsonl): the best
+    // shapes per (N, K) class, dispatch-event timed over weights rotated past the MALL.
+    int rpw, occ = 8;
+    if (S <= 2) {  // K <= 4096: one wave walks the whole row pair; huge N wants 4-row waves
+      if (N >= 32768) { rpw = 4; sh = {2, 2}; } else { rpw = 2; sh = {1, 4}; }
+    } else if (S <= 4) {  // K <= 8192
+      if (N >= 8192) { rpw = 4; occ = 4; sh = {S, 1}; } else { rpw = 2; sh = {S, 1}; }
+    } else {  // K > 8192: split K across the workgroup unless N alone fills the chip
+      rpw = 4;
+      occ = 4;
+      sh = {(N >= 8192 && S > 8) ? 1 : (S < 8 ? S : 8), 1};
+    }
+    const int trpw = g_tune_rpw.load(std::memory_order_relaxed);
+    const int tocc = g_tune_occ.load(std::memory_order_relaxed);
+    const int twk = g_tune_wk.load(std::memory_order_relaxed);
+    const int tg = g_tune_g.load(std::memory_order_relaxed);
+    if (trpw > 0) rpw = trpw;
+    if (tocc > 0) occ = tocc;
+    if (twk > 0) sh.wk = twk;
+    if (tg > 0) sh.g = tg;
+    if (rpw == 1) return launch_gemv<1, 1, 8>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
+    if (rpw == 2) return launch_gemv<1, 2, 8>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
+    if (rpw == 8) return launch_gemv<1, 8, 4>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
+    if (occ == 4) return launch_gemv<1, 4, 4>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
+    return launch_gemv<1, 4, 8>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
+  }
+  if (M <= 2) return launch_gemv<2, 4, 1>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
+  if (M <= 4) return launch_gemv<4, 4, 1>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
+  return launch_gemv<8, 1, 1>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
 }
 
 int int4_check_linear_args(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
@@ -203,3 +242,17 @@ int int4_check_linear_args(const uint16_t* x, const uint32_t* packed, const uint
 }
 
 }  // namespace tao
+
+extern "C" int tao_tune_int4_gemv(int rows_per_wave, int waves_k, int row_groups, int occupancy) {
+  TAO_CHECK_ARG(rows_per_wave == 0 || rows_per_wave == 1 || rows_per_wave == 2 ||
+                    rows_per_wave == 4 || rows_per_wave == 8,
+                "tune: rows_per_wave must be 0 (auto), 1, 2, 4 or 8");
+  TAO_CHECK_ARG(waves_k >= 0 && row_groups >= 0 && waves_k * (row_groups ? row_groups : 1) <= 8,
+                "tune: waves_k * row_groups must be <= 8");
+  TAO_CHECK_ARG(occupancy == 0 || occupancy == 4 || occupancy == 8, "tune: occupancy 0, 4 or 8");
+  tao::g_tune_rpw.store(rows_per_wave);
+  tao::g_tune_wk.store(waves_k);
+  tao::g_tune_g.store(row_groups);
+  tao::g_tune_occ.store(occupancy);
+  return TAO_OK;
+}

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void int8_scaled_mm_kernel(
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int n_blk = blockIdx.x * kBN;
   const int m_blk = blockIdx.y * BM;
   const int nvec = K >> 4;  // 16-B vectors per row

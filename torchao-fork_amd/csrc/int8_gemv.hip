@@ -21,7 +21,7 @@ __global__ __launch_bounds__(512) void int8wo_gemv_kernel(
   constexpr int V = RPW * MT;
   extern __shared__ float red[];  // [G][Wk][V]
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int wk = wave % Wk;
   const int rg = wave / Wk;
   const int row0 = (blockIdx.x * G + rg) * RPW;
@@ -45,40 +45,36 @@ __global__ __launch_bounds__(512) void int8wo_gemv_kernel(
       const int nn = n < N ? n : N - 1;
       wv[r] = ld_nt_u4(w + (size_t)nn * nchunk + cc);
     }
-    float xf[MT][16];
-    float sx128[MT];
+    // x is streamed one row of M at a time: 16 live f32 values whatever M is.
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const int mm = m < M ? m : M - 1;
       const uint4* xp = reinterpret_cast<const uint4*>(x + (size_t)mm * K + (size_t)cc * 16);
       const uint4 a = xp[0], b = xp[1];
-      const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      const uint32_t d8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      float xf[16];
       float t = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const uint32_t di = cval ? d[i] : 0u;
-        xf[m][2 * i] = bf16lo_to_f32(di);
-        xf[m][2 * i + 1] = bf16hi_to_f32(di);
+        const uint32_t di = cval ? d8[i] : 0u;
+        xf[2 * i] = bf16lo_to_f32(di);
+        xf[2 * i + 1] = bf16hi_to_f32(di);
         t = dot2_bf16(di, 0x3F803F80u, t);
       }
-      sx128[m] = 128.f * t;
-    }
-
+      const float sx128 = 128.f * t;
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-      const uint32_t wd[4] = {wv[r].x ^ 0x80808080u, wv[r].y ^ 0x80808080u,
-                              wv[r].z ^ 0x80808080u, wv[r].w ^ 0x80808080u};
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
+      for (int r = 0; r < RPW; ++r) {
+        const uint32_t wd[4] = {wv[r].x ^ 0x80808080u, wv[r].y ^ 0x80808080u,
+                                wv[r].z ^ 0x80808080u, wv[r].w ^ 0x80808080u};
         float d = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          d = fmaf(xf[m][4 * j + 0], (float)(wd[j] & 0xFF), d);
-          d = fmaf(xf[m][4 * j + 1], (float)((wd[j] >> 8) & 0xFF), d);
-          d = fmaf(xf[m][4 * j + 2], (float)((wd[j] >> 16) & 0xFF), d);
-          d = fmaf(xf[m][4 * j + 3], (float)(wd[j] >> 24), d);
+          d = fmaf(xf[4 * j + 0], (float)(wd[j] & 0xFF), d);
+          d = fmaf(xf[4 * j + 1], (float)((wd[j] >> 8) & 0xFF), d);
+          d = fmaf(xf[4 * j + 2], (float)((wd[j] >> 16) & 0xFF), d);
+          d = fmaf(xf[4 * j + 3], (float)(wd[j] >> 24), d);
         }
-        acc[r][m] += d - sx128[m];
+        acc[r][m] += d - sx128;
       }
     }
   }
@@ -140,7 +136,7 @@ int int8wo_gemv(const uint16_t* x, const int8_t* w, const uint16_t* scale, const
   if (M <= 1) return launch_gemv<1, 4>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream);
   if (M <= 2) return launch_gemv<2, 4>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream);
   if (M <= 4) return launch_gemv<4, 2>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream);
-  return launch_gemv<8, 2>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream);
+  return launch_gemv<8, 1>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream);
 }
 
 }  // namespace tao
