@@ -173,8 +173,8 @@ def main():
         assert N % P == 0, (name, N, P)
         n_loc = N // P
         packed, sz = make_int4_weight(n_loc, K, g, seed=1000 * i + rank, device=device)
-        y_loc = torch.empty(1, n_loc, device=device, dtype=torch.bfloat16)
-        y_full = torch.empty(1, N, device=device, dtype=torch.bfloat16) if P > 1 else y_loc
+        y_loc = torch.empty(n_loc, device=device, dtype=torch.bfloat16)  # M = 1 row
+        y_full = torch.empty(N, device=device, dtype=torch.bfloat16) if P > 1 else y_loc
         plan.append((name, n_loc, K, packed, sz, y_loc, y_full))
         bytes_per_step += int4_alg_bytes(N, K, g)
     torch.cuda.synchronize()
