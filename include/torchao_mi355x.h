@@ -73,6 +73,15 @@ int tao_int4wo_linear_bf16(const uint16_t* x, const uint32_t* packed, const uint
  * 0 for any field keeps the built-in choice; all zeros restores the defaults. */
 int tao_tune_int4_gemv(int rows_per_wave, int waves_k, int row_groups, int occupancy);
 
+/* Tuning hook: the weight-only linears (int4 and int8) use the GEMV kernels for M <= max_gemv_m
+ * and the MFMA skinny GEMM above it. 0 restores the built-in crossover (4). Process-wide. */
+int tao_tune_linear_crossover(int max_gemv_m);
+
+/* Tuning hook: force the MFMA skinny GEMM's M tile (16/32/64/128), k-groups per workgroup
+ * (1/2/4; 4 waves each) and K slices across workgroups (1..64); 0 = the built-in choice for
+ * each. Process-wide. */
+int tao_tune_gemm(int m_tile, int k_groups, int splits);
+
 /* packed[N][K/8] <- q[N][K] (int32 values 0..15).
  * Replaces aten._convert_weight_to_int4pack(u8, inner_k_tiles) at
  * torchao/dtypes/uintx/tensor_core_tiled_layout.py:279 (device kernel). K % 8 == 0. */

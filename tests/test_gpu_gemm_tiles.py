@@ -1,0 +1,176 @@
+"""GPU parity of the MFMA skinny GEMM (gemm_mfma.hip) across its M tiles and edge shapes.
+
+The kernel picks BM in {16, 32, 64, 128} from (M, N) so the grid covers the chip; the shapes
+below force each tile, partial last M tiles, N not a multiple of the 64-column block, and K
+that is not a multiple of the macro-step (128 bf16 k / 256 int8 k) or shorter than the
+prefetch depth. The GEMV <-> MFMA crossover is moved with tao_tune_linear_crossover so M 5..8
+is checked on both kernels.
+"""
+
+import pytest
+import torch
+
+from oracle import oracle
+
+from torchao import _lib
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL_REF = 1e-2
+TOL_FP32 = 4e-3
+
+# (M, N, K): tile chosen by choose_bm in brackets
+SHAPES = [
+    (5, 4096, 1024),    # [16] smallest MFMA M
+    (48, 4096, 1024),   # [16] 3 M tiles
+    (129, 4096, 1024),  # [32] partial last tile
+    (300, 4096, 1024),  # [64] partial last tile
+    (600, 4096, 1024),  # [128] partial last tile
+    (128, 200, 352),    # [16] ragged N, K not a multiple of the step
+    (40, 72, 32),       # [16] single partial step, N tail of 8
+]
+
+
+@pytest.fixture
+def crossover():
+    yield lambda m: _lib.call("tao_tune_linear_crossover", m)
+    _lib.call("tao_tune_linear_crossover", 0)
+
+
+@pytest.fixture
+def gemm_shape():
+    yield lambda bm, kg, splits: _lib.call("tao_tune_gemm", bm, kg, splits)
+    _lib.call("tao_tune_gemm", 0, 0, 0)
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_int4_mfma_tiles(M, N, K):
+    g = 32
+    w = oracle.make_linear_weight(N, K, seed=M + N)
+    s, z = oracle.int4_qparams(w, g)
+    q = oracle.int4_quantize(w, s, z, g)
+    x = oracle.make_activation(M, K, seed=M)
+    bias = oracle.make_activation(1, N, seed=7).reshape(N)
+    packed = torch.ops.torchao.int4_pack(q.to(DEV))
+    sz = torch.stack([s, z], dim=-1).contiguous().to(DEV)
+    y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, bias.to(DEV)).cpu()
+    assert oracle.rel_l2(y, oracle.int4_linear(x, q, s, z, g, bias)) < TOL_REF
+    assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, g, bias)) < TOL_FP32
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_int8wo_mfma_tiles(M, N, K):
+    w = oracle.make_linear_weight(N, K, seed=M + N)
+    s = oracle.int8_weight_qparams(w)
+    q = oracle.int8_weight_quantize(w, s)
+    x = oracle.make_activation(M, K, seed=M)
+    y = torch.ops.torchao.int8_weight_only_linear(x.to(DEV), q.to(DEV), s.to(DEV), None).cpu()
+    assert oracle.rel_l2(y, oracle.int8wo_linear(x, q, s)) < TOL_REF
+    exact = (x.double() @ q.double().t()) * s.double()
+    assert oracle.rel_l2(y, exact) < TOL_FP32
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES + [(512, 4096, 4096), (7, 64, 16)])
+def test_int8dyn_mfma_tiles_bit_exact(M, N, K):
+    w = oracle.make_linear_weight(N, K, seed=M + N)
+    wq, ws = oracle.int8_dyn_weight(w)
+    x = oracle.make_activation(M, K, seed=M)
+    xq, xs = oracle.int8_act_quant(x)
+    bias = oracle.make_activation(1, N, seed=3).reshape(N)
+    y = torch.ops.torchao.int8_scaled_mm(
+        xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), bias.to(DEV)
+    ).cpu()
+    # integer accumulation is exact, the epilogue follows the reference's rounding order
+    assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, bias, epilogue="cpu"))
+
+
+@pytest.mark.parametrize("M", [5, 6, 7, 8])
+@pytest.mark.parametrize("max_gemv_m", [4, 8])
+def test_crossover_both_kernels(crossover, M, max_gemv_m):
+    crossover(max_gemv_m)
+    N, K, g = 1024, 2048, 64
+    w = oracle.make_linear_weight(N, K, seed=M)
+    s, z = oracle.int4_qparams(w, g)
+    q = oracle.int4_quantize(w, s, z, g)
+    x = oracle.make_activation(M, K, seed=M + 9)
+    packed = torch.ops.torchao.int4_pack(q.to(DEV))
+    sz = torch.stack([s, z], dim=-1).contiguous().to(DEV)
+    y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, None).cpu()
+    assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, g)) < TOL_FP32
+    s8 = oracle.int8_weight_qparams(w)
+    q8 = oracle.int8_weight_quantize(w, s8)
+    y8 = torch.ops.torchao.int8_weight_only_linear(x.to(DEV), q8.to(DEV), s8.to(DEV), None).cpu()
+    assert oracle.rel_l2(y8, oracle.int8wo_linear(x, q8, s8)) < TOL_REF
+
+
+def test_crossover_rejects_out_of_range():
+    with pytest.raises(RuntimeError, match="max_gemv_m"):
+        _lib.call("tao_tune_linear_crossover", 9)
+
+
+# forced (M tile, k-groups, K slices): every tile with and without both K splits, uneven
+# slices and k-groups with idle steps (K=1056 has 9 int4 steps / 5 int8 steps), more slices
+# than steps (clamped), the partial-sum protocol reused back to back (counters reset by the
+# last arriver)
+FORCED = [(16, 1, 1), (16, 4, 1), (16, 2, 3), (32, 4, 4), (32, 1, 2), (64, 2, 2), (64, 1, 1),
+          (128, 1, 5), (16, 4, 64), (32, 2, 16)]
+
+
+@pytest.mark.parametrize("bm,kg,splits", FORCED)
+def test_forced_tiles_and_split_k(gemm_shape, bm, kg, splits):
+    gemm_shape(bm, kg, splits)
+    M, N, K, g = 70, 320, 1056, 32
+    w = oracle.make_linear_weight(N, K, seed=bm + kg + splits)
+    s, z = oracle.int4_qparams(w, g)
+    q = oracle.int4_quantize(w, s, z, g)
+    x = oracle.make_activation(M, K, seed=splits)
+    bias = oracle.make_activation(1, N, seed=5).reshape(N)
+    packed = torch.ops.torchao.int4_pack(q.to(DEV))
+    sz = torch.stack([s, z], dim=-1).contiguous().to(DEV)
+    xd, bd = x.to(DEV), bias.to(DEV)
+    y = torch.ops.torchao.int4_weight_only_linear(xd, packed, sz, g, bd)
+    y2 = torch.ops.torchao.int4_weight_only_linear(xd, packed, sz, g, bd)
+    assert torch.equal(y, y2)  # slices are summed in a fixed order
+    assert oracle.rel_l2(y.cpu(), oracle.int4_linear_fp32(x, q, s, z, g, bias)) < TOL_FP32
+
+    s8 = oracle.int8_weight_qparams(w)
+    q8 = oracle.int8_weight_quantize(w, s8)
+    y8 = torch.ops.torchao.int8_weight_only_linear(xd, q8.to(DEV), s8.to(DEV), bd).cpu()
+    assert oracle.rel_l2(y8, oracle.int8wo_linear(x, q8, s8, bias)) < TOL_REF
+
+    wq, ws = oracle.int8_dyn_weight(w)
+    xq, xs = oracle.int8_act_quant(x)
+    yd = torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), bd)
+    assert torch.equal(yd.cpu(), oracle.int8_scaled_mm(xq, xs, wq, ws, bias, epilogue="cpu"))
+
+
+def test_split_k_under_graph_capture(gemm_shape):
+    """The workspace is reserved by the eager call; the captured launch reuses it."""
+    gemm_shape(16, 4, 8)
+    M, N, K, g = 16, 512, 2048, 32
+    w = oracle.make_linear_weight(N, K, seed=3)
+    s, z = oracle.int4_qparams(w, g)
+    q = oracle.int4_quantize(w, s, z, g)
+    x = oracle.make_activation(M, K, seed=4).to(DEV)
+    packed = torch.ops.torchao.int4_pack(q.to(DEV))
+    sz = torch.stack([s, z], dim=-1).contiguous().to(DEV)
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        ref = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)
+        stream.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            out = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+
+
+def test_tune_gemm_rejects_bad_values():
+    with pytest.raises(RuntimeError, match="m_tile"):
+        _lib.call("tao_tune_gemm", 48, 0, 0)
+    with pytest.raises(RuntimeError, match="k_groups"):
+        _lib.call("tao_tune_gemm", 0, 3, 0)
+    with pytest.raises(RuntimeError, match="splits"):
+        _lib.call("tao_tune_gemm", 0, 0, 65)

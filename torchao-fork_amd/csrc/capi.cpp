@@ -4,6 +4,10 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "tao_common.h"
@@ -51,6 +55,68 @@ static void profile_release() {
   g_prof.stop.clear();
   g_prof.used = 0;
   g_prof.active = false;
+}
+
+// ---- split-K workspace --------------------------------------------------------------------------
+struct Workspace {
+  void* slab = nullptr;
+  size_t slab_cap = 0;
+  unsigned* cnt = nullptr;
+  size_t cnt_cap = 0;
+};
+static std::mutex g_ws_mu;
+static std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
+
+int split_workspace(hipStream_t stream, size_t slab_bytes, size_t counters, void** slab,
+                    unsigned** cnt) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return set_error(TAO_ERR_HIP, "hipGetDevice failed");
+  std::lock_guard<std::mutex> lock(g_ws_mu);
+  Workspace& w = g_ws[{dev, stream}];
+  if (w.slab_cap < slab_bytes || w.cnt_cap < counters) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+      // No allocation inside a capture. A warm-up on another stream of this device (the usual
+      // torch.cuda.graph pattern) reserved one: the graph borrows it.
+      for (auto& kv : g_ws) {
+        const Workspace& o = kv.second;
+        if (kv.first.first == dev && o.slab_cap >= slab_bytes && o.cnt_cap >= counters) {
+          *slab = o.slab;
+          *cnt = o.cnt;
+          return TAO_OK;
+        }
+      }
+      return set_error(TAO_ERR_UNSUPPORTED,
+                       "split-K workspace of %zu B not reserved on this device: run the op once "
+                       "at this shape before graph capture",
+                       slab_bytes);
+    }
+    // the old buffers may still be read by work queued on this stream
+    if (hipStreamSynchronize(stream) != hipSuccess)
+      return set_error(TAO_ERR_HIP, "hipStreamSynchronize failed");
+    const size_t sb = std::max(slab_bytes, w.slab_cap);
+    const size_t nc = std::max(counters, w.cnt_cap);
+    if (w.slab_cap < sb) {
+      (void)hipFree(w.slab);
+      w.slab = nullptr;
+      w.slab_cap = 0;
+      if (hipMalloc(&w.slab, sb) != hipSuccess)
+        return set_error(TAO_ERR_HIP, "hipMalloc of %zu B split-K slabs failed", sb);
+      w.slab_cap = sb;
+    }
+    if (w.cnt_cap < nc) {
+      (void)hipFree(w.cnt);
+      w.cnt = nullptr;
+      w.cnt_cap = 0;
+      if (hipMalloc(reinterpret_cast<void**>(&w.cnt), nc * sizeof(unsigned)) != hipSuccess ||
+          hipMemset(w.cnt, 0, nc * sizeof(unsigned)) != hipSuccess)
+        return set_error(TAO_ERR_HIP, "split-K counter allocation failed");
+      w.cnt_cap = nc;
+    }
+  }
+  *slab = w.slab;
+  *cnt = w.cnt;
+  return TAO_OK;
 }
 
 }  // namespace tao

@@ -1,0 +1,666 @@
+// Skinny GEMM on MFMA for the quantized linears at M > 4 (prefill / batched decode):
+//   y[M][N] = epilogue( x[M][K] . W[N][K]^T )
+// three weight/activation formats share one kernel template:
+//   Int4WO  : bf16 x, int4 group-quant W (gfx950 row-stream layout), v_mfma_f32_16x16x32_bf16
+//   Int8WO  : bf16 x, int8 per-channel W,                            v_mfma_f32_16x16x32_bf16
+//   Int8Dyn : int8 x (per-token scale), int8 W (per-channel scale),   v_mfma_i32_16x16x64_i8
+// Replaces aten._weight_int4pack_mm (tensor_core_tiled_layout.py:104), mm(x, w.to(bf16)) * s
+// (plain_layout.py:256-266) and int_scaled_matmul + scales (plain_layout.py:294-315,
+// kernel/intmm.py:108-143).
+//
+// Tile: 4 waves x 16 output columns (BN = 64) x BM rows per k-group; each wave owns 16 columns
+// and all BM rows. K advances in macro-steps of 256 B of x per row (128 bf16 k or 256 int8 k).
+// k order inside a macro-step is permuted identically for A and B: MFMA s (0..3) of lane l
+// (n = l & 15, kq = l >> 4) covers the kq-th quarter of the step, sub-block s. So a lane's
+// weight load for a step is one contiguous piece of its row (16 B int4, 32 B int8-WO,
+// 64 B int8-dyn) feeding all four MFMAs, and an int4 lane needs one (scale, zero) dword.
+// x goes global -> registers (D-deep prefetch ring, T14) -> double-buffered, XOR-swizzled LDS
+// image -> A fragments; one barrier per step. W goes straight to registers (read once per
+// tile, dequantised in registers, reused for BM/16 MFMAs). K is split across k-groups inside
+// the workgroup and across workgroups (split-K) so every SIMD holds several waves; the launch
+// shape (BM, k-groups, slices) comes from measured sweeps (experiments/sweep_gemm.py).
+#include <atomic>
+#include <tuple>
+#include <type_traits>
+
+#include "tao_common.h"
+
+// Experiment switch (experiments/gemm_debug.sh builds variants; 0 in the product):
+// 1 = no x global loads, 2 = no weight global loads, 3 = no x LDS traffic, 4 = no step barrier,
+// 5 = weights read as contiguous 1-KiB blocks per wave-instruction (wrong values, same bytes).
+#ifndef TAO_GEMM_DEBUG
+#define TAO_GEMM_DEBUG 0
+#endif
+
+namespace tao {
+
+int int4wo_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
+                const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K,
+                int64_t group_size, hipStream_t stream);
+int int4_check_linear_args(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
+                           uint16_t* y, int64_t M, int64_t N, int64_t K, int64_t group_size);
+int int8wo_gemv(const uint16_t* x, const int8_t* w, const uint16_t* scale, const uint16_t* bias,
+                uint16_t* y, int64_t M, int64_t N, int64_t K, hipStream_t stream);
+
+namespace {
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kBN = 64;
+
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+// one v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  const f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+
+__device__ __forceinline__ bf16x8_t as_bf16x8(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  u32x4_t v = {a, b, c, d};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// ---- buffer resources --------------------------------------------------------------------------
+// All operand loads are raw buffer loads: a wave-uniform 128-bit descriptor, a per-lane 32-bit
+// voffset fixed for the whole launch and a per-step wave-uniform soffset, so the k loop spends
+// no VALU on 64-bit address arithmetic (cdna guide T8/T20). Loads past the descriptor's byte
+// count return 0; callers keep every operand below 4 GiB.
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+constexpr int kNT = 2;  // aux: non-temporal (streamed-once weights)
+
+__device__ __forceinline__ Rsrc make_rsrc(const void* base, uint32_t bytes) {
+  // readfirstlane on the inputs makes the descriptor provably uniform (no waterfall loops)
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)__builtin_amdgcn_readfirstlane(bytes),
+                                           0x00020000);
+}
+template <int AUX = 0>
+__device__ __forceinline__ uint4 bload16(Rsrc r, uint32_t voff, uint32_t soff) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v =
+      __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX));
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+template <int AUX = 0>
+__device__ __forceinline__ uint32_t bload4(Rsrc r, uint32_t voff, uint32_t soff) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, AUX);
+}
+
+// ---- policies -------------------------------------------------------------------------------
+// setup(): per-lane state for lane (n, kq) — descriptors and voffsets (once per launch).
+// load(): the raw bytes of the lane's weight piece for step `st` (wave-uniform, clamped to the
+// slice), never predicated: a select on a freshly loaded value makes hipcc wait for the load on
+// the spot, or branch around it, which collapses the prefetch pipeline. No weight is masked:
+// columns past N (clamped to row N - 1) are computed and dropped, and a K tail reads the next
+// row's finite weights against x that the LDS store zeroes. prep()/frag(): B fragments.
+struct Int4WO {
+  static constexpr int kABytes = 2;  // bf16 x
+  static constexpr int kKStep = 128;
+  typedef f32x4_t Acc;
+  const uint4* wq;     // [N][K/32] 16-B chunks
+  const uint32_t* sz;  // [N][K/g] (scale, zero)
+  int gshift;          // log2(g / 32)
+  struct Lane {
+    Rsrc w, z;
+    uint32_t wv, zv;
+  };
+  struct Chunk {
+    uint4 w;
+    uint32_t szw;
+  };
+  struct Prep {
+    uint32_t w[4];
+    float s, zc;
+  };
+  __device__ __forceinline__ Lane setup(int n, int kq, int N, int K) const {
+    Lane L;
+    const uint32_t zrow = (uint32_t)(K >> 5 >> gshift);  // (scale, zero) dwords per row
+    L.w = make_rsrc(wq, (uint32_t)N * (uint32_t)(K >> 1));
+    L.z = make_rsrc(sz, (uint32_t)N * zrow * 4u);
+    L.wv = (uint32_t)n * (uint32_t)(K >> 1) + kq * 16;
+    if (TAO_GEMM_DEBUG == 5) L.wv = (uint32_t)(n >> 4) * (uint32_t)(K >> 1) * 16 + ((n & 15) * 4 + kq) * 16;
+    // chunk 4 st + kq -> group (4 st + kq) >> gshift == ((4 st) >> gshift) + (kq >> gshift)
+    L.zv = ((uint32_t)n * zrow + (kq >> gshift)) * 4;
+    return L;
+  }
+  __device__ __forceinline__ Chunk load(const Lane& L, int st) const {
+    Chunk ch;
+    ch.w = bload16<kNT>(L.w, L.wv, st * (TAO_GEMM_DEBUG == 5 ? 1024 : 64));
+    ch.szw = bload4<kNT>(L.z, L.zv, ((4 * st) >> gshift) * 4);
+    return ch;
+  }
+  __device__ __forceinline__ Prep prep(const Chunk& ch) const {
+    Prep p;
+    p.w[0] = ch.w.x;
+    p.w[1] = ch.w.y;
+    p.w[2] = ch.w.z;
+    p.w[3] = ch.w.w;
+    p.s = bf16lo_to_f32(ch.szw);
+    p.zc = bf16hi_to_f32(ch.szw) - 8.f * p.s;  // q*s + zc == (q-8)*s + z
+    return p;
+  }
+  // B fragment of MFMA s: bf16(fma(q, s, z - 8 s)) for the 8 nibbles of dword s. Row-stream
+  // nibble order (bits 4i: q[2i], bits 16+4i: q[2i+1]) puts q0,q4,q1,q5 in the bytes of
+  // w & 0x0F0F0F0F and q2,q6,q3,q7 in those of (w >> 4) & 0x0F0F0F0F. A byte b < 16 read as
+  // OCP e4m3 is exactly b / 512 (subnormals for b < 8, exponent 1 above), so one
+  // v_cvt_scalef32_pk_f32_fp8 with scale 512 turns two of them into exact fp32 integers; then
+  // one v_pk_fma_f32 and one v_cvt_pk_bf16_f32 per pair: ~1.9 VALU per weight.
+  __device__ __forceinline__ bf16x8_t frag(const Prep& p, int s) const {
+    const uint32_t lo = p.w[s] & 0x0F0F0F0Fu, hi = (p.w[s] >> 4) & 0x0F0F0F0Fu;
+    const f32x2_t q04 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(lo, 512.f, false);
+    const f32x2_t q15 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(lo, 512.f, true);
+    const f32x2_t q26 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, false);
+    const f32x2_t q37 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, true);
+    const f32x2_t sv = {p.s, p.s}, zv = {p.zc, p.zc};
+    const f32x2_t w04 = q04 * sv + zv, w15 = q15 * sv + zv;  // v_pk_fma_f32 (contracted)
+    const f32x2_t w26 = q26 * sv + zv, w37 = q37 * sv + zv;
+    return as_bf16x8(pack_bf16x2(w04[0], w15[0]), pack_bf16x2(w26[0], w37[0]),
+                     pack_bf16x2(w04[1], w15[1]), pack_bf16x2(w26[1], w37[1]));
+  }
+  static __device__ __forceinline__ Acc mfma(const uint4& a, const bf16x8_t& b, Acc c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), b, c, 0, 0, 0);
+  }
+  // int4 output: bf16(acc) (+ bias added by the caller, tensor_core_tiled_layout.py:104-114)
+  __device__ __forceinline__ float epilogue(float acc, int, int) const { return round_bf16(acc); }
+};
+
+struct Int8WO {
+  static constexpr int kABytes = 2;
+  static constexpr int kKStep = 128;
+  typedef f32x4_t Acc;
+  const uint4* w;         // [N][K/16]
+  const uint16_t* scale;  // [N]
+  struct Lane {
+    Rsrc w;
+    uint32_t wv;
+  };
+  struct Chunk {
+    uint4 a, b;
+  };
+  typedef Chunk Prep;
+  __device__ __forceinline__ Lane setup(int n, int kq, int N, int K) const {
+    Lane L;
+    L.w = make_rsrc(w, (uint32_t)N * (uint32_t)K);
+    L.wv = (uint32_t)n * (uint32_t)K + kq * 32;
+    return L;
+  }
+  __device__ __forceinline__ Chunk load(const Lane& L, int st) const {
+    Chunk ch;
+    ch.a = bload16<kNT>(L.w, L.wv, st * 128);
+    ch.b = bload16<kNT>(L.w, L.wv + 16, st * 128);
+    return ch;
+  }
+  __device__ __forceinline__ Prep prep(const Chunk& ch) const { return ch; }
+  // int8 -> bf16 is exact: (q ^ 0x80) is q + 128 as an unsigned byte (one v_cvt_f32_ubyteN),
+  // minus 128 in fp32 (exact), packed.
+  __device__ __forceinline__ bf16x8_t frag(const Prep& p, int s) const {
+    const uint32_t d0 = ((s == 0) ? p.a.x : (s == 1) ? p.a.z : (s == 2) ? p.b.x : p.b.z) ^ 0x80808080u;
+    const uint32_t d1 = ((s == 0) ? p.a.y : (s == 1) ? p.a.w : (s == 2) ? p.b.y : p.b.w) ^ 0x80808080u;
+    auto cv = [](uint32_t d, int b) { return (float)((d >> (8 * b)) & 0xFF) - 128.f; };
+    return as_bf16x8(pack_bf16x2(cv(d0, 0), cv(d0, 1)), pack_bf16x2(cv(d0, 2), cv(d0, 3)),
+                     pack_bf16x2(cv(d1, 0), cv(d1, 1)), pack_bf16x2(cv(d1, 2), cv(d1, 3)));
+  }
+  static __device__ __forceinline__ Acc mfma(const uint4& a, const bf16x8_t& b, Acc c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), b, c, 0, 0, 0);
+  }
+  // bf16 mm output, then * scale (plain_layout.py:258-262)
+  __device__ __forceinline__ float epilogue(float acc, int, int n) const {
+    return round_bf16(round_bf16(acc) * bf16_to_f32(scale[n]));
+  }
+};
+
+struct Int8Dyn {
+  static constexpr int kABytes = 1;  // int8 x
+  static constexpr int kKStep = 256;
+  typedef i32x4_t Acc;
+  const uint4* w;           // [N][K/16]
+  const uint16_t* wscale;   // [N]
+  const uint16_t* xscale;   // [M]
+  struct Lane {
+    Rsrc w;
+    uint32_t wv;
+  };
+  struct Chunk {
+    uint4 v[4];
+  };
+  typedef Chunk Prep;
+  __device__ __forceinline__ Lane setup(int n, int kq, int N, int K) const {
+    Lane L;
+    L.w = make_rsrc(w, (uint32_t)N * (uint32_t)K);
+    L.wv = (uint32_t)n * (uint32_t)K + kq * 64;
+    if (TAO_GEMM_DEBUG == 5) L.wv = (uint32_t)(n >> 4) * (uint32_t)K * 16 + ((n & 15) * 4 + kq) * 16;
+    return L;
+  }
+  __device__ __forceinline__ Chunk load(const Lane& L, int st) const {
+    Chunk ch;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      ch.v[s] = TAO_GEMM_DEBUG == 5 ? bload16<kNT>(L.w, L.wv + 1024 * s, st * 4096)
+                                    : bload16<kNT>(L.w, L.wv + 16 * s, st * 256);
+    return ch;
+  }
+  __device__ __forceinline__ Prep prep(const Chunk& ch) const { return ch; }
+  __device__ __forceinline__ i32x4_t frag(const Prep& p, int s) const {
+    return __builtin_bit_cast(i32x4_t, p.v[s]);
+  }
+  static __device__ __forceinline__ Acc mfma(const uint4& a, const i32x4_t& b, Acc c) {
+    return __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4_t, a), b, c, 0, 0, 0);
+  }
+  // bf16(c) * x_scale, * w_scale, each rounded (intmm.py:133-137, plain_layout.py:301-315)
+  __device__ __forceinline__ float epilogue(int acc, int m, int n) const {
+    const float v = round_bf16(round_bf16((float)acc) * bf16_to_f32(xscale[m]));
+    return round_bf16(v * bf16_to_f32(wscale[n]));
+  }
+};
+
+// LDS image of one x tile: [BM rows][16 slots of 16 B], slot XOR-swizzled with row & 15 so the
+// 16 rows of an A fragment read spread over all banks (cdna guide §5.5 T2).
+__device__ __forceinline__ int lds_slot(int row, int slot) { return row * 16 + (slot ^ (row & 15)); }
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// One k-step ring of depth D holds both operands' loads: vector-memory loads retire in issue
+// order (one vmcnt), so an x ring shallower than the weight ring would drain the weight loads
+// issued before each x load anyway. The k loop is unrolled by D so every ring index is a
+// compile-time constant (no scratch), and the steady-state body is straight-line code: loads
+// past the last step re-read it (clamped), so hipcc counts outstanding loads (vmcnt(N))
+// instead of draining them every step.
+//
+// Latency hiding comes from waves per SIMD, so K is split twice:
+//  * inside the workgroup: KG k-groups of 4 waves (256 x KG threads) take interleaved steps
+//    (k-group g: steps s0 + g, s0 + g + KG, ...), each with its own double-buffered x tile;
+//    their accumulators are summed through LDS in k-group order at the end;
+//  * across workgroups (gridDim.z = S slices of `sps` steps): each slice stores its raw
+//    accumulator tile to a slab, and the tile's last arriver (agent-scope counter) sums the S
+//    slabs in slice order and runs the epilogue. Both sums have a fixed order, so results do
+//    not depend on arrival order. Protocol: cdna guide §5 "Projection GEMM at M = 256" item 2
+//    (release fence before the ticket, acquire after it, flag through the one LDS array).
+template <int BM, int D, int KG, class P>
+__global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
+    const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
+    uint16_t* __restrict__ y, int M, int N, int K, int sps, typename P::Acc* __restrict__ slab,
+    unsigned* __restrict__ cnt) {
+  typedef typename P::Acc Acc;
+  constexpr int MT = BM / 16;
+  constexpr int XLOADS = BM * 16 / 256;  // 16-B x pieces per thread per step
+  constexpr int TILE = BM * 16;          // uint4 per x tile
+  static_assert((KG - 1) * 4 * MT * 64 <= KG * 2 * TILE, "k-group reduction must fit in LDS");
+  __shared__ uint4 lds[KG * 2 * TILE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int kg = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int wave = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+  const int ktid = tid & 255;
+  const int n_blk = blockIdx.x * kBN;
+  const int m_blk = blockIdx.y * BM;
+  const int nsteps = (K + P::kKStep - 1) / P::kKStep;
+  const int s0 = blockIdx.z * sps;
+  const int s1 = s0 + sps < nsteps ? s0 + sps : nsteps;  // launcher: no empty slice
+  const int J = (s1 - s0 + KG - 1) / KG;                 // steps per k-group (all k-groups)
+  const int row_bytes = K * P::kABytes;
+  uint4* xs = lds + kg * 2 * TILE;
+
+  const int bn = n_blk + wave * 16 + (lane & 15);
+  const bool nok = bn < N;
+  const int bnc = nok ? bn : N - 1;
+  const int kq = lane >> 4;
+  const typename P::Lane wl = pol.setup(bnc, kq, N, K);
+
+  // this thread's x pieces: rows row0 + 16 i (i < XLOADS), 16-B slot xslot of each; rows past
+  // M are clamped to M - 1 (computed and dropped). A k tail past the row end reads the next
+  // row (or 0 past the buffer) and is masked at the LDS store.
+  const int row0 = ktid >> 4, xslot = ktid & 15;
+  const int xslot_b = xslot * 16;
+  const int xlds0 = lds_slot(row0, xslot);  // + 256 i: (row0 + 16 i) & 15 == row0 & 15
+  const Rsrc xrs = make_rsrc(x, (uint32_t)M * (uint32_t)row_bytes);
+  uint32_t xv[XLOADS];
+#pragma unroll
+  for (int i = 0; i < XLOADS; ++i) {
+    const int gm = m_blk + row0 + 16 * i;
+    xv[i] = (uint32_t)(gm < M ? gm : M - 1) * (uint32_t)row_bytes + xslot_b;
+  }
+  const bool ragged = (row_bytes & 255) != 0;
+
+  Acc acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = Acc{0, 0, 0, 0};
+
+  uint4 xr[D][XLOADS];
+  typename P::Chunk wr[D];
+
+  // local step j of this k-group -> absolute step (may be >= s1: then inactive)
+  auto abs_step = [&](int j) __attribute__((always_inline)) { return s0 + kg + j * KG; };
+  auto load_step = [&](int j, uint4 (&xdst)[XLOADS], typename P::Chunk& wdst)
+      __attribute__((always_inline)) {
+    const int st0 = abs_step(j);
+    const int st = st0 < s1 ? st0 : s1 - 1;
+    if (TAO_GEMM_DEBUG != 1) {
+#pragma unroll
+      for (int i = 0; i < XLOADS; ++i) xdst[i] = bload16(xrs, xv[i], st * 256);
+    } else {
+#pragma unroll
+      for (int i = 0; i < XLOADS; ++i) xdst[i] = make_uint4(st, i, 0x3c003c00u, 0);
+    }
+    if (TAO_GEMM_DEBUG != 2) {
+      wdst = pol.load(wl, st);
+    } else {
+      wdst = typename P::Chunk{};
+      reinterpret_cast<uint32_t*>(&wdst)[0] = st * 0x01010101u;
+    }
+  };
+  auto store_x = [&](const uint4 (&src)[XLOADS], int j) __attribute__((always_inline)) {
+    const int st = abs_step(j);
+    uint4* dst = xs + (j & 1) * TILE;
+    if (TAO_GEMM_DEBUG == 3) return;
+    if (!ragged && st < s1) {
+#pragma unroll
+      for (int i = 0; i < XLOADS; ++i) dst[xlds0 + 256 * i] = src[i];
+    } else {
+      // k tail / inactive step -> 0 (an AND mask: a select here compiles to a branch)
+      const uint32_t keep = st < s1 && st * 256 + xslot_b < row_bytes ? ~0u : 0u;
+#pragma unroll
+      for (int i = 0; i < XLOADS; ++i)
+        dst[xlds0 + 256 * i] =
+            make_uint4(src[i].x & keep, src[i].y & keep, src[i].z & keep, src[i].w & keep);
+    }
+  };
+  // local step j; u = j % D at compile time
+  auto body = [&](auto uc, int j) __attribute__((always_inline)) {
+    constexpr int u = decltype(uc)::value;
+    load_step(j + D - 1, xr[(u + D - 1) % D], wr[(u + D - 1) % D]);
+    if (abs_step(j) < s1) {  // uniform: a k-group's idle tail iterations skip the math
+      const typename P::Prep pw = pol.prep(wr[u]);
+      const uint4* xb = xs + (j & 1) * TILE;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const auto bfrag = pol.frag(pw, s);
+        const int slot = kq * 4 + s;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          const int row = t * 16 + (lane & 15);
+          const uint4 a = TAO_GEMM_DEBUG == 3 ? xr[u][0] : xb[lds_slot(row, slot)];
+          acc[t] = P::mfma(a, bfrag, acc[t]);
+        }
+      }
+    }
+    if (j + 1 < J) store_x(xr[(u + 1) % D], j + 1);
+    if (TAO_GEMM_DEBUG != 4) __syncthreads();
+  };
+
+  static_for<0, D - 1>([&](auto i) __attribute__((always_inline)) {
+    load_step(decltype(i)::value, xr[decltype(i)::value], wr[decltype(i)::value]);
+  });
+  store_x(xr[0], 0);
+  __syncthreads();
+
+  int j = 0;
+  for (; j + D <= J; j += D)
+    static_for<0, D>([&](auto uc) __attribute__((always_inline)) {
+      body(uc, j + decltype(uc)::value);
+    });
+  static_for<0, D - 1>([&](auto uc) __attribute__((always_inline)) {
+    if (j + decltype(uc)::value < J) body(uc, j + decltype(uc)::value);
+  });
+
+  // k-groups 1..KG-1 hand their accumulators to k-group 0 through LDS (summed in order)
+  if constexpr (KG > 1) {
+    Acc* red = reinterpret_cast<Acc*>(lds);
+    if (kg > 0) {
+#pragma unroll
+      for (int t = 0; t < MT; ++t) red[(((kg - 1) * 4 + wave) * MT + t) * 64 + lane] = acc[t];
+    }
+    __syncthreads();
+    if (kg == 0) {
+      for (int g = 1; g < KG; ++g) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[t] += red[(((g - 1) * 4 + wave) * MT + t) * 64 + lane];
+      }
+    }
+    __syncthreads();  // LDS free again (the split-K flag below reuses it)
+  }
+
+  const int S = gridDim.z;
+  if (S > 1) {
+    const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
+    if (kg == 0) {
+      Acc* mine = slab + (((size_t)tile * S + blockIdx.z) * 4 + wave) * MT * 64 + lane;
+#pragma unroll
+      for (int t = 0; t < MT; ++t) mine[t * 64] = acc[t];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* flag = reinterpret_cast<unsigned*>(lds);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned ticket =
+          __hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = ticket == (unsigned)S - 1;
+      if (last) {
+        __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = last ? 1u : 0u;
+    }
+    __syncthreads();
+    if (*flag == 0 || kg != 0) return;
+    const Acc* all = slab + ((size_t)tile * S * 4 + wave) * MT * 64 + lane;
+    const size_t zstride = (size_t)4 * MT * 64;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[t] = Acc{0, 0, 0, 0};
+    // 4 slabs per round, all loads issued before the first add (clamped, then masked)
+    for (int z0 = 0; z0 < S; z0 += 4) {
+      Acc part[4][MT];
+#pragma unroll
+      for (int zz = 0; zz < 4; ++zz) {
+        const int z = z0 + zz < S ? z0 + zz : S - 1;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) part[zz][t] = all[z * zstride + t * 64];
+      }
+#pragma unroll
+      for (int zz = 0; zz < 4; ++zz) {
+        if (z0 + zz < S) {
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc[t] += part[zz][t];
+        }
+      }
+    }
+  } else if (kg != 0) {
+    return;
+  }
+
+  // C/D map: col = lane & 15 (n), row = 4*(lane >> 4) + i (m).
+  if (nok) {
+    const float bv = bias != nullptr ? bf16_to_f32(bias[bn]) : 0.f;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m_blk + t * 16 + 4 * (lane >> 4) + i;
+        if (m < M) {
+          float v = pol.epilogue(acc[t][i], m, bn);
+          if (bias != nullptr) v = round_bf16(v + bv);
+          y[(size_t)m * N + bn] = f32_to_bf16(v);
+        }
+      }
+    }
+  }
+}
+
+// Launch shape: M tile, k-groups per workgroup and K slices. Per-workgroup time is set by its
+// load latency chain, so the grid should put several waves on every SIMD.
+struct GemmShape {
+  int bm, kg, splits;
+};
+std::atomic<int> g_tune_bm{0}, g_tune_kg{0}, g_tune_splits{0};
+
+GemmShape choose_shape(int M, int N, int nsteps) {
+  const long nb = (N + kBN - 1) / kBN;
+  GemmShape sh{16, 1, 1};
+  const int cands[3] = {128, 64, 32};
+  for (int bm : cands)
+    if (bm < 2 * M && nb * ((M + bm - 1) / bm) >= 240) {
+      sh.bm = bm;
+      break;
+    }
+  sh.kg = sh.bm <= 32 ? 4 : (sh.bm == 64 ? 2 : 1);
+  const long tiles = nb * ((M + sh.bm - 1) / sh.bm);
+  int s = 1;
+  while (tiles * s * 2 <= 256 && s * 2 <= 8 && nsteps / (s * 2) >= 2 * sh.kg) s *= 2;
+  sh.splits = s;
+  const int tb = g_tune_bm.load(std::memory_order_relaxed);
+  const int tk = g_tune_kg.load(std::memory_order_relaxed);
+  const int ts = g_tune_splits.load(std::memory_order_relaxed);
+  if (tb) sh.bm = tb;
+  if (tk) sh.kg = tk;
+  if (ts) sh.splits = ts < nsteps ? ts : nsteps;
+  // LDS: KG x 2 x BM x 256 B <= 64 KiB
+  while (sh.kg > 1 && sh.kg * sh.bm > 128) sh.kg >>= 1;
+  return sh;
+}
+
+template <int BM, int KG, class P>
+void launch_one(dim3 grid, hipStream_t stream, const uint8_t* xb, const P& pol,
+                const uint16_t* bias, uint16_t* y, int M, int N, int K, int sps,
+                typename P::Acc* slab, unsigned* cnt) {
+  // ring depth: 4 steps, 3 where int8-dyn's 64-B weight pieces would spill at 16 waves / CU
+  constexpr int D = BM <= 16 ? 4 : (BM <= 32 ? (sizeof(typename P::Chunk) > 32 ? 3 : 4) : 2);
+  launch((gemm_mfma_kernel<BM, D, KG, P>), grid, dim3(256 * KG), 0, stream, xb, pol, bias, y, M,
+         N, K, sps, slab, cnt);
+}
+
+template <class P>
+int launch_gemm(const void* x, const P& pol, const uint16_t* bias, uint16_t* y, int M, int N,
+                int K, hipStream_t stream) {
+  const int nsteps = (K + P::kKStep - 1) / P::kKStep;
+  GemmShape sh = choose_shape(M, N, nsteps);
+  const int sps = (nsteps + sh.splits - 1) / sh.splits;
+  const int S = (nsteps + sps - 1) / sps;  // no empty slice
+  dim3 grid((N + kBN - 1) / kBN, (M + sh.bm - 1) / sh.bm, S);
+  typename P::Acc* slab = nullptr;
+  unsigned* cnt = nullptr;
+  if (S > 1) {
+    const size_t tiles = (size_t)grid.x * grid.y;
+    void* ws = nullptr;
+    const int rc = split_workspace(stream, tiles * S * sh.bm * kBN * sizeof(float), tiles, &ws,
+                                   &cnt);
+    if (rc != TAO_OK) return rc;
+    slab = reinterpret_cast<typename P::Acc*>(ws);
+  }
+  const uint8_t* xb = reinterpret_cast<const uint8_t*>(x);
+  const auto args = std::make_tuple(grid, stream, xb, pol, bias, y, M, N, K, sps, slab, cnt);
+  auto go = [&](auto fn) { std::apply(fn, args); };
+  switch (sh.bm * 8 + sh.kg) {
+    case 16 * 8 + 1: go(launch_one<16, 1, P>); break;
+    case 16 * 8 + 2: go(launch_one<16, 2, P>); break;
+    case 16 * 8 + 4: go(launch_one<16, 4, P>); break;
+    case 32 * 8 + 1: go(launch_one<32, 1, P>); break;
+    case 32 * 8 + 2: go(launch_one<32, 2, P>); break;
+    case 32 * 8 + 4: go(launch_one<32, 4, P>); break;
+    case 64 * 8 + 1: go(launch_one<64, 1, P>); break;
+    case 64 * 8 + 2: go(launch_one<64, 2, P>); break;
+    default: go(launch_one<128, 1, P>); break;
+  }
+  return check_launch("gemm_mfma_kernel");
+}
+
+// Largest M served by the GEMV kernels (tao_tune_linear_crossover; 0 = built-in).
+std::atomic<int> g_max_gemv_m{0};
+int max_gemv_m() {
+  const int v = g_max_gemv_m.load(std::memory_order_relaxed);
+  return v > 0 ? v : 4;
+}
+
+int gshift_of(int64_t g) {
+  switch (g) {
+    case 32: return 0;
+    case 64: return 1;
+    case 128: return 2;
+    case 256: return 3;
+    default: return -1;
+  }
+}
+
+}  // namespace
+
+int int8_scaled_mm_launch(const int8_t* xq, const uint16_t* xs, const int8_t* wq,
+                          const uint16_t* ws, const uint16_t* bias, uint16_t* y, int M, int N,
+                          int K, hipStream_t stream) {
+  Int8Dyn pol;
+  pol.w = reinterpret_cast<const uint4*>(wq);
+  pol.wscale = ws;
+  pol.xscale = xs;
+  return launch_gemm(xq, pol, bias, y, M, N, K, stream);
+}
+
+}  // namespace tao
+
+extern "C" int tao_int4wo_linear_bf16(const uint16_t* x, const uint32_t* packed,
+                                      const uint16_t* sz, const uint16_t* bias, uint16_t* y,
+                                      int64_t M, int64_t N, int64_t K, int64_t group_size,
+                                      void* stream) {
+  int rc = tao::int4_check_linear_args(x, packed, sz, y, M, N, K, group_size);
+  if (rc != TAO_OK) return rc;
+  if (M == 0 || N == 0) return TAO_OK;
+  hipStream_t st = tao::as_stream(stream);
+  if (M <= tao::max_gemv_m()) return tao::int4wo_gemv(x, packed, sz, bias, y, M, N, K, group_size, st);
+  tao::Int4WO pol;
+  pol.wq = reinterpret_cast<const uint4*>(packed);
+  pol.sz = reinterpret_cast<const uint32_t*>(sz);
+  pol.gshift = tao::gshift_of(group_size);
+  return tao::launch_gemm(x, pol, bias, y, (int)M, (int)N, (int)K, st);
+}
+
+extern "C" int tao_int8wo_linear_bf16(const uint16_t* x, const int8_t* w, const uint16_t* scale,
+                                      const uint16_t* bias, uint16_t* y, int64_t M, int64_t N,
+                                      int64_t K, void* stream) {
+  TAO_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "int8 weight-only linear: negative size");
+  TAO_CHECK_ARG(K % 32 == 0, "int8 weight-only linear: K (%lld) must be a multiple of 32",
+                (long long)K);
+  TAO_CHECK_ARG(N < (1LL << 31) && K < (1LL << 31) && M < (1LL << 31),
+                "int8 weight-only linear: size out of range");
+  if (M == 0 || N == 0) return TAO_OK;
+  TAO_CHECK_ARG(K > 0, "int8 weight-only linear: K must be > 0");
+  TAO_CHECK_ALIGN(x, 16, "x");
+  TAO_CHECK_ALIGN(w, 16, "w");
+  TAO_CHECK_ALIGN(scale, 2, "scale");
+  hipStream_t st = tao::as_stream(stream);
+  if (M <= tao::max_gemv_m()) return tao::int8wo_gemv(x, w, scale, bias, y, M, N, K, st);
+  tao::Int8WO pol;
+  pol.w = reinterpret_cast<const uint4*>(w);
+  pol.scale = scale;
+  return tao::launch_gemm(x, pol, bias, y, (int)M, (int)N, (int)K, st);
+}
+
+extern "C" int tao_tune_linear_crossover(int max_gemv_m) {
+  TAO_CHECK_ARG(max_gemv_m >= 0 && max_gemv_m <= 8, "tune: max_gemv_m must be in [0, 8]");
+  tao::g_max_gemv_m.store(max_gemv_m);
+  return TAO_OK;
+}
+
+extern "C" int tao_tune_gemm(int m_tile, int k_groups, int splits) {
+  TAO_CHECK_ARG(m_tile == 0 || m_tile == 16 || m_tile == 32 || m_tile == 64 || m_tile == 128,
+                "tune: m_tile must be 0 (auto), 16, 32, 64 or 128");
+  TAO_CHECK_ARG(k_groups == 0 || k_groups == 1 || k_groups == 2 || k_groups == 4,
+                "tune: k_groups must be 0 (auto), 1, 2 or 4");
+  TAO_CHECK_ARG(splits >= 0 && splits <= 64, "tune: splits must be in [0, 64]");
+  tao::g_tune_bm.store(m_tile);
+  tao::g_tune_kg.store(k_groups);
+  tao::g_tune_splits.store(splits);
+  return TAO_OK;
+}

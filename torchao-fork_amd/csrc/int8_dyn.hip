@@ -4,18 +4,12 @@
 //      which the reference runs as ~6 eager kernels (amin/amax/div/round/clamp/cast);
 //   2. tao_int8_scaled_mm_bf16: int32 MFMA GEMM with the fused two-scale epilogue, replacing
 //      int_scaled_matmul + the weight-scale multiply (torchao/kernel/intmm.py:108-143,
-//      torchao/dtypes/uintx/plain_layout.py:294-315).
-//
-// GEMM tile: 4 waves x 16 output columns = BN 64, BM rows; macro-step 256 k;
-// v_mfma_i32_16x16x64_i8 with a permuted k order: MFMA s of lane l (r = l&15, kq = l>>4) uses
-// k = k0 + 64*kq + 16*s + (0..15), identically for A and B, so a lane's 64-B weight load
-// feeds all four MFMAs. x (int8) is staged through LDS with 16-B slots XOR-swizzled by row.
+//      torchao/dtypes/uintx/plain_layout.py:294-315). The GEMM is the Int8Dyn instance of the
+//      shared skinny-GEMM template in gemm_mfma.hip.
 #include "tao_common.h"
 
 namespace tao {
 namespace {
-
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
 // ---- per-token quantisation ------------------------------------------------------------------
 constexpr int kQBlock = 256;
@@ -72,111 +66,12 @@ __global__ __launch_bounds__(kQBlock) void int8_quant_per_token_kernel(
   }
 }
 
-// ---- int8 x int8 -> int32 MFMA GEMM ----------------------------------------------------------
-constexpr int kBN = 64;
-constexpr int kKStep = 256;
-
-__device__ __forceinline__ int lds_slot(int row, int slot) { return row * 16 + (slot ^ (row & 15)); }
-
-template <int BM>
-__global__ __launch_bounds__(256) void int8_scaled_mm_kernel(
-    const int8_t* __restrict__ xq, const uint16_t* __restrict__ xs, const uint4* __restrict__ wq,
-    const uint16_t* __restrict__ ws, const uint16_t* __restrict__ bias, uint16_t* __restrict__ y,
-    int M, int N, int K) {
-  constexpr int MT = BM / 16;
-  constexpr int XLOADS = BM * 16 / 256;
-  __shared__ uint4 xsm[BM * 16];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
-  const int n_blk = blockIdx.x * kBN;
-  const int m_blk = blockIdx.y * BM;
-  const int nvec = K >> 4;  // 16-B vectors per row
-  const int nsteps = (K + kKStep - 1) / kKStep;
-
-  const int bn = n_blk + wave * 16 + (lane & 15);
-  const int bnc = bn < N ? bn : N - 1;
-  const int kq = lane >> 4;
-
-  i32x4_t acc[MT];
-#pragma unroll
-  for (int t = 0; t < MT; ++t) acc[t] = i32x4_t{0, 0, 0, 0};
-
-  uint4 xr[XLOADS];
-  uint4 wr[4];
-
-  auto load_step = [&](int step) {
-    const int k0 = step * kKStep;
-#pragma unroll
-    for (int i = 0; i < XLOADS; ++i) {
-      const int piece = tid + i * 256;
-      const int row = piece >> 4, slot = piece & 15;
-      const int gm = m_blk + row;
-      const int gk = k0 + slot * 16;
-      const bool ok = gm < M && gk < K;
-      const int gmc = gm < M ? gm : M - 1;
-      const int gkc = gk < K ? gk : 0;
-      const uint4 v = *reinterpret_cast<const uint4*>(xq + (size_t)gmc * K + gkc);
-      xr[i] = ok ? v : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int vec = (k0 >> 4) + kq * 4 + s;
-      const bool ok = vec < nvec && bn < N;
-      const int vc = vec < nvec ? vec : nvec - 1;
-      const uint4 v = ld_nt_u4(wq + (size_t)bnc * nvec + vc);
-      wr[s] = ok ? v : make_uint4(0, 0, 0, 0);
-    }
-  };
-
-  load_step(0);
-  for (int step = 0; step < nsteps; ++step) {
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < XLOADS; ++i) {
-      const int piece = tid + i * 256;
-      xsm[lds_slot(piece >> 4, piece & 15)] = xr[i];
-    }
-    uint4 wcur[4] = {wr[0], wr[1], wr[2], wr[3]};
-    __syncthreads();
-    if (step + 1 < nsteps) load_step(step + 1);
-
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const i32x4_t bfrag = __builtin_bit_cast(i32x4_t, wcur[s]);
-      const int slot = kq * 4 + s;
-#pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        const int row = t * 16 + (lane & 15);
-        const i32x4_t afrag = __builtin_bit_cast(i32x4_t, xsm[lds_slot(row, slot)]);
-        acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag, bfrag, acc[t], 0, 0, 0);
-      }
-    }
-  }
-
-  if (bn < N) {
-    const float wsc = bf16_to_f32(ws[bn]);
-    const float bv = bias != nullptr ? bf16_to_f32(bias[bn]) : 0.f;
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = m_blk + t * 16 + 4 * (lane >> 4) + i;
-        if (m < M) {
-          // bf16(c) * x_scale, * w_scale, + bias: each rounded to bf16, the op order of the
-          // reference (intmm.py:133-137 then plain_layout.py:301-315).
-          float v = round_bf16(round_bf16((float)acc[t][i]) * bf16_to_f32(xs[m]));
-          v = round_bf16(v * wsc);
-          if (bias != nullptr) v = round_bf16(v + bv);
-          y[(size_t)m * N + bn] = f32_to_bf16(v);
-        }
-      }
-    }
-  }
-}
-
 }  // namespace
+
+int int8_scaled_mm_launch(const int8_t* xq, const uint16_t* xs, const int8_t* wq,
+                          const uint16_t* ws, const uint16_t* bias, uint16_t* y, int M, int N,
+                          int K, hipStream_t stream);  // gemm_mfma.hip
+
 }  // namespace tao
 
 using namespace tao;
@@ -207,20 +102,8 @@ int tao_int8_scaled_mm_bf16(const int8_t* xq, const uint16_t* xs, const int8_t* 
   TAO_CHECK_ARG(K > 0, "int8 scaled mm: K must be > 0");
   TAO_CHECK_ALIGN(xq, 16, "xq");
   TAO_CHECK_ALIGN(wq, 16, "wq");
-  hipStream_t st = as_stream(stream);
-  const int bm = M <= 16 ? 16 : (M <= 32 ? 32 : 64);
-  dim3 grid((unsigned)((N + kBN - 1) / kBN), (unsigned)((M + bm - 1) / bm));
-  const uint4* w4 = reinterpret_cast<const uint4*>(wq);
-  if (bm == 16)
-    launch(int8_scaled_mm_kernel<16>, grid, dim3(256), 0, st, xq, xs, w4, ws, bias, y,
-                       (int)M, (int)N, (int)K);
-  else if (bm == 32)
-    launch(int8_scaled_mm_kernel<32>, grid, dim3(256), 0, st, xq, xs, w4, ws, bias, y,
-                       (int)M, (int)N, (int)K);
-  else
-    launch(int8_scaled_mm_kernel<64>, grid, dim3(256), 0, st, xq, xs, w4, ws, bias, y,
-                       (int)M, (int)N, (int)K);
-  return check_launch("int8_scaled_mm_kernel");
+  return int8_scaled_mm_launch(xq, xs, wq, ws, bias, y, (int)M, (int)N, (int)K,
+                               as_stream(stream));
 }
 
 }  // extern "C"

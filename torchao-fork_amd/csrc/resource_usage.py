@@ -1,6 +1,6 @@
 """Print VGPRs / scratch / occupancy per kernel of the HIP sources (hipcc remarks)."""
 import re, subprocess, sys
-srcs = sys.argv[1:] or ["int4_gemv.hip", "int8_gemv.hip", "wo_mfma.hip", "int8_dyn.hip", "int4_pack.hip"]
+srcs = sys.argv[1:] or ["int4_gemv.hip", "int8_gemv.hip", "gemm_mfma.hip", "int8_dyn.hip", "int4_pack.hip"]
 for s in srcs:
     out = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
                           "-Rpass-analysis=kernel-resource-usage", "-c", s, "-o", "/dev/null"],

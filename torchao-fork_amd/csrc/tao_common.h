@@ -28,6 +28,14 @@ int check_launch(const char* what);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ---- split-K workspace (capi.cpp) ------------------------------------------------------------
+// Per (device, stream) scratch for the partial-sum slabs of split-K launches plus a zeroed array
+// of arrival counters (each reset by its tile's last arriver). Grows outside graph capture
+// only: a capture borrows a large-enough workspace reserved on the device by an earlier eager
+// call (on any stream), else it is an error (run the op once at that shape before capturing).
+int split_workspace(hipStream_t stream, size_t slab_bytes, size_t counters, void** slab,
+                    unsigned** cnt);
+
 // ---- optional per-kernel timing (tao_profile_begin / tao_profile_end, capi.cpp) ---------------
 // While a profile session is open on this thread, each launch gets a start/stop hipEvent pair
 // recorded by the kernel's own dispatch packet (hipExtLaunchKernelGGL): the same interval

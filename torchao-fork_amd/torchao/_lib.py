@@ -14,7 +14,10 @@ import os
 from typing import Optional
 
 _LIB_NAME = "libtorchao_mi355x.so"
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), _LIB_NAME)
+# TORCHAO_MI355X_LIB overrides the in-tree build (experiment variants)
+_LIB_PATH = os.environ.get("TORCHAO_MI355X_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), _LIB_NAME
+)
 
 _lib: Optional[ctypes.CDLL] = None
 _load_error: Optional[str] = None
@@ -32,6 +35,8 @@ _SIGNATURES = {
     "tao_profile_end": [_p, _int, _p],
     "tao_int4wo_linear_bf16": [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p],
     "tao_tune_int4_gemv": [_int, _int, _int, _int],
+    "tao_tune_linear_crossover": [_int],
+    "tao_tune_gemm": [_int, _int, _int],
     "tao_int4_pack": [_p, _p, _i64, _i64, _p],
     "tao_int4_pack_u8": [_p, _p, _i64, _i64, _p],
     "tao_int4_unpack": [_p, _p, _i64, _i64, _p],
