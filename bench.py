@@ -17,9 +17,12 @@ bytes once per step.
 Reported (one JSON line, rank 0):
   value        = algorithmic bytes per step x steps / wall time  (GB/s, whole job)
   tokens_per_s = steps / wall time
-  roofline     = the GEMV kernel: sum of algorithmic bytes / sum of kernel durations, measured
-                 live with HIP events written by each kernel's dispatch (tao_profile_*), against
-                 the MI355X HBM3E peak of 8 TB/s
+  roofline     = the GEMV kernel: algorithmic bytes per step / GPU time per step of the
+                 GEMV-only graph replayed back to back (HIP events on the replay stream, i.e. the
+                 sum of the 161 kernels' durations in the timed regime), against the MI355X
+                 HBM3E peak of 8 TB/s; per_shape = one eager step timed per kernel by events the
+                 dispatch packets write (tao_profile_*); traffic = HBM bytes per step from the
+                 committed rocprofv3 FETCH_SIZE pass (profiles/, gfx950 x2 correction)
   cpu_baseline = the reference's CPU "dequant path" (dequantize -> F.linear, bf16) restated in
                  oracle/, timed on this host's cores over a bounded sample (rank 0, N = 1)
 """
@@ -38,6 +41,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E, spec (MI355X_MICROARCH.md chip table)
+PMC_FILE = os.path.join(ROOT, "profiles", "r1_pmc_fetch_bench.json")
 
 LLAMA3_8B = dict(dim=4096, n_layer=32, n_head=32, n_kv_head=8, head_dim=128,
                  intermediate=14336, vocab=128256)
@@ -231,14 +235,33 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # ---- roofline: per-kernel durations of one eager step, HIP events from the dispatch ----
+    # ---- roofline: GEMV-only graph replayed back to back, GPU events on the replay stream ----
+    groof = graph if (graph is not None and P == 1) else None
+    if groof is None and graph is not None:
+        groof = capture(do_comm=False)
+    kernel_ms = None
+    if groof is not None:
+        reps = max(args.steps, 10)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(stream):
+            groof.replay()
+            ev0.record(stream)
+            for _ in range(reps):
+                groof.replay()
+            ev1.record(stream)
+        ev1.synchronize()
+        kernel_ms = ev0.elapsed_time(ev1) / reps
+
+    # per-shape breakdown: one eager step, events written by each kernel's dispatch packet
     with _lib.KernelTimer(len(plan)) as timer:
         step(do_comm=False)
     torch.cuda.synchronize()
     durs = timer.durations_ms
     assert len(durs) == len(plan)
     gemv_bytes = [int4_alg_bytes(n_loc, K, g) for (_, n_loc, K, *_r) in plan]
-    achieved = sum(gemv_bytes) / (sum(durs) * 1e-3) / 1e9
+    if kernel_ms is None:
+        kernel_ms = sum(durs)
+    achieved = sum(gemv_bytes) / (kernel_ms * 1e-3) / 1e9
     per_shape = {}
     for (name, n_loc, K, *_r), d, b in zip(plan, durs, gemv_bytes):
         key = f"{n_loc}x{K}"
@@ -248,6 +271,14 @@ def main():
     for key, e in per_shape.items():
         e["us"] = round(e["us"] / e["launches"], 3)
         e["GBps"] = round(e["bytes"] / (e["us"] * 1e-6) / 1e9, 1)
+
+    # HBM traffic from the committed counter pass (rocprofv3 --pmc FETCH_SIZE of this bench,
+    # P = 1 shapes): bytes per step, to set against the algorithmic bytes
+    traffic = None
+    if P == 1 and os.path.exists(PMC_FILE):
+        with open(PMC_FILE) as f:
+            pmc = json.load(f)
+        traffic = pmc.get("hbm_bytes_per_step")
 
     comm_ms = None
     if P > 1:
@@ -301,10 +332,14 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "HBM bytes per step (161 launches)",
+                "alg_bytes_per_step": bytes_per_step,
+                "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic else None,
                 "launches": len(durs),
-                "kernel_ms_per_step": round(sum(durs), 4),
-                "per_shape": per_shape,
+                "kernel_ms_per_step": round(kernel_ms, 4),
+                "eager_kernel_ms_per_step": round(sum(durs), 4),
+                "per_shape_eager": per_shape,
             },
             "cpu_baseline": cpu,
         }

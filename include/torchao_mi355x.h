@@ -74,7 +74,8 @@ int tao_int4wo_linear_bf16(const uint16_t* x, const uint32_t* packed, const uint
 int tao_tune_int4_gemv(int rows_per_wave, int waves_k, int row_groups, int occupancy);
 
 /* Tuning hook: the weight-only linears (int4 and int8) use the GEMV kernels for M <= max_gemv_m
- * and the MFMA skinny GEMM above it. 0 restores the built-in crossover (4). Process-wide. */
+ * and the MFMA skinny GEMM above it. 0 restores the built-in crossover (M <= 2, or M <= 4 for
+ * weights of at most 32 Mi elements). Process-wide. */
 int tao_tune_linear_crossover(int max_gemv_m);
 
 /* Tuning hook: force the MFMA skinny GEMM's M tile (16/32/64/128), k-groups per workgroup

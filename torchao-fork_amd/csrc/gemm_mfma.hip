@@ -10,10 +10,11 @@
 //
 // Tile: 4 waves x 16 output columns (BN = 64) x BM rows per k-group; each wave owns 16 columns
 // and all BM rows. K advances in macro-steps of 256 B of x per row (128 bf16 k or 256 int8 k).
-// k order inside a macro-step is permuted identically for A and B: MFMA s (0..3) of lane l
-// (n = l & 15, kq = l >> 4) covers the kq-th quarter of the step, sub-block s. So a lane's
-// weight load for a step is one contiguous piece of its row (16 B int4, 32 B int8-WO,
-// 64 B int8-dyn) feeding all four MFMAs, and an int4 lane needs one (scale, zero) dword.
+// k order inside a macro-step is permuted identically for A and B (policy slot(s, kq): the
+// 16-B x slot MFMA s of lane l = (n = l & 15, kq = l >> 4) reads). Every weight load
+// instruction covers 64 contiguous bytes of each of the wave's 16 rows, the 16-B pieces of one
+// lane feed the four MFMAs of the step, and an int4 lane (one 32-k chunk) needs one
+// (scale, zero) dword.
 // x goes global -> registers (D-deep prefetch ring, T14) -> double-buffered, XOR-swizzled LDS
 // image -> A fragments; one barrier per step. W goes straight to registers (read once per
 // tile, dequantised in registers, reused for BM/16 MFMAs). K is split across k-groups inside
@@ -164,6 +165,8 @@ struct Int4WO {
     return as_bf16x8(pack_bf16x2(w04[0], w15[0]), pack_bf16x2(w26[0], w37[0]),
                      pack_bf16x2(w04[1], w15[1]), pack_bf16x2(w26[1], w37[1]));
   }
+  // lane (n, kq) holds chunk kq (32 k); MFMA s takes its dword s = 16-B x slot 4 kq + s
+  static __device__ __forceinline__ int slot(int s, int kq) { return kq * 4 + s; }
   static __device__ __forceinline__ Acc mfma(const uint4& a, const bf16x8_t& b, Acc c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), b, c, 0, 0, 0);
   }
@@ -188,13 +191,14 @@ struct Int8WO {
   __device__ __forceinline__ Lane setup(int n, int kq, int N, int K) const {
     Lane L;
     L.w = make_rsrc(w, (uint32_t)N * (uint32_t)K);
-    L.wv = (uint32_t)n * (uint32_t)K + kq * 32;
+    L.wv = (uint32_t)n * (uint32_t)K + kq * 16;
     return L;
   }
+  // each load instruction covers 64 contiguous bytes of each of the wave's 16 rows
   __device__ __forceinline__ Chunk load(const Lane& L, int st) const {
     Chunk ch;
     ch.a = bload16<kNT>(L.w, L.wv, st * 128);
-    ch.b = bload16<kNT>(L.w, L.wv + 16, st * 128);
+    ch.b = bload16<kNT>(L.w, L.wv + 64, st * 128);
     return ch;
   }
   __device__ __forceinline__ Prep prep(const Chunk& ch) const { return ch; }
@@ -207,6 +211,9 @@ struct Int8WO {
     return as_bf16x8(pack_bf16x2(cv(d0, 0), cv(d0, 1)), pack_bf16x2(cv(d0, 2), cv(d0, 3)),
                      pack_bf16x2(cv(d1, 0), cv(d1, 1)), pack_bf16x2(cv(d1, 2), cv(d1, 3)));
   }
+  // lane (n, kq) holds k 16 kq .. +16 (a) and 64 + 16 kq .. +16 (b): 8-k slots 2 kq, 2 kq + 1,
+  // 8 + 2 kq, 9 + 2 kq for MFMA s = 0..3
+  static __device__ __forceinline__ int slot(int s, int kq) { return (s >> 1) * 8 + kq * 2 + (s & 1); }
   static __device__ __forceinline__ Acc mfma(const uint4& a, const bf16x8_t& b, Acc c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), b, c, 0, 0, 0);
   }
@@ -234,7 +241,7 @@ struct Int8Dyn {
   __device__ __forceinline__ Lane setup(int n, int kq, int N, int K) const {
     Lane L;
     L.w = make_rsrc(w, (uint32_t)N * (uint32_t)K);
-    L.wv = (uint32_t)n * (uint32_t)K + kq * 64;
+    L.wv = (uint32_t)n * (uint32_t)K + kq * 16;
     if (TAO_GEMM_DEBUG == 5) L.wv = (uint32_t)(n >> 4) * (uint32_t)K * 16 + ((n & 15) * 4 + kq) * 16;
     return L;
   }
@@ -243,13 +250,16 @@ struct Int8Dyn {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
       ch.v[s] = TAO_GEMM_DEBUG == 5 ? bload16<kNT>(L.w, L.wv + 1024 * s, st * 4096)
-                                    : bload16<kNT>(L.w, L.wv + 16 * s, st * 256);
+                                    : bload16<kNT>(L.w, L.wv + 64 * s, st * 256);
     return ch;
   }
   __device__ __forceinline__ Prep prep(const Chunk& ch) const { return ch; }
   __device__ __forceinline__ i32x4_t frag(const Prep& p, int s) const {
     return __builtin_bit_cast(i32x4_t, p.v[s]);
   }
+  // load s covers 64 contiguous bytes of each row: lane (n, kq) holds k 64 s + 16 kq .. +16,
+  // i.e. MFMA s is the contiguous k block 64 s .. +64 (16-B x slot 4 s + kq)
+  static __device__ __forceinline__ int slot(int s, int kq) { return s * 4 + kq; }
   static __device__ __forceinline__ Acc mfma(const uint4& a, const i32x4_t& b, Acc c) {
     return __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4_t, a), b, c, 0, 0, 0);
   }
@@ -388,7 +398,7 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const auto bfrag = pol.frag(pw, s);
-        const int slot = kq * 4 + s;
+        const int slot = P::slot(s, kq);
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
           const int row = t * 16 + (lane & 15);
@@ -510,19 +520,23 @@ struct GemmShape {
 std::atomic<int> g_tune_bm{0}, g_tune_kg{0}, g_tune_splits{0};
 
 GemmShape choose_shape(int M, int N, int nsteps) {
+  // From experiments/sweep_gemm.py (profiles/r1_sweep_gemm.jsonl): the largest M tile that
+  // still gives >= 224 tiles (~0.9 x 256 CUs) without padding M 2x, else 16; split-K only to
+  // lift a small tile count towards 256 (its slab hand-off costs microseconds), and two
+  // k-groups per workgroup when the grid is at most one round.
   const long nb = (N + kBN - 1) / kBN;
   GemmShape sh{16, 1, 1};
   const int cands[3] = {128, 64, 32};
   for (int bm : cands)
-    if (bm < 2 * M && nb * ((M + bm - 1) / bm) >= 240) {
+    if (bm < 2 * M && nb * ((M + bm - 1) / bm) >= 224) {
       sh.bm = bm;
       break;
     }
-  sh.kg = sh.bm <= 32 ? 4 : (sh.bm == 64 ? 2 : 1);
   const long tiles = nb * ((M + sh.bm - 1) / sh.bm);
   int s = 1;
-  while (tiles * s * 2 <= 256 && s * 2 <= 8 && nsteps / (s * 2) >= 2 * sh.kg) s *= 2;
+  while (tiles * s * 2 <= 256 && s * 2 <= 8 && nsteps >= 8 * s) s *= 2;
   sh.splits = s;
+  sh.kg = (s == 1 && sh.bm <= 64 && tiles <= 256) ? 2 : 1;
   const int tb = g_tune_bm.load(std::memory_order_relaxed);
   const int tk = g_tune_kg.load(std::memory_order_relaxed);
   const int ts = g_tune_splits.load(std::memory_order_relaxed);
@@ -581,9 +595,12 @@ int launch_gemm(const void* x, const P& pol, const uint16_t* bias, uint16_t* y, 
 
 // Largest M served by the GEMV kernels (tao_tune_linear_crossover; 0 = built-in).
 std::atomic<int> g_max_gemv_m{0};
-int max_gemv_m() {
+// Built-in crossover (experiments/bench_paths.py --crossover): the GEMV wins at M <= 2, and at
+// M <= 4 for small weights; the MFMA kernel's per-M cost is nearly flat.
+bool use_gemv(int64_t M, int64_t N, int64_t K) {
   const int v = g_max_gemv_m.load(std::memory_order_relaxed);
-  return v > 0 ? v : 4;
+  if (v > 0) return M <= v;
+  return M <= 2 || (M <= 4 && N * K <= (32LL << 20));
 }
 
 int gshift_of(int64_t g) {
@@ -618,7 +635,8 @@ extern "C" int tao_int4wo_linear_bf16(const uint16_t* x, const uint32_t* packed,
   if (rc != TAO_OK) return rc;
   if (M == 0 || N == 0) return TAO_OK;
   hipStream_t st = tao::as_stream(stream);
-  if (M <= tao::max_gemv_m()) return tao::int4wo_gemv(x, packed, sz, bias, y, M, N, K, group_size, st);
+  if (tao::use_gemv(M, N, K))
+    return tao::int4wo_gemv(x, packed, sz, bias, y, M, N, K, group_size, st);
   tao::Int4WO pol;
   pol.wq = reinterpret_cast<const uint4*>(packed);
   pol.sz = reinterpret_cast<const uint32_t*>(sz);
@@ -640,7 +658,7 @@ extern "C" int tao_int8wo_linear_bf16(const uint16_t* x, const int8_t* w, const 
   TAO_CHECK_ALIGN(w, 16, "w");
   TAO_CHECK_ALIGN(scale, 2, "scale");
   hipStream_t st = tao::as_stream(stream);
-  if (M <= tao::max_gemv_m()) return tao::int8wo_gemv(x, w, scale, bias, y, M, N, K, st);
+  if (tao::use_gemv(M, N, K)) return tao::int8wo_gemv(x, w, scale, bias, y, M, N, K, st);
   tao::Int8WO pol;
   pol.w = reinterpret_cast<const uint4*>(w);
   pol.scale = scale;

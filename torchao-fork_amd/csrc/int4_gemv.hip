@@ -24,7 +24,7 @@ namespace {
 
 // WPE: minimum waves per SIMD the register allocation must allow (8 -> <= 64 VGPRs, so four
 // 512-thread workgroups fit on a CU and mid-size grids run in a single resident round).
-template <int MT, int RPW, int WPE>
+template <int MT, int RPW, int WPE, bool PAIR>
 __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     const uint16_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
     const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K, int gshift,
@@ -45,13 +45,14 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[r][m] = 0.f;
 
-  for (int s = wk; s < S; s += Wk) {
+  // PAIR (waves owning >= 2 slices): slices are processed two at a time, both slices' weight
+  // and (scale, zero) loads issued before either is consumed, so a wave walking two slices pays
+  // one memory round trip, not two.
+  auto load_slice = [&](int s, uint4 (&wv)[RPW], uint32_t (&szv)[RPW], int& cc, bool& cval)
+      __attribute__((always_inline)) {
     const int c = s * 64 + lane;
-    const bool cval = c < nchunk;
-    const int cc = cval ? c : nchunk - 1;  // clamped: every load stays in bounds, no branches
-
-    uint4 wv[RPW];
-    uint32_t szv[RPW];
+    cval = s < S && c < nchunk;
+    cc = c < nchunk ? c : nchunk - 1;  // clamped: every load stays in bounds, no branches
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
       const int n = row0 + r;
@@ -59,6 +60,9 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
       wv[r] = ld_nt_u4(wq + (size_t)nn * nchunk + cc);
       szv[r] = ld_nt(sz + (size_t)nn * ngroups + (cc >> gshift));
     }
+  };
+  auto do_slice = [&](const uint4 (&wv)[RPW], const uint32_t (&szv)[RPW], int cc, bool cval)
+      __attribute__((always_inline)) {
     // Lanes past K contribute nothing: zero their (s, z) so the chunk term vanishes.
     float sc[RPW], zp[RPW];
 #pragma unroll
@@ -99,6 +103,28 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
           for (int i = 0; i < 4; ++i) d = dot2_bf16(xd[j][i], nib_pair_bf16(wd[j], i), d);
         acc[r][m] = fmaf(sc[r], d - sx136, fmaf(zp[r], sx, acc[r][m]));
       }
+    }
+  };
+
+  if constexpr (PAIR) {
+    for (int s = wk; s < S; s += 2 * Wk) {
+      uint4 wv0[RPW], wv1[RPW];
+      uint32_t szv0[RPW], szv1[RPW];
+      int cc0, cc1;
+      bool cv0, cv1;
+      load_slice(s, wv0, szv0, cc0, cv0);
+      load_slice(s + Wk, wv1, szv1, cc1, cv1);
+      do_slice(wv0, szv0, cc0, cv0);
+      if (s + Wk < S) do_slice(wv1, szv1, cc1, cv1);  // wave-uniform
+    }
+  } else {
+    for (int s = wk; s < S; s += Wk) {
+      uint4 wv0[RPW];
+      uint32_t szv0[RPW];
+      int cc0;
+      bool cv0;
+      load_slice(s, wv0, szv0, cc0, cv0);
+      do_slice(wv0, szv0, cc0, cv0);
     }
   }
 
@@ -170,9 +196,14 @@ int launch_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
   const int grid = (N + rows_per_wg - 1) / rows_per_wg;
   const int threads = 64 * wk * sh.g;
   const size_t lds = (size_t)sh.g * wk * RPW * MT * sizeof(float);
-  launch((int4wo_gemv_kernel<MT, RPW, WPE>), dim3(grid), dim3(threads), lds, stream, x,
-         reinterpret_cast<const uint4*>(packed), reinterpret_cast<const uint32_t*>(sz), bias, y,
-         M, N, K, gshift, wk, sh.g, S);
+  if (S > wk)
+    launch((int4wo_gemv_kernel<MT, RPW, WPE, true>), dim3(grid), dim3(threads), lds, stream, x,
+           reinterpret_cast<const uint4*>(packed), reinterpret_cast<const uint32_t*>(sz), bias,
+           y, M, N, K, gshift, wk, sh.g, S);
+  else
+    launch((int4wo_gemv_kernel<MT, RPW, WPE, false>), dim3(grid), dim3(threads), lds, stream,
+           x, reinterpret_cast<const uint4*>(packed), reinterpret_cast<const uint32_t*>(sz),
+           bias, y, M, N, K, gshift, wk, sh.g, S);
   return check_launch("int4wo_gemv_kernel");
 }
 
@@ -193,14 +224,22 @@ int int4wo_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
     // Measured on MI355X (experiments/sweep_gemv.py, profiles/r1_sweep_gemv.jsonl): the best
     // shapes per (N, K) class, dispatch-event timed over weights rotated past the MALL.
     int rpw, occ = 8;
-    if (S <= 2) {  // K <= 4096: one wave walks the whole row pair; huge N wants 4-row waves
-      if (N >= 32768) { rpw = 4; sh = {2, 2}; } else { rpw = 2; sh = {1, 4}; }
-    } else if (S <= 4) {  // K <= 8192
-      if (N >= 8192) { rpw = 4; occ = 4; sh = {S, 1}; } else { rpw = 2; sh = {S, 1}; }
-    } else {  // K > 8192: split K across the workgroup unless N alone fills the chip
+    if (S <= 2) {  // K <= 4096
+      if (N >= 32768) {
+        rpw = 4;
+        sh = {2, 2};
+      } else if (N >= 8192) {  // one wave walks both slices of 4 rows (PAIR)
+        rpw = 4;
+        occ = 4;
+        sh = {1, 1};
+      } else {
+        rpw = 2;
+        sh = {2, N <= 4096 ? 1 : 4};
+      }
+    } else {  // K > 4096: waves split K (each walking its slices in pairs) while N is small
       rpw = 4;
       occ = 4;
-      sh = {(N >= 8192 && S > 8) ? 1 : (S < 8 ? S : 8), 1};
+      sh = {N <= 4096 ? 2 : (S >= 8 ? 1 : 4), 1};
     }
     const int trpw = g_tune_rpw.load(std::memory_order_relaxed);
     const int tocc = g_tune_occ.load(std::memory_order_relaxed);

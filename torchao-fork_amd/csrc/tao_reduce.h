@@ -27,10 +27,14 @@ __device__ __forceinline__ void wave_reduce_scatter(float (&v)[V], int lane) {
     const int cur = V >> step;
     const int half = cur >> 1;
     const bool up = (lane & off) != 0;
+    // select by bit mask on register values (a select between two array elements can be
+    // canonicalised into a dynamically indexed load, which spills the array to scratch)
+    const uint32_t m = up ? ~0u : 0u;
 #pragma unroll
     for (int i = 0; i < half; ++i) {
-      const float send = up ? v[i] : v[i + half];
-      const float keep = up ? v[i + half] : v[i];
+      const uint32_t a = __float_as_uint(v[i]), b = __float_as_uint(v[i + half]);
+      const float send = __uint_as_float((a & m) | (b & ~m));
+      const float keep = __uint_as_float((b & m) | (a & ~m));
       v[i] = keep + __shfl_xor(send, off, 64);
     }
     off >>= 1;
