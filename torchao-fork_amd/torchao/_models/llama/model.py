@@ -1,0 +1,232 @@
+"""Llama-family decoder for the end-to-end decode harness (BASELINE config 4).
+
+Same module tree and parameter names as the reference's gpt-fast model
+(torchao/_models/llama/model.py:243-501: ``tok_embeddings``, ``layers.{i}.attention.{wqkv,wo}``,
+``layers.{i}.feed_forward.{w1,w2,w3}``, ``{attention,ffn}_norm``, ``norm``, ``output``), so
+``quantize_`` filters and checkpoints keyed by those names apply unchanged. Every linear is a
+plain ``nn.Linear``: after ``quantize_(model, Int4WeightOnlyConfig(...))`` its forward goes
+through the AQT F.linear dispatch to the gfx950 HIP kernels.
+
+Decode-time structure for one process per GPU and HIP graphs (no tracing compiler):
+  * static KV cache [B, H_kv, T, D] per layer, written with ``index_copy_`` at ``input_pos``
+    (a device tensor) and a causal mask row gathered by ``input_pos``, so a decode step is
+    graph-capturable and each replay advances by incrementing ``input_pos`` in place;
+  * grouped-query attention through ``F.scaled_dot_product_attention(enable_gqa=True)``;
+  * rotary tables precomputed once (Llama-3.1 frequency scaling where configured).
+"""
+
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from torchao.utils import find_multiple
+
+__all__ = ["ModelArgs", "Transformer", "KVCache", "llama_configs"]
+
+
+@dataclass
+class ModelArgs:
+    block_size: int = 2048
+    vocab_size: int = 32000
+    n_layer: int = 32
+    n_head: int = 32
+    dim: int = 4096
+    intermediate_size: Optional[int] = None
+    n_local_heads: int = -1  # key/value heads (GQA); -1 = n_head
+    head_dim: int = 0
+    rope_base: float = 10000.0
+    norm_eps: float = 1e-5
+    rope_scaling: Optional[dict] = field(default=None)
+
+    def __post_init__(self):
+        if self.n_local_heads == -1:
+            self.n_local_heads = self.n_head
+        if self.intermediate_size is None:
+            self.intermediate_size = find_multiple(int(2 * 4 * self.dim / 3), 256)
+        self.head_dim = self.dim // self.n_head
+
+    @classmethod
+    def from_name(cls, name: str) -> "ModelArgs":
+        """Exact config name, else the longest config name contained in ``name``
+        (reference model.py:54-75 semantics: "Meta-Llama-3-8B" -> "Llama-3-8B")."""
+        if name in llama_configs:
+            return cls(**llama_configs[name])
+        hits = sorted((k for k in llama_configs if k in name or k.upper() in name.upper()),
+                      key=len, reverse=True)
+        if not hits:
+            raise ValueError(f"unknown model {name!r}; known: {sorted(llama_configs)}")
+        return cls(**llama_configs[hits[0]])
+
+
+_LLAMA31_SCALING = dict(factor=8.0, low_freq_factor=1.0, high_freq_factor=4.0,
+                        original_max_position_embeddings=8192)
+
+# the reference's shapes (model.py:76-140) for the families the harness exercises
+llama_configs = {
+    "stories15M": dict(n_layer=6, n_head=6, dim=288),
+    "stories110M": dict(n_layer=12, n_head=12, dim=768),
+    "7B": dict(n_layer=32, n_head=32, dim=4096),
+    "13B": dict(n_layer=40, n_head=40, dim=5120),
+    "70B": dict(n_layer=80, n_head=64, dim=8192, n_local_heads=8, intermediate_size=28672),
+    "Mistral-7B": dict(n_layer=32, n_head=32, n_local_heads=8, dim=4096,
+                       intermediate_size=14336, vocab_size=32000),
+    "Llama-3-8B": dict(block_size=8192, n_layer=32, n_head=32, n_local_heads=8, dim=4096,
+                       intermediate_size=14336, vocab_size=128256, rope_base=500000),
+    "Llama-3.1-8B": dict(block_size=131072, n_layer=32, n_head=32, n_local_heads=8, dim=4096,
+                         intermediate_size=14336, vocab_size=128256, rope_base=500000,
+                         rope_scaling=_LLAMA31_SCALING),
+    "Llama-3-70B": dict(block_size=8192, n_layer=80, n_head=64, n_local_heads=8, dim=8192,
+                        intermediate_size=28672, vocab_size=128256, rope_base=500000),
+    "Llama-3.1-70B": dict(block_size=131072, n_layer=80, n_head=64, n_local_heads=8,
+                          dim=8192, intermediate_size=28672, vocab_size=128256,
+                          rope_base=500000, rope_scaling=_LLAMA31_SCALING),
+}
+
+
+class KVCache(nn.Module):
+    """Static [B, H_kv, T, D] key/value buffers, updated in place at ``input_pos``."""
+
+    def __init__(self, batch: int, seq_len: int, n_heads: int, head_dim: int, dtype, device=None):
+        super().__init__()
+        shape = (batch, n_heads, seq_len, head_dim)
+        self.register_buffer("k_cache", torch.zeros(shape, dtype=dtype, device=device),
+                             persistent=False)
+        self.register_buffer("v_cache", torch.zeros(shape, dtype=dtype, device=device),
+                             persistent=False)
+
+    def update(self, input_pos: torch.Tensor, k: torch.Tensor, v: torch.Tensor):
+        # k, v: [B, H_kv, S, D] at positions input_pos [S]
+        self.k_cache.index_copy_(2, input_pos, k)
+        self.v_cache.index_copy_(2, input_pos, v)
+        return self.k_cache, self.v_cache
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, dim: int, eps: float = 1e-5):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        xf = x.float()
+        y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps)
+        return y.type_as(x) * self.weight
+
+
+def _rope_freqs(cfg: ModelArgs, seq_len: int) -> torch.Tensor:
+    """[seq_len, head_dim/2, 2] (cos, sin) in fp32; Llama-3.1 wavelength-dependent scaling."""
+    d = cfg.head_dim
+    inv = 1.0 / (cfg.rope_base ** (torch.arange(0, d, 2, dtype=torch.float64)[: d // 2] / d))
+    sc = cfg.rope_scaling
+    if sc is not None:
+        old = sc["original_max_position_embeddings"]
+        lo_wl = old / sc["low_freq_factor"]
+        hi_wl = old / sc["high_freq_factor"]
+        wl = 2 * torch.pi / inv
+        smooth = (old / wl - sc["low_freq_factor"]) / (sc["high_freq_factor"] - sc["low_freq_factor"])
+        scaled = torch.where(wl > lo_wl, inv / sc["factor"], inv)
+        mid = (wl <= lo_wl) & (wl >= hi_wl)
+        inv = torch.where(mid, (1 - smooth) * inv / sc["factor"] + smooth * inv, scaled)
+    t = torch.arange(seq_len, dtype=torch.float64)
+    ang = torch.outer(t, inv)
+    return torch.stack([ang.cos(), ang.sin()], dim=-1).float()
+
+
+def _apply_rope(x: torch.Tensor, freqs: torch.Tensor) -> torch.Tensor:
+    # x: [B, S, H, D] (pairs along D); freqs: [S, D/2, 2]
+    xs = x.float().reshape(*x.shape[:-1], -1, 2)
+    f = freqs.view(1, xs.size(1), 1, xs.size(3), 2)
+    out = torch.stack([xs[..., 0] * f[..., 0] - xs[..., 1] * f[..., 1],
+                       xs[..., 1] * f[..., 0] + xs[..., 0] * f[..., 1]], dim=-1)
+    return out.flatten(3).type_as(x)
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: ModelArgs):
+        super().__init__()
+        self.n_head, self.n_kv, self.head_dim = cfg.n_head, cfg.n_local_heads, cfg.head_dim
+        qkv = (cfg.n_head + 2 * cfg.n_local_heads) * cfg.head_dim
+        self.wqkv = nn.Linear(cfg.dim, qkv, bias=False)
+        self.wo = nn.Linear(cfg.dim, cfg.dim, bias=False)
+        self.kv_cache: Optional[KVCache] = None
+
+    def forward(self, x, freqs, mask, input_pos):
+        B, S, _ = x.shape
+        q_sz, kv_sz = self.n_head * self.head_dim, self.n_kv * self.head_dim
+        q, k, v = self.wqkv(x).split([q_sz, kv_sz, kv_sz], dim=-1)
+        q = _apply_rope(q.view(B, S, self.n_head, self.head_dim), freqs)
+        k = _apply_rope(k.view(B, S, self.n_kv, self.head_dim), freqs)
+        v = v.view(B, S, self.n_kv, self.head_dim)
+        q, k, v = (t.transpose(1, 2) for t in (q, k, v))
+        if self.kv_cache is not None:
+            k, v = self.kv_cache.update(input_pos, k, v)
+        y = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, enable_gqa=True)
+        return self.wo(y.transpose(1, 2).reshape(B, S, q_sz))
+
+
+class FeedForward(nn.Module):
+    def __init__(self, cfg: ModelArgs):
+        super().__init__()
+        self.w1 = nn.Linear(cfg.dim, cfg.intermediate_size, bias=False)
+        self.w3 = nn.Linear(cfg.dim, cfg.intermediate_size, bias=False)
+        self.w2 = nn.Linear(cfg.intermediate_size, cfg.dim, bias=False)
+
+    def forward(self, x):
+        return self.w2(F.silu(self.w1(x)) * self.w3(x))
+
+
+class TransformerBlock(nn.Module):
+    def __init__(self, cfg: ModelArgs):
+        super().__init__()
+        self.attention = Attention(cfg)
+        self.feed_forward = FeedForward(cfg)
+        self.attention_norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.ffn_norm = RMSNorm(cfg.dim, cfg.norm_eps)
+
+    def forward(self, x, freqs, mask, input_pos):
+        h = x + self.attention(self.attention_norm(x), freqs, mask, input_pos)
+        return h + self.feed_forward(self.ffn_norm(h))
+
+
+class Transformer(nn.Module):
+    def __init__(self, cfg: ModelArgs):
+        super().__init__()
+        self.config = cfg
+        self.tok_embeddings = nn.Embedding(cfg.vocab_size, cfg.dim)
+        self.layers = nn.ModuleList(TransformerBlock(cfg) for _ in range(cfg.n_layer))
+        self.norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.output = nn.Linear(cfg.dim, cfg.vocab_size, bias=False)
+        self.max_batch = self.max_seq = -1
+
+    @classmethod
+    def from_name(cls, name: str) -> "Transformer":
+        return cls(ModelArgs.from_name(name))
+
+    def setup_caches(self, max_batch_size: int, max_seq_length: int):
+        """Allocate the static KV caches, rotary table and causal mask on the model's device."""
+        cfg = self.config
+        max_seq_length = find_multiple(max_seq_length, 8)
+        if self.max_batch >= max_batch_size and self.max_seq >= max_seq_length:
+            return
+        self.max_batch, self.max_seq = max_batch_size, max_seq_length
+        dev = self.norm.weight.device
+        dtype = self.norm.weight.dtype
+        for blk in self.layers:
+            blk.attention.kv_cache = KVCache(max_batch_size, max_seq_length, cfg.n_local_heads,
+                                             cfg.head_dim, dtype, dev)
+        self.register_buffer("freqs", _rope_freqs(cfg, cfg.block_size).to(dev), persistent=False)
+        mask = torch.tril(torch.ones(max_seq_length, max_seq_length, dtype=torch.bool, device=dev))
+        self.register_buffer("causal_mask", mask, persistent=False)
+
+    def forward(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
+        """idx [B, S] token ids at positions input_pos [S] -> logits [B, S, vocab] (fp32)."""
+        assert self.max_seq > 0, "call setup_caches() first"
+        mask = self.causal_mask[None, None, input_pos]  # [1, 1, S, T]
+        freqs = self.freqs[input_pos]
+        x = self.tok_embeddings(idx)
+        for blk in self.layers:
+            x = blk(x, freqs, mask, input_pos)
+        return self.output(self.norm(x)).float()
