@@ -155,6 +155,35 @@ int tao_int8_scaled_mm_bf16(const int8_t* xq, const uint16_t* xs, const int8_t* 
                             const uint16_t* ws, const uint16_t* bias, uint16_t* y, int64_t M,
                             int64_t N, int64_t K, void* stream);
 
+/* ---- fused decode-step kernels of the end-to-end harness (torchao/_models/llama) -------------
+ * Not on the int4 path: the fusions the reference gets from torch.compile in its gpt-fast
+ * harness (torchao/_models/llama/generate.py:865-875, model.py:405-501). */
+
+/* y[r] = bf16(bf16(x[r] * rsqrt(mean(x[r]^2) + eps)) * w), rows of `dim` bf16 (dim % 8 == 0).
+ * Replaces RMSNorm.forward (torchao/_models/llama/model.py:489-501). */
+int tao_rmsnorm_bf16(const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t rows,
+                     int64_t dim, float eps, void* stream);
+
+/* qkv [B*S][(H + 2 Hkv) * D] bf16 -> q_out [B][H][S][D] rotated; k (rotated) and v written to
+ * k_cache / v_cache [B][Hkv][T][D] at positions pos[S] (int64). freqs: rotary table
+ * [rows][D/2][2] fp32 (cos, sin), row pos[s]. Replaces apply_rotary_emb + KVCache.update
+ * (model.py:547-557, 175-196). */
+int tao_rope_kv_bf16(const uint16_t* qkv, const float* freqs, const int64_t* pos,
+                     uint16_t* q_out, uint16_t* k_cache, uint16_t* v_cache, int64_t B, int64_t S,
+                     int64_t H, int64_t Hkv, int64_t D, int64_t T, void* stream);
+
+/* One-query attention over keys 0..pos[0] of the caches, GQA (H % Hkv == 0, H/Hkv <= 8),
+ * D == 128: out [B][1][H*D] bf16. partial: fp32 workspace of B*Hkv*ceil(T/64)*(H/Hkv)*(D+2).
+ * Replaces F.scaled_dot_product_attention at decode (model.py:441-476). */
+int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                         const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
+                         int64_t Hkv, int64_t D, int64_t T, float scale, void* stream);
+
+/* y = bf16(bf16(silu(a)) * b) elementwise over n bf16 (n even). Replaces FeedForward's
+ * F.silu(w1(x)) * w3(x) (model.py:485-486). */
+int tao_silu_mul_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t n,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2,6 +2,8 @@
 CPU (bf16 model, no quantization), and on the GPU with int4 weights: graph-replayed decode ==
 eager decode token for token, and int4 logits track the bf16 model's."""
 
+import math
+
 import pytest
 import torch
 
@@ -79,3 +81,102 @@ def test_graph_decode_matches_eager_gpu(quant):
     tok = prefill(model, prompt, torch.arange(P, device=dev))
     nxt = decode_one_token(model, tok, torch.tensor([P], device=dev))
     assert int(nxt) == int(eager[0, P + 1])
+
+
+# a head_dim-128 GQA model small enough for a unit test (the fused kernels need head_dim 128)
+TINY = dict(dim=512, n_layer=2, n_head=4, n_local_heads=2, vocab_size=1000, block_size=256)
+
+
+def _tiny(dev, seed=2):
+    import math
+
+    from torchao._models.llama.model import Transformer
+
+    torch.manual_seed(seed)
+    model = Transformer(ModelArgs(**TINY)).to(dev).to(torch.bfloat16)
+    with torch.no_grad():
+        for mod in model.modules():
+            if isinstance(mod, torch.nn.Linear):
+                b = 1 / math.sqrt(mod.in_features)
+                mod.weight.uniform_(-b, b)
+        for blk in model.layers:  # non-trivial norm weights
+            blk.attention_norm.weight.uniform_(0.5, 1.5)
+            blk.ffn_norm.weight.uniform_(0.5, 1.5)
+    return model.eval()
+
+
+@pytest.mark.gpu
+def test_fused_kernels_match_torch_ops_gpu():
+    import torch.nn.functional as F
+
+    from torchao._models.llama import kernels
+    from torchao._models.llama.model import RMSNorm, _apply_rope, _rope_freqs
+
+    dev = torch.device("cuda")
+    x = torch.randn(3, 4096, device=dev, dtype=torch.bfloat16) * 2
+    norm = RMSNorm(4096).to(dev).to(torch.bfloat16)
+    with torch.no_grad():
+        norm.weight.uniform_(0.5, 1.5)
+    ref = norm(x)
+    got = kernels.rmsnorm(x, norm.weight, norm.eps)
+    assert (got.float() - ref.float()).abs().max() <= 2 * ref.float().abs().max() * 2 ** -8
+
+    a = torch.randn(5, 1000, device=dev, dtype=torch.bfloat16) * 3
+    b = torch.randn(5, 1000, device=dev, dtype=torch.bfloat16)
+    torch.testing.assert_close(kernels.silu_mul(a, b), F.silu(a) * b, rtol=1e-2, atol=1e-2)
+
+    cfg = ModelArgs(**TINY)
+    H, Hkv, D, T = cfg.n_head, cfg.n_local_heads, cfg.head_dim, 64
+    freqs = _rope_freqs(cfg, cfg.block_size).to(dev)
+    qkv = torch.randn(1, 1, (H + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16)
+    kc = torch.zeros(1, Hkv, T, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    pos = torch.tensor([17], device=dev)
+    q = kernels.rope_kv(qkv, freqs, pos, kc, vc, H)
+    qr, kr, vr = qkv.split([H * D, Hkv * D, Hkv * D], dim=-1)
+    q_ref = _apply_rope(qr.view(1, 1, H, D), freqs[pos]).transpose(1, 2)
+    k_ref = _apply_rope(kr.view(1, 1, Hkv, D), freqs[pos]).transpose(1, 2)
+    torch.testing.assert_close(q, q_ref, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(kc[:, :, 17:18], k_ref, rtol=1e-2, atol=1e-2)
+    assert torch.equal(vc[:, :, 17:18], vr.view(1, 1, Hkv, D).transpose(1, 2))
+
+    # attention over keys 0..L-1 with L spanning several 64-key chunks
+    for L in (1, 63, 64, 65, 200):
+        T = 256
+        kc = torch.randn(2, Hkv, T, D, device=dev, dtype=torch.bfloat16)
+        vc = torch.randn_like(kc)
+        q = torch.randn(2, H, 1, D, device=dev, dtype=torch.bfloat16)
+        pos = torch.tensor([L - 1], device=dev)
+        got = kernels.attn_decode(q, kc, vc, pos, 1 / math.sqrt(D))
+        ref = F.scaled_dot_product_attention(q.float(), kc[:, :, :L].float(), vc[:, :, :L].float(),
+                                             enable_gqa=True)
+        ref = ref.transpose(1, 2).reshape(2, 1, H * D)
+        torch.testing.assert_close(got.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("quant", [None, "int4wo-32"])
+def test_fused_decode_matches_unfused_gpu(quant):
+    dev = torch.device("cuda")
+    model = _tiny(dev)
+    apply_quantization(model, quant)
+    P, T = 9, 12
+    model.setup_caches(1, P + T)
+    prompt = torch.randint(0, 1000, (1, P), device=dev)
+    pos = torch.arange(P, device=dev)
+    assert not model.fused
+    model(prompt, pos)
+    ref = [model(prompt[:, -1:], torch.tensor([P], device=dev))]
+    model.setup_caches(1, P + T)
+    assert model.enable_fused_kernels()
+    model(prompt, pos)  # prefill stays on torch ops
+    got = [model(prompt[:, -1:], torch.tensor([P], device=dev))]
+    rel = (got[0] - ref[0]).norm() / ref[0].norm()
+    assert rel < 2e-2, float(rel)
+    # graph-replayed fused decode == eager fused decode
+    eager, _, _ = generate(model, prompt, T, None)
+    dec = GraphDecoder(model, 1, P + T, dev)
+    dec.reset(prompt, prefill(model, prompt, pos))
+    dec.capture()
+    graphed, _, _ = generate(model, prompt, T, dec)
+    assert torch.equal(graphed, eager)

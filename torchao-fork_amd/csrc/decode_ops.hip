@@ -1,0 +1,317 @@
+// Fused decode-step kernels for the end-to-end harness (torchao/_models/llama).
+//
+// The reference gets these fusions from torch.compile (generate.py:865-875); here each is one
+// hand-written gfx950 kernel so a decoded token is ~11 launches per layer instead of ~50 eager
+// ones. None is on the int4 hot path; all are tiny and latency-bound (a few KiB per call except
+// the KV-cache reads of attention).
+//   * RMSNorm:   y = bf16(bf16(x * rsqrt(mean(x^2) + eps)) * w)        (model.py RMSNorm)
+//   * RoPE + KV: rotate q, k of the wqkv output in fp32 (interleaved pairs, rotary table row
+//                pos[s]), write q as [B][H][S][D] and k, v into the static caches at pos[S]
+//   * attention: one query per (batch, head), keys 0..pos (GQA: a workgroup serves the G query
+//                heads of one kv head); split over 64-key chunks (flash-decoding), then a
+//                combine kernel merges the chunks' (max, sum, o) in fp32 -> bf16
+//   * SiLU-mul:  y = bf16(bf16(silu(a)) * b)                             (F.silu(w1 x) * w3 x)
+#include "tao_common.h"
+
+namespace tao {
+namespace {
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+// ---- RMSNorm: one workgroup per row, 8 bf16 per thread per pass --------------------------------
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const uint16_t* __restrict__ x,
+                                                      const uint16_t* __restrict__ w,
+                                                      uint16_t* __restrict__ y, int D, float eps) {
+  __shared__ float red[4];
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)blockIdx.x * D);
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
+  uint4* yr = reinterpret_cast<uint4*>(y + (size_t)blockIdx.x * D);
+  const int nv = D / 8;
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < nv; i += 256) {
+    const uint4 v = xr[i];
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a = bf16lo_to_f32(d[j]), b = bf16hi_to_f32(d[j]);
+      ss = fmaf(a, a, fmaf(b, b, ss));
+    }
+  }
+  const float r = rsqrtf(block_sum(ss, red) / (float)D + eps);
+  for (int i = threadIdx.x; i < nv; i += 256) {
+    const uint4 v = xr[i], g = wr[i];
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w}, e[4] = {g.x, g.y, g.z, g.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float lo = round_bf16(bf16lo_to_f32(d[j]) * r) * bf16lo_to_f32(e[j]);
+      const float hi = round_bf16(bf16hi_to_f32(d[j]) * r) * bf16hi_to_f32(e[j]);
+      o[j] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+    }
+    yr[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// ---- RoPE on q, k + KV-cache write: one workgroup per token, one thread per pair -------------
+__global__ __launch_bounds__(256) void rope_kv_kernel(
+    const uint16_t* __restrict__ qkv, const float* __restrict__ freqs,
+    const int64_t* __restrict__ pos, uint16_t* __restrict__ q_out, uint16_t* __restrict__ kc,
+    uint16_t* __restrict__ vc, int S, int H, int Hkv, int D, int T) {
+  const int tok = blockIdx.x;  // b * S + s
+  const int b = tok / S, s = tok % S;
+  const int half = D / 2;
+  const int64_t p = pos[s];
+  const uint32_t* row = reinterpret_cast<const uint32_t*>(qkv + (size_t)tok * (H + 2 * Hkv) * D);
+  const float2* f = reinterpret_cast<const float2*>(freqs) + (size_t)p * half;  // table row pos
+  const int rot_pairs = (H + Hkv) * half;
+  for (int i = threadIdx.x; i < rot_pairs + Hkv * half; i += blockDim.x) {
+    const uint32_t w = row[i];  // pairs are interleaved: (x[2j], x[2j+1]) = one dword
+    if (i < rot_pairs) {
+      const int head = i / half, j = i % half;
+      const float2 cs = f[j];
+      const float x0 = bf16lo_to_f32(w), x1 = bf16hi_to_f32(w);
+      const float o0 = x0 * cs.x - x1 * cs.y, o1 = x1 * cs.x + x0 * cs.y;
+      const uint32_t o = (uint32_t)f32_to_bf16(o0) | ((uint32_t)f32_to_bf16(o1) << 16);
+      if (head < H) {
+        reinterpret_cast<uint32_t*>(q_out)[(((size_t)b * H + head) * S + s) * half + j] = o;
+      } else {
+        const int kh = head - H;
+        reinterpret_cast<uint32_t*>(kc)[(((size_t)b * Hkv + kh) * T + p) * half + j] = o;
+      }
+    } else {
+      const int k = i - rot_pairs;
+      const int vh = k / half, j = k % half;
+      reinterpret_cast<uint32_t*>(vc)[(((size_t)b * Hkv + vh) * T + p) * half + j] = w;
+    }
+  }
+}
+
+// ---- decode attention, phase 1: partial (m, l, o) per 64-key chunk --------------------------
+constexpr int kChunk = 64;
+
+template <int G, int D>
+__global__ __launch_bounds__(256) void attn_partial_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, float* __restrict__ part,
+    int Hkv, int T, float scale) {
+  static_assert(D == 128, "head_dim 128");
+  __shared__ float qs[G][D];
+  __shared__ float ps[G][kChunk];
+  __shared__ float mls[G][2];
+  const int bk = blockIdx.x;  // b * Hkv + kvh
+  const int b = bk / Hkv, kvh = bk % Hkv;
+  const int c = blockIdx.y, NC = gridDim.y;
+  const int L = (int)pos[0] + 1;
+  const int t0 = c * kChunk;
+  if (t0 >= L) return;  // uniform: the combine kernel skips this chunk too
+  const int tid = threadIdx.x;
+  const int H = Hkv * G;
+  for (int i = tid; i < G * D; i += 256) {
+    const int g = i / D, d = i % D;
+    qs[g][d] = bf16_to_f32(q[((size_t)b * H + kvh * G + g) * D + d]);
+  }
+  __syncthreads();
+
+  // scores: thread = (key j = tid / 4, quarter p = tid % 4 of the 128 dims)
+  const int j = tid >> 2, p = tid & 3;
+  const int kk = t0 + j;
+  float sc[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) sc[g] = 0.f;
+  if (kk < L) {
+    const uint4* kr =
+        reinterpret_cast<const uint4*>(kc + (((size_t)b * Hkv + kvh) * T + kk) * D + p * 32);
+#pragma unroll
+    for (int v4 = 0; v4 < 4; ++v4) {
+      const uint4 kv = kr[v4];
+      const uint32_t w[4] = {kv.x, kv.y, kv.z, kv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int d = p * 32 + v4 * 8 + 2 * e;
+        const float k0 = bf16lo_to_f32(w[e]), k1 = bf16hi_to_f32(w[e]);
+#pragma unroll
+        for (int g = 0; g < G; ++g) sc[g] = fmaf(qs[g][d], k0, fmaf(qs[g][d + 1], k1, sc[g]));
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    sc[g] += __shfl_xor(sc[g], 1, 64);
+    sc[g] += __shfl_xor(sc[g], 2, 64);
+  }
+  if (p == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) ps[g][j] = kk < L ? sc[g] * scale : -INFINITY;
+  }
+  __syncthreads();
+
+  // chunk softmax: wave w handles heads w, w + 4, ...
+  const int wave = tid >> 6, lane = tid & 63;
+  for (int g = wave; g < G; g += 4) {
+    const float v = ps[g][lane];
+    float m = v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    const float e = lane + t0 < L ? __expf(v - m) : 0.f;
+    float l = e;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o, 64);
+    ps[g][lane] = e;
+    if (lane == 0) {
+      mls[g][0] = m;
+      mls[g][1] = l;
+    }
+  }
+  __syncthreads();
+
+  // o[g][d] = sum_j p[g][j] v[j][d]; thread = (dim pair tid % 64, heads tid / 64, +4, ...)
+  const int dp = tid & 63;
+  const int nk = L - t0 < kChunk ? L - t0 : kChunk;
+  const uint32_t* vr =
+      reinterpret_cast<const uint32_t*>(vc + (((size_t)b * Hkv + kvh) * T + t0) * D) + dp;
+  for (int g = wave; g < G; g += 4) {
+    float o0 = 0.f, o1 = 0.f;
+    for (int jj = 0; jj < nk; ++jj) {
+      const uint32_t w = vr[(size_t)jj * (D / 2)];
+      const float pj = ps[g][jj];
+      o0 = fmaf(pj, bf16lo_to_f32(w), o0);
+      o1 = fmaf(pj, bf16hi_to_f32(w), o1);
+    }
+    float* dst = part + (((size_t)bk * NC + c) * G + g) * (D + 2);
+    dst[2 * dp] = o0;
+    dst[2 * dp + 1] = o1;
+    if (dp == 0) {
+      dst[D] = mls[g][0];
+      dst[D + 1] = mls[g][1];
+    }
+  }
+}
+
+// ---- decode attention, phase 2: merge chunks -> bf16 [B][1][H * D] ---------------------------
+template <int G, int D>
+__global__ __launch_bounds__(64) void attn_combine_kernel(const float* __restrict__ part,
+                                                          const int64_t* __restrict__ pos,
+                                                          uint16_t* __restrict__ out, int Hkv,
+                                                          int NC) {
+  const int bh = blockIdx.x;  // b * H + h
+  const int H = Hkv * G;
+  const int b = bh / H, h = bh % H, kvh = h / G, g = h % G;
+  const int L = (int)pos[0] + 1;
+  const int nc = (L + kChunk - 1) / kChunk < NC ? (L + kChunk - 1) / kChunk : NC;
+  const float* base = part + ((size_t)(b * Hkv + kvh) * NC * G + g) * (D + 2);
+  const size_t cstride = (size_t)G * (D + 2);
+  float M = -INFINITY;
+  for (int c = 0; c < nc; ++c) M = fmaxf(M, base[c * cstride + D]);
+  const int dp = threadIdx.x;
+  float o0 = 0.f, o1 = 0.f, l = 0.f;
+  for (int c = 0; c < nc; ++c) {
+    const float* pc = base + c * cstride;
+    const float wgt = __expf(pc[D] - M);
+    l = fmaf(pc[D + 1], wgt, l);
+    o0 = fmaf(pc[2 * dp], wgt, o0);
+    o1 = fmaf(pc[2 * dp + 1], wgt, o1);
+  }
+  const float inv = 1.f / l;
+  reinterpret_cast<uint32_t*>(out)[((size_t)b * H + h) * (D / 2) + dp] =
+      (uint32_t)f32_to_bf16(o0 * inv) | ((uint32_t)f32_to_bf16(o1 * inv) << 16);
+}
+
+// ---- SiLU(a) * b ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void silu_mul_kernel(const uint32_t* __restrict__ a,
+                                                       const uint32_t* __restrict__ b,
+                                                       uint32_t* __restrict__ y, int64_t n2) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n2; i += (int64_t)gridDim.x * 256) {
+    const uint32_t x = a[i], z = b[i];
+    auto f = [](float v, float m) {
+      const float s = round_bf16(v / (1.f + __expf(-v)));
+      return f32_to_bf16(s * m);
+    };
+    y[i] = (uint32_t)f(bf16lo_to_f32(x), bf16lo_to_f32(z)) |
+           ((uint32_t)f(bf16hi_to_f32(x), bf16hi_to_f32(z)) << 16);
+  }
+}
+
+}  // namespace
+}  // namespace tao
+
+using namespace tao;
+
+extern "C" {
+
+int tao_rmsnorm_bf16(const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t rows,
+                     int64_t dim, float eps, void* stream) {
+  TAO_CHECK_ARG(rows >= 0 && dim > 0 && dim % 8 == 0 && dim < (1 << 24),
+                "rmsnorm: dim (%lld) must be a positive multiple of 8", (long long)dim);
+  if (rows == 0) return TAO_OK;
+  TAO_CHECK_ALIGN(x, 16, "x");
+  TAO_CHECK_ALIGN(w, 16, "w");
+  TAO_CHECK_ALIGN(y, 16, "y");
+  launch(rmsnorm_kernel, dim3((unsigned)rows), dim3(256), 0, as_stream(stream), x, w, y,
+         (int)dim, eps);
+  return check_launch("rmsnorm_kernel");
+}
+
+int tao_rope_kv_bf16(const uint16_t* qkv, const float* freqs, const int64_t* pos,
+                     uint16_t* q_out, uint16_t* k_cache, uint16_t* v_cache, int64_t B, int64_t S,
+                     int64_t H, int64_t Hkv, int64_t D, int64_t T, void* stream) {
+  TAO_CHECK_ARG(B > 0 && S > 0 && H > 0 && Hkv > 0 && H % Hkv == 0 && D % 2 == 0 && T >= S,
+                "rope_kv: bad sizes");
+  TAO_CHECK_ALIGN(qkv, 4, "qkv");
+  launch(rope_kv_kernel, dim3((unsigned)(B * S)), dim3(256), 0, as_stream(stream), qkv, freqs,
+         pos, q_out, k_cache, v_cache, (int)S, (int)H, (int)Hkv, (int)D, (int)T);
+  return check_launch("rope_kv_kernel");
+}
+
+int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                         const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
+                         int64_t Hkv, int64_t D, int64_t T, float scale, void* stream) {
+  TAO_CHECK_ARG(D == 128, "attn_decode: head_dim must be 128 (got %lld)", (long long)D);
+  TAO_CHECK_ARG(B > 0 && Hkv > 0 && H % Hkv == 0 && T > 0, "attn_decode: bad sizes");
+  const int G = (int)(H / Hkv);
+  TAO_CHECK_ARG(G == 1 || G == 2 || G == 4 || G == 8, "attn_decode: H / Hkv must be 1, 2, 4 or 8");
+  TAO_CHECK_ALIGN(k_cache, 16, "k_cache");
+  const int NC = (int)((T + kChunk - 1) / kChunk);
+  hipStream_t st = as_stream(stream);
+  const dim3 g1((unsigned)(B * Hkv), (unsigned)NC), g2((unsigned)(B * H));
+  switch (G) {
+#define TAO_ATTN(GG)                                                                          \
+  case GG:                                                                                    \
+    launch(attn_partial_kernel<GG, 128>, g1, dim3(256), 0, st, q, k_cache, v_cache, pos,      \
+           partial, (int)Hkv, (int)T, scale);                                                 \
+    launch(attn_combine_kernel<GG, 128>, g2, dim3(64), 0, st, partial, pos, out, (int)Hkv, NC); \
+    break;
+    TAO_ATTN(1)
+    TAO_ATTN(2)
+    TAO_ATTN(4)
+    TAO_ATTN(8)
+#undef TAO_ATTN
+  }
+  return check_launch("attn_decode");
+}
+
+int tao_silu_mul_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t n,
+                      void* stream) {
+  TAO_CHECK_ARG(n >= 0 && n % 2 == 0, "silu_mul: n (%lld) must be even", (long long)n);
+  if (n == 0) return TAO_OK;
+  TAO_CHECK_ALIGN(a, 4, "a");
+  TAO_CHECK_ALIGN(b, 4, "b");
+  const int64_t n2 = n / 2;
+  int64_t grid = (n2 + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  launch(silu_mul_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream),
+         reinterpret_cast<const uint32_t*>(a), reinterpret_cast<const uint32_t*>(b),
+         reinterpret_cast<uint32_t*>(y), n2);
+  return check_launch("silu_mul_kernel");
+}
+
+}  // extern "C"

@@ -49,6 +49,11 @@ _SIGNATURES = {
     "tao_int8wo_linear_bf16": [_p, _p, _p, _p, _p, _i64, _i64, _i64, _p],
     "tao_int8_quant_per_token": [_p, _p, _p, _i64, _i64, _p],
     "tao_int8_scaled_mm_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p],
+    "tao_rmsnorm_bf16": [_p, _p, _p, _i64, _i64, ctypes.c_float, _p],
+    "tao_rope_kv_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p],
+    "tao_attn_decode_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
+                             ctypes.c_float, _p],
+    "tao_silu_mul_bf16": [_p, _p, _p, _i64, _p],
 }
 _RESTYPES = {"tao_version": ctypes.c_char_p, "tao_last_error": ctypes.c_char_p}
 

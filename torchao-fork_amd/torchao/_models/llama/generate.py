@@ -186,6 +186,8 @@ def main(argv=None):
     ap.add_argument("--num_samples", type=int, default=3)
     ap.add_argument("--batch_size", type=int, default=1)
     ap.add_argument("--no_graph", action="store_true", help="eager decode (no HIP graph)")
+    ap.add_argument("--no_fused", action="store_true",
+                    help="torch ops for norms / rope / attention / silu (no fused kernels)")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--write_result", type=Path, default=None)
@@ -205,6 +207,8 @@ def main(argv=None):
 
     B, P, T = args.batch_size, args.prompt_length, args.max_new_tokens
     model.setup_caches(B, P + T)
+    if not args.no_fused:
+        model.enable_fused_kernels()
     gen = torch.Generator(device="cpu").manual_seed(args.seed + 1)
     prompt = torch.randint(0, model.config.vocab_size, (B, P), generator=gen).to(device)
 
@@ -231,6 +235,7 @@ def main(argv=None):
         "prompt_length": P,
         "max_new_tokens": T,
         "hip_graph": decoder is not None,
+        "fused_decode_kernels": model.fused,
         "decode_tokens_per_s": round(dec_tok_s, 2),
         "decode_ms_per_token": round(t_dec / (T - 1) * 1e3, 3),
         "prefill_ms": round(t_pre * 1e3, 3),

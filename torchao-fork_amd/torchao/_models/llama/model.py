@@ -8,13 +8,18 @@ plain ``nn.Linear``: after ``quantize_(model, Int4WeightOnlyConfig(...))`` its f
 through the AQT F.linear dispatch to the gfx950 HIP kernels.
 
 Decode-time structure for one process per GPU and HIP graphs (no tracing compiler):
-  * static KV cache [B, H_kv, T, D] per layer, written with ``index_copy_`` at ``input_pos``
-    (a device tensor) and a causal mask row gathered by ``input_pos``, so a decode step is
-    graph-capturable and each replay advances by incrementing ``input_pos`` in place;
-  * grouped-query attention through ``F.scaled_dot_product_attention(enable_gqa=True)``;
+  * static KV cache [B, H_kv, T, D] per layer addressed by ``input_pos`` (a device tensor), so a
+    decode step is graph-capturable and each replay advances by incrementing it in place;
+  * ``enable_fused_kernels()`` (bf16, head_dim 128, GPU) switches one-token steps to the fused
+    gfx950 kernels of csrc/decode_ops.hip: RMSNorm, RoPE + KV-cache write, flash-decoding
+    attention, SiLU-mul, and the residual add folded into the wo / w2 linears as their bias
+    (bf16(x + bf16(W a)) is exactly the bias epilogue at M = 1) — ~11 launches per layer;
+  * otherwise (prefill, CPU): torch ops, ``index_copy_`` into the caches, a causal-mask row
+    gathered by ``input_pos``, ``F.scaled_dot_product_attention(enable_gqa=True)``;
   * rotary tables precomputed once (Llama-3.1 frequency scaling where configured).
 """
 
+import math
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -126,7 +131,8 @@ def _rope_freqs(cfg: ModelArgs, seq_len: int) -> torch.Tensor:
         lo_wl = old / sc["low_freq_factor"]
         hi_wl = old / sc["high_freq_factor"]
         wl = 2 * torch.pi / inv
-        smooth = (old / wl - sc["low_freq_factor"]) / (sc["high_freq_factor"] - sc["low_freq_factor"])
+        lo_f, hi_f = sc["low_freq_factor"], sc["high_freq_factor"]
+        smooth = (old / wl - lo_f) / (hi_f - lo_f)
         scaled = torch.where(wl > lo_wl, inv / sc["factor"], inv)
         mid = (wl <= lo_wl) & (wl >= hi_wl)
         inv = torch.where(mid, (1 - smooth) * inv / sc["factor"] + smooth * inv, scaled)
@@ -142,6 +148,13 @@ def _apply_rope(x: torch.Tensor, freqs: torch.Tensor) -> torch.Tensor:
     out = torch.stack([xs[..., 0] * f[..., 0] - xs[..., 1] * f[..., 1],
                        xs[..., 1] * f[..., 0] + xs[..., 0] * f[..., 1]], dim=-1)
     return out.flatten(3).type_as(x)
+
+
+def _linear_plus(x: torch.Tensor, lin: nn.Linear, residual: torch.Tensor) -> torch.Tensor:
+    """residual + lin(x); at one token the add rides on the linear's bias epilogue."""
+    if x.numel() == x.shape[-1]:
+        return F.linear(x, lin.weight, residual.reshape(-1))
+    return residual + lin(x)
 
 
 class Attention(nn.Module):
@@ -166,6 +179,16 @@ class Attention(nn.Module):
         y = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, enable_gqa=True)
         return self.wo(y.transpose(1, 2).reshape(B, S, q_sz))
 
+    def forward_fused(self, x, freqs_table, input_pos, residual):
+        from torchao._models.llama import kernels
+
+        kv = self.kv_cache
+        q = kernels.rope_kv(self.wqkv(x), freqs_table, input_pos, kv.k_cache, kv.v_cache,
+                            self.n_head)
+        y = kernels.attn_decode(q, kv.k_cache, kv.v_cache, input_pos,
+                                1.0 / math.sqrt(self.head_dim))
+        return _linear_plus(y, self.wo, residual)
+
 
 class FeedForward(nn.Module):
     def __init__(self, cfg: ModelArgs):
@@ -176,6 +199,11 @@ class FeedForward(nn.Module):
 
     def forward(self, x):
         return self.w2(F.silu(self.w1(x)) * self.w3(x))
+
+    def forward_fused(self, x, residual):
+        from torchao._models.llama import kernels
+
+        return _linear_plus(kernels.silu_mul(self.w1(x), self.w3(x)), self.w2, residual)
 
 
 class TransformerBlock(nn.Module):
@@ -190,6 +218,14 @@ class TransformerBlock(nn.Module):
         h = x + self.attention(self.attention_norm(x), freqs, mask, input_pos)
         return h + self.feed_forward(self.ffn_norm(h))
 
+    def forward_fused(self, x, freqs_table, input_pos):
+        from torchao._models.llama import kernels
+
+        a = kernels.rmsnorm(x, self.attention_norm.weight, self.attention_norm.eps)
+        h = self.attention.forward_fused(a, freqs_table, input_pos, x)
+        f = kernels.rmsnorm(h, self.ffn_norm.weight, self.ffn_norm.eps)
+        return self.feed_forward.forward_fused(f, h)
+
 
 class Transformer(nn.Module):
     def __init__(self, cfg: ModelArgs):
@@ -200,6 +236,7 @@ class Transformer(nn.Module):
         self.norm = RMSNorm(cfg.dim, cfg.norm_eps)
         self.output = nn.Linear(cfg.dim, cfg.vocab_size, bias=False)
         self.max_batch = self.max_seq = -1
+        self.fused = False
 
     @classmethod
     def from_name(cls, name: str) -> "Transformer":
@@ -221,9 +258,27 @@ class Transformer(nn.Module):
         mask = torch.tril(torch.ones(max_seq_length, max_seq_length, dtype=torch.bool, device=dev))
         self.register_buffer("causal_mask", mask, persistent=False)
 
+    def enable_fused_kernels(self, enable: bool = True) -> bool:
+        """Route one-token steps through the fused gfx950 decode kernels (bf16 activations,
+        head_dim 128, GPU). Returns whether they are on."""
+        cfg = self.config
+        ok = (self.norm.weight.is_cuda and self.norm.weight.dtype == torch.bfloat16
+              and cfg.head_dim == 128 and cfg.n_head % cfg.n_local_heads == 0
+              and cfg.n_head // cfg.n_local_heads in (1, 2, 4, 8) and cfg.dim % 8 == 0)
+        self.fused = bool(enable and ok)
+        return self.fused
+
     def forward(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
         """idx [B, S] token ids at positions input_pos [S] -> logits [B, S, vocab] (fp32)."""
         assert self.max_seq > 0, "call setup_caches() first"
+        if self.fused and idx.shape[1] == 1:
+            from torchao._models.llama import kernels
+
+            x = self.tok_embeddings(idx)
+            for blk in self.layers:
+                x = blk.forward_fused(x, self.freqs, input_pos)
+            x = kernels.rmsnorm(x, self.norm.weight, self.norm.eps)
+            return self.output(x).float()
         mask = self.causal_mask[None, None, input_pos]  # [1, 1, S, T]
         freqs = self.freqs[input_pos]
         x = self.tok_embeddings(idx)
