@@ -4,14 +4,14 @@
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 if [ "$1" = build ]; then
-  for v in 0 2 5; do
+  for v in 0 5 6; do
     make -s -C "$R/torchao-fork_amd/csrc" -j8 OBJDIR="$R/experiments/build/obj$v" \
       OUT="$R/experiments/build/libdbg$v.so" \
       CXXFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -munsafe-fp-atomics -DTAO_GEMM_DEBUG=$v"
   done
 else
   shift
-  for v in 0 2 5; do
+  for v in 0 5 6; do
     echo -n "variant $v: "
     TORCHAO_MI355X_LIB="$R/experiments/build/libdbg$v.so" timeout -k 10 120 python3 "$R/experiments/prof_gemm.py" "$@" | tail -1
   done

@@ -180,3 +180,33 @@ def test_fused_decode_matches_unfused_gpu(quant):
     dec.capture()
     graphed, _, _ = generate(model, prompt, T, dec)
     assert torch.equal(graphed, eager)
+
+
+def test_fuse_w13_is_exact_cpu():
+    model = build_model("stories15M", torch.device("cpu"), dtype=torch.float32, seed=4)
+    P = 6
+    model.setup_caches(1, P)
+    ids = torch.randint(0, model.config.vocab_size, (1, P))
+    ref = model(ids, torch.arange(P))
+    model.fuse_w13()
+    assert model.layers[0].feed_forward.w1 is None
+    model.setup_caches(1, P)
+    got = model(ids, torch.arange(P))
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_fuse_w13_int4_gpu():
+    dev = torch.device("cuda")
+    ref = _tiny(dev, seed=6)
+    model = _tiny(dev, seed=6).fuse_w13()
+    for m in (ref, model):
+        apply_quantization(m, "int4wo-32")
+        m.setup_caches(1, 16)
+        m.enable_fused_kernels()
+    prompt = torch.randint(0, 1000, (1, 8), device=dev)
+    pos = torch.arange(8, device=dev)
+    torch.testing.assert_close(model(prompt, pos), ref(prompt, pos), rtol=2e-2, atol=2e-2)
+    one = torch.tensor([8], device=dev)
+    a, b = model(prompt[:, -1:], one), ref(prompt[:, -1:], one)
+    assert (a - b).norm() / b.norm() < 1e-2

@@ -28,7 +28,8 @@
 
 // Experiment switch (experiments/gemm_debug.sh builds variants; 0 in the product):
 // 1 = no x global loads, 2 = no weight global loads, 3 = no x LDS traffic, 4 = no step barrier,
-// 5 = weights read as contiguous 1-KiB blocks per wave-instruction (wrong values, same bytes).
+// 5 = int4 weights read as contiguous 1-KiB blocks per wave-instruction (wrong values, same
+// bytes).
 #ifndef TAO_GEMM_DEBUG
 #define TAO_GEMM_DEBUG 0
 #endif
@@ -120,7 +121,9 @@ struct Int4WO {
     uint32_t w[4];
     float s, zc;
   };
-  __device__ __forceinline__ Lane setup(int n, int kq, int N, int K) const {
+  static constexpr int kStage = 0;  // no LDS staging of weights
+  __device__ __forceinline__ Lane setup(int bn, int lane, int N, int K) const {
+    const int n = bn < N ? bn : N - 1, kq = lane >> 4;
     Lane L;
     const uint32_t zrow = (uint32_t)(K >> 5 >> gshift);  // (scale, zero) dwords per row
     L.w = make_rsrc(wq, (uint32_t)N * (uint32_t)(K >> 1));
@@ -137,7 +140,7 @@ struct Int4WO {
     ch.szw = bload4<kNT>(L.z, L.zv, ((4 * st) >> gshift) * 4);
     return ch;
   }
-  __device__ __forceinline__ Prep prep(const Chunk& ch) const {
+  __device__ __forceinline__ Prep prep(const Chunk& ch, uint4*, int) const {
     Prep p;
     p.w[0] = ch.w.x;
     p.w[1] = ch.w.y;
@@ -180,28 +183,45 @@ struct Int8WO {
   typedef f32x4_t Acc;
   const uint4* w;         // [N][K/16]
   const uint16_t* scale;  // [N]
+  // Weights are loaded in full 128-B lines (8 rows x 128 B per wave instruction: lane l reads
+  // row 8 g + l / 8, bytes 16 (l % 8) of the step) and regrouped to the MFMA layout through a
+  // 2-KiB per-wave LDS stage ([16 rows][8 slots], slot XOR-swizzled by row): measured ~1.4x
+  // over 16 rows x 64 B per instruction on the streaming-bound shapes.
+  static constexpr int kStage = 128;  // uint4 per wave
   struct Lane {
     Rsrc w;
-    uint32_t wv;
+    uint32_t wv0, wv1;
   };
   struct Chunk {
     uint4 a, b;
   };
   typedef Chunk Prep;
-  __device__ __forceinline__ Lane setup(int n, int kq, int N, int K) const {
+  __device__ __forceinline__ Lane setup(int bn, int lane, int N, int K) const {
     Lane L;
     L.w = make_rsrc(w, (uint32_t)N * (uint32_t)K);
-    L.wv = (uint32_t)n * (uint32_t)K + kq * 16;
+    const int base = bn - (lane & 15);  // the wave's first row
+    const int r0 = base + (lane >> 3), r1 = r0 + 8;
+    L.wv0 = (uint32_t)(r0 < N ? r0 : N - 1) * (uint32_t)K + 16 * (lane & 7);
+    L.wv1 = (uint32_t)(r1 < N ? r1 : N - 1) * (uint32_t)K + 16 * (lane & 7);
     return L;
   }
-  // each load instruction covers 64 contiguous bytes of each of the wave's 16 rows
   __device__ __forceinline__ Chunk load(const Lane& L, int st) const {
     Chunk ch;
-    ch.a = bload16<kNT>(L.w, L.wv, st * 128);
-    ch.b = bload16<kNT>(L.w, L.wv + 64, st * 128);
+    ch.a = bload16<kNT>(L.w, L.wv0, st * 128);
+    ch.b = bload16<kNT>(L.w, L.wv1, st * 128);
     return ch;
   }
-  __device__ __forceinline__ Prep prep(const Chunk& ch) const { return ch; }
+  // stage: write the two full-line pieces, read back lane (n, kq)'s bytes 16 kq and 64 + 16 kq
+  __device__ __forceinline__ Prep prep(const Chunk& ch, uint4* stage, int lane) const {
+    const int r = lane >> 3, c = lane & 7;
+    stage[r * 8 + (c ^ r)] = ch.a;
+    stage[(r + 8) * 8 + (c ^ r)] = ch.b;
+    const int n = lane & 15, kq = lane >> 4;
+    Prep p;
+    p.a = stage[n * 8 + (kq ^ (n & 7))];
+    p.b = stage[n * 8 + ((4 + kq) ^ (n & 7))];
+    return p;
+  }
   // int8 -> bf16 is exact: (q ^ 0x80) is q + 128 as an unsigned byte (one v_cvt_f32_ubyteN),
   // minus 128 in fp32 (exact), packed.
   __device__ __forceinline__ bf16x8_t frag(const Prep& p, int s) const {
@@ -230,30 +250,50 @@ struct Int8Dyn {
   const uint4* w;           // [N][K/16]
   const uint16_t* wscale;   // [N]
   const uint16_t* xscale;   // [M]
+  // Full 128-B lines per wave instruction (lane l: row 8 g + l / 8, bytes 128 h + 16 (l % 8))
+  // regrouped to the MFMA layout through a 4-KiB per-wave LDS stage ([16 rows][16 slots],
+  // XOR-swizzled by row): 15.1 -> ~11 us at M=128, 4096^2 (experiments/gemm_debug.sh, 5/6).
+  static constexpr int kStage = 256;  // uint4 per wave
   struct Lane {
     Rsrc w;
-    uint32_t wv;
+    uint32_t wv0, wv1;
   };
   struct Chunk {
-    uint4 v[4];
+    uint4 v[4];  // (g, h) = (0,0), (1,0), (0,1), (1,1)
   };
-  typedef Chunk Prep;
-  __device__ __forceinline__ Lane setup(int n, int kq, int N, int K) const {
+  struct Prep {
+    uint4 v[4];  // MFMA s: bytes 64 s + 16 kq of row n
+  };
+  __device__ __forceinline__ Lane setup(int bn, int lane, int N, int K) const {
     Lane L;
     L.w = make_rsrc(w, (uint32_t)N * (uint32_t)K);
-    L.wv = (uint32_t)n * (uint32_t)K + kq * 16;
-    if (TAO_GEMM_DEBUG == 5) L.wv = (uint32_t)(n >> 4) * (uint32_t)K * 16 + ((n & 15) * 4 + kq) * 16;
+    const int base = bn - (lane & 15);
+    const int r0 = base + (lane >> 3), r1 = r0 + 8;
+    L.wv0 = (uint32_t)(r0 < N ? r0 : N - 1) * (uint32_t)K + 16 * (lane & 7);
+    L.wv1 = (uint32_t)(r1 < N ? r1 : N - 1) * (uint32_t)K + 16 * (lane & 7);
     return L;
   }
   __device__ __forceinline__ Chunk load(const Lane& L, int st) const {
     Chunk ch;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-      ch.v[s] = TAO_GEMM_DEBUG == 5 ? bload16<kNT>(L.w, L.wv + 1024 * s, st * 4096)
-                                    : bload16<kNT>(L.w, L.wv + 64 * s, st * 256);
+    ch.v[0] = bload16<kNT>(L.w, L.wv0, st * 256);
+    ch.v[1] = bload16<kNT>(L.w, L.wv1, st * 256);
+    ch.v[2] = bload16<kNT>(L.w, L.wv0 + 128, st * 256);
+    ch.v[3] = bload16<kNT>(L.w, L.wv1 + 128, st * 256);
     return ch;
   }
-  __device__ __forceinline__ Prep prep(const Chunk& ch) const { return ch; }
+  __device__ __forceinline__ Prep prep(const Chunk& ch, uint4* stage, int lane) const {
+    const int r = lane >> 3, c = lane & 7;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int row = r + 8 * (x & 1), slot = c + 8 * (x >> 1);
+      stage[row * 16 + (slot ^ row)] = ch.v[x];
+    }
+    const int n = lane & 15, kq = lane >> 4;
+    Prep p;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) p.v[s] = stage[n * 16 + ((4 * s + kq) ^ n)];
+    return p;
+  }
   __device__ __forceinline__ i32x4_t frag(const Prep& p, int s) const {
     return __builtin_bit_cast(i32x4_t, p.v[s]);
   }
@@ -308,7 +348,9 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
   constexpr int XLOADS = BM * 16 / 256;  // 16-B x pieces per thread per step
   constexpr int TILE = BM * 16;          // uint4 per x tile
   static_assert((KG - 1) * 4 * MT * 64 <= KG * 2 * TILE, "k-group reduction must fit in LDS");
-  __shared__ uint4 lds[KG * 2 * TILE];
+  // one LDS array (a second __shared__ object can de-pipeline the loop, cdna guide §5 item 4a):
+  // [KG][2][x tile] then the per-wave weight stages
+  __shared__ uint4 lds[KG * 2 * TILE + KG * 4 * P::kStage + (P::kStage == 0)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -326,9 +368,9 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
 
   const int bn = n_blk + wave * 16 + (lane & 15);
   const bool nok = bn < N;
-  const int bnc = nok ? bn : N - 1;
   const int kq = lane >> 4;
-  const typename P::Lane wl = pol.setup(bnc, kq, N, K);
+  const typename P::Lane wl = pol.setup(bn, lane, N, K);
+  uint4* wstage = lds + KG * 2 * TILE + (kg * 4 + wave) * P::kStage;
 
   // this thread's x pieces: rows row0 + 16 i (i < XLOADS), 16-B slot xslot of each; rows past
   // M are clamped to M - 1 (computed and dropped). A k tail past the row end reads the next
@@ -393,7 +435,7 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
     constexpr int u = decltype(uc)::value;
     load_step(j + D - 1, xr[(u + D - 1) % D], wr[(u + D - 1) % D]);
     if (abs_step(j) < s1) {  // uniform: a k-group's idle tail iterations skip the math
-      const typename P::Prep pw = pol.prep(wr[u]);
+      const typename P::Prep pw = pol.prep(wr[u], wstage, lane);
       const uint4* xb = xs + (j & 1) * TILE;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {

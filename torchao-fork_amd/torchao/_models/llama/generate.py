@@ -188,6 +188,8 @@ def main(argv=None):
     ap.add_argument("--no_graph", action="store_true", help="eager decode (no HIP graph)")
     ap.add_argument("--no_fused", action="store_true",
                     help="torch ops for norms / rope / attention / silu (no fused kernels)")
+    ap.add_argument("--no_fuse_w13", action="store_true",
+                    help="keep w1 and w3 as two linears (the reference module layout)")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--write_result", type=Path, default=None)
@@ -199,6 +201,8 @@ def main(argv=None):
                         seed=args.seed)
     torch.cuda.synchronize()
     t_build = time.perf_counter() - t
+    if not args.no_fuse_w13:
+        model.fuse_w13()
     t = time.perf_counter()
     apply_quantization(model, args.quantization)
     torch.cuda.synchronize()
@@ -236,6 +240,7 @@ def main(argv=None):
         "max_new_tokens": T,
         "hip_graph": decoder is not None,
         "fused_decode_kernels": model.fused,
+        "fused_w13": not args.no_fuse_w13,
         "decode_tokens_per_s": round(dec_tok_s, 2),
         "decode_ms_per_token": round(t_dec / (T - 1) * 1e3, 3),
         "prefill_ms": round(t_pre * 1e3, 3),

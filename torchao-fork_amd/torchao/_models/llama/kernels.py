@@ -63,7 +63,7 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
 def silu_mul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     _check(a, torch.bfloat16, "silu_mul a")
     _check(b, torch.bfloat16, "silu_mul b")
-    y = torch.empty_like(a)
+    y = torch.empty(a.shape, dtype=a.dtype, device=a.device)
     _lib.call("tao_silu_mul_bf16", a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(),
               _stream(a))
     return y

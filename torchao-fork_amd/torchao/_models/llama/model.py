@@ -196,14 +196,36 @@ class FeedForward(nn.Module):
         self.w1 = nn.Linear(cfg.dim, cfg.intermediate_size, bias=False)
         self.w3 = nn.Linear(cfg.dim, cfg.intermediate_size, bias=False)
         self.w2 = nn.Linear(cfg.intermediate_size, cfg.dim, bias=False)
+        self.w13: Optional[nn.Linear] = None
+
+    def fuse_w13(self):
+        """Merge w1 and w3 (same input) into one [2I, dim] linear: one weight stream and one
+        launch per token instead of two. Row-wise quantization makes quantizing the merged
+        weight identical to quantizing w1 and w3 apart, so fuse before or after loading."""
+        w = torch.cat([self.w1.weight.detach(), self.w3.weight.detach()], dim=0)
+        self.w13 = nn.Linear(w.shape[1], w.shape[0], bias=False, device="meta")
+        self.w13.weight = nn.Parameter(w, requires_grad=False)
+        del self.w1, self.w3
+        self.w1 = self.w3 = None
+
+    def _gate_up(self, x):
+        if self.w13 is None:
+            return self.w1(x), self.w3(x)
+        h = self.w13(x)
+        n = h.shape[-1] // 2
+        return h[..., :n], h[..., n:]
 
     def forward(self, x):
-        return self.w2(F.silu(self.w1(x)) * self.w3(x))
+        a, b = self._gate_up(x)
+        return self.w2(F.silu(a) * b)
 
     def forward_fused(self, x, residual):
         from torchao._models.llama import kernels
 
-        return _linear_plus(kernels.silu_mul(self.w1(x), self.w3(x)), self.w2, residual)
+        a, b = self._gate_up(x)
+        if x.numel() != x.shape[-1]:  # the kernel wants contiguous halves (one token)
+            a, b = a.contiguous(), b.contiguous()
+        return _linear_plus(kernels.silu_mul(a, b), self.w2, residual)
 
 
 class TransformerBlock(nn.Module):
@@ -257,6 +279,11 @@ class Transformer(nn.Module):
         self.register_buffer("freqs", _rope_freqs(cfg, cfg.block_size).to(dev), persistent=False)
         mask = torch.tril(torch.ones(max_seq_length, max_seq_length, dtype=torch.bool, device=dev))
         self.register_buffer("causal_mask", mask, persistent=False)
+
+    def fuse_w13(self) -> "Transformer":
+        for blk in self.layers:
+            blk.feed_forward.fuse_w13()
+        return self
 
     def enable_fused_kernels(self, enable: bool = True) -> bool:
         """Route one-token steps through the fused gfx950 decode kernels (bf16 activations,
