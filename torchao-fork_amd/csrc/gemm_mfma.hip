@@ -9,12 +9,11 @@
 // kernel/intmm.py:108-143).
 //
 // Tile: 4 waves x 16 output columns (BN = 64) x BM rows per k-group; each wave owns 16 columns
-// and all BM rows. K advances in macro-steps of 256 B of x per row (128 bf16 k or 256 int8 k).
-// k order inside a macro-step is permuted identically for A and B (policy slot(s, kq): the
-// 16-B x slot MFMA s of lane l = (n = l & 15, kq = l >> 4) reads). Every weight load
-// instruction covers 64 contiguous bytes of each of the wave's 16 rows, the 16-B pieces of one
-// lane feed the four MFMAs of the step, and an int4 lane (one 32-k chunk) needs one
-// (scale, zero) dword.
+// and all BM rows. K advances in macro-steps (256 bf16 k for int4, 128 bf16 k for int8-WO,
+// 256 int8 k for int8-dyn) in which every weight load instruction reads full 128-B lines
+// (8 rows x 128 B); a per-wave LDS stage regroups them into the MFMA B layout. The k order
+// inside a step is permuted identically for A and B (policy slot(s, kq): the 16-B x slot
+// MFMA s of lane l = (n = l & 15, kq = l >> 4) reads).
 // x goes global -> registers (D-deep prefetch ring, T14) -> double-buffered, XOR-swizzled LDS
 // image -> A fragments; one barrier per step. W goes straight to registers (read once per
 // tile, dequantised in registers, reused for BM/16 MFMAs). K is split across k-groups inside
@@ -27,9 +26,7 @@
 #include "tao_common.h"
 
 // Experiment switch (experiments/gemm_debug.sh builds variants; 0 in the product):
-// 1 = no x global loads, 2 = no weight global loads, 3 = no x LDS traffic, 4 = no step barrier,
-// 5 = int4 weights read as contiguous 1-KiB blocks per wave-instruction (wrong values, same
-// bytes).
+// 1 = no x global loads, 2 = no weight global loads, 3 = no x LDS traffic, 4 = no step barrier.
 #ifndef TAO_GEMM_DEBUG
 #define TAO_GEMM_DEBUG 0
 #endif
@@ -103,73 +100,101 @@ __device__ __forceinline__ uint32_t bload4(Rsrc r, uint32_t voff, uint32_t soff)
 // columns past N (clamped to row N - 1) are computed and dropped, and a K tail reads the next
 // row's finite weights against x that the LDS store zeroes. prep()/frag(): B fragments.
 struct Int4WO {
-  static constexpr int kABytes = 2;  // bf16 x
-  static constexpr int kKStep = 128;
+  static constexpr int kABytes = 2;   // bf16 x
+  static constexpr int kKStep = 256;  // 128 B of nibbles per row per step: one full line
+  static constexpr int kMfma = 8;
+  static constexpr int kMaxBM = 64;  // 512-B x rows: BM 128 would need 64 x VGPRs per stage
+  // Weights in full 128-B lines (8 rows x 128 B per wave instruction: lane l reads row
+  // 8 g + l / 8, 16-B chunk l % 8 of the step) regrouped to the MFMA layout through a 2-KiB
+  // per-wave LDS stage ([16 rows][8 chunks], XOR-swizzled by row); lane (n, kq) then holds
+  // chunks kq and 4 + kq (32 k each, one (scale, zero) dword each).
+  static constexpr int kStage = 128;  // uint4 per wave
   typedef f32x4_t Acc;
   const uint4* wq;     // [N][K/32] 16-B chunks
   const uint32_t* sz;  // [N][K/g] (scale, zero)
   int gshift;          // log2(g / 32)
   struct Lane {
     Rsrc w, z;
-    uint32_t wv, zv;
+    uint32_t wv0, wv1, zv0, zv1;
   };
   struct Chunk {
-    uint4 w;
-    uint32_t szw;
+    uint4 a, b;
+    uint32_t sz0, sz1;
   };
   struct Prep {
-    uint32_t w[4];
-    float s, zc;
+    uint32_t w[8];  // dwords of chunks kq (0..3) and 4 + kq (4..7)
+    float s0, zc0, s1, zc1;
   };
-  static constexpr int kStage = 0;  // no LDS staging of weights
   __device__ __forceinline__ Lane setup(int bn, int lane, int N, int K) const {
     const int n = bn < N ? bn : N - 1, kq = lane >> 4;
     Lane L;
     const uint32_t zrow = (uint32_t)(K >> 5 >> gshift);  // (scale, zero) dwords per row
     L.w = make_rsrc(wq, (uint32_t)N * (uint32_t)(K >> 1));
     L.z = make_rsrc(sz, (uint32_t)N * zrow * 4u);
-    L.wv = (uint32_t)n * (uint32_t)(K >> 1) + kq * 16;
-    if (TAO_GEMM_DEBUG == 5) L.wv = (uint32_t)(n >> 4) * (uint32_t)(K >> 1) * 16 + ((n & 15) * 4 + kq) * 16;
-    // chunk 4 st + kq -> group (4 st + kq) >> gshift == ((4 st) >> gshift) + (kq >> gshift)
-    L.zv = ((uint32_t)n * zrow + (kq >> gshift)) * 4;
+    const int base = bn - (lane & 15);
+    const int r0 = base + (lane >> 3), r1 = r0 + 8;
+    L.wv0 = (uint32_t)(r0 < N ? r0 : N - 1) * (uint32_t)(K >> 1) + 16 * (lane & 7);
+    L.wv1 = (uint32_t)(r1 < N ? r1 : N - 1) * (uint32_t)(K >> 1) + 16 * (lane & 7);
+    // chunk 8 st + c -> group ((8 st) >> gshift) + (c >> gshift) (c < 8, gshift <= 3)
+    L.zv0 = ((uint32_t)n * zrow + (kq >> gshift)) * 4;
+    L.zv1 = ((uint32_t)n * zrow + ((4 + kq) >> gshift)) * 4;
     return L;
   }
   __device__ __forceinline__ Chunk load(const Lane& L, int st) const {
     Chunk ch;
-    ch.w = bload16<kNT>(L.w, L.wv, st * (TAO_GEMM_DEBUG == 5 ? 1024 : 64));
-    ch.szw = bload4<kNT>(L.z, L.zv, ((4 * st) >> gshift) * 4);
+    ch.a = bload16<kNT>(L.w, L.wv0, st * 128);
+    ch.b = bload16<kNT>(L.w, L.wv1, st * 128);
+    const uint32_t zo = ((8 * st) >> gshift) * 4;
+    ch.sz0 = bload4<kNT>(L.z, L.zv0, zo);
+    ch.sz1 = bload4<kNT>(L.z, L.zv1, zo);
     return ch;
   }
-  __device__ __forceinline__ Prep prep(const Chunk& ch, uint4*, int) const {
+  __device__ __forceinline__ Prep prep(const Chunk& ch, uint4* stage, int lane) const {
+    const int r = lane >> 3, c = lane & 7;
+    stage[r * 8 + (c ^ r)] = ch.a;
+    stage[(r + 8) * 8 + (c ^ r)] = ch.b;
+    const int n = lane & 15, kq = lane >> 4;
+    const uint4 p0 = stage[n * 8 + (kq ^ (n & 7))];
+    const uint4 p1 = stage[n * 8 + ((4 + kq) ^ (n & 7))];
     Prep p;
-    p.w[0] = ch.w.x;
-    p.w[1] = ch.w.y;
-    p.w[2] = ch.w.z;
-    p.w[3] = ch.w.w;
-    p.s = bf16lo_to_f32(ch.szw);
-    p.zc = bf16hi_to_f32(ch.szw) - 8.f * p.s;  // q*s + zc == (q-8)*s + z
+    p.w[0] = p0.x;
+    p.w[1] = p0.y;
+    p.w[2] = p0.z;
+    p.w[3] = p0.w;
+    p.w[4] = p1.x;
+    p.w[5] = p1.y;
+    p.w[6] = p1.z;
+    p.w[7] = p1.w;
+    p.s0 = bf16lo_to_f32(ch.sz0);
+    p.zc0 = bf16hi_to_f32(ch.sz0) - 8.f * p.s0;  // q*s + zc == (q-8)*s + z
+    p.s1 = bf16lo_to_f32(ch.sz1);
+    p.zc1 = bf16hi_to_f32(ch.sz1) - 8.f * p.s1;
     return p;
   }
-  // B fragment of MFMA s: bf16(fma(q, s, z - 8 s)) for the 8 nibbles of dword s. Row-stream
-  // nibble order (bits 4i: q[2i], bits 16+4i: q[2i+1]) puts q0,q4,q1,q5 in the bytes of
-  // w & 0x0F0F0F0F and q2,q6,q3,q7 in those of (w >> 4) & 0x0F0F0F0F. A byte b < 16 read as
-  // OCP e4m3 is exactly b / 512 (subnormals for b < 8, exponent 1 above), so one
-  // v_cvt_scalef32_pk_f32_fp8 with scale 512 turns two of them into exact fp32 integers; then
-  // one v_pk_fma_f32 and one v_cvt_pk_bf16_f32 per pair: ~1.9 VALU per weight.
+  // B fragment of MFMA s (chunk s >> 2, dword s & 3): bf16(fma(q, s, z - 8 s)) for its 8
+  // nibbles. Row-stream nibble order (bits 4i: q[2i], bits 16+4i: q[2i+1]) puts q0,q4,q1,q5
+  // in the bytes of w & 0x0F0F0F0F and q2,q6,q3,q7 in those of (w >> 4) & 0x0F0F0F0F. A byte
+  // b < 16 read as OCP e4m3 is exactly b / 512 (subnormals for b < 8, exponent 1 above), so
+  // one v_cvt_scalef32_pk_f32_fp8 with scale 512 turns two of them into exact fp32 integers;
+  // then one v_pk_fma_f32 and one v_cvt_pk_bf16_f32 per pair: ~1.9 VALU per weight.
   __device__ __forceinline__ bf16x8_t frag(const Prep& p, int s) const {
-    const uint32_t lo = p.w[s] & 0x0F0F0F0Fu, hi = (p.w[s] >> 4) & 0x0F0F0F0Fu;
+    const uint32_t w = p.w[s];
+    const float sc = s < 4 ? p.s0 : p.s1, zc = s < 4 ? p.zc0 : p.zc1;
+    const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
     const f32x2_t q04 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(lo, 512.f, false);
     const f32x2_t q15 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(lo, 512.f, true);
     const f32x2_t q26 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, false);
     const f32x2_t q37 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, true);
-    const f32x2_t sv = {p.s, p.s}, zv = {p.zc, p.zc};
+    const f32x2_t sv = {sc, sc}, zv = {zc, zc};
     const f32x2_t w04 = q04 * sv + zv, w15 = q15 * sv + zv;  // v_pk_fma_f32 (contracted)
     const f32x2_t w26 = q26 * sv + zv, w37 = q37 * sv + zv;
     return as_bf16x8(pack_bf16x2(w04[0], w15[0]), pack_bf16x2(w26[0], w37[0]),
                      pack_bf16x2(w04[1], w15[1]), pack_bf16x2(w26[1], w37[1]));
   }
-  // lane (n, kq) holds chunk kq (32 k); MFMA s takes its dword s = 16-B x slot 4 kq + s
-  static __device__ __forceinline__ int slot(int s, int kq) { return kq * 4 + s; }
+  // MFMA s = 4 h + t takes dword t of chunk 4 h + kq: x slot 4 (4 h + kq) + t
+  static __device__ __forceinline__ int slot(int s, int kq) {
+    return 16 * (s >> 2) + 4 * kq + (s & 3);
+  }
   static __device__ __forceinline__ Acc mfma(const uint4& a, const bf16x8_t& b, Acc c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), b, c, 0, 0, 0);
   }
@@ -180,6 +205,8 @@ struct Int4WO {
 struct Int8WO {
   static constexpr int kABytes = 2;
   static constexpr int kKStep = 128;
+  static constexpr int kMfma = 4;
+  static constexpr int kMaxBM = 128;
   typedef f32x4_t Acc;
   const uint4* w;         // [N][K/16]
   const uint16_t* scale;  // [N]
@@ -246,6 +273,8 @@ struct Int8WO {
 struct Int8Dyn {
   static constexpr int kABytes = 1;  // int8 x
   static constexpr int kKStep = 256;
+  static constexpr int kMfma = 4;
+  static constexpr int kMaxBM = 128;
   typedef i32x4_t Acc;
   const uint4* w;           // [N][K/16]
   const uint16_t* wscale;   // [N]
@@ -312,7 +341,10 @@ struct Int8Dyn {
 
 // LDS image of one x tile: [BM rows][16 slots of 16 B], slot XOR-swizzled with row & 15 so the
 // 16 rows of an A fragment read spread over all banks (cdna guide §5.5 T2).
-__device__ __forceinline__ int lds_slot(int row, int slot) { return row * 16 + (slot ^ (row & 15)); }
+template <int SLOTS>
+__device__ __forceinline__ int lds_slot(int row, int slot) {
+  return row * SLOTS + (slot ^ (row & 15));
+}
 
 template <int I, int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -345,8 +377,11 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
     unsigned* __restrict__ cnt) {
   typedef typename P::Acc Acc;
   constexpr int MT = BM / 16;
-  constexpr int XLOADS = BM * 16 / 256;  // 16-B x pieces per thread per step
-  constexpr int TILE = BM * 16;          // uint4 per x tile
+  constexpr int XSB = P::kABytes * P::kKStep;  // x bytes per row per step (256 or 512)
+  constexpr int SLOTS = XSB / 16;               // 16-B x slots per row per step
+  constexpr int RPP = 256 / SLOTS;              // x rows loaded per 256-thread pass
+  constexpr int XLOADS = BM * SLOTS / 256;      // 16-B x pieces per thread per step
+  constexpr int TILE = BM * SLOTS;              // uint4 per x tile
   static_assert((KG - 1) * 4 * MT * 64 <= KG * 2 * TILE, "k-group reduction must fit in LDS");
   // one LDS array (a second __shared__ object can de-pipeline the loop, cdna guide §5 item 4a):
   // [KG][2][x tile] then the per-wave weight stages
@@ -372,20 +407,21 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
   const typename P::Lane wl = pol.setup(bn, lane, N, K);
   uint4* wstage = lds + KG * 2 * TILE + (kg * 4 + wave) * P::kStage;
 
-  // this thread's x pieces: rows row0 + 16 i (i < XLOADS), 16-B slot xslot of each; rows past
-  // M are clamped to M - 1 (computed and dropped). A k tail past the row end reads the next
-  // row (or 0 past the buffer) and is masked at the LDS store.
-  const int row0 = ktid >> 4, xslot = ktid & 15;
+  // this thread's x pieces: rows row0 + RPP i (i < XLOADS), 16-B slot xslot of each; rows
+  // past M are clamped to M - 1 (computed and dropped). A k tail past the row end reads the
+  // next row (or 0 past the buffer) and is masked at the LDS store.
+  const int row0 = ktid / SLOTS, xslot = ktid % SLOTS;
   const int xslot_b = xslot * 16;
-  const int xlds0 = lds_slot(row0, xslot);  // + 256 i: (row0 + 16 i) & 15 == row0 & 15
   const Rsrc xrs = make_rsrc(x, (uint32_t)M * (uint32_t)row_bytes);
   uint32_t xv[XLOADS];
+  int xlds[XLOADS];
 #pragma unroll
   for (int i = 0; i < XLOADS; ++i) {
-    const int gm = m_blk + row0 + 16 * i;
+    const int gm = m_blk + row0 + RPP * i;
     xv[i] = (uint32_t)(gm < M ? gm : M - 1) * (uint32_t)row_bytes + xslot_b;
+    xlds[i] = lds_slot<SLOTS>(row0 + RPP * i, xslot);
   }
-  const bool ragged = (row_bytes & 255) != 0;
+  const bool ragged = (row_bytes % XSB) != 0;
 
   Acc acc[MT];
 #pragma unroll
@@ -402,7 +438,7 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
     const int st = st0 < s1 ? st0 : s1 - 1;
     if (TAO_GEMM_DEBUG != 1) {
 #pragma unroll
-      for (int i = 0; i < XLOADS; ++i) xdst[i] = bload16(xrs, xv[i], st * 256);
+      for (int i = 0; i < XLOADS; ++i) xdst[i] = bload16(xrs, xv[i], st * XSB);
     } else {
 #pragma unroll
       for (int i = 0; i < XLOADS; ++i) xdst[i] = make_uint4(st, i, 0x3c003c00u, 0);
@@ -420,13 +456,13 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
     if (TAO_GEMM_DEBUG == 3) return;
     if (!ragged && st < s1) {
 #pragma unroll
-      for (int i = 0; i < XLOADS; ++i) dst[xlds0 + 256 * i] = src[i];
+      for (int i = 0; i < XLOADS; ++i) dst[xlds[i]] = src[i];
     } else {
       // k tail / inactive step -> 0 (an AND mask: a select here compiles to a branch)
-      const uint32_t keep = st < s1 && st * 256 + xslot_b < row_bytes ? ~0u : 0u;
+      const uint32_t keep = st < s1 && st * XSB + xslot_b < row_bytes ? ~0u : 0u;
 #pragma unroll
       for (int i = 0; i < XLOADS; ++i)
-        dst[xlds0 + 256 * i] =
+        dst[xlds[i]] =
             make_uint4(src[i].x & keep, src[i].y & keep, src[i].z & keep, src[i].w & keep);
     }
   };
@@ -438,13 +474,13 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
       const typename P::Prep pw = pol.prep(wr[u], wstage, lane);
       const uint4* xb = xs + (j & 1) * TILE;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
+      for (int s = 0; s < P::kMfma; ++s) {
         const auto bfrag = pol.frag(pw, s);
         const int slot = P::slot(s, kq);
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
           const int row = t * 16 + (lane & 15);
-          const uint4 a = TAO_GEMM_DEBUG == 3 ? xr[u][0] : xb[lds_slot(row, slot)];
+          const uint4 a = TAO_GEMM_DEBUG == 3 ? xr[u][0] : xb[lds_slot<SLOTS>(row, slot)];
           acc[t] = P::mfma(a, bfrag, acc[t]);
         }
       }
@@ -561,8 +597,8 @@ struct GemmShape {
 };
 std::atomic<int> g_tune_bm{0}, g_tune_kg{0}, g_tune_splits{0};
 
-GemmShape choose_shape(int M, int N, int nsteps) {
-  // From experiments/sweep_gemm.py (profiles/r1_sweep_gemm.jsonl): the largest M tile that
+GemmShape choose_shape(int M, int N, int nsteps, int max_bm, int xsb) {
+  // From experiments/sweep_gemm.py (profiles/r1_sweep_gemm*.jsonl): the largest M tile that
   // still gives >= 224 tiles (~0.9 x 256 CUs) without padding M 2x, else 16; split-K only to
   // lift a small tile count towards 256 (its slab hand-off costs microseconds), and two
   // k-groups per workgroup when the grid is at most one round.
@@ -570,7 +606,7 @@ GemmShape choose_shape(int M, int N, int nsteps) {
   GemmShape sh{16, 1, 1};
   const int cands[3] = {128, 64, 32};
   for (int bm : cands)
-    if (bm < 2 * M && nb * ((M + bm - 1) / bm) >= 224) {
+    if (bm <= max_bm && bm < 2 * M && nb * ((M + bm - 1) / bm) >= 224) {
       sh.bm = bm;
       break;
     }
@@ -582,11 +618,11 @@ GemmShape choose_shape(int M, int N, int nsteps) {
   const int tb = g_tune_bm.load(std::memory_order_relaxed);
   const int tk = g_tune_kg.load(std::memory_order_relaxed);
   const int ts = g_tune_splits.load(std::memory_order_relaxed);
-  if (tb) sh.bm = tb;
+  if (tb) sh.bm = tb < max_bm ? tb : max_bm;
   if (tk) sh.kg = tk;
   if (ts) sh.splits = ts < nsteps ? ts : nsteps;
-  // LDS: KG x 2 x BM x 256 B <= 64 KiB
-  while (sh.kg > 1 && sh.kg * sh.bm > 128) sh.kg >>= 1;
+  // LDS: KG x 2 x BM x xsb (double-buffered x tiles) <= 64 KiB
+  while (sh.kg > 1 && sh.kg * sh.bm * xsb > 32768) sh.kg >>= 1;
   return sh;
 }
 
@@ -594,17 +630,21 @@ template <int BM, int KG, class P>
 void launch_one(dim3 grid, hipStream_t stream, const uint8_t* xb, const P& pol,
                 const uint16_t* bias, uint16_t* y, int M, int N, int K, int sps,
                 typename P::Acc* slab, unsigned* cnt) {
-  // ring depth: 4 steps, 3 where int8-dyn's 64-B weight pieces would spill at 16 waves / CU
-  constexpr int D = BM <= 16 ? 4 : (BM <= 32 ? (sizeof(typename P::Chunk) > 32 ? 3 : 4) : 2);
-  launch((gemm_mfma_kernel<BM, D, KG, P>), grid, dim3(256 * KG), 0, stream, xb, pol, bias, y, M,
-         N, K, sps, slab, cnt);
+  if constexpr (BM <= P::kMaxBM) {
+    // ring depth: 4 steps, 3 where the per-stage registers grow (int8-dyn's 64-B pieces,
+    // int4's 512-B x rows), 2 at BM >= 64
+    constexpr bool big = sizeof(typename P::Chunk) > 32 || P::kABytes * P::kKStep > 256;
+    constexpr int D = BM <= 16 ? 4 : (BM <= 32 ? (big ? 3 : 4) : 2);
+    launch((gemm_mfma_kernel<BM, D, KG, P>), grid, dim3(256 * KG), 0, stream, xb, pol, bias, y,
+           M, N, K, sps, slab, cnt);
+  }
 }
 
 template <class P>
 int launch_gemm(const void* x, const P& pol, const uint16_t* bias, uint16_t* y, int M, int N,
                 int K, hipStream_t stream) {
   const int nsteps = (K + P::kKStep - 1) / P::kKStep;
-  GemmShape sh = choose_shape(M, N, nsteps);
+  GemmShape sh = choose_shape(M, N, nsteps, P::kMaxBM, P::kABytes * P::kKStep);
   const int sps = (nsteps + sh.splits - 1) / sh.splits;
   const int S = (nsteps + sps - 1) / sps;  // no empty slice
   dim3 grid((N + kBN - 1) / kBN, (M + sh.bm - 1) / sh.bm, S);
