@@ -104,6 +104,8 @@ struct Int4WO {
   static constexpr int kKStep = 256;  // 128 B of nibbles per row per step: one full line
   static constexpr int kMfma = 8;
   static constexpr int kMaxBM = 64;  // 512-B x rows: BM 128 would need 64 x VGPRs per stage
+  static constexpr int kPrefKG = 2;
+  static constexpr int kMinSlice = 8;  // steps per split-K slice
   // Weights in full 128-B lines (8 rows x 128 B per wave instruction: lane l reads row
   // 8 g + l / 8, 16-B chunk l % 8 of the step) regrouped to the MFMA layout through a 2-KiB
   // per-wave LDS stage ([16 rows][8 chunks], XOR-swizzled by row); lane (n, kq) then holds
@@ -207,6 +209,8 @@ struct Int8WO {
   static constexpr int kKStep = 128;
   static constexpr int kMfma = 4;
   static constexpr int kMaxBM = 128;
+  static constexpr int kPrefKG = 2;
+  static constexpr int kMinSlice = 14;
   typedef f32x4_t Acc;
   const uint4* w;         // [N][K/16]
   const uint16_t* scale;  // [N]
@@ -275,6 +279,8 @@ struct Int8Dyn {
   static constexpr int kKStep = 256;
   static constexpr int kMfma = 4;
   static constexpr int kMaxBM = 128;
+  static constexpr int kPrefKG = 1;
+  static constexpr int kMinSlice = 14;
   typedef i32x4_t Acc;
   const uint4* w;           // [N][K/16]
   const uint16_t* wscale;   // [N]
@@ -597,24 +603,45 @@ struct GemmShape {
 };
 std::atomic<int> g_tune_bm{0}, g_tune_kg{0}, g_tune_splits{0};
 
-GemmShape choose_shape(int M, int N, int nsteps, int max_bm, int xsb) {
-  // From experiments/sweep_gemm.py (profiles/r1_sweep_gemm*.jsonl): the largest M tile that
-  // still gives >= 224 tiles (~0.9 x 256 CUs) without padding M 2x, else 16; split-K only to
-  // lift a small tile count towards 256 (its slab hand-off costs microseconds), and two
-  // k-groups per workgroup when the grid is at most one round.
+GemmShape choose_shape(int M, int N, int nsteps, int max_bm, int xsb, int pref_kg,
+                       int min_slice) {
+  // From the full sweep (experiments/sweep_gemm.py, profiles/r1_sweep_gemm_full*.jsonl):
+  //  * the largest M tile (no 2x padding of M) that gives ~one round of workgroups
+  //    (>= 224 tiles of 256 CUs) unsplit; 128 gives way to 64 while that still fits in two
+  //    rounds (<= 512 tiles);
+  //  * only when even 16-row tiles are too few: split-K with the largest tile that reaches
+  //    the round, <= 256 workgroups and >= min_slice steps per slice (the slab hand-off costs
+  //    microseconds);
+  //  * the policy's preferred k-groups (int4 / int8-WO 2, int8-dyn 1).
   const long nb = (N + kBN - 1) / kBN;
-  GemmShape sh{16, 1, 1};
-  const int cands[3] = {128, 64, 32};
-  for (int bm : cands)
-    if (bm <= max_bm && bm < 2 * M && nb * ((M + bm - 1) / bm) >= 224) {
+  auto tiles_of = [&](int bm) { return nb * ((M + bm - 1) / bm); };
+  auto splits_of = [&](long tiles) {
+    int s = 1;
+    while (tiles * s * 2 <= 256 && s * 2 <= 8 && nsteps >= min_slice * s * 2) s *= 2;
+    return s;
+  };
+  GemmShape sh{16, pref_kg, 1};
+  const int cands[4] = {128, 64, 32, 16};
+  bool found = false;
+  for (int bm : cands)  // first choice: no split
+    if (bm <= max_bm && (bm < 2 * M || bm == 16) && tiles_of(bm) >= 224) {
       sh.bm = bm;
+      found = true;
       break;
     }
-  const long tiles = nb * ((M + sh.bm - 1) / sh.bm);
-  int s = 1;
-  while (tiles * s * 2 <= 256 && s * 2 <= 8 && nsteps >= 8 * s) s *= 2;
-  sh.splits = s;
-  sh.kg = (s == 1 && sh.bm <= 64 && tiles <= 256) ? 2 : 1;
+  if (found && sh.bm == 128 && tiles_of(64) <= 512) sh.bm = 64;
+  if (!found) {  // too few tiles even at 16 rows: split K, with the largest tile that fills
+    sh.splits = splits_of(tiles_of(16));
+    for (int bm : cands) {
+      if (bm > max_bm || (bm >= 2 * M && bm != 16)) continue;
+      const int sp = splits_of(tiles_of(bm));
+      if (tiles_of(bm) * sp >= 224) {
+        sh.bm = bm;
+        sh.splits = sp;
+        break;
+      }
+    }
+  }
   const int tb = g_tune_bm.load(std::memory_order_relaxed);
   const int tk = g_tune_kg.load(std::memory_order_relaxed);
   const int ts = g_tune_splits.load(std::memory_order_relaxed);
@@ -644,7 +671,8 @@ template <class P>
 int launch_gemm(const void* x, const P& pol, const uint16_t* bias, uint16_t* y, int M, int N,
                 int K, hipStream_t stream) {
   const int nsteps = (K + P::kKStep - 1) / P::kKStep;
-  GemmShape sh = choose_shape(M, N, nsteps, P::kMaxBM, P::kABytes * P::kKStep);
+  GemmShape sh = choose_shape(M, N, nsteps, P::kMaxBM, P::kABytes * P::kKStep, P::kPrefKG,
+                              P::kMinSlice);
   const int sps = (nsteps + sh.splits - 1) / sh.splits;
   const int S = (nsteps + sps - 1) / sps;  // no empty slice
   dim3 grid((N + kBN - 1) / kBN, (M + sh.bm - 1) / sh.bm, S);
