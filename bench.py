@@ -2,12 +2,15 @@
 """Benchmark: int4 group-32 weight-only linear GB/s + tokens/s, Llama-3-8B shapes, M = 1 decode.
 
 One "step" = one decoded token through every int4 linear of a Llama-3-8B-shaped stack
-(32 layers x {wqkv 6144x4096, wo 4096x4096, w1 14336x4096, w3 14336x4096, w2 4096x14336}
-+ output 128256x4096): 161 launches of the gfx950 int4 GEMV, 4.70 GB of packed weights and
-scales per token (> 256 MiB Infinity Cache, so every byte comes from HBM). Weights are
-random-init nn.Linear-distributed bf16, quantized with the Int4WeightOnlyConfig(group_size=32)
-math and packed by the HIP pack kernel; activations are synthetic N(0,1) bf16; everything is
-resident in HBM before timing. The step is captured once in a HIP graph and replayed.
+(32 layers x {wqkv 6144x4096, wo 4096x4096, w1||w3 28672x4096, w2 4096x14336} + output
+128256x4096): 129 launches of the gfx950 int4 GEMV, 4.70 GB of packed weights and scales per
+token (> 256 MiB Infinity Cache, so every byte comes from HBM). The gate and up projections
+share their input and run as one merged linear, as the e2e harness runs them; --no-fuse-w13
+gives the reference's module layout (w1 and w3 apart, 161 launches, the same bytes).
+Weights are random-init nn.Linear-distributed bf16, quantized with the
+Int4WeightOnlyConfig(group_size=32) math and packed by the HIP pack kernel; activations are
+synthetic N(0,1) bf16; everything is resident in HBM before timing. The step is captured once
+in a HIP graph and replayed.
 
 N GPUs (torchrun, one rank per GPU): every linear is column-sharded (rank r owns output rows
 [r N/P, (r+1) N/P)) and its output is all-gathered over RCCL after each GEMV (north star,
@@ -19,7 +22,7 @@ Reported (one JSON line, rank 0):
   tokens_per_s = steps / wall time
   roofline     = the GEMV kernel: algorithmic bytes per step / GPU time per step of the
                  GEMV-only graph replayed back to back (HIP events on the replay stream, i.e. the
-                 sum of the 161 kernels' durations in the timed regime), against the MI355X
+                 sum of the step's kernel durations in the timed regime), against the MI355X
                  HBM3E peak of 8 TB/s; per_shape = one eager step timed per kernel by events the
                  dispatch packets write (tao_profile_*); traffic = HBM bytes per step from the
                  committed rocprofv3 FETCH_SIZE pass (profiles/, gfx950 x2 correction)
@@ -47,19 +50,26 @@ LLAMA3_8B = dict(dim=4096, n_layer=32, n_head=32, n_kv_head=8, head_dim=128,
                  intermediate=14336, vocab=128256)
 
 
-def llama_linears(cfg):
-    """(name, N, K) of every nn.Linear quantize_ touches in gpt-fast's Llama (model.py)."""
-    d, hd = cfg["dim"], cfg["head_dim"]
+def llama_linears(cfg, fuse_w13=True):
+    """(name, N, K) of every nn.Linear quantize_ touches in gpt-fast's Llama (model.py); with
+    fuse_w13 the gate and up projections (same input) are one [2I, dim] linear, as the e2e
+    harness runs them (torchao/_models/llama/model.py FeedForward.fuse_w13)."""
+    d, hd, inter = cfg["dim"], cfg["head_dim"], cfg["intermediate"]
     qkv = (cfg["n_head"] + 2 * cfg["n_kv_head"]) * hd
     out = []
     for layer in range(cfg["n_layer"]):
         out += [
             (f"layers.{layer}.attention.wqkv", qkv, d),
             (f"layers.{layer}.attention.wo", d, d),
-            (f"layers.{layer}.feed_forward.w1", cfg["intermediate"], d),
-            (f"layers.{layer}.feed_forward.w3", cfg["intermediate"], d),
-            (f"layers.{layer}.feed_forward.w2", d, cfg["intermediate"]),
         ]
+        if fuse_w13:
+            out.append((f"layers.{layer}.feed_forward.w13", 2 * inter, d))
+        else:
+            out += [
+                (f"layers.{layer}.feed_forward.w1", inter, d),
+                (f"layers.{layer}.feed_forward.w3", inter, d),
+            ]
+        out.append((f"layers.{layer}.feed_forward.w2", d, inter))
     out.append(("output", cfg["vocab"], d))
     return out
 
@@ -150,6 +160,8 @@ def main():
     ap.add_argument("--group-size", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-fuse-w13", action="store_true",
+                    help="w1 and w3 as two linears (the reference's module layout, 161 launches)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -168,7 +180,7 @@ def main():
 
     _lib.lib()  # fail loudly if the native library is missing
     cfg, g, P = LLAMA3_8B, args.group_size, world
-    lins = llama_linears(cfg)
+    lins = llama_linears(cfg, fuse_w13=not args.no_fuse_w13)
 
     # ---- build the sharded weights, inputs and outputs (all resident in HBM) ----
     plan, bytes_per_step = [], 0
@@ -315,8 +327,10 @@ def main():
             "data": "synthetic (random-init nn.Linear weights quantized int4 g32; N(0,1) bf16 activations)",
             "config": {
                 "workload": "Llama-3-8B int4 g32 weight-only linears, M=1 decode: 32 layers x "
-                            "{wqkv 6144x4096, wo 4096x4096, w1/w3 14336x4096, w2 4096x14336} + "
-                            "output 128256x4096 (161 GEMV launches/step)",
+                            + ("{wqkv 6144x4096, wo 4096x4096, w1||w3 28672x4096, w2 4096x14336}"
+                               if not args.no_fuse_w13 else
+                               "{wqkv 6144x4096, wo 4096x4096, w1/w3 14336x4096, w2 4096x14336}")
+                            + f" + output 128256x4096 ({len(plan)} GEMV launches/step)",
                 "model": "Llama-3-8B (linears only)",
                 "global_batch": 1,
                 "seq_len": 1,
@@ -333,7 +347,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "traffic_unit": "HBM bytes per step (161 launches)",
+                "traffic_unit": f"HBM bytes per step ({len(plan)} launches)",
                 "alg_bytes_per_step": bytes_per_step,
                 "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic else None,
                 "launches": len(durs),

@@ -231,7 +231,7 @@ int int4wo_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
       } else if (N >= 8192) {  // one wave walks both slices of 4 rows (PAIR)
         rpw = 4;
         occ = 4;
-        sh = {1, 1};
+        sh = {1, N >= 16384 ? 4 : 1};
       } else {
         rpw = 2;
         sh = {2, N <= 4096 ? 1 : 4};
