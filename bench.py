@@ -12,10 +12,13 @@ Int4WeightOnlyConfig(group_size=32) math and packed by the HIP pack kernel; acti
 synthetic N(0,1) bf16; everything is resident in HBM before timing. The step is captured once
 in a HIP graph and replayed.
 
-N GPUs (torchrun, one rank per GPU): every linear is column-sharded (rank r owns output rows
-[r N/P, (r+1) N/P)) and its output is all-gathered over RCCL after each GEMV (north star,
-SURVEY §8e). Total work is fixed as P grows ("strong" scaling); value counts the whole model's
-bytes once per step.
+N GPUs (torchrun, one rank per GPU): the large linears (N*K >= --shard-min-elems: the merged
+w1||w3 and the output head of the 8B; every linear of a 70B) are column-sharded (rank r owns
+output rows [r N/P, (r+1) N/P)) and their outputs all-gathered over RCCL after each GEMV
+(north star); the small ones run whole on every rank, because an M = 1 gather
+(~10 µs, latency-bound) costs more than their GEMV (4-9 µs). --shard-all shards every linear.
+Total work is fixed as P grows ("strong" scaling); value counts the whole model's bytes once
+per step.
 
 Reported (one JSON line, rank 0):
   value        = algorithmic bytes per step x steps / wall time  (GB/s, whole job)
@@ -160,6 +163,12 @@ def main():
     ap.add_argument("--group-size", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--shard-min-elems", type=int, default=64 << 20,
+                    help="P > 1: column-shard a linear when N*K >= this (default 64 Mi: the "
+                         "8B w1||w3 and output head; every 70B linear)")
+    ap.add_argument("--shard-all", action="store_true", help="P > 1: shard every linear")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo = rehearsal of the P > 1 path on one GPU (all ranks on device 0)")
     ap.add_argument("--no-fuse-w13", action="store_true",
                     help="w1 and w3 as two linears (the reference's module layout, 161 launches)")
     args = ap.parse_args()
@@ -169,11 +178,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # rehearsal of the P > 1 logic on a one-GPU box: every rank on device 0, gloo collectives
+    # through host memory (no graph); the real runs use one GPU per rank and RCCL
+    rehearsal = args.backend == "gloo"
+    if rehearsal:
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=device)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     import torchao
     from torchao import _lib
@@ -185,12 +202,17 @@ def main():
     # ---- build the sharded weights, inputs and outputs (all resident in HBM) ----
     plan, bytes_per_step = [], 0
     xs = {K: torch.randn(1, K, device=device, dtype=torch.bfloat16) for K in {K for _, _, K in lins}}
+    n_sharded = 0
     for i, (name, N, K) in enumerate(lins):
-        assert N % P == 0, (name, N, P)
-        n_loc = N // P
-        packed, sz = make_int4_weight(n_loc, K, g, seed=1000 * i + rank, device=device)
+        # column-shard the large linears (north star); a small one is cheaper to run whole on
+        # every rank than to shard and gather (an M = 1 gather costs more than its GEMV)
+        shard = P > 1 and N % P == 0 and (args.shard_all or N * K >= args.shard_min_elems)
+        n_sharded += shard
+        n_loc = N // P if shard else N
+        packed, sz = make_int4_weight(n_loc, K, g, seed=1000 * i + (rank if shard else 0),
+                                      device=device)
         y_loc = torch.empty(n_loc, device=device, dtype=torch.bfloat16)  # M = 1 row
-        y_full = torch.empty(N, device=device, dtype=torch.bfloat16) if P > 1 else y_loc
+        y_full = torch.empty(N, device=device, dtype=torch.bfloat16) if shard else y_loc
         plan.append((name, n_loc, K, packed, sz, y_loc, y_full))
         bytes_per_step += int4_alg_bytes(N, K, g)
     torch.cuda.synchronize()
@@ -206,8 +228,13 @@ def main():
                                                 None, y_loc.data_ptr(), 1, n_loc, K, g, sp)
                 if rc:
                     raise RuntimeError(lib.tao_last_error().decode())
-            if P > 1 and do_comm:
-                dist.all_gather_into_tensor(y_full, y_loc)
+            if do_comm and y_full is not y_loc:
+                if rehearsal:
+                    parts = [torch.empty_like(y_loc, device="cpu") for _ in range(P)]
+                    dist.all_gather(parts, y_loc.cpu())
+                    y_full.copy_(torch.cat(parts))
+                else:
+                    dist.all_gather_into_tensor(y_full, y_loc)
 
     def capture(**kw):
         graph = torch.cuda.CUDAGraph()
@@ -221,7 +248,7 @@ def main():
         return graph
 
     graph = None
-    if not args.no_graph:
+    if not args.no_graph and not rehearsal:
         try:
             graph = capture()
         except Exception as e:  # graph capture of collectives is runtime dependent
@@ -243,7 +270,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if P > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed], device="cpu" if rehearsal else device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -336,7 +363,9 @@ def main():
                 "seq_len": 1,
                 "group_size": g,
                 "bytes_per_step": bytes_per_step,
-                "parallelism": f"colwise-tp{P} + RCCL all-gather" if P > 1 else "single-gpu",
+                "parallelism": (f"colwise-tp{P} + RCCL all-gather on {n_sharded} of {len(plan)} "
+                                f"linears (N*K >= {args.shard_min_elems}), rest replicated"
+                                if P > 1 else "single-gpu"),
                 "hip_graph": graph is not None,
             },
             "roofline": {
