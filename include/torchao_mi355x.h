@@ -180,9 +180,35 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
                          int64_t Hkv, int64_t D, int64_t T, float scale, void* stream);
 
 /* y = bf16(bf16(silu(a)) * b) elementwise over n bf16 (n even). Replaces FeedForward's
- * F.silu(w1(x)) * w3(x) (model.py:485-486). */
+ * F.silu(w1(x)) * w3(x) (model.py:485-486). b == NULL: a holds n interleaved (gate, up) pairs
+ * (2n bf16, the output of an interleaved w13 linear) and y[i] = silu(a[2i]) * a[2i+1]. */
 int tao_silu_mul_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t n,
                       void* stream);
+
+/* out[r] = argmax over n bf16 logits of row r (first index of the maximum; NaN counts as the
+ * maximum) as int64. Replaces logits.argmax(dim=-1) of the greedy decode
+ * (generate.py:111-142, sample with temperature 0). */
+int tao_argmax_bf16(const uint16_t* x, int64_t* out, int64_t rows, int64_t n, void* stream);
+
+/* Decode-step fused int4 linear, M = 1: y = epilogue(rmsnorm(x) W^T) in one launch, with the
+ * operands of tao_int4wo_linear_bf16 (x [K] bf16, packed [N][K/8], scales_and_zeros [N][K/g]).
+ *   norm_weight  NULL: x is used as is; else [K] bf16 and x -> bf16(bf16(x * rsqrt(mean(x^2) +
+ *                eps)) * norm_weight) first (= tao_rmsnorm_bf16; RMSNorm, model.py:489-501).
+ *   epilogue 0   y [N] bf16 (the plain linear).
+ *   epilogue 1   rows (2i, 2i+1) are (w1_i, w3_i): y [N/2] = bf16(bf16(silu(a)) * b)
+ *                (= tao_silu_mul_bf16 over w1 and w3 outputs; FeedForward, model.py:485-486).
+ *   epilogue 2   rows are wqkv's [q | k | v] heads, N = (n_head + 2 n_kv_head) * head_dim:
+ *                y [n_head * head_dim] = rotated q, k rotated and v stored into k_cache /
+ *                v_cache [n_kv_head][max_seq][head_dim] at pos[0] (= tao_rope_kv_bf16 with
+ *                B = S = 1; Attention.forward, model.py:547-557).
+ * freqs/pos/caches/head sizes are read only by epilogue 2. Same bf16 roundings as the unfused
+ * kernels; the one difference is the order of the fp32 sum of squares in the RMSNorm. */
+int tao_int4wo_decode_bf16(const uint16_t* x, const uint32_t* packed,
+                           const uint16_t* scales_and_zeros, int64_t N, int64_t K,
+                           int64_t group_size, const uint16_t* norm_weight, float eps,
+                           int epilogue, uint16_t* y, const float* freqs, const int64_t* pos,
+                           uint16_t* k_cache, uint16_t* v_cache, int64_t n_head,
+                           int64_t n_kv_head, int64_t head_dim, int64_t max_seq, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,177 @@
+"""The decode-fused int4 GEMV (tao_int4wo_decode_bf16) against the unfused chain it replaces:
+RMSNorm kernel -> int4 linear -> SiLU-mul / RoPE + KV write. Without the RMSNorm prologue the
+fused kernel runs the same launch shape and the same bf16 roundings as the unfused kernels, so
+the comparison is bit-exact; with it, the only difference is the order of the fp32 sum of
+squares inside rsqrt(mean(x^2) + eps), so the normalised activations may differ by one bf16
+ulp in rare elements (tolerance written per check)."""
+
+import math
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from torchao.quantization import Int4WeightOnlyConfig, quantize_
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _int4_linear(N, K, g=32, seed=0):
+    torch.manual_seed(seed)
+    lin = nn.Linear(K, N, bias=False, device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        lin.weight.uniform_(-1 / math.sqrt(K), 1 / math.sqrt(K))
+    quantize_(lin, Int4WeightOnlyConfig(group_size=g))
+    from torchao._models.llama.model import _int4_parts
+
+    parts = _int4_parts(lin)
+    assert parts is not None and parts[2] == g
+    return lin, parts
+
+
+def _norm_w(K, seed=1):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return (torch.rand(K, device=DEV, generator=g) + 0.5).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("N,K,g", [(512, 4096, 32), (6144, 4096, 32), (28672, 4096, 32),
+                                   (4096, 14336, 128), (1000, 512, 64), (8192, 8192, 256)])
+def test_plain_matches_linear(N, K, g):
+    from torchao._models.llama import kernels
+
+    lin, parts = _int4_linear(N, K, g)
+    x = torch.randn(1, 1, K, device=DEV, dtype=torch.bfloat16)
+    got = kernels.int4_decode(x, *parts)
+    assert torch.equal(got, lin(x))
+
+
+@pytest.mark.parametrize("N,K", [(512, 4096), (6144, 4096), (128256, 4096), (2048, 8192)])
+def test_rmsnorm_prologue(N, K):
+    from torchao._models.llama import kernels
+
+    lin, parts = _int4_linear(N, K)
+    x = torch.randn(1, 1, K, device=DEV, dtype=torch.bfloat16) * 3
+    w = _norm_w(K)
+    got = kernels.int4_decode(x, *parts, norm_weight=w, eps=1e-5)
+    ref = lin(kernels.rmsnorm(x, w, 1e-5))
+    rel = (got.float() - ref.float()).norm() / ref.float().norm()
+    assert rel < 2e-3, float(rel)
+    # against the fp32 restatement of the chain (RMSNorm.forward, then dequant -> linear)
+    xf = x.float()
+    xn = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)).bfloat16() * w
+    ref32 = F.linear(xn.float(), _dequant(lin).float())
+    rel = (got.float() - ref32).norm() / ref32.norm()
+    assert rel < 1e-2, float(rel)
+
+
+def _dequant(lin):
+    impl = lin.weight.tensor_impl
+    return torch.ops.torchao.int4_dequantize(impl.packed_weight, impl.scale_and_zero,
+                                             lin.weight.block_size[-1])
+
+
+@pytest.mark.parametrize("norm", [False, True])
+@pytest.mark.parametrize("I,K", [(256, 512), (14336, 4096)])
+def test_swiglu_epilogue(norm, I, K):
+    from torchao._models.llama import kernels
+
+    lin, parts = _int4_linear(2 * I, K, seed=2)  # rows interleaved (gate_i, up_i)
+    x = torch.randn(1, 1, K, device=DEV, dtype=torch.bfloat16)
+    w = _norm_w(K) if norm else None
+    got = kernels.int4_decode(x, *parts, norm_weight=w, eps=1e-5, epilogue="swiglu")
+    assert got.shape == (1, 1, I)
+    xin = kernels.rmsnorm(x, w, 1e-5) if norm else x
+    h = lin(xin)
+    ref = kernels.silu_mul(h)  # pair mode of the unfused kernel
+    hp = h.unflatten(-1, (-1, 2))
+    assert torch.equal(ref, kernels.silu_mul(hp[..., 0].contiguous(), hp[..., 1].contiguous()))
+    if norm:
+        rel = (got.float() - ref.float()).norm() / ref.float().norm()
+        assert rel < 2e-3, float(rel)
+    else:
+        assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("norm", [False, True])
+@pytest.mark.parametrize("H,Hkv,pos", [(32, 8, 17), (4, 4, 0), (8, 2, 63)])
+def test_rope_kv_epilogue(norm, H, Hkv, pos):
+    from torchao._models.llama import kernels
+    from torchao._models.llama.model import ModelArgs, _rope_freqs
+
+    D, T = 128, 64
+    K = 1024 if H < 32 else 4096
+    N = (H + 2 * Hkv) * D
+    lin, parts = _int4_linear(N, K, seed=3)
+    cfg = ModelArgs(n_layer=1, n_head=H, n_local_heads=Hkv, dim=H * D, rope_base=500000)
+    freqs = _rope_freqs(cfg, T).to(DEV)
+    x = torch.randn(1, 1, K, device=DEV, dtype=torch.bfloat16)
+    w = _norm_w(K) if norm else None
+    p = torch.tensor([pos], device=DEV)
+    kc = torch.randn(1, Hkv, T, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    kc_ref, vc_ref = kc.clone(), vc.clone()
+    q = kernels.int4_decode(x, *parts, norm_weight=w, eps=1e-5, epilogue="rope_kv",
+                            rope=(freqs, p, kc, vc, H))
+    xin = kernels.rmsnorm(x, w, 1e-5) if norm else x
+    q_ref = kernels.rope_kv(lin(xin), freqs, p, kc_ref, vc_ref, H)
+    if norm:
+        for a, b in ((q, q_ref), (kc, kc_ref), (vc, vc_ref)):
+            rel = (a.float() - b.float()).norm() / b.float().norm()
+            assert rel < 2e-3, float(rel)
+    else:
+        assert torch.equal(q, q_ref)
+        assert torch.equal(kc, kc_ref)  # rows other than pos untouched as well
+        assert torch.equal(vc, vc_ref)
+
+
+def test_graph_capture_and_errors():
+    from torchao import _lib
+    from torchao._models.llama import kernels
+
+    lin, parts = _int4_linear(6144, 4096)
+    x = torch.randn(1, 1, 4096, device=DEV, dtype=torch.bfloat16)
+    w = _norm_w(4096)
+    eager = kernels.int4_decode(x, *parts, norm_weight=w, eps=1e-5)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        kernels.int4_decode(x, *parts, norm_weight=w, eps=1e-5)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            out = kernels.int4_decode(x, *parts, norm_weight=w, eps=1e-5)
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, eager)
+
+    with pytest.raises(RuntimeError, match="one token"):
+        kernels.int4_decode(torch.randn(2, 4096, device=DEV, dtype=torch.bfloat16), *parts)
+    with pytest.raises(RuntimeError, match="epilogue"):
+        _lib.call("tao_int4wo_decode_bf16", x.data_ptr(), parts[0].data_ptr(),
+                  parts[1].data_ptr(), 6144, 4096, 32, None, 0.0, 7, eager.data_ptr(), None,
+                  None, None, None, 0, 0, 0, 0, None)
+    with pytest.raises(RuntimeError, match="n_head"):
+        _lib.call("tao_int4wo_decode_bf16", x.data_ptr(), parts[0].data_ptr(),
+                  parts[1].data_ptr(), 6144, 4096, 32, None, 0.0, 2, eager.data_ptr(), None,
+                  None, None, None, 32, 4, 128, 64, None)
+
+
+@pytest.mark.parametrize("rows,n", [(1, 128256), (3, 1000), (2, 7), (1, 32000)])
+def test_argmax_matches_torch(rows, n):
+    from torchao._models.llama import kernels
+
+    torch.manual_seed(rows * n)
+    x = torch.randn(rows, n, device=DEV).to(torch.bfloat16)
+    assert torch.equal(kernels.argmax(x), x.float().argmax(-1, keepdim=True))
+    # ties: torch returns the first index of the maximum; negative rows; -inf entries
+    x = torch.full((rows, n), -3.0, device=DEV, dtype=torch.bfloat16)
+    x[:, n // 2:] = -2.5
+    x[:, 0] = float("-inf")
+    assert torch.equal(kernels.argmax(x), x.float().argmax(-1, keepdim=True))
+    # an unaligned row view (odd offset) takes the scalar path
+    if n > 2:
+        y = torch.randn(rows * n + 1, device=DEV).to(torch.bfloat16)[1:].view(rows, n)
+        assert torch.equal(kernels.argmax(y), y.float().argmax(-1, keepdim=True))

@@ -11,6 +11,7 @@
 //                heads of one kv head); split over 64-key chunks (flash-decoding), then a
 //                combine kernel merges the chunks' (max, sum, o) in fp32 -> bf16
 //   * SiLU-mul:  y = bf16(bf16(silu(a)) * b)                             (F.silu(w1 x) * w3 x)
+//   * argmax:    greedy next token over bf16 logits, torch.argmax's first-index tie rule
 #include "tao_common.h"
 
 namespace tao {
@@ -227,17 +228,79 @@ __global__ __launch_bounds__(64) void attn_combine_kernel(const float* __restric
 }
 
 // ---- SiLU(a) * b ----------------------------------------------------------------------------
+__device__ __forceinline__ uint16_t silu_mul1(float v, float m) {
+  return f32_to_bf16(round_bf16(v / (1.f + __expf(-v))) * m);
+}
+
+// b == nullptr: a holds interleaved (gate, up) pairs, the row order of an interleaved w13.
 __global__ __launch_bounds__(256) void silu_mul_kernel(const uint32_t* __restrict__ a,
                                                        const uint32_t* __restrict__ b,
                                                        uint32_t* __restrict__ y, int64_t n2) {
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n2; i += (int64_t)gridDim.x * 256) {
-    const uint32_t x = a[i], z = b[i];
-    auto f = [](float v, float m) {
-      const float s = round_bf16(v / (1.f + __expf(-v)));
-      return f32_to_bf16(s * m);
-    };
-    y[i] = (uint32_t)f(bf16lo_to_f32(x), bf16lo_to_f32(z)) |
-           ((uint32_t)f(bf16hi_to_f32(x), bf16hi_to_f32(z)) << 16);
+    uint32_t x, z;
+    if (b != nullptr) {
+      x = a[i];
+      z = b[i];
+    } else {
+      const uint2 p = reinterpret_cast<const uint2*>(a)[i];  // (g0, u0), (g1, u1)
+      x = (p.x & 0xFFFFu) | (p.y << 16);
+      z = (p.x >> 16) | (p.y & 0xFFFF0000u);
+    }
+    y[i] = (uint32_t)silu_mul1(bf16lo_to_f32(x), bf16lo_to_f32(z)) |
+           ((uint32_t)silu_mul1(bf16hi_to_f32(x), bf16hi_to_f32(z)) << 16);
+  }
+}
+
+// ---- greedy argmax over bf16 logits: one workgroup per row ------------------------------------
+// Key = order-preserving 16-bit image of the bf16 value (NaN above +inf, as torch.argmax treats
+// NaN as the maximum) in the high word, ~index in the low word: the max key is the first index
+// of the max value, torch.argmax's tie rule.
+__device__ __forceinline__ uint64_t argmax_key(uint32_t b, uint32_t idx) {
+  uint32_t k = (b & 0x8000u) ? (~b & 0xFFFFu) : (b | 0x8000u);
+  if ((b & 0x7F80u) == 0x7F80u && (b & 0x7Fu)) k = 0xFFFFu;  // NaN
+  return ((uint64_t)k << 32) | (uint32_t)~idx;
+}
+
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+__global__ __launch_bounds__(1024) void argmax_kernel(const uint16_t* __restrict__ x,
+                                                      int64_t* __restrict__ out, int64_t n) {
+  __shared__ uint64_t red[16];
+  const uint16_t* row = x + (size_t)blockIdx.x * n;
+  uint64_t best = 0;
+  const int64_t nv = ((reinterpret_cast<uintptr_t>(row) & 15) == 0) ? n / 8 : 0;
+  const uint4* rv = reinterpret_cast<const uint4*>(row);
+  // 8 loads in flight per thread per round (a 128K-vocab row is two rounds), clamped indices
+  // and masks instead of branches around the loads
+  constexpr int U = 8;
+  for (int64_t base = 0; base < nv; base += U * 1024) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + u * 1024 + threadIdx.x;
+      v[u] = rv[i < nv ? i : nv - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + u * 1024 + threadIdx.x;
+      const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t k = (uint32_t)(i * 8 + 2 * j);
+        const uint64_t m = umax64(argmax_key(d[j] & 0xFFFFu, k), argmax_key(d[j] >> 16, k + 1));
+        best = i < nv ? umax64(best, m) : best;
+      }
+    }
+  }
+  for (int64_t i = nv * 8 + threadIdx.x; i < n; i += 1024)  // tail (or unaligned rows)
+    best = umax64(best, argmax_key(row[i], (uint32_t)i));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) best = umax64(best, __shfl_xor(best, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = umax64(best, red[w]);
+    out[blockIdx.x] = (int64_t)(uint32_t)~(uint32_t)best;
   }
 }
 
@@ -303,7 +366,7 @@ int tao_silu_mul_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t
                       void* stream) {
   TAO_CHECK_ARG(n >= 0 && n % 2 == 0, "silu_mul: n (%lld) must be even", (long long)n);
   if (n == 0) return TAO_OK;
-  TAO_CHECK_ALIGN(a, 4, "a");
+  TAO_CHECK_ALIGN(a, b != nullptr ? 4 : 8, "a");
   TAO_CHECK_ALIGN(b, 4, "b");
   const int64_t n2 = n / 2;
   int64_t grid = (n2 + 255) / 256;
@@ -312,6 +375,15 @@ int tao_silu_mul_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t
          reinterpret_cast<const uint32_t*>(a), reinterpret_cast<const uint32_t*>(b),
          reinterpret_cast<uint32_t*>(y), n2);
   return check_launch("silu_mul_kernel");
+}
+
+int tao_argmax_bf16(const uint16_t* x, int64_t* out, int64_t rows, int64_t n, void* stream) {
+  TAO_CHECK_ARG(rows >= 0 && n > 0 && n < (1LL << 31), "argmax: n (%lld) must be in [1, 2^31)",
+                (long long)n);
+  if (rows == 0) return TAO_OK;
+  TAO_CHECK_ALIGN(x, 2, "x");
+  launch(argmax_kernel, dim3((unsigned)rows), dim3(1024), 0, as_stream(stream), x, out, n);
+  return check_launch("argmax_kernel");
 }
 
 }  // extern "C"

@@ -15,6 +15,7 @@
 //   * cross-lane: reduce-scatter over the RPW*M partials (V/2 + V/4 + ... shuffles), then a
 //     butterfly over the remaining lanes; cross-wave: LDS, one wave finishes and writes y.
 #include <atomic>
+#include <type_traits>
 
 #include "tao_common.h"
 #include "tao_reduce.h"
@@ -22,15 +23,43 @@
 namespace tao {
 namespace {
 
+// Decode-step fusions of the M == 1 GEMV (tao_int4wo_decode_bf16). They fold
+// the small ops around a Llama block's linears into the linear itself, so a decode token costs
+// fewer launches; each keeps the unfused kernels' op order and bf16 roundings
+// (decode_ops.hip: rmsnorm_kernel, silu_mul_kernel, rope_kv_kernel).
+//   PRO         x -> bf16(bf16(x * rsqrt(mean(x^2) + eps)) * norm_w) on the fly (RMSNorm,
+//               reference torchao/_models/llama/model.py RMSNorm.forward);
+//   kEpiSwiGLU  rows (2i, 2i+1) hold (w1_i, w3_i): y[i] = bf16(bf16(silu(a)) * b);
+//   kEpiRopeKV  rows = [q | k | v] heads of wqkv: q rotated into y, k rotated and v stored
+//               into the caches at pos[0] (Attention.forward + KVCache.update).
+enum { kEpiNone = 0, kEpiSwiGLU = 1, kEpiRopeKV = 2 };
+constexpr int kNormPT = 2;  // 16-B pieces of x per thread in the RMSNorm prologue
+struct GemvFuse {
+  const uint16_t* norm_w;  // [K] RMSNorm weight (PRO)
+  float eps;
+  const float* freqs;      // [T][D/2] (cos, sin) pairs (kEpiRopeKV)
+  const int64_t* pos;
+  uint16_t* k_cache;       // [Hkv][T][D]
+  uint16_t* v_cache;
+  int H, Hkv, D, T;
+};
+
+__device__ __forceinline__ uint32_t rmsnorm_pair(uint32_t xv, uint32_t wv, float r) {
+  const float lo = round_bf16(bf16lo_to_f32(xv) * r) * bf16lo_to_f32(wv);
+  const float hi = round_bf16(bf16hi_to_f32(xv) * r) * bf16hi_to_f32(wv);
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+
 // WPE: minimum waves per SIMD the register allocation must allow (8 -> <= 64 VGPRs, so four
 // 512-thread workgroups fit on a CU and mid-size grids run in a single resident round).
-template <int MT, int RPW, int WPE, bool PAIR>
+template <int MT, int RPW, int WPE, bool PAIR, bool PRO = false, int EPI = kEpiNone>
 __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     const uint16_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
     const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K, int gshift,
-    int Wk, int G, int S) {
+    int Wk, int G, int S, GemvFuse fu) {
+  static_assert(!(PRO || EPI) || (MT == 1 && RPW % 2 == 0), "fusions are M == 1, row pairs");
   constexpr int V = RPW * MT;
-  extern __shared__ float red[];  // [G][Wk][V]
+  extern __shared__ float red[];  // [G][Wk][V] (PRO: + [8] partial sums, + normalised x [K])
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int wk = wave % Wk;
@@ -44,6 +73,61 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
   for (int r = 0; r < RPW; ++r)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[r][m] = 0.f;
+
+  // RMSNorm prologue (PRO): the workgroup normalises x once into LDS. Each thread loads its
+  // <= kNormPT 16-B pieces of x and of the norm weight (the launcher guarantees
+  // K <= 8 * kNormPT * blockDim.x) BEFORE its first slice's weight loads, so the in-order vmcnt
+  // wait for them does not wait for the weights: the sum of squares, the two barriers (reached
+  // exactly once by every wave) and the LDS fill all run under the weight-load latency.
+  // LDS copy: chunk c (32 k) keeps its four 16-B pieces rotated by c >> 2, so the 16 lanes of a
+  // ds_read_b128 pass (consecutive chunks) hit 16 distinct 16-B bank groups.
+  uint4* xs = reinterpret_cast<uint4*>(red + ((G * Wk * V + 8 + 3) & ~3));
+  uint4 xv[kNormPT], gv[kNormPT];
+  auto norm_load = [&]() __attribute__((always_inline)) {
+    const uint4* xr = reinterpret_cast<const uint4*>(x);
+    const uint4* gr = reinterpret_cast<const uint4*>(fu.norm_w);
+    const int nx = K >> 3;
+#pragma unroll
+    for (int u = 0; u < kNormPT; ++u) {
+      const int i = threadIdx.x + u * (int)blockDim.x;
+      const int ic = i < nx ? i : nx - 1;  // clamped, masked below
+      xv[u] = xr[ic];
+      gv[u] = gr[ic];
+    }
+  };
+  auto norm_finish = [&]() __attribute__((always_inline)) {
+    const int nx = K >> 3;
+    float ss = 0.f;
+#pragma unroll
+    for (int u = 0; u < kNormPT; ++u) {
+      const bool ok = threadIdx.x + u * (int)blockDim.x < nx;
+      const uint32_t d[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a = ok ? bf16lo_to_f32(d[j]) : 0.f, b = ok ? bf16hi_to_f32(d[j]) : 0.f;
+        ss = fmaf(a, a, fmaf(b, b, ss));
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+    float* ssr = red + G * Wk * V;
+    if (lane == 0) ssr[wave] = ss;
+    __syncthreads();
+    float t = 0.f;
+    for (int w = 0; w < G * Wk; ++w) t += ssr[w];
+    const float r = rsqrtf(t / (float)K + fu.eps);
+#pragma unroll
+    for (int u = 0; u < kNormPT; ++u) {
+      const int i = threadIdx.x + u * (int)blockDim.x;
+      if (i < nx) {
+        const int c = i >> 2;
+        xs[c * 4 + (((i & 3) + (c >> 2)) & 3)] =
+            make_uint4(rmsnorm_pair(xv[u].x, gv[u].x, r), rmsnorm_pair(xv[u].y, gv[u].y, r),
+                       rmsnorm_pair(xv[u].z, gv[u].z, r), rmsnorm_pair(xv[u].w, gv[u].w, r));
+      }
+    }
+    __syncthreads();
+  };
 
   // PAIR (waves owning >= 2 slices): slices are processed two at a time, both slices' weight
   // and (scale, zero) loads issued before either is consumed, so a wave walking two slices pays
@@ -81,7 +165,7 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
       uint32_t xd[4][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint4 t4 = xp[j];
+        const uint4 t4 = PRO ? xs[cc * 4 + ((j + (cc >> 2)) & 3)] : xp[j];
         xd[j][0] = t4.x;
         xd[j][1] = t4.y;
         xd[j][2] = t4.z;
@@ -106,7 +190,34 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     }
   };
 
-  if constexpr (PAIR) {
+  // With PRO the first slice (every wave has one: Wk <= S) is peeled so the RMSNorm prologue
+  // can sit around its loads.
+  auto pair_step = [&](int s, auto first) __attribute__((always_inline)) {
+    uint4 wv0[RPW], wv1[RPW];
+    uint32_t szv0[RPW], szv1[RPW];
+    int cc0, cc1;
+    bool cv0, cv1;
+    if constexpr (PRO && decltype(first)::value) norm_load();
+    load_slice(s, wv0, szv0, cc0, cv0);
+    load_slice(s + Wk, wv1, szv1, cc1, cv1);
+    if constexpr (PRO && decltype(first)::value) norm_finish();
+    do_slice(wv0, szv0, cc0, cv0);
+    if (s + Wk < S) do_slice(wv1, szv1, cc1, cv1);  // wave-uniform
+  };
+  auto single_step = [&](int s, auto first) __attribute__((always_inline)) {
+    uint4 wv0[RPW];
+    uint32_t szv0[RPW];
+    int cc0;
+    bool cv0;
+    if constexpr (PRO && decltype(first)::value) norm_load();
+    load_slice(s, wv0, szv0, cc0, cv0);
+    if constexpr (PRO && decltype(first)::value) norm_finish();
+    do_slice(wv0, szv0, cc0, cv0);
+  };
+  if constexpr (PAIR && PRO) {
+    pair_step(wk, std::true_type{});
+    for (int s = wk + 2 * Wk; s < S; s += 2 * Wk) pair_step(s, std::false_type{});
+  } else if constexpr (PAIR) {
     for (int s = wk; s < S; s += 2 * Wk) {
       uint4 wv0[RPW], wv1[RPW];
       uint32_t szv0[RPW], szv1[RPW];
@@ -117,6 +228,9 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
       do_slice(wv0, szv0, cc0, cv0);
       if (s + Wk < S) do_slice(wv1, szv1, cc1, cv1);  // wave-uniform
     }
+  } else if constexpr (PRO) {
+    single_step(wk, std::true_type{});
+    for (int s = wk + Wk; s < S; s += Wk) single_step(s, std::false_type{});
   } else {
     for (int s = wk; s < S; s += Wk) {
       uint4 wv0[RPW];
@@ -152,13 +266,46 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
       for (int kk = 0; kk < Wk; ++kk) total += red[(rg * Wk + kk) * V + widx];
     }
   }
-  if (writer) {
-    const int r = widx / MT, m = widx % MT;
-    const int n = row0 + r;
-    if (n < N && m < M) {
-      uint16_t out = f32_to_bf16(total);
-      if (bias != nullptr) out = f32_to_bf16(bf16_to_f32(out) + bf16_to_f32(bias[n]));
-      y[(size_t)m * N + n] = out;
+  if constexpr (EPI == kEpiNone) {
+    if (writer) {
+      const int r = widx / MT, m = widx % MT;
+      const int n = row0 + r;
+      if (n < N && m < M) {
+        uint16_t out = f32_to_bf16(total);
+        if (bias != nullptr) out = f32_to_bf16(bf16_to_f32(out) + bf16_to_f32(bias[n]));
+        y[(size_t)m * N + n] = out;
+      }
+    }
+  } else {
+    // Row pair (2p, 2p+1) meets in lane p of the writing wave. Row r's total sits in lane r
+    // (Wk > 1) or in owner lane r << (6 - T) (Wk == 1); every lane takes part in the shuffles.
+    const float o = round_bf16(total);
+    const int sh = Wk > 1 ? 0 : 6 - T;
+    const int pl = lane < RPW / 2 ? lane : 0;
+    const float a = __shfl(o, (2 * pl) << sh);
+    const float b = __shfl(o, (2 * pl + 1) << sh);
+    const int n = row0 + 2 * pl;
+    if ((Wk == 1 || wk == 0) && lane < RPW / 2 && n < N) {
+      if constexpr (EPI == kEpiSwiGLU) {
+        y[n >> 1] = f32_to_bf16(round_bf16(a / (1.f + __expf(-a))) * b);
+      } else {
+        const int D = fu.D, HD = fu.H * fu.D, KD = fu.Hkv * fu.D;
+        const int64_t p = fu.pos[0];
+        uint32_t ov = (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
+        if (n < HD + KD) {
+          const float2 cs = reinterpret_cast<const float2*>(fu.freqs)[p * (D >> 1) + ((n % D) >> 1)];
+          const float o0 = a * cs.x - b * cs.y, o1 = b * cs.x + a * cs.y;
+          ov = (uint32_t)f32_to_bf16(o0) | ((uint32_t)f32_to_bf16(o1) << 16);
+        }
+        if (n < HD) {
+          reinterpret_cast<uint32_t*>(y)[n >> 1] = ov;
+        } else {
+          const int nk = n < HD + KD ? n - HD : n - HD - KD;
+          uint16_t* cache = n < HD + KD ? fu.k_cache : fu.v_cache;
+          const size_t off = ((size_t)(nk / D) * fu.T + p) * D + nk % D;
+          reinterpret_cast<uint32_t*>(cache)[off >> 1] = ov;
+        }
+      }
     }
   }
 }
@@ -185,30 +332,99 @@ GemvShape default_shape(int S) {
   return {wk, g};
 }
 
-template <int MT, int RPW, int WPE>
+template <int MT, int RPW, int WPE, bool PRO = false, int EPI = kEpiNone>
 int launch_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
                 const uint16_t* bias, uint16_t* y, int M, int N, int K, int gshift,
-                GemvShape sh, hipStream_t stream) {
+                GemvShape sh, hipStream_t stream, const GemvFuse& fu = GemvFuse{}) {
   const int nchunk = K / 32;
   const int S = (nchunk + 63) / 64;
   const int wk = sh.wk < S ? sh.wk : S;
   const int rows_per_wg = sh.g * RPW;
   const int grid = (N + rows_per_wg - 1) / rows_per_wg;
   const int threads = 64 * wk * sh.g;
-  const size_t lds = (size_t)sh.g * wk * RPW * MT * sizeof(float);
+  const size_t lds = PRO ? (((size_t)sh.g * wk * RPW * MT + 8 + 3) & ~(size_t)3) * sizeof(float) +
+                               (size_t)K * 2
+                         : (size_t)sh.g * wk * RPW * MT * sizeof(float);
   if (S > wk)
-    launch((int4wo_gemv_kernel<MT, RPW, WPE, true>), dim3(grid), dim3(threads), lds, stream, x,
-           reinterpret_cast<const uint4*>(packed), reinterpret_cast<const uint32_t*>(sz), bias,
-           y, M, N, K, gshift, wk, sh.g, S);
+    launch((int4wo_gemv_kernel<MT, RPW, WPE, true, PRO, EPI>), dim3(grid), dim3(threads), lds,
+           stream, x, reinterpret_cast<const uint4*>(packed),
+           reinterpret_cast<const uint32_t*>(sz), bias, y, M, N, K, gshift, wk, sh.g, S, fu);
   else
-    launch((int4wo_gemv_kernel<MT, RPW, WPE, false>), dim3(grid), dim3(threads), lds, stream,
-           x, reinterpret_cast<const uint4*>(packed), reinterpret_cast<const uint32_t*>(sz),
-           bias, y, M, N, K, gshift, wk, sh.g, S);
+    launch((int4wo_gemv_kernel<MT, RPW, WPE, false, PRO, EPI>), dim3(grid), dim3(threads), lds,
+           stream, x, reinterpret_cast<const uint4*>(packed),
+           reinterpret_cast<const uint32_t*>(sz), bias, y, M, N, K, gshift, wk, sh.g, S, fu);
   return check_launch("int4wo_gemv_kernel");
 }
 
 // Process-wide override of the M == 1 launch shape (tao_tune_int4_gemv; 0 = heuristic).
 std::atomic<int> g_tune_rpw{0}, g_tune_wk{0}, g_tune_g{0}, g_tune_occ{0};
+
+// M == 1 launch shape. Measured on MI355X (experiments/sweep_gemv.py,
+// profiles/r1_sweep_gemv*.jsonl): the best shapes per (N, K) class, dispatch-event timed over
+// weights rotated past the MALL.
+struct M1Shape {
+  int rpw, occ;
+  GemvShape sh;
+};
+
+M1Shape m1_shape(int N, int S) {
+  M1Shape c{4, 8, default_shape(S)};
+  if (S <= 2) {  // K <= 4096
+    if (N >= 32768) {
+      c.sh = {2, 2};
+    } else if (N >= 8192) {  // one wave walks both slices of 4 rows (PAIR)
+      c.occ = 4;
+      c.sh = {1, N >= 16384 ? 4 : 1};
+    } else {
+      c.rpw = 2;
+      c.sh = {2, N <= 4096 ? 1 : 4};
+    }
+  } else {  // K > 4096: waves split K (each walking its slices in pairs) while N is small
+    c.occ = 4;
+    c.sh = {N <= 4096 ? 2 : (S >= 8 ? 1 : 4), 1};
+  }
+  const int trpw = g_tune_rpw.load(std::memory_order_relaxed);
+  const int tocc = g_tune_occ.load(std::memory_order_relaxed);
+  const int twk = g_tune_wk.load(std::memory_order_relaxed);
+  const int tg = g_tune_g.load(std::memory_order_relaxed);
+  if (trpw > 0) c.rpw = trpw;
+  if (tocc > 0) c.occ = tocc;
+  if (twk > 0) c.sh.wk = twk;
+  if (tg > 0) c.sh.g = tg;
+  return c;
+}
+
+template <bool PRO, int EPI>
+int launch_decode(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, uint16_t* y,
+                  int N, int K, int gs, hipStream_t stream, const GemvFuse& fu) {
+  const int S = (K / 32 + 63) / 64;
+  M1Shape c = m1_shape(N, S);
+  if (PRO) {
+    // Measured (experiments/bench_decode.py, profiles/r1_bench_decode.jsonl): with the prologue
+    // a workgroup should own whole rows (no K split) and 4 waves of them, so the per-workgroup
+    // normalisation is amortised over 8-16 rows; 2 rows per wave below N = 8192.
+    if (g_tune_rpw.load(std::memory_order_relaxed) == 0) c.rpw = N < 8192 ? 2 : 4;
+    if (g_tune_wk.load(std::memory_order_relaxed) == 0) c.sh.wk = 1;
+    if (g_tune_g.load(std::memory_order_relaxed) == 0) c.sh.g = 4;
+    // enough threads to hold x in the prologue: K <= 8 * kNormPT * threads
+    const int wk = c.sh.wk < S ? c.sh.wk : S;
+    while (64 * wk * c.sh.g * 8 * kNormPT < K && wk * c.sh.g * 2 <= 8) c.sh.g *= 2;
+  }
+  // row pairs stay inside one wave: 2 or 4 rows per wave; the RMSNorm prologue (the first
+  // slices' loads live across it) does not fit 64 VGPRs, so it runs at <= 4 waves per SIMD
+  if (c.rpw <= 2) {
+    if constexpr (PRO)
+      return launch_gemv<1, 2, 4, PRO, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream,
+                                            fu);
+    else
+      return launch_gemv<1, 2, 8, PRO, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream,
+                                            fu);
+  }
+  if (c.occ == 4 || PRO)
+    return launch_gemv<1, 4, 4, PRO, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream, fu);
+  return launch_gemv<1, 4, 8, false, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream,
+                                          fu);
+}
 
 }  // namespace
 
@@ -221,38 +437,12 @@ int int4wo_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
   GemvShape sh = default_shape(S);
   const int iM = (int)M, iN = (int)N, iK = (int)K;
   if (M <= 1) {
-    // Measured on MI355X (experiments/sweep_gemv.py, profiles/r1_sweep_gemv.jsonl): the best
-    // shapes per (N, K) class, dispatch-event timed over weights rotated past the MALL.
-    int rpw, occ = 8;
-    if (S <= 2) {  // K <= 4096
-      if (N >= 32768) {
-        rpw = 4;
-        sh = {2, 2};
-      } else if (N >= 8192) {  // one wave walks both slices of 4 rows (PAIR)
-        rpw = 4;
-        occ = 4;
-        sh = {1, N >= 16384 ? 4 : 1};
-      } else {
-        rpw = 2;
-        sh = {2, N <= 4096 ? 1 : 4};
-      }
-    } else {  // K > 4096: waves split K (each walking its slices in pairs) while N is small
-      rpw = 4;
-      occ = 4;
-      sh = {N <= 4096 ? 2 : (S >= 8 ? 1 : 4), 1};
-    }
-    const int trpw = g_tune_rpw.load(std::memory_order_relaxed);
-    const int tocc = g_tune_occ.load(std::memory_order_relaxed);
-    const int twk = g_tune_wk.load(std::memory_order_relaxed);
-    const int tg = g_tune_g.load(std::memory_order_relaxed);
-    if (trpw > 0) rpw = trpw;
-    if (tocc > 0) occ = tocc;
-    if (twk > 0) sh.wk = twk;
-    if (tg > 0) sh.g = tg;
-    if (rpw == 1) return launch_gemv<1, 1, 8>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
-    if (rpw == 2) return launch_gemv<1, 2, 8>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
-    if (rpw == 8) return launch_gemv<1, 8, 4>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
-    if (occ == 4) return launch_gemv<1, 4, 4>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
+    const M1Shape c = m1_shape(iN, S);
+    sh = c.sh;
+    if (c.rpw == 1) return launch_gemv<1, 1, 8>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
+    if (c.rpw == 2) return launch_gemv<1, 2, 8>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
+    if (c.rpw == 8) return launch_gemv<1, 8, 4>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
+    if (c.occ == 4) return launch_gemv<1, 4, 4>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
     return launch_gemv<1, 4, 8>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
   }
   if (M <= 2) return launch_gemv<2, 4, 1>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
@@ -294,4 +484,65 @@ extern "C" int tao_tune_int4_gemv(int rows_per_wave, int waves_k, int row_groups
   tao::g_tune_g.store(row_groups);
   tao::g_tune_occ.store(occupancy);
   return TAO_OK;
+}
+
+extern "C" int tao_int4wo_decode_bf16(const uint16_t* x, const uint32_t* packed,
+                                      const uint16_t* scales_and_zeros, int64_t N, int64_t K,
+                                      int64_t group_size, const uint16_t* norm_weight, float eps,
+                                      int epilogue, uint16_t* y, const float* freqs,
+                                      const int64_t* pos, uint16_t* k_cache, uint16_t* v_cache,
+                                      int64_t n_head, int64_t n_kv_head, int64_t head_dim,
+                                      int64_t max_seq, void* stream) {
+  int rc = tao::int4_check_linear_args(x, packed, scales_and_zeros, y, 1, N, K, group_size);
+  if (rc != TAO_OK) return rc;
+  TAO_CHECK_ARG(epilogue >= tao::kEpiNone && epilogue <= tao::kEpiRopeKV,
+                "int4 decode: epilogue must be 0 (none), 1 (swiglu) or 2 (rope_kv)");
+  TAO_CHECK_ARG(epilogue == tao::kEpiNone || N % 2 == 0, "int4 decode: N (%lld) must be even",
+                (long long)N);
+  if (norm_weight != nullptr) {
+    TAO_CHECK_ALIGN(norm_weight, 16, "norm_weight");
+    TAO_CHECK_ARG(K <= 8 * tao::kNormPT * 512, "int4 decode: RMSNorm prologue needs K <= %d",
+                  8 * tao::kNormPT * 512);
+  }
+  tao::GemvFuse fu{};
+  fu.norm_w = norm_weight;
+  fu.eps = eps;
+  if (epilogue == tao::kEpiRopeKV) {
+    TAO_CHECK_ARG(n_head > 0 && n_kv_head > 0 && head_dim > 0 && head_dim % 2 == 0 &&
+                      max_seq > 0 && N == (n_head + 2 * n_kv_head) * head_dim,
+                  "int4 decode rope_kv: N (%lld) must be (n_head + 2 n_kv_head) * head_dim",
+                  (long long)N);
+    TAO_CHECK_ARG(freqs != nullptr && pos != nullptr && k_cache != nullptr && v_cache != nullptr,
+                  "int4 decode rope_kv: freqs, pos and caches are required");
+    TAO_CHECK_ALIGN(k_cache, 4, "k_cache");
+    TAO_CHECK_ALIGN(v_cache, 4, "v_cache");
+    TAO_CHECK_ALIGN(y, 4, "y");
+    fu.freqs = freqs;
+    fu.pos = pos;
+    fu.k_cache = k_cache;
+    fu.v_cache = v_cache;
+    fu.H = (int)n_head;
+    fu.Hkv = (int)n_kv_head;
+    fu.D = (int)head_dim;
+    fu.T = (int)max_seq;
+  }
+  if (N == 0) return TAO_OK;
+  const int gs = tao::gshift_of(group_size);
+  hipStream_t st = tao::as_stream(stream);
+  const int iN = (int)N, iK = (int)K;
+  const bool pro = norm_weight != nullptr;
+#define TAO_DEC(P, E) \
+  return tao::launch_decode<P, E>(x, packed, scales_and_zeros, y, iN, iK, gs, st, fu)
+  switch (epilogue) {
+    case tao::kEpiSwiGLU:
+      if (pro) TAO_DEC(true, tao::kEpiSwiGLU);
+      TAO_DEC(false, tao::kEpiSwiGLU);
+    case tao::kEpiRopeKV:
+      if (pro) TAO_DEC(true, tao::kEpiRopeKV);
+      TAO_DEC(false, tao::kEpiRopeKV);
+    default:
+      if (pro) TAO_DEC(true, tao::kEpiNone);
+      TAO_DEC(false, tao::kEpiNone);
+  }
+#undef TAO_DEC
 }

@@ -54,6 +54,9 @@ _SIGNATURES = {
     "tao_attn_decode_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
                              ctypes.c_float, _p],
     "tao_silu_mul_bf16": [_p, _p, _p, _i64, _p],
+    "tao_argmax_bf16": [_p, _p, _i64, _i64, _p],
+    "tao_int4wo_decode_bf16": [_p, _p, _p, _i64, _i64, _i64, _p, ctypes.c_float, _int, _p, _p,
+                               _p, _p, _p, _i64, _i64, _i64, _i64, _p],
 }
 _RESTYPES = {"tao_version": ctypes.c_char_p, "tao_last_error": ctypes.c_char_p}
 

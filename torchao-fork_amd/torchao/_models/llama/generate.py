@@ -92,8 +92,7 @@ def prefill(model: Transformer, prompt: torch.Tensor, input_pos: torch.Tensor) -
 @torch.no_grad()
 def decode_one_token(model: Transformer, cur: torch.Tensor,
                      input_pos: torch.Tensor) -> torch.Tensor:
-    logits = model(cur, input_pos)
-    return logits[:, -1].argmax(dim=-1, keepdim=True).to(cur.dtype)
+    return model.decode_next(cur, input_pos)
 
 
 class GraphDecoder:

@@ -6,7 +6,7 @@ import torch
 
 from torchao import _lib
 
-__all__ = ["rmsnorm", "rope_kv", "attn_decode", "silu_mul"]
+__all__ = ["rmsnorm", "rope_kv", "attn_decode", "silu_mul", "int4_decode", "argmax"]
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -60,10 +60,60 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     return out
 
 
-def silu_mul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+def silu_mul(a: torch.Tensor, b=None) -> torch.Tensor:
+    """bf16(bf16(silu(a)) * b); with b None, ``a`` [..., 2n] holds interleaved (gate, up) pairs
+    (an interleaved w13 output) and the result is [..., n]."""
     _check(a, torch.bfloat16, "silu_mul a")
+    if b is None:
+        y = torch.empty(*a.shape[:-1], a.shape[-1] // 2, dtype=a.dtype, device=a.device)
+        _lib.call("tao_silu_mul_bf16", a.data_ptr(), None, y.data_ptr(), y.numel(), _stream(a))
+        return y
     _check(b, torch.bfloat16, "silu_mul b")
     y = torch.empty(a.shape, dtype=a.dtype, device=a.device)
     _lib.call("tao_silu_mul_bf16", a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(),
               _stream(a))
     return y
+
+
+_EPILOGUES = {"none": 0, "swiglu": 1, "rope_kv": 2}
+
+
+def int4_decode(x: torch.Tensor, packed: torch.Tensor, scale_and_zero: torch.Tensor,
+                group_size: int, norm_weight=None, eps: float = 0.0, epilogue: str = "none",
+                rope=None) -> torch.Tensor:
+    """One token through an int4 linear with its neighbours fused (tao_int4wo_decode_bf16):
+    optional RMSNorm of x first; epilogue "none" -> [..., N], "swiglu" (rows interleaved
+    (w1_i, w3_i)) -> [..., N/2], "rope_kv" with rope = (freqs, pos, k_cache, v_cache, n_head)
+    -> rotated q [1, n_head, 1, D], k / v written into the caches at pos[0]."""
+    _check(x, torch.bfloat16, "int4_decode x")
+    N, K = packed.shape[0], x.shape[-1]
+    if x.numel() != K:
+        raise RuntimeError(f"int4_decode takes one token, got x of shape {tuple(x.shape)}")
+    if norm_weight is not None:
+        _check(norm_weight, torch.bfloat16, "int4_decode norm_weight")
+    epi = _EPILOGUES[epilogue]
+    freqs = pos = kc = vc = None
+    H = Hkv = D = T = 0
+    if epi == 2:
+        freqs, pos, kc, vc, H = rope
+        _, Hkv, T, D = kc.shape
+        y = torch.empty(1, H, 1, D, dtype=x.dtype, device=x.device)
+    elif epi == 1:
+        y = torch.empty(*x.shape[:-1], N // 2, dtype=x.dtype, device=x.device)
+    else:
+        y = torch.empty(*x.shape[:-1], N, dtype=x.dtype, device=x.device)
+    ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    _lib.call("tao_int4wo_decode_bf16", x.data_ptr(), packed.data_ptr(), scale_and_zero.data_ptr(),
+              N, K, int(group_size), ptr(norm_weight), float(eps), epi, y.data_ptr(), ptr(freqs),
+              ptr(pos), ptr(kc), ptr(vc), H, Hkv, D, T, _stream(x))
+    return y
+
+
+def argmax(logits: torch.Tensor) -> torch.Tensor:
+    """bf16 logits [..., V] -> int64 [..., 1] index of the maximum (first on ties)."""
+    _check(logits, torch.bfloat16, "argmax logits")
+    out = torch.empty(*logits.shape[:-1], 1, dtype=torch.int64, device=logits.device)
+    V = logits.shape[-1]
+    _lib.call("tao_argmax_bf16", logits.data_ptr(), out.data_ptr(), logits.numel() // V, V,
+              _stream(logits))
+    return out

@@ -13,7 +13,9 @@ Decode-time structure for one process per GPU and HIP graphs (no tracing compile
   * ``enable_fused_kernels()`` (bf16, head_dim 128, GPU) switches one-token steps to the fused
     gfx950 kernels of csrc/decode_ops.hip: RMSNorm, RoPE + KV-cache write, flash-decoding
     attention, SiLU-mul, and the residual add folded into the wo / w2 linears as their bias
-    (bf16(x + bf16(W a)) is exactly the bias epilogue at M = 1) — ~11 launches per layer;
+    (bf16(x + bf16(W a)) is exactly the bias epilogue at M = 1); with int4 weights the norms,
+    RoPE + KV write and SwiGLU ride inside the wqkv / w13 / output GEMVs
+    (tao_int4wo_decode_bf16) — 6 launches per layer;
   * otherwise (prefill, CPU): torch ops, ``index_copy_`` into the caches, a causal-mask row
     gathered by ``input_pos``, ``F.scaled_dot_product_attention(enable_gqa=True)``;
   * rotary tables precomputed once (Llama-3.1 frequency scaling where configured).
@@ -157,6 +159,18 @@ def _linear_plus(x: torch.Tensor, lin: nn.Linear, residual: torch.Tensor) -> tor
     return residual + lin(x)
 
 
+def _int4_parts(lin: Optional[nn.Linear]):
+    """(packed_weight, scale_and_zero, group_size) of an int4 weight-only linear on the gfx950
+    row-stream layout (Int4WeightOnlyConfig), else None: the fused decode kernels read those
+    operands directly."""
+    w = getattr(lin, "weight", None)
+    impl = getattr(w, "tensor_impl", None)
+    packed = getattr(impl, "packed_weight", None)
+    if packed is None or packed.dim() != 2 or not packed.is_cuda or lin.bias is not None:
+        return None
+    return packed, impl.scale_and_zero, w.block_size[-1]
+
+
 class Attention(nn.Module):
     def __init__(self, cfg: ModelArgs):
         super().__init__()
@@ -179,12 +193,22 @@ class Attention(nn.Module):
         y = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, enable_gqa=True)
         return self.wo(y.transpose(1, 2).reshape(B, S, q_sz))
 
-    def forward_fused(self, x, freqs_table, input_pos, residual):
+    def forward_fused(self, x, freqs_table, input_pos, residual, norm=None):
         from torchao._models.llama import kernels
 
         kv = self.kv_cache
-        q = kernels.rope_kv(self.wqkv(x), freqs_table, input_pos, kv.k_cache, kv.v_cache,
-                            self.n_head)
+        wqkv = _int4_parts(self.wqkv) if norm is not None else None
+        if wqkv is not None and x.numel() == x.shape[-1]:
+            # RMSNorm -> wqkv -> RoPE + KV-cache write in one launch
+            q = kernels.int4_decode(x, *wqkv, norm_weight=norm.weight, eps=norm.eps,
+                                    epilogue="rope_kv",
+                                    rope=(freqs_table, input_pos, kv.k_cache, kv.v_cache,
+                                          self.n_head))
+        else:
+            if norm is not None:
+                x = kernels.rmsnorm(x, norm.weight, norm.eps)
+            q = kernels.rope_kv(self.wqkv(x), freqs_table, input_pos, kv.k_cache, kv.v_cache,
+                                self.n_head)
         y = kernels.attn_decode(q, kv.k_cache, kv.v_cache, input_pos,
                                 1.0 / math.sqrt(self.head_dim))
         return _linear_plus(y, self.wo, residual)
@@ -200,9 +224,12 @@ class FeedForward(nn.Module):
 
     def fuse_w13(self):
         """Merge w1 and w3 (same input) into one [2I, dim] linear: one weight stream and one
-        launch per token instead of two. Row-wise quantization makes quantizing the merged
-        weight identical to quantizing w1 and w3 apart, so fuse before or after loading."""
-        w = torch.cat([self.w1.weight.detach(), self.w3.weight.detach()], dim=0)
+        launch per token instead of two. Rows interleave (w1_0, w3_0, w1_1, w3_1, ...) so
+        each gate / up pair lands in adjacent outputs, which is what the SwiGLU epilogue of
+        the fused int4 decode kernel and the pair mode of silu_mul read. Row-wise quantization
+        makes quantizing the merged weight identical to quantizing w1 and w3 apart, so fuse
+        before or after loading."""
+        w = torch.stack([self.w1.weight.detach(), self.w3.weight.detach()], dim=1).flatten(0, 1)
         self.w13 = nn.Linear(w.shape[1], w.shape[0], bias=False, device="meta")
         self.w13.weight = nn.Parameter(w, requires_grad=False)
         del self.w1, self.w3
@@ -211,21 +238,28 @@ class FeedForward(nn.Module):
     def _gate_up(self, x):
         if self.w13 is None:
             return self.w1(x), self.w3(x)
-        h = self.w13(x)
-        n = h.shape[-1] // 2
-        return h[..., :n], h[..., n:]
+        h = self.w13(x).unflatten(-1, (-1, 2))
+        return h[..., 0], h[..., 1]
 
     def forward(self, x):
         a, b = self._gate_up(x)
         return self.w2(F.silu(a) * b)
 
-    def forward_fused(self, x, residual):
+    def forward_fused(self, x, residual, norm=None):
         from torchao._models.llama import kernels
 
-        a, b = self._gate_up(x)
-        if x.numel() != x.shape[-1]:  # the kernel wants contiguous halves (one token)
-            a, b = a.contiguous(), b.contiguous()
-        return _linear_plus(kernels.silu_mul(a, b), self.w2, residual)
+        if norm is not None:
+            w13 = _int4_parts(self.w13)
+            if w13 is not None:  # RMSNorm -> w13 -> SwiGLU in one launch
+                g = kernels.int4_decode(x, *w13, norm_weight=norm.weight, eps=norm.eps,
+                                        epilogue="swiglu")
+                return _linear_plus(g, self.w2, residual)
+            x = kernels.rmsnorm(x, norm.weight, norm.eps)
+        if self.w13 is not None:
+            g = kernels.silu_mul(self.w13(x))
+        else:
+            g = kernels.silu_mul(self.w1(x), self.w3(x))
+        return _linear_plus(g, self.w2, residual)
 
 
 class TransformerBlock(nn.Module):
@@ -241,12 +275,8 @@ class TransformerBlock(nn.Module):
         return h + self.feed_forward(self.ffn_norm(h))
 
     def forward_fused(self, x, freqs_table, input_pos):
-        from torchao._models.llama import kernels
-
-        a = kernels.rmsnorm(x, self.attention_norm.weight, self.attention_norm.eps)
-        h = self.attention.forward_fused(a, freqs_table, input_pos, x)
-        f = kernels.rmsnorm(h, self.ffn_norm.weight, self.ffn_norm.eps)
-        return self.feed_forward.forward_fused(f, h)
+        h = self.attention.forward_fused(x, freqs_table, input_pos, x, self.attention_norm)
+        return self.feed_forward.forward_fused(h, h, self.ffn_norm)
 
 
 class Transformer(nn.Module):
@@ -295,17 +325,32 @@ class Transformer(nn.Module):
         self.fused = bool(enable and ok)
         return self.fused
 
+    def _forward_fused(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
+        """One token per sequence through the fused kernels -> bf16 logits [B, 1, vocab]."""
+        from torchao._models.llama import kernels
+
+        x = self.tok_embeddings(idx)
+        for blk in self.layers:
+            x = blk.forward_fused(x, self.freqs, input_pos)
+        head = _int4_parts(self.output) if x.numel() == x.shape[-1] else None
+        if head is not None:  # final RMSNorm inside the head GEMV
+            return kernels.int4_decode(x, *head, norm_weight=self.norm.weight, eps=self.norm.eps)
+        return self.output(kernels.rmsnorm(x, self.norm.weight, self.norm.eps))
+
+    def decode_next(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
+        """Greedy next token [B, 1] for one token per sequence; on the fused path the argmax
+        runs on the bf16 logits (the same maximum as on their fp32 image, no conversion)."""
+        if self.fused and idx.shape[1] == 1:
+            from torchao._models.llama import kernels
+
+            return kernels.argmax(self._forward_fused(idx, input_pos)[:, -1]).to(idx.dtype)
+        return self(idx, input_pos)[:, -1].argmax(dim=-1, keepdim=True).to(idx.dtype)
+
     def forward(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
         """idx [B, S] token ids at positions input_pos [S] -> logits [B, S, vocab] (fp32)."""
         assert self.max_seq > 0, "call setup_caches() first"
         if self.fused and idx.shape[1] == 1:
-            from torchao._models.llama import kernels
-
-            x = self.tok_embeddings(idx)
-            for blk in self.layers:
-                x = blk.forward_fused(x, self.freqs, input_pos)
-            x = kernels.rmsnorm(x, self.norm.weight, self.norm.eps)
-            return self.output(x).float()
+            return self._forward_fused(idx, input_pos).float()
         mask = self.causal_mask[None, None, input_pos]  # [1, 1, S, T]
         freqs = self.freqs[input_pos]
         x = self.tok_embeddings(idx)
