@@ -173,7 +173,8 @@ int tao_rope_kv_bf16(const uint16_t* qkv, const float* freqs, const int64_t* pos
                      int64_t H, int64_t Hkv, int64_t D, int64_t T, void* stream);
 
 /* One-query attention over keys 0..pos[0] of the caches, GQA (H % Hkv == 0, H/Hkv <= 8),
- * D == 128: out [B][1][H*D] bf16. partial: fp32 workspace of B*Hkv*ceil(T/64)*(H/Hkv)*(D+2).
+ * D == 128: out [B][1][H*D] bf16. partial: fp32 workspace of B*Hkv*ceil(T/64)*(H/Hkv)*(D+2),
+ * used only when T > 1024 (shorter caches run one single-pass kernel and may pass NULL).
  * Replaces F.scaled_dot_product_attention at decode (model.py:441-476). */
 int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
                          const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,

@@ -143,9 +143,10 @@ def test_fused_kernels_match_torch_ops_gpu():
     torch.testing.assert_close(kc[:, :, 17:18], k_ref, rtol=1e-2, atol=1e-2)
     assert torch.equal(vc[:, :, 17:18], vr.view(1, 1, Hkv, D).transpose(1, 2))
 
-    # attention over keys 0..L-1 with L spanning several 64-key chunks
-    for L in (1, 63, 64, 65, 200):
-        T = 256
+    # attention over keys 0..L-1: the single-pass kernel (T <= 1024: L across its 16-key wave
+    # steps and 128-key rounds) and the chunk-split pair (T > 1024: L across 64-key chunks)
+    for T, L in ((256, 1), (256, 15), (256, 17), (256, 63), (256, 128), (256, 129), (256, 200),
+                 (1024, 1024), (1536, 1), (1536, 65), (1536, 1100), (1536, 1536)):
         kc = torch.randn(2, Hkv, T, D, device=dev, dtype=torch.bfloat16)
         vc = torch.randn_like(kc)
         q = torch.randn(2, H, 1, D, device=dev, dtype=torch.bfloat16)

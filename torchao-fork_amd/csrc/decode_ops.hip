@@ -7,9 +7,10 @@
 //   * RMSNorm:   y = bf16(bf16(x * rsqrt(mean(x^2) + eps)) * w)        (model.py RMSNorm)
 //   * RoPE + KV: rotate q, k of the wqkv output in fp32 (interleaved pairs, rotary table row
 //                pos[s]), write q as [B][H][S][D] and k, v into the static caches at pos[S]
-//   * attention: one query per (batch, head), keys 0..pos (GQA: a workgroup serves the G query
-//                heads of one kv head); split over 64-key chunks (flash-decoding), then a
-//                combine kernel merges the chunks' (max, sum, o) in fp32 -> bf16
+//   * attention: one query per (batch, head), keys 0..pos. Caches of <= 1024 rows: one kernel,
+//                a workgroup per query head (online softmax per wave, LDS merge). Longer:
+//                split over 64-key chunks (flash-decoding; GQA: a workgroup serves the G query
+//                heads of one kv head), then a combine kernel merges the chunks' (max, sum, o)
 //   * SiLU-mul:  y = bf16(bf16(silu(a)) * b)                             (F.silu(w1 x) * w3 x)
 //   * argmax:    greedy next token over bf16 logits, torch.argmax's first-index tie rule
 #include "tao_common.h"
@@ -227,6 +228,110 @@ __global__ __launch_bounds__(64) void attn_combine_kernel(const float* __restric
       (uint32_t)f32_to_bf16(o0 * inv) | ((uint32_t)f32_to_bf16(o1 * inv) << 16);
 }
 
+// ---- decode attention in one launch (short caches): one workgroup per (batch, query head) -----
+// 8 waves; wave w takes keys w*16 + 128 i: 4 lanes per key (lane p holds dims v*32 + 8p + e of
+// q in registers, so each 16-B K load of 4 lanes is 64 contiguous bytes), the 16 keys' V rows
+// loaded in the same round trip (lane = dim pair). Online softmax per wave in fp32, waves
+// merged through LDS. Every wave walks ceil((L - 16 w) / 128) steps, so at T <= 1024 the chain
+// is <= 8 round trips; longer caches take the two-kernel split above.
+constexpr int kSingleMaxT = 1024;
+
+template <int D>
+__global__ __launch_bounds__(512) void attn_single_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
+    int H, int Hkv, int T, float scale) {
+  static_assert(D == 128, "head_dim 128");
+  constexpr int NW = 8;
+  __shared__ float qs[D];
+  __shared__ float wm[NW], wl[NW];
+  __shared__ float wo[NW][D];
+  const int bh = blockIdx.x;  // b * H + h
+  const int b = bh / H, h = bh % H, kvh = h / (H / Hkv);
+  const int L = (int)pos[0] + 1;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (tid < D) qs[tid] = bf16_to_f32(q[(size_t)bh * D + tid]);
+  __syncthreads();
+  const int kq = lane >> 2, p = lane & 3;
+  float qr[32];
+#pragma unroll
+  for (int v = 0; v < 4; ++v)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qr[v * 8 + e] = qs[v * 32 + p * 8 + e];
+  const size_t head = (size_t)(b * Hkv + kvh) * T;
+  const uint16_t* kb = kc + head * D + p * 8;
+  const uint32_t* vb = reinterpret_cast<const uint32_t*>(vc + head * D) + lane;
+
+  float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
+  for (int t0 = wave * 16; t0 < L; t0 += NW * 16) {
+    const int t = t0 + kq;
+    const int tc = t < L ? t : L - 1;  // clamped loads, masked below
+    uint4 kv[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) kv[v] = *reinterpret_cast<const uint4*>(kb + (size_t)tc * D + v * 32);
+    uint32_t vv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int tj = t0 + j < L ? t0 + j : L - 1;
+      vv[j] = vb[(size_t)tj * (D / 2)];
+    }
+    float sc = 0.f;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const uint32_t w[4] = {kv[v].x, kv[v].y, kv[v].z, kv[v].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        sc = fmaf(qr[v * 8 + 2 * e], bf16lo_to_f32(w[e]),
+                  fmaf(qr[v * 8 + 2 * e + 1], bf16hi_to_f32(w[e]), sc));
+    }
+    sc += __shfl_xor(sc, 1, 64);
+    sc += __shfl_xor(sc, 2, 64);
+    sc = t < L ? sc * scale : -INFINITY;
+    float mx = sc;
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    const float mn = fmaxf(m, mx);  // finite: key t0 < L is valid
+    const float corr = __expf(m - mn);
+    const float e = t < L ? __expf(sc - mn) : 0.f;
+    float es = e;  // each key sits in 4 lanes; the xor 4..32 sum counts it once
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) es += __shfl_xor(es, o, 64);
+    l = fmaf(l, corr, es);
+    o0 *= corr;
+    o1 *= corr;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float pj = __shfl(e, j * 4, 64);
+      o0 = fmaf(pj, bf16lo_to_f32(vv[j]), o0);
+      o1 = fmaf(pj, bf16hi_to_f32(vv[j]), o1);
+    }
+    m = mn;
+  }
+  if (lane == 0) {
+    wm[wave] = m;
+    wl[wave] = l;
+  }
+  wo[wave][2 * lane] = o0;
+  wo[wave][2 * lane + 1] = o1;
+  __syncthreads();
+  if (wave == 0) {
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w]);
+    float a0 = 0.f, a1 = 0.f, ls = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const float f = wm[w] == -INFINITY ? 0.f : __expf(wm[w] - M);  // waves with no keys
+      ls = fmaf(wl[w], f, ls);
+      a0 = fmaf(wo[w][2 * lane], f, a0);
+      a1 = fmaf(wo[w][2 * lane + 1], f, a1);
+    }
+    const float inv = 1.f / ls;
+    reinterpret_cast<uint32_t*>(out)[(size_t)bh * (D / 2) + lane] =
+        (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
+  }
+}
+
 // ---- SiLU(a) * b ----------------------------------------------------------------------------
 __device__ __forceinline__ uint16_t silu_mul1(float v, float m) {
   return f32_to_bf16(round_bf16(v / (1.f + __expf(-v))) * m);
@@ -343,8 +448,13 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
   const int G = (int)(H / Hkv);
   TAO_CHECK_ARG(G == 1 || G == 2 || G == 4 || G == 8, "attn_decode: H / Hkv must be 1, 2, 4 or 8");
   TAO_CHECK_ALIGN(k_cache, 16, "k_cache");
-  const int NC = (int)((T + kChunk - 1) / kChunk);
   hipStream_t st = as_stream(stream);
+  if (T <= kSingleMaxT) {  // partial is not touched
+    launch(attn_single_kernel<128>, dim3((unsigned)(B * H)), dim3(512), 0, st, q, k_cache,
+           v_cache, pos, out, (int)H, (int)Hkv, (int)T, scale);
+    return check_launch("attn_single_kernel");
+  }
+  const int NC = (int)((T + kChunk - 1) / kChunk);
   const dim3 g1((unsigned)(B * Hkv), (unsigned)NC), g2((unsigned)(B * H));
   switch (G) {
 #define TAO_ATTN(GG)                                                                          \

@@ -51,12 +51,15 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     B, H, S, D = q.shape
     assert S == 1, "attn_decode takes one query per (batch, head)"
     _, Hkv, T, _ = k_cache.shape
-    nc = (T + 63) // 64
-    part = torch.empty(B * Hkv * nc * (H // Hkv) * (D + 2), dtype=torch.float32, device=q.device)
+    part = None
+    if T > 1024:  # split-over-chunks path (shorter caches run one single-pass kernel)
+        nc = (T + 63) // 64
+        part = torch.empty(B * Hkv * nc * (H // Hkv) * (D + 2), dtype=torch.float32,
+                           device=q.device)
     out = torch.empty(B, 1, H * D, dtype=q.dtype, device=q.device)
     _lib.call("tao_attn_decode_bf16", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
-              pos.data_ptr(), part.data_ptr(), out.data_ptr(), B, H, Hkv, D, T, float(scale),
-              _stream(q))
+              pos.data_ptr(), None if part is None else part.data_ptr(), out.data_ptr(), B, H,
+              Hkv, D, T, float(scale), _stream(q))
     return out
 
 
