@@ -186,8 +186,24 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
 int tao_silu_mul_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t n,
                       void* stream);
 
-/* out[r] = argmax over n bf16 logits of row r (first index of the maximum; NaN counts as the
- * maximum) as int64. Replaces logits.argmax(dim=-1) of the greedy decode
+/* Fused int4 weight quantizer (Int4WeightOnlyConfig's from_hp_to_intx in one pass):
+ * w [rows][K] bf16 -> packed [rows][K/8] (row-stream nibbles, as tao_int4_pack) and
+ * scales_and_zeros [rows][K/g][2] bf16, per group of g: s = clamp(bf16(bf16(max-min)/15), eps),
+ * z = bf16(min + 8 s), q = clamp(rint(bf16(bf16(w - bf16(z - 8 s)) / s)), 0, 15), each step
+ * rounded to bf16 as the reference's torch ops do (_choose_qparams_affine_tinygemm
+ * quant_primitives.py:1238-1307, _quantize_affine_tinygemm :461-573). g in {32,64,128,256}. */
+int tao_int4_quantize_bf16(const uint16_t* w, uint32_t* packed, uint16_t* scales_and_zeros,
+                           int64_t rows, int64_t K, int64_t group_size, float eps, void* stream);
+
+/* Fused symmetric per-row int8 weight quantizer (Int8WeightOnlyConfig /
+ * Int8DynamicActivationInt8WeightConfig weights; choose_qparams_affine SYMMETRIC +
+ * quantize_affine, quant_primitives.py): s[r] = bf16(max(bf16(max|w[r]| / 127.5), eps)),
+ * q = clamp(rint(bf16(w * bf16(1 / s))), -128, 127). K % 8 == 0. */
+int tao_int8_quantize_rows_bf16(const uint16_t* w, int8_t* q, uint16_t* scale, int64_t rows,
+                                int64_t K, float eps, void* stream);
+
+/* out[r] = argmax over n bf16 logits of row r (first index of the maximum; a positive-sign NaN
+ * counts as the maximum, as in torch.argmax) as int64. Replaces logits.argmax(dim=-1) of the greedy decode
  * (generate.py:111-142, sample with temperature 0). */
 int tao_argmax_bf16(const uint16_t* x, int64_t* out, int64_t rows, int64_t n, void* stream);
 

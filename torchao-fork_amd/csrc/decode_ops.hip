@@ -357,13 +357,20 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(const uint32_t* __restric
 }
 
 // ---- greedy argmax over bf16 logits: one workgroup per row ------------------------------------
-// Key = order-preserving 16-bit image of the bf16 value (NaN above +inf, as torch.argmax treats
-// NaN as the maximum) in the high word, ~index in the low word: the max key is the first index
-// of the max value, torch.argmax's tie rule.
-__device__ __forceinline__ uint64_t argmax_key(uint32_t b, uint32_t idx) {
-  uint32_t k = (b & 0x8000u) ? (~b & 0xFFFFu) : (b | 0x8000u);
-  if ((b & 0x7F80u) == 0x7F80u && (b & 0x7Fu)) k = 0xFFFFu;  // NaN
-  return ((uint64_t)k << 32) | (uint32_t)~idx;
+// bf16 bits b -> signed 16-bit key b ^ (b < 0 ? 0x7FFF : 0), order-preserving (positive-sign NaN
+// above +inf, as torch.argmax ranks NaN the maximum; a negative-sign NaN ranks below -inf). Per
+// round each thread takes 8 x 16 B: packed v_pk_max_i16 over its words, then a second pass over
+// the same registers finds the first index holding that key; across rounds and threads the
+// 64-bit (key, ~index) maximum keeps torch's first-index tie rule.
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s16x2_t argmax_keys(uint32_t w) {
+  const s16x2_t v = __builtin_bit_cast(s16x2_t, w);
+  return v ^ ((v >> (short)15) & (short)0x7FFF);
+}
+
+__device__ __forceinline__ uint64_t pack_key(int k, uint32_t idx) {
+  return ((uint64_t)(uint32_t)(k + 32768) << 32) | (uint32_t)~idx;
 }
 
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
@@ -375,30 +382,42 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const uint16_t* __restrict
   uint64_t best = 0;
   const int64_t nv = ((reinterpret_cast<uintptr_t>(row) & 15) == 0) ? n / 8 : 0;
   const uint4* rv = reinterpret_cast<const uint4*>(row);
-  // 8 loads in flight per thread per round (a 128K-vocab row is two rounds), clamped indices
-  // and masks instead of branches around the loads
-  constexpr int U = 8;
+  constexpr int U = 8;  // 16-B loads in flight per thread per round (a 128K-vocab row: 2 rounds)
   for (int64_t base = 0; base < nv; base += U * 1024) {
     uint4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t i = base + u * 1024 + threadIdx.x;
-      v[u] = rv[i < nv ? i : nv - 1];
+      v[u] = rv[i < nv ? i : nv - 1];  // clamped: a duplicate never beats the first index
     }
+    s16x2_t mx = {(short)-32768, (short)-32768};
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      mx = __builtin_elementwise_max(mx, argmax_keys(v[u].x));
+      mx = __builtin_elementwise_max(mx, argmax_keys(v[u].y));
+      mx = __builtin_elementwise_max(mx, argmax_keys(v[u].z));
+      mx = __builtin_elementwise_max(mx, argmax_keys(v[u].w));
+    }
+    const int km = mx.x > mx.y ? mx.x : mx.y;
+    uint32_t first = 0xFFFFFFFFu;
+#pragma unroll
+    for (int u = U - 1; u >= 0; --u) {  // descending, so the last hit written is the first index
       const int64_t i = base + u * 1024 + threadIdx.x;
       const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t k = (uint32_t)(i * 8 + 2 * j);
-        const uint64_t m = umax64(argmax_key(d[j] & 0xFFFFu, k), argmax_key(d[j] >> 16, k + 1));
-        best = i < nv ? umax64(best, m) : best;
+      for (int j = 3; j >= 0; --j) {
+        const s16x2_t k = argmax_keys(d[j]);
+        const uint32_t e = (uint32_t)(i * 8 + 2 * j);
+        first = (int)k.y == km ? e + 1 : first;
+        first = (int)k.x == km ? e : first;
       }
     }
+    best = umax64(best, pack_key(km, first));
   }
-  for (int64_t i = nv * 8 + threadIdx.x; i < n; i += 1024)  // tail (or unaligned rows)
-    best = umax64(best, argmax_key(row[i], (uint32_t)i));
+  for (int64_t i = nv * 8 + threadIdx.x; i < n; i += 1024) {  // tail (or unaligned rows)
+    const s16x2_t k = argmax_keys(row[i]);
+    best = umax64(best, pack_key(k.x, (uint32_t)i));
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) best = umax64(best, __shfl_xor(best, o, 64));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;

@@ -55,6 +55,8 @@ _SIGNATURES = {
                              ctypes.c_float, _p],
     "tao_silu_mul_bf16": [_p, _p, _p, _i64, _p],
     "tao_argmax_bf16": [_p, _p, _i64, _i64, _p],
+    "tao_int4_quantize_bf16": [_p, _p, _p, _i64, _i64, _i64, ctypes.c_float, _p],
+    "tao_int8_quantize_rows_bf16": [_p, _p, _p, _i64, _i64, ctypes.c_float, _p],
     "tao_int4wo_decode_bf16": [_p, _p, _p, _i64, _i64, _i64, _p, ctypes.c_float, _int, _p, _p,
                                _p, _p, _p, _i64, _i64, _i64, _i64, _p],
 }

@@ -38,6 +38,64 @@ __all__ = [
 ]
 
 
+def _fused_weight_quant(x, mapping_type, block_size, target_dtype, quant_min, quant_max, eps,
+                        scale_dtype, zero_point_dtype, preserve_zero, zero_point_domain, layout):
+    """The tensor impl from one fused gfx950 quantizer kernel, or None to take the torch-op
+    path. Covers the two weight recipes of the hot path on bf16 CUDA weights, with results
+    bit-identical to the torch-op path (tests/test_gpu_quantize.py):
+      * int4 tinygemm (Int4WeightOnlyConfig): ASYMMETRIC, FLOAT zero domain, preserve_zero
+        False, [0, 15], blocks (1, ..., g) -> torchao::int4_quantize_pack straight into the
+        TensorCoreTiledLayout impl (no int32 [N, K] intermediate, no separate pack);
+      * int8 symmetric per row (Int8WeightOnlyConfig, int8 dyn weights): SYMMETRIC, blocks
+        (1, ..., K), [-128, 127] -> torchao::int8_quantize_rows into the PlainLayout impl."""
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() in (2, 3) and eps is not None):
+        return None
+    if any(b != 1 for b in block_size[:-1]):
+        return None
+    K = x.shape[-1]
+    g = block_size[-1]
+    from torchao.dtypes.uintx.tensor_core_tiled_layout import (
+        TensorCoreTiledAQTTensorImpl,
+        TensorCoreTiledLayout,
+    )
+
+    if (
+        isinstance(layout, TensorCoreTiledLayout)
+        and mapping_type is MappingType.ASYMMETRIC
+        and zero_point_domain == ZeroPointDomain.FLOAT
+        and not preserve_zero
+        and target_dtype == torch.int32
+        and (quant_min, quant_max) == (0, 15)
+        and g in (32, 64, 128, 256)
+        and K % g == 0
+        and scale_dtype in (None, torch.bfloat16)
+        and zero_point_dtype in (None, torch.bfloat16)
+    ):
+        packed, sz = torch.ops.torchao.int4_quantize_pack(x, g, float(eps))
+        return TensorCoreTiledAQTTensorImpl(packed, sz, False, layout)
+    if (
+        type(layout) is PlainLayout
+        and mapping_type is MappingType.SYMMETRIC
+        and zero_point_domain in (ZeroPointDomain.INT, ZeroPointDomain.NONE)
+        and preserve_zero
+        and target_dtype == torch.int8
+        and quant_min in (None, -128)
+        and quant_max in (None, 127)
+        and g == K
+        and K % 8 == 0
+        and scale_dtype in (None, torch.bfloat16)
+    ):
+        q, scale = torch.ops.torchao.int8_quantize_rows(x, float(eps))
+        zero_point = None
+        if zero_point_domain == ZeroPointDomain.INT:
+            zero_point = torch.zeros_like(scale, dtype=zero_point_dtype or torch.int32)
+        q, scale, zero_point = layout.post_process(q, scale, zero_point, block_size)
+        return AffineQuantizedTensor.get_tensor_impl_constructor(type(layout))(
+            q, scale, zero_point, layout
+        )
+    return None
+
+
 class AffineQuantizedTensor(TorchAOBaseTensor):
     """float_tensor ~= dequantize(tensor_impl) with qparams shared over ``block_size`` blocks.
 
@@ -178,6 +236,20 @@ class AffineQuantizedTensor(TorchAOBaseTensor):
             raise NotImplementedError("HQQ quantization is outside the MI355X hot-path scope")
         original_shape = input_float.shape
         input_float = _layout.pre_process(input_float)
+        fused = _fused_weight_quant(
+            input_float, mapping_type, block_size, target_dtype, quant_min, quant_max, eps,
+            scale_dtype, zero_point_dtype, preserve_zero, zero_point_domain, _layout,
+        )
+        if fused is not None:
+            return cls(
+                fused,
+                block_size,
+                original_shape,
+                quant_min,
+                quant_max,
+                zero_point_domain,
+                dtype=input_float.dtype,
+            )
         if zero_point_domain == ZeroPointDomain.FLOAT and not preserve_zero:
             scale, zero_point = _choose_qparams_affine_tinygemm(
                 input_float, mapping_type, block_size, target_dtype, quant_min, quant_max, eps,

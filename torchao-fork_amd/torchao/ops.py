@@ -18,6 +18,9 @@ Operators:
   * ``int8_weight_only_linear`` — replaces mm + scale (plain_layout.py:256-266).
   * ``int8_quantize_per_token`` / ``int8_scaled_mm`` — replace the activation quant
     (quant_api.py:1258-1273) and ``int_scaled_matmul`` + weight scale (plain_layout.py:294-315).
+  * ``int4_quantize_pack`` / ``int8_quantize_rows`` — the weight quantizers of
+    ``from_hp_to_intx`` in one pass each (tinygemm qparams + quantize + row-stream pack;
+    symmetric per-row int8), bit-exact to the bf16 torch-op formulation.
 """
 
 import ctypes
@@ -50,6 +53,8 @@ lib.define(
     "int8_weight_only_linear(Tensor x, Tensor w_int8, Tensor scale, Tensor? bias=None) -> Tensor"
 )
 lib.define("int8_quantize_per_token(Tensor x) -> (Tensor, Tensor)")
+lib.define("int4_quantize_pack(Tensor w, int group_size, float eps) -> (Tensor, Tensor)")
+lib.define("int8_quantize_rows(Tensor w, float eps) -> (Tensor, Tensor)")
 lib.define(
     "int8_scaled_mm(Tensor x_int8, Tensor x_scale, Tensor w_int8, Tensor w_scale, "
     "Tensor? bias=None) -> Tensor"
@@ -386,6 +391,58 @@ def _int8_scaled_mm_cuda(x_int8, x_scale, w_int8, w_scale, bias=None):
     return y.reshape(_linear_out_shape(x_int8, N))
 
 
+@torch.library.register_fake("torchao::int4_quantize_pack")
+def _(w, group_size, eps):
+    torch._check(group_size in _GROUP_SIZES, lambda: "group_size must be 32, 64, 128, or 256")
+    K = w.size(-1)
+    torch._check(K % group_size == 0, lambda: f"K ({K}) must be divisible by group_size")
+    lead = w.shape[:-1]
+    return (w.new_empty((*lead, K // 8), dtype=torch.int32),
+            w.new_empty((*lead, K // group_size, 2), dtype=torch.bfloat16))
+
+
+def _int4_quantize_pack_cuda(w: Tensor, group_size: int, eps: float):
+    """bf16 W [..., K] -> (packed int32 [..., K/8], scales_and_zeros bf16 [..., K/g, 2])."""
+    torch._check(w.dtype is torch.bfloat16, lambda: "int4 quantize (HIP) needs a bf16 weight")
+    torch._check(group_size in _GROUP_SIZES, lambda: "group_size must be 32, 64, 128, or 256")
+    K = w.size(-1)
+    torch._check(K % group_size == 0, lambda: f"K ({K}) must be divisible by group_size")
+    w2 = w.reshape(-1, K)
+    if not w2.is_contiguous() or w2.data_ptr() % 16:
+        w2 = w2.contiguous()
+    R = w2.size(0)
+    packed = torch.empty((R, K // 8), dtype=torch.int32, device=w.device)
+    sz = torch.empty((R, K // group_size, 2), dtype=torch.bfloat16, device=w.device)
+    with torch.cuda.device(w.device):
+        _lib.call("tao_int4_quantize_bf16", _ptr(w2), _ptr(packed), _ptr(sz), R, K, group_size,
+                  ctypes.c_float(eps), _stream(w))
+    lead = w.shape[:-1]
+    return packed.reshape(*lead, K // 8), sz.reshape(*lead, K // group_size, 2)
+
+
+@torch.library.register_fake("torchao::int8_quantize_rows")
+def _(w, eps):
+    return (w.new_empty(w.shape, dtype=torch.int8),
+            w.new_empty(w.shape[:-1], dtype=torch.bfloat16))
+
+
+def _int8_quantize_rows_cuda(w: Tensor, eps: float):
+    """bf16 W [..., K] -> (int8 [..., K], per-row scale bf16 [...]), symmetric [-128, 127]."""
+    torch._check(w.dtype is torch.bfloat16, lambda: "int8 quantize (HIP) needs a bf16 weight")
+    K = w.size(-1)
+    torch._check(K % 8 == 0, lambda: f"K ({K}) must be a multiple of 8")
+    w2 = w.reshape(-1, K)
+    if not w2.is_contiguous() or w2.data_ptr() % 16:
+        w2 = w2.contiguous()
+    R = w2.size(0)
+    q = torch.empty((R, K), dtype=torch.int8, device=w.device)
+    s = torch.empty((R,), dtype=torch.bfloat16, device=w.device)
+    with torch.cuda.device(w.device):
+        _lib.call("tao_int8_quantize_rows_bf16", _ptr(w2), _ptr(q), _ptr(s), R, K,
+                  ctypes.c_float(eps), _stream(w))
+    return q.reshape(w.shape), s.reshape(w.shape[:-1])
+
+
 # ---- register device impls ------------------------------------------------------------------
 for _name, _fn in [
     ("unpack_tensor_core_tiled_layout", _unpack_tile_cuda),
@@ -398,6 +455,8 @@ for _name, _fn in [
     ("int4_weight_only_linear", _int4_linear_cuda),
     ("int8_weight_only_linear", _int8wo_linear_cuda),
     ("int8_quantize_per_token", _int8_quant_cuda),
+    ("int4_quantize_pack", _int4_quantize_pack_cuda),
+    ("int8_quantize_rows", _int8_quantize_rows_cuda),
     ("int8_scaled_mm", _int8_scaled_mm_cuda),
 ]:
     lib.impl(_name, _fn, "CUDA")
