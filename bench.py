@@ -12,11 +12,12 @@ Int4WeightOnlyConfig(group_size=32) math and packed by the HIP pack kernel; acti
 synthetic N(0,1) bf16; everything is resident in HBM before timing. The step is captured once
 in a HIP graph and replayed.
 
-N GPUs (torchrun, one rank per GPU): the large linears (N*K >= --shard-min-elems: the merged
-w1||w3 and the output head of the 8B; every linear of a 70B) are column-sharded (rank r owns
-output rows [r N/P, (r+1) N/P)) and their outputs all-gathered over RCCL after each GEMV
-(north star); the small ones run whole on every rank, because an M = 1 gather
-(~10 µs, latency-bound) costs more than their GEMV (4-9 µs). --shard-all shards every linear.
+N GPUs (torchrun, one rank per GPU): a linear is column-sharded (rank r owns output rows
+[r N/P, (r+1) N/P)) with its output all-gathered over RCCL after each GEMV (north star,
+SURVEY §8e) when that is faster than running it whole on every rank: at startup every distinct
+(N, K) is timed both ways (whole GEMV vs N/P GEMV + all-gather, max over ranks;
+--shard-policy auto). An M = 1 gather is latency-bound (~10 µs class), so at 8B sizes only the
+large linears can gain. --shard-policy size / all / none override the measurement.
 Total work is fixed as P grows ("strong" scaling); value counts the whole model's bytes once
 per step.
 
@@ -104,6 +105,66 @@ def make_int4_weight(N, K, g, seed, device):
     return packed, sz
 
 
+def calibrate_sharding(shapes, P, g, device, rehearsal, reps=20):
+    """Per (N, K): time the whole-N GEMV and the N/P GEMV + its all-gather (eager launches on
+    the current stream, each shape's weights rotated over copies past the 256 MiB Infinity
+    Cache; GPU events; max over ranks so every rank takes the same decision). An M = 1
+    all-gather is latency-bound (~10 µs class), so only linears whose GEMV saves more than
+    that are worth sharding."""
+    from torchao import _lib
+
+    lib = _lib.lib()
+    sp = torch.cuda.current_stream(device).cuda_stream
+
+    def gemv_us(N, K):
+        copies = max(2, min(32, (512 << 20) // max(1, int4_alg_bytes(N, K, g))))
+        ws = [make_int4_weight(N, K, g, seed=7 + c, device=device) for c in range(copies)]
+        x = torch.randn(1, K, device=device, dtype=torch.bfloat16)
+        y = torch.empty(N, device=device, dtype=torch.bfloat16)
+
+        def go(c):
+            lib.tao_int4wo_linear_bf16(x.data_ptr(), ws[c][0].data_ptr(), ws[c][1].data_ptr(),
+                                       None, y.data_ptr(), 1, N, K, g, sp)
+
+        for c in range(copies):
+            go(c)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(reps):
+            go(i % copies)
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / reps
+
+    def gather_us(N):
+        y_loc = torch.zeros(N // P, device=device, dtype=torch.bfloat16)
+        y = torch.empty(N, device=device, dtype=torch.bfloat16)
+        if rehearsal:
+            return 1e9  # host-staged gloo gathers: never worth it
+        for _ in range(3):
+            dist.all_gather_into_tensor(y, y_loc)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            dist.all_gather_into_tensor(y, y_loc)
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / reps
+
+    out = {}
+    for N, K in shapes:
+        if N % P:
+            continue
+        t = torch.tensor([gemv_us(N, K), gemv_us(N // P, K), gather_us(N)], dtype=torch.float64,
+                         device="cpu" if rehearsal else device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        whole, part, gather = (float(v) for v in t.tolist())
+        out[(N, K)] = {"whole_us": round(whole, 2), "shard_us": round(part, 2),
+                       "allgather_us": round(gather, 2), "shard": part + gather < 0.95 * whole}
+        torch.cuda.empty_cache()
+    return out
+
+
 def cpu_baseline(cfg, g, budget_s=12.0):
     """The reference CPU dequant path (oracle restatement) on one layer's five linears, M = 1."""
     from oracle import oracle
@@ -163,10 +224,13 @@ def main():
     ap.add_argument("--group-size", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--shard-policy", default="auto", choices=["auto", "size", "all", "none"],
+                    help="P > 1: which linears to column-shard. auto = per (N, K), whichever of "
+                         "{whole GEMV on every rank, N/P GEMV + all-gather} measured faster "
+                         "at startup (max over ranks); size = N*K >= --shard-min-elems")
     ap.add_argument("--shard-min-elems", type=int, default=64 << 20,
-                    help="P > 1: column-shard a linear when N*K >= this (default 64 Mi: the "
-                         "8B w1||w3 and output head; every 70B linear)")
-    ap.add_argument("--shard-all", action="store_true", help="P > 1: shard every linear")
+                    help="--shard-policy size: shard when N*K >= this")
+    ap.add_argument("--shard-all", action="store_true", help="= --shard-policy all")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = rehearsal of the P > 1 path on one GPU (all ranks on device 0)")
     ap.add_argument("--no-fuse-w13", action="store_true",
@@ -198,6 +262,11 @@ def main():
     _lib.lib()  # fail loudly if the native library is missing
     cfg, g, P = LLAMA3_8B, args.group_size, world
     lins = llama_linears(cfg, fuse_w13=not args.no_fuse_w13)
+    policy = "all" if args.shard_all else args.shard_policy
+    calib = {}
+    if P > 1 and policy == "auto":
+        calib = calibrate_sharding(sorted({(N, K) for _, N, K in lins}), P, g, device,
+                                   rehearsal)
 
     # ---- build the sharded weights, inputs and outputs (all resident in HBM) ----
     plan, bytes_per_step = [], 0
@@ -206,7 +275,12 @@ def main():
     for i, (name, N, K) in enumerate(lins):
         # column-shard the large linears (north star); a small one is cheaper to run whole on
         # every rank than to shard and gather (an M = 1 gather costs more than its GEMV)
-        shard = P > 1 and N % P == 0 and (args.shard_all or N * K >= args.shard_min_elems)
+        if P == 1 or N % P or policy == "none":
+            shard = False
+        elif policy == "auto":
+            shard = calib[(N, K)]["shard"]
+        else:
+            shard = policy == "all" or N * K >= args.shard_min_elems
         n_sharded += shard
         n_loc = N // P if shard else N
         packed, sz = make_int4_weight(n_loc, K, g, seed=1000 * i + (rank if shard else 0),
@@ -364,7 +438,7 @@ def main():
                 "group_size": g,
                 "bytes_per_step": bytes_per_step,
                 "parallelism": (f"colwise-tp{P} + RCCL all-gather on {n_sharded} of {len(plan)} "
-                                f"linears (N*K >= {args.shard_min_elems}), rest replicated"
+                                f"linears (shard policy {policy}), rest replicated"
                                 if P > 1 else "single-gpu"),
                 "hip_graph": graph is not None,
             },
@@ -388,6 +462,8 @@ def main():
         }
         if comm_ms is not None:
             rec["allgather_ms_per_step"] = round(comm_ms, 4)
+        if calib:
+            rec["shard_calibration_us"] = {f"{N}x{K}": v for (N, K), v in calib.items()}
         if cpu is not None:
             rec["speedup_vs_cpu_baseline"] = round(rec["value"] / cpu["value"], 1)
         print(json.dumps(rec), flush=True)
