@@ -98,3 +98,32 @@ def test_quantize_fast_path_is_bit_identical(config):
         assert torch.equal(a, b), n
     x = torch.randn(3, 1024, dtype=torch.bfloat16, device=DEV)
     assert torch.equal(fast(x), slow(x))
+
+
+def test_moe_3d_weights_per_expert():
+    """3-D [E, N, K] weights (reference per-expert packing, tensor_core_tiled_layout.py:283-294):
+    the fused quantizer packs all experts in one launch, each expert slice equals quantizing that
+    expert alone, and an expert's linear (AQT index, as the MoE modules do) runs the int4 kernel."""
+    import torch.nn.functional as F
+
+    from torchao.dtypes import TensorCoreTiledLayout, to_affine_quantized_intx
+    from torchao.quantization.quant_primitives import MappingType, ZeroPointDomain
+
+    def quant(w):
+        return to_affine_quantized_intx(
+            w, MappingType.ASYMMETRIC, tuple([1] * (w.dim() - 1) + [32]), torch.int32, 0, 15,
+            1e-6, zero_point_dtype=torch.bfloat16, preserve_zero=False,
+            zero_point_domain=ZeroPointDomain.FLOAT, _layout=TensorCoreTiledLayout(8))
+
+    E, N, K = 4, 256, 512
+    w = torch.stack([orc.make_linear_weight(N, K, seed=50 + e) for e in range(E)]).to(DEV)
+    qw = quant(w)
+    assert qw.shape == (E, N, K) and qw.tensor_impl.packed_weight.shape == (E, N, K // 8)
+    x = torch.randn(5, K, dtype=torch.bfloat16, device=DEV)
+    for e in range(E):
+        alone = quant(w[e].contiguous())
+        assert torch.equal(qw[e].tensor_impl.packed_weight, alone.tensor_impl.packed_weight)
+        assert torch.equal(qw[e].tensor_impl.scale_and_zero, alone.tensor_impl.scale_and_zero)
+        y = F.linear(x, qw[e])
+        ref = F.linear(x.float(), qw[e].dequantize().float())
+        assert ((y.float() - ref).norm() / ref.norm()) < 1e-2
