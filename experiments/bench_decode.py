@@ -2,7 +2,7 @@
 shapes, one graph of L launches over L distinct weight copies (no cache reuse across layers,
 like the real decode step). Prints one JSON line per (op, variant, tune shape).
 
-    python experiments/bench_decode.py [--layers 32] [--sweep]
+    python experiments/bench_decode.py [--layers 32] [--sweep] [--model 8b|70b]
 """
 import argparse
 import itertools
@@ -51,9 +51,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--model", default="8b", choices=["8b", "70b"])
     args = ap.parse_args()
     L = args.layers
     K, H, Hkv, D, T, I = 4096, 32, 8, 128, 512, 14336
+    if args.model == "70b":
+        K, H, I = 8192, 64, 28672
     x = torch.randn(1, 1, K, device=DEV, dtype=torch.bfloat16)
     nw = (torch.rand(K, device=DEV) + 0.5).to(torch.bfloat16)
     freqs = torch.randn(T, D // 2, 2, device=DEV)
@@ -94,7 +97,7 @@ def main():
                 kernels.int4_decode(x, p, sz, g, norm_weight=nw if use_norm else None, eps=1e-5,
                                     epilogue=epi, rope=rope)
 
-            res = {"op": name, "tune": t, "fused_us": round(time_graph(fused, n), 3),
+            res = {"model": args.model, "op": name, "tune": t, "fused_us": round(time_graph(fused, n), 3),
                    "fused_nonorm_us": round(time_graph(lambda i: fused(i, False), n), 3)}
             if t == (0, 0, 0, 0):
                 res["unfused_us"] = round(time_graph(unfused, n), 3)

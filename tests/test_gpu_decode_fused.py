@@ -48,7 +48,8 @@ def test_plain_matches_linear(N, K, g):
     assert torch.equal(got, lin(x))
 
 
-@pytest.mark.parametrize("N,K", [(512, 4096), (6144, 4096), (128256, 4096), (2048, 8192)])
+@pytest.mark.parametrize("N,K", [(512, 4096), (6144, 4096), (128256, 4096), (2048, 8192),
+                                 (16384, 8192)])  # the last: separate RMSNorm launch
 def test_rmsnorm_prologue(N, K):
     from torchao._models.llama import kernels
 

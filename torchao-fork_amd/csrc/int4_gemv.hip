@@ -33,7 +33,7 @@ namespace {
 //   kEpiRopeKV  rows = [q | k | v] heads of wqkv: q rotated into y, k rotated and v stored
 //               into the caches at pos[0] (Attention.forward + KVCache.update).
 enum { kEpiNone = 0, kEpiSwiGLU = 1, kEpiRopeKV = 2 };
-constexpr int kNormPT = 2;  // 16-B pieces of x per thread in the RMSNorm prologue
+constexpr int kMaxNormPT = 4;  // max 16-B pieces of x per thread in the RMSNorm prologue
 struct GemvFuse {
   const uint16_t* norm_w;  // [K] RMSNorm weight (PRO)
   float eps;
@@ -52,11 +52,13 @@ __device__ __forceinline__ uint32_t rmsnorm_pair(uint32_t xv, uint32_t wv, float
 
 // WPE: minimum waves per SIMD the register allocation must allow (8 -> <= 64 VGPRs, so four
 // 512-thread workgroups fit on a CU and mid-size grids run in a single resident round).
-template <int MT, int RPW, int WPE, bool PAIR, bool PRO = false, int EPI = kEpiNone>
+// NPT > 0 enables the RMSNorm prologue with NPT 16-B pieces of x per thread (PRO).
+template <int MT, int RPW, int WPE, bool PAIR, int NPT = 0, int EPI = kEpiNone>
 __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     const uint16_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
     const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K, int gshift,
     int Wk, int G, int S, GemvFuse fu) {
+  constexpr bool PRO = NPT > 0;
   static_assert(!(PRO || EPI) || (MT == 1 && RPW % 2 == 0), "fusions are M == 1, row pairs");
   constexpr int V = RPW * MT;
   extern __shared__ float red[];  // [G][Wk][V] (PRO: + [8] partial sums, + normalised x [K])
@@ -75,20 +77,20 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     for (int m = 0; m < MT; ++m) acc[r][m] = 0.f;
 
   // RMSNorm prologue (PRO): the workgroup normalises x once into LDS. Each thread loads its
-  // <= kNormPT 16-B pieces of x and of the norm weight (the launcher guarantees
-  // K <= 8 * kNormPT * blockDim.x) BEFORE its first slice's weight loads, so the in-order vmcnt
+  // NPT 16-B pieces of x and of the norm weight (the launcher guarantees
+  // K <= 8 * NPT * blockDim.x) BEFORE its first slice's weight loads, so the in-order vmcnt
   // wait for them does not wait for the weights: the sum of squares, the two barriers (reached
   // exactly once by every wave) and the LDS fill all run under the weight-load latency.
   // LDS copy: chunk c (32 k) keeps its four 16-B pieces rotated by c >> 2, so the 16 lanes of a
   // ds_read_b128 pass (consecutive chunks) hit 16 distinct 16-B bank groups.
   uint4* xs = reinterpret_cast<uint4*>(red + ((G * Wk * V + 8 + 3) & ~3));
-  uint4 xv[kNormPT], gv[kNormPT];
+  uint4 xv[NPT > 0 ? NPT : 1], gv[NPT > 0 ? NPT : 1];
   auto norm_load = [&]() __attribute__((always_inline)) {
     const uint4* xr = reinterpret_cast<const uint4*>(x);
     const uint4* gr = reinterpret_cast<const uint4*>(fu.norm_w);
     const int nx = K >> 3;
 #pragma unroll
-    for (int u = 0; u < kNormPT; ++u) {
+    for (int u = 0; u < NPT; ++u) {
       const int i = threadIdx.x + u * (int)blockDim.x;
       const int ic = i < nx ? i : nx - 1;  // clamped, masked below
       xv[u] = xr[ic];
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     const int nx = K >> 3;
     float ss = 0.f;
 #pragma unroll
-    for (int u = 0; u < kNormPT; ++u) {
+    for (int u = 0; u < NPT; ++u) {
       const bool ok = threadIdx.x + u * (int)blockDim.x < nx;
       const uint32_t d[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
 #pragma unroll
@@ -117,7 +119,7 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     for (int w = 0; w < G * Wk; ++w) t += ssr[w];
     const float r = rsqrtf(t / (float)K + fu.eps);
 #pragma unroll
-    for (int u = 0; u < kNormPT; ++u) {
+    for (int u = 0; u < NPT; ++u) {
       const int i = threadIdx.x + u * (int)blockDim.x;
       if (i < nx) {
         const int c = i >> 2;
@@ -332,7 +334,7 @@ GemvShape default_shape(int S) {
   return {wk, g};
 }
 
-template <int MT, int RPW, int WPE, bool PRO = false, int EPI = kEpiNone>
+template <int MT, int RPW, int WPE, int NPT = 0, int EPI = kEpiNone>
 int launch_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
                 const uint16_t* bias, uint16_t* y, int M, int N, int K, int gshift,
                 GemvShape sh, hipStream_t stream, const GemvFuse& fu = GemvFuse{}) {
@@ -342,15 +344,16 @@ int launch_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
   const int rows_per_wg = sh.g * RPW;
   const int grid = (N + rows_per_wg - 1) / rows_per_wg;
   const int threads = 64 * wk * sh.g;
+  constexpr bool PRO = NPT > 0;
   const size_t lds = PRO ? (((size_t)sh.g * wk * RPW * MT + 8 + 3) & ~(size_t)3) * sizeof(float) +
                                (size_t)K * 2
                          : (size_t)sh.g * wk * RPW * MT * sizeof(float);
   if (S > wk)
-    launch((int4wo_gemv_kernel<MT, RPW, WPE, true, PRO, EPI>), dim3(grid), dim3(threads), lds,
+    launch((int4wo_gemv_kernel<MT, RPW, WPE, true, NPT, EPI>), dim3(grid), dim3(threads), lds,
            stream, x, reinterpret_cast<const uint4*>(packed),
            reinterpret_cast<const uint32_t*>(sz), bias, y, M, N, K, gshift, wk, sh.g, S, fu);
   else
-    launch((int4wo_gemv_kernel<MT, RPW, WPE, false, PRO, EPI>), dim3(grid), dim3(threads), lds,
+    launch((int4wo_gemv_kernel<MT, RPW, WPE, false, NPT, EPI>), dim3(grid), dim3(threads), lds,
            stream, x, reinterpret_cast<const uint4*>(packed),
            reinterpret_cast<const uint32_t*>(sz), bias, y, M, N, K, gshift, wk, sh.g, S, fu);
   return check_launch("int4wo_gemv_kernel");
@@ -394,36 +397,48 @@ M1Shape m1_shape(int N, int S) {
   return c;
 }
 
+template <int NPT, int EPI>
+int launch_decode_rows(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
+                       uint16_t* y, int N, int K, int gs, hipStream_t stream, const GemvFuse& fu,
+                       const M1Shape& c) {
+  // row pairs stay inside one wave: 2 or 4 rows per wave; the RMSNorm prologue (the first
+  // slices' loads live across it) does not fit 64 VGPRs, so it runs at <= 4 waves per SIMD
+  if (c.rpw <= 2) {
+    if constexpr (NPT > 0)
+      return launch_gemv<1, 2, 4, NPT, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream,
+                                            fu);
+    else
+      return launch_gemv<1, 2, 8, NPT, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream,
+                                            fu);
+  }
+  if (c.occ == 4 || NPT > 0)
+    return launch_gemv<1, 4, 4, NPT, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream, fu);
+  return launch_gemv<1, 4, 8, 0, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream, fu);
+}
+
 template <bool PRO, int EPI>
 int launch_decode(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, uint16_t* y,
                   int N, int K, int gs, hipStream_t stream, const GemvFuse& fu) {
   const int S = (K / 32 + 63) / 64;
   M1Shape c = m1_shape(N, S);
-  if (PRO) {
-    // Measured (experiments/bench_decode.py, profiles/r1_bench_decode.jsonl): with the prologue
-    // a workgroup should own whole rows (no K split) and 4 waves of them, so the per-workgroup
-    // normalisation is amortised over 8-16 rows; 2 rows per wave below N = 8192.
-    if (g_tune_rpw.load(std::memory_order_relaxed) == 0) c.rpw = N < 8192 ? 2 : 4;
+  if constexpr (PRO) {
+    // Measured (experiments/bench_decode.py, profiles/r1_bench_decode*.jsonl): with the
+    // prologue a workgroup should own whole rows (no K split) and 4 waves of them, so the
+    // per-workgroup normalisation is amortised over 8-16 rows; 2 rows per wave below
+    // N = 16384 (Llama-3-70B wqkv 10240x8192: 14.0 vs 18.0 µs at 4 rows).
+    if (g_tune_rpw.load(std::memory_order_relaxed) == 0) c.rpw = N < 16384 ? 2 : 4;
     if (g_tune_wk.load(std::memory_order_relaxed) == 0) c.sh.wk = 1;
     if (g_tune_g.load(std::memory_order_relaxed) == 0) c.sh.g = 4;
-    // enough threads to hold x in the prologue: K <= 8 * kNormPT * threads
+    // enough threads to hold x in the prologue: K <= 8 * NPT * threads, NPT <= kMaxNormPT
     const int wk = c.sh.wk < S ? c.sh.wk : S;
-    while (64 * wk * c.sh.g * 8 * kNormPT < K && wk * c.sh.g * 2 <= 8) c.sh.g *= 2;
+    while (64 * wk * c.sh.g * 8 * kMaxNormPT < K && wk * c.sh.g * 2 <= 8) c.sh.g *= 2;
+    const int threads = 64 * wk * c.sh.g;
+    if (threads * 8 * 2 >= K)
+      return launch_decode_rows<2, EPI>(x, packed, sz, y, N, K, gs, stream, fu, c);
+    return launch_decode_rows<4, EPI>(x, packed, sz, y, N, K, gs, stream, fu, c);
+  } else {
+    return launch_decode_rows<0, EPI>(x, packed, sz, y, N, K, gs, stream, fu, c);
   }
-  // row pairs stay inside one wave: 2 or 4 rows per wave; the RMSNorm prologue (the first
-  // slices' loads live across it) does not fit 64 VGPRs, so it runs at <= 4 waves per SIMD
-  if (c.rpw <= 2) {
-    if constexpr (PRO)
-      return launch_gemv<1, 2, 4, PRO, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream,
-                                            fu);
-    else
-      return launch_gemv<1, 2, 8, PRO, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream,
-                                            fu);
-  }
-  if (c.occ == 4 || PRO)
-    return launch_gemv<1, 4, 4, PRO, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream, fu);
-  return launch_gemv<1, 4, 8, false, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream,
-                                          fu);
 }
 
 }  // namespace
@@ -501,8 +516,8 @@ extern "C" int tao_int4wo_decode_bf16(const uint16_t* x, const uint32_t* packed,
                 (long long)N);
   if (norm_weight != nullptr) {
     TAO_CHECK_ALIGN(norm_weight, 16, "norm_weight");
-    TAO_CHECK_ARG(K <= 8 * tao::kNormPT * 512, "int4 decode: RMSNorm prologue needs K <= %d",
-                  8 * tao::kNormPT * 512);
+    TAO_CHECK_ARG(K <= 8 * tao::kMaxNormPT * 512,
+                  "int4 decode: RMSNorm prologue needs K <= %d", 8 * tao::kMaxNormPT * 512);
   }
   tao::GemvFuse fu{};
   fu.norm_w = norm_weight;

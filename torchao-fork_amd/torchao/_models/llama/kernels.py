@@ -81,6 +81,15 @@ def silu_mul(a: torch.Tensor, b=None) -> torch.Tensor:
 _EPILOGUES = {"none": 0, "swiglu": 1, "rope_kv": 2}
 
 
+def prologue_pays(N: int, K: int) -> bool:
+    """Whether the RMSNorm prologue inside the GEMV beats a separate RMSNorm launch: every
+    workgroup of the GEMV re-normalises the row, so it pays while K or the grid is small.
+    Measured (experiments/bench_decode.py; profiles/r1_bench_decode*.jsonl): Llama-3-8B wqkv,
+    w1||w3 and head and 70B wqkv gain 2-7 µs; 70B w1||w3 (57344x8192) and head (128256x8192)
+    lose 3-9 µs."""
+    return K <= 4096 or N < 16384
+
+
 def int4_decode(x: torch.Tensor, packed: torch.Tensor, scale_and_zero: torch.Tensor,
                 group_size: int, norm_weight=None, eps: float = 0.0, epilogue: str = "none",
                 rope=None) -> torch.Tensor:
@@ -94,6 +103,8 @@ def int4_decode(x: torch.Tensor, packed: torch.Tensor, scale_and_zero: torch.Ten
         raise RuntimeError(f"int4_decode takes one token, got x of shape {tuple(x.shape)}")
     if norm_weight is not None:
         _check(norm_weight, torch.bfloat16, "int4_decode norm_weight")
+        if not prologue_pays(N, K):  # normalise once in its own launch instead
+            x, norm_weight = rmsnorm(x, norm_weight, eps), None
     epi = _EPILOGUES[epilogue]
     freqs = pos = kc = vc = None
     H = Hkv = D = T = 0
