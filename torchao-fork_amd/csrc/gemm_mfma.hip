@@ -63,35 +63,6 @@ __device__ __forceinline__ bf16x8_t as_bf16x8(uint32_t a, uint32_t b, uint32_t c
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-// ---- buffer resources --------------------------------------------------------------------------
-// All operand loads are raw buffer loads: a wave-uniform 128-bit descriptor, a per-lane 32-bit
-// voffset fixed for the whole launch and a per-step wave-uniform soffset, so the k loop spends
-// no VALU on 64-bit address arithmetic (cdna guide T8/T20). Loads past the descriptor's byte
-// count return 0; callers keep every operand below 4 GiB.
-typedef __amdgpu_buffer_rsrc_t Rsrc;
-constexpr int kNT = 2;  // aux: non-temporal (streamed-once weights)
-
-__device__ __forceinline__ Rsrc make_rsrc(const void* base, uint32_t bytes) {
-  // readfirstlane on the inputs makes the descriptor provably uniform (no waterfall loops)
-  const uint64_t b = reinterpret_cast<uint64_t>(base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-  void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)__builtin_amdgcn_readfirstlane(bytes),
-                                           0x00020000);
-}
-template <int AUX = 0>
-__device__ __forceinline__ uint4 bload16(Rsrc r, uint32_t voff, uint32_t soff) {
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 v =
-      __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX));
-  return make_uint4(v[0], v[1], v[2], v[3]);
-}
-template <int AUX = 0>
-__device__ __forceinline__ uint32_t bload4(Rsrc r, uint32_t voff, uint32_t soff) {
-  return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, AUX);
-}
-
 // ---- policies -------------------------------------------------------------------------------
 // setup(): per-lane state for lane (n, kq) — descriptors and voffsets (once per launch).
 // load(): the raw bytes of the lane's weight piece for step `st` (wave-uniform, clamped to the

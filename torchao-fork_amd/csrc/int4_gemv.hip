@@ -383,8 +383,20 @@ M1Shape m1_shape(int N, int S) {
       c.sh = {2, N <= 4096 ? 1 : 4};
     }
   } else {  // K > 4096: waves split K (each walking its slices in pairs) while N is small
+    // (profiles/r1_sweep_gemv_70b.jsonl, r1_sweep_gemv_shards.jsonl: Llama-3-70B linears and
+    // their 2/4/8-way column shards)
     c.occ = 4;
-    c.sh = {N <= 4096 ? 2 : (S >= 8 ? 1 : 4), 1};
+    if (N >= 32768) {  // heads: 8 rows per wave (128256x8192 93.9 vs 99.7 µs at 4)
+      c.rpw = 8;
+      c.sh = {4, 1};
+    } else if (N <= 2560 && S <= 4) {
+      c.rpw = 2;
+      c.sh = {2, 1};
+    } else if (N <= 2048) {  // few rows, long K: more waves along K (1024x28672 5.7 vs 9.0 µs)
+      c.sh = {N <= 1024 ? 8 : 4, 1};
+    } else {
+      c.sh = {N <= 4096 ? 2 : (S >= 8 ? 1 : 4), 1};
+    }
   }
   const int trpw = g_tune_rpw.load(std::memory_order_relaxed);
   const int tocc = g_tune_occ.load(std::memory_order_relaxed);
@@ -401,6 +413,10 @@ template <int NPT, int EPI>
 int launch_decode_rows(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
                        uint16_t* y, int N, int K, int gs, hipStream_t stream, const GemvFuse& fu,
                        const M1Shape& c) {
+  if constexpr (NPT == 0 && EPI == kEpiNone) {  // the plain linear: the product path's shapes
+    if (c.rpw == 8)
+      return launch_gemv<1, 8, 4>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream);
+  }
   // row pairs stay inside one wave: 2 or 4 rows per wave; the RMSNorm prologue (the first
   // slices' loads live across it) does not fit 64 VGPRs, so it runs at <= 4 waves per SIMD
   if (c.rpw <= 2) {
