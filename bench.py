@@ -21,6 +21,10 @@ large linears can gain. --shard-policy size / all / none override the measuremen
 Total work is fixed as P grows ("strong" scaling); value counts the whole model's bytes once
 per step.
 
+--model 70b runs BASELINE config 5's shapes instead (Llama-3-70B: 80 layers, 43.4 GB of int4
+weights per step; the 1/2/4/8-GPU column-sharded curve of the north star); the default and
+headline workload is the 8B.
+
 Reported (one JSON line, rank 0):
   value        = algorithmic bytes per step x steps / wall time  (GB/s, whole job)
   tokens_per_s = steps / wall time
@@ -52,6 +56,9 @@ PMC_FILE = os.path.join(ROOT, "profiles", "r1_pmc_fetch_bench.json")
 
 LLAMA3_8B = dict(dim=4096, n_layer=32, n_head=32, n_kv_head=8, head_dim=128,
                  intermediate=14336, vocab=128256)
+LLAMA3_70B = dict(dim=8192, n_layer=80, n_head=64, n_kv_head=8, head_dim=128,
+                  intermediate=28672, vocab=128256)  # BASELINE config 5 (--model 70b)
+MODELS = {"8b": ("Llama-3-8B", LLAMA3_8B), "70b": ("Llama-3-70B", LLAMA3_70B)}
 
 
 def llama_linears(cfg, fuse_w13=True):
@@ -76,6 +83,18 @@ def llama_linears(cfg, fuse_w13=True):
         out.append((f"layers.{layer}.feed_forward.w2", d, inter))
     out.append(("output", cfg["vocab"], d))
     return out
+
+
+def workload_desc(cfg, fuse_w13=True):
+    """'32 layers x {wqkv 6144x4096, ...} + output 128256x4096' for the config."""
+    shapes = {}
+    for name, N, K in llama_linears(cfg, fuse_w13):
+        shapes.setdefault(name.split(".")[-1], (N, K))
+    names = {"w13": "w1||w3", "w1": "w1/w3"}
+    body = ", ".join(f"{names.get(k, k)} {N}x{K}" for k, (N, K) in shapes.items()
+                     if k not in ("output", "w3"))
+    N, K = shapes["output"]
+    return f"{cfg['n_layer']} layers x {{{body}}} + output {N}x{K}"
 
 
 def int4_alg_bytes(N, K, g, M=1):
@@ -233,6 +252,9 @@ def main():
     ap.add_argument("--shard-all", action="store_true", help="= --shard-policy all")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = rehearsal of the P > 1 path on one GPU (all ranks on device 0)")
+    ap.add_argument("--model", default="8b", choices=sorted(MODELS),
+                    help="8b = the headline workload (BASELINE config 2); 70b = config 5's "
+                         "shapes (43 GB of int4 weights per step)")
     ap.add_argument("--no-fuse-w13", action="store_true",
                     help="w1 and w3 as two linears (the reference's module layout, 161 launches)")
     args = ap.parse_args()
@@ -260,7 +282,8 @@ def main():
     from torchao import _lib
 
     _lib.lib()  # fail loudly if the native library is missing
-    cfg, g, P = LLAMA3_8B, args.group_size, world
+    model_name, cfg = MODELS[args.model]
+    g, P = args.group_size, world
     lins = llama_linears(cfg, fuse_w13=not args.no_fuse_w13)
     policy = "all" if args.shard_all else args.shard_policy
     calib = {}
@@ -388,7 +411,7 @@ def main():
     # HBM traffic from the committed counter pass (rocprofv3 --pmc FETCH_SIZE of this bench,
     # P = 1 shapes): bytes per step, to set against the algorithmic bytes
     traffic = None
-    if P == 1 and os.path.exists(PMC_FILE):
+    if P == 1 and args.model == "8b" and os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
             pmc = json.load(f)
         traffic = pmc.get("hbm_bytes_per_step")
@@ -407,13 +430,13 @@ def main():
         comm_ms = (time.perf_counter() - tc) / args.steps * 1e3
 
     cpu = None
-    if rank == 0 and P == 1 and not args.no_cpu_baseline:
+    if rank == 0 and P == 1 and not args.no_cpu_baseline and args.model == "8b":
         cpu = cpu_baseline(cfg, g)
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         rec = {
-            "metric": "int4 WO linear GB/s + tokens/s vs CPU dequant path, Llama-3-8B shapes M=1",
+            "metric": f"int4 WO linear GB/s + tokens/s vs CPU dequant path, {model_name} shapes M=1",
             "value": round(bytes_per_step * args.steps / elapsed / 1e9, 2),
             "unit": "GB/s",
             "tokens_per_s": round(args.steps / elapsed, 2),
@@ -427,12 +450,10 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (random-init nn.Linear weights quantized int4 g32; N(0,1) bf16 activations)",
             "config": {
-                "workload": "Llama-3-8B int4 g32 weight-only linears, M=1 decode: 32 layers x "
-                            + ("{wqkv 6144x4096, wo 4096x4096, w1||w3 28672x4096, w2 4096x14336}"
-                               if not args.no_fuse_w13 else
-                               "{wqkv 6144x4096, wo 4096x4096, w1/w3 14336x4096, w2 4096x14336}")
-                            + f" + output 128256x4096 ({len(plan)} GEMV launches/step)",
-                "model": "Llama-3-8B (linears only)",
+                "workload": f"{model_name} int4 g{g} weight-only linears, M=1 decode: "
+                            + workload_desc(cfg, not args.no_fuse_w13)
+                            + f" ({len(plan)} GEMV launches/step)",
+                "model": f"{model_name} (linears only)",
                 "global_batch": 1,
                 "seq_len": 1,
                 "group_size": g,
