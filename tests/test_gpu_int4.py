@@ -100,7 +100,10 @@ def test_linear_all_m_paths(M, g):
 @pytest.mark.parametrize(
     "N,K,g",
     [(4096, 4096, 32), (6144, 4096, 32), (14336, 4096, 32), (4096, 14336, 32),
-     (11008, 4096, 32), (4096, 11008, 32), (8192, 28672, 64), (4096, 4096, 256)],
+     (11008, 4096, 32), (4096, 11008, 32), (8192, 28672, 64), (4096, 4096, 256),
+     # 70B-style shard launch shapes: few rows with long K (waves split K 8 / 4 ways), a
+     # K > 4096 head-like N >= 32768 (8 rows per wave), a 2-rows-per-wave K = 8192 shard
+     (1024, 28672, 32), (2048, 14336, 32), (2560, 8192, 32), (33000, 5120, 128)],
 )
 def test_llama_shapes_m1(N, K, g):
     w, q, s, z = _qparams(N, K, g, seed=N ^ K)
