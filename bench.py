@@ -36,6 +36,9 @@ Reported (one JSON line, rank 0):
                  committed rocprofv3 FETCH_SIZE pass (profiles/, gfx950 x2 correction)
   cpu_baseline = the reference's CPU "dequant path" (dequantize -> F.linear, bf16) restated in
                  oracle/, timed on this host's cores over a bounded sample (rank 0, N = 1)
+  prefill_mfma = BASELINE config 3 (int8 dyn-act int8-weight linear, M = 128, 4096x4096, the
+                 int8 MFMA path) and the int4 g32 linear at M = 128 on its bf16 MFMA path:
+                 kernel us, TOPS, fraction of the dense MFMA peak, attainable-roofline fraction
 """
 
 import argparse
@@ -184,6 +187,86 @@ def calibrate_sharding(shapes, P, g, device, rehearsal, reps=20):
     return out
 
 
+INT8_PEAK_TOPS = 5000.0   # MI355X dense int8 MFMA, 2x the bf16 rate (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA
+
+
+def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
+    """BASELINE config 3 (int8 dynamic-activation int8-weight linear, M = 128, the MFMA int8
+    path) and the int4 g32 linear at the same M on its bf16-MFMA path, timed per kernel by the
+    dispatch packets' own events (tao_profile_*, as rocprofv3 reports them), weights rotated
+    over copies past the 256 MiB Infinity Cache. Roofline: max(ops / MFMA peak, bytes / HBM
+    peak) is the attainable time; `frac` = attainable / measured."""
+    from torchao import _lib
+
+    def timed(fn, copies, launches):
+        for c in range(copies):
+            fn(c)
+        torch.cuda.synchronize()
+        with _lib.KernelTimer(reps * launches) as kt:
+            for i in range(reps):
+                fn(i % copies)
+        torch.cuda.synchronize()
+        d = kt.durations_ms
+        if len(d) != reps * launches:
+            raise RuntimeError(f"prefill_mfma: expected {reps * launches} kernels, got {len(d)}")
+        return [sorted(d[j::launches])[len(d[j::launches]) // 2] * 1e3 for j in range(launches)]
+
+    out = {}
+    # int8 dyn: per-token quant kernel + int8 MFMA GEMM with the fused scale epilogue
+    copies = max(2, int(320e6 // (N * K)))
+    gen = torch.Generator(device=device).manual_seed(3)
+    ws = [torch.randint(-127, 128, (N, K), dtype=torch.int8, device=device, generator=gen)
+          for _ in range(copies)]
+    wsc = (torch.rand(N, device=device, generator=gen) * 0.01 + 1e-3).to(torch.bfloat16)
+    x = torch.randn(M, K, device=device, dtype=torch.bfloat16, generator=gen)
+
+    def int8dyn(c):
+        q, s = torch.ops.torchao.int8_quantize_per_token(x)
+        torch.ops.torchao.int8_scaled_mm(q, s, ws[c], wsc, None)
+
+    quant_us, gemm_us = timed(int8dyn, copies, 2)
+    ops = 2 * M * N * K
+    nbytes = N * K + N * 2 + M * K + M * 4 + M * N * 2  # int8 W + scales, int8 x + scales, bf16 y
+    att = max(ops / (INT8_PEAK_TOPS * 1e12), nbytes / (HBM_PEAK_GBPS * 1e9)) * 1e6
+    out["int8_dyn"] = {
+        "config": f"BASELINE config 3: int8 dyn-act int8-weight linear M={M} N={N} K={K}",
+        "kernel": "gemm_mfma_kernel<Int8Dyn> (v_mfma_i32_16x16x64_i8)",
+        "gemm_us": round(gemm_us, 2), "quant_us": round(quant_us, 2),
+        "TOPS": round(ops / (gemm_us * 1e-6) / 1e12, 1),
+        "mfma_frac": round(ops / (gemm_us * 1e-6) / 1e12 / INT8_PEAK_TOPS, 4),
+        "GBps": round(nbytes / (gemm_us * 1e-6) / 1e9, 1),
+        "attainable_us": round(att, 2), "roofline_frac": round(att / gemm_us, 4),
+    }
+    del ws
+    # int4 g32 weight-only at the same M: bf16 MFMA with in-register nibble dequant
+    copies = max(2, int(320e6 // (N * K // 2)))
+    w4 = []
+    for c in range(copies):
+        q = torch.randint(0, 16, (N, K), dtype=torch.int32, device=device, generator=gen)
+        sz = (torch.rand(N, K // g, 2, device=device, generator=gen) * 0.02).to(torch.bfloat16)
+        w4.append((torch.ops.torchao.int4_pack(q), sz))
+        del q
+
+    def int4(c):
+        torch.ops.torchao.int4_weight_only_linear(x, w4[c][0], w4[c][1], g, None)
+
+    (us4,) = timed(int4, copies, 1)
+    nbytes4 = int4_alg_bytes(N, K, g, M)
+    att4 = max(ops / (BF16_PEAK_TFLOPS * 1e12), nbytes4 / (HBM_PEAK_GBPS * 1e9)) * 1e6
+    out["int4_wo"] = {
+        "config": f"int4 g{g} weight-only linear M={M} N={N} K={K} (prefill)",
+        "kernel": "gemm_mfma_kernel<Int4WO> (v_mfma_f32_16x16x32_bf16)",
+        "gemm_us": round(us4, 2),
+        "TFLOPS": round(ops / (us4 * 1e-6) / 1e12, 1),
+        "mfma_frac": round(ops / (us4 * 1e-6) / 1e12 / BF16_PEAK_TFLOPS, 4),
+        "attainable_us": round(att4, 2), "roofline_frac": round(att4 / us4, 4),
+    }
+    del w4
+    torch.cuda.empty_cache()
+    return out
+
+
 def cpu_baseline(cfg, g, budget_s=12.0):
     """The reference CPU dequant path (oracle restatement) on one layer's five linears, M = 1."""
     from oracle import oracle
@@ -243,6 +326,8 @@ def main():
     ap.add_argument("--group-size", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-prefill", action="store_true",
+                    help="skip the config-3 MFMA prefill measurement (prefill_mfma)")
     ap.add_argument("--shard-policy", default="auto", choices=["auto", "size", "all", "none"],
                     help="P > 1: which linears to column-shard. auto = per (N, K), whichever of "
                          "{whole GEMV on every rank, N/P GEMV + all-gather} measured faster "
@@ -429,6 +514,10 @@ def main():
         barrier()
         comm_ms = (time.perf_counter() - tc) / args.steps * 1e3
 
+    prefill = None
+    if P == 1 and args.model == "8b" and not args.no_prefill:
+        prefill = prefill_mfma(device)
+
     cpu = None
     if rank == 0 and P == 1 and not args.no_cpu_baseline and args.model == "8b":
         cpu = cpu_baseline(cfg, g)
@@ -481,6 +570,8 @@ def main():
             },
             "cpu_baseline": cpu,
         }
+        if prefill is not None:
+            rec["prefill_mfma"] = prefill
         if comm_ms is not None:
             rec["allgather_ms_per_step"] = round(comm_ms, 4)
         if calib:

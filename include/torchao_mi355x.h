@@ -155,6 +155,21 @@ int tao_int8_scaled_mm_bf16(const int8_t* xq, const uint16_t* xs, const int8_t* 
                             const uint16_t* ws, const uint16_t* bias, uint16_t* y, int64_t M,
                             int64_t N, int64_t K, void* stream);
 
+/* One token (M <= 1) through both steps above in ONE launch: every workgroup quantises x [K]
+ * bf16 per token into LDS (tao_int8_quant_per_token's arithmetic) and runs the int8 x int8 GEMV
+ * on it. Bit-identical to tao_int8_quant_per_token + tao_int8_scaled_mm_bf16 (K % 16 == 0,
+ * K <= 65536). Replaces LinearActivationQuantizedTensor's quantize-then-F.linear for the default
+ * Int8DynamicActivationInt8WeightConfig recipe at decode (linear_activation_quantized_tensor.py
+ * _quantized_linear_op; quant_api.py:1258-1273 + plain_layout.py:294-315). */
+int tao_int8_dyn_linear_bf16(const uint16_t* x, const int8_t* wq, const uint16_t* ws,
+                             const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K,
+                             void* stream);
+
+/* Tuning hook: M == 1 launch shape of the int8 decode GEMVs (int8 weight-only and int8 x int8:
+ * rows per wave 2/4/8, waves along K, row groups per workgroup; 0 = built-in heuristic).
+ * Process-wide; for sweeps (experiments/sweep_int8.py). */
+int tao_tune_int8_gemv(int rows_per_wave, int waves_k, int row_groups);
+
 /* ---- fused decode-step kernels of the end-to-end harness (torchao/_models/llama) -------------
  * Not on the int4 path: the fusions the reference gets from torch.compile in its gpt-fast
  * harness (torchao/_models/llama/generate.py:865-875, model.py:405-501). */

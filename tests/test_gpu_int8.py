@@ -3,6 +3,7 @@
 import pytest
 import torch
 
+import torchao  # noqa: F401  (registers torch.ops.torchao)
 from conftest import bf16, golden_files, golden_ms, load_golden
 from oracle import oracle
 
@@ -98,3 +99,97 @@ def test_int8_configs_end_to_end():
         # (test_integration.py:978-1004 use >= 40 dB for int8wo; dynamic int8 is looser)
         sqnr = 20 * torch.log10(ref.norm() / (ref - y.float()).norm())
         assert sqnr > (35 if isinstance(cfg, Int8WeightOnlyConfig) else 25), (cfg, float(sqnr))
+
+
+# ---- int8 x int8 decode GEMV (M <= 4) and the fused one-token linear -------------------------
+# Integer products are exact and the epilogue is the reference's op order, so every check below
+# is bit-exact (torch.equal) against the CPU oracle (oracle.int8_scaled_mm, epilogue "cpu").
+DYN_SHAPES = [(256, 256), (40, 352), (4096, 4096), (6144, 4096), (4096, 14336), (1000, 11008),
+              (128256 // 8, 4096)]
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,K", DYN_SHAPES)
+def test_int8dyn_gemv_bit_exact(M, N, K):
+    w = oracle.make_linear_weight(N, K, seed=N + K)
+    wq, ws = oracle.int8_dyn_weight(w)
+    x = oracle.make_activation(M, K, seed=M + K) * 2
+    if M > 1:
+        x[1] = 0.0           # all-zero token: scale clamps to eps
+    x[0, K // 3] = 500.0     # outlier
+    xq, xs = oracle.int8_act_quant(x)
+    bias = oracle.make_activation(1, N, seed=5).reshape(-1)
+    for b in (None, bias):
+        y = torch.ops.torchao.int8_scaled_mm(
+            xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), None if b is None else b.to(DEV)
+        ).cpu()
+        assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, b, epilogue="cpu"))
+
+
+@pytest.mark.parametrize("N,K", DYN_SHAPES + [(28672, 4096), (4096, 28672)])
+def test_int8_dyn_linear_fused_bit_exact(N, K):
+    w = oracle.make_linear_weight(N, K, seed=N)
+    wq, ws = oracle.int8_dyn_weight(w)
+    bias = oracle.make_activation(1, N, seed=9).reshape(-1)
+    for seed, scale in ((1, 1.0), (2, 1e3), (3, 0.0)):
+        x = oracle.make_activation(1, K, seed=seed) * scale
+        xq, xs = oracle.int8_act_quant(x)
+        for b in (None, bias):
+            y = torch.ops.torchao.int8_dyn_linear(
+                x.to(DEV), wq.to(DEV), ws.to(DEV), None if b is None else b.to(DEV)
+            ).cpu()
+            assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, b, epilogue="cpu"))
+
+
+def test_int8_dyn_gemv_launch_shapes_identical():
+    """Every launch shape of the decode GEMV gives the same bits (exact integer sums)."""
+    from torchao import _lib
+
+    N, K = 1000, 11008
+    w = oracle.make_linear_weight(N, K, seed=3)
+    wq, ws = (t.to(DEV) for t in oracle.int8_dyn_weight(w))
+    x = oracle.make_activation(1, K, seed=4).to(DEV)
+    ref = torch.ops.torchao.int8_dyn_linear(x, wq, ws, None)
+    try:
+        for rpw in (2, 4, 8):
+            for wk, g in ((1, 1), (2, 4), (4, 2), (8, 1), (3, 2)):
+                _lib.call("tao_tune_int8_gemv", rpw, wk, g)
+                assert torch.equal(torch.ops.torchao.int8_dyn_linear(x, wq, ws, None), ref)
+                q, s = torch.ops.torchao.int8_quantize_per_token(x)
+                assert torch.equal(torch.ops.torchao.int8_scaled_mm(q, s, wq, ws, None), ref)
+    finally:
+        _lib.call("tao_tune_int8_gemv", 0, 0, 0)
+
+
+def test_int8_dyn_linear_args_fail_loudly():
+    w = torch.zeros(64, 256, dtype=torch.int8, device=DEV)
+    s = torch.ones(64, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(RuntimeError):
+        torch.ops.torchao.int8_dyn_linear(torch.zeros(2, 256, dtype=torch.bfloat16, device=DEV),
+                                          w, s, None)
+    with pytest.raises(RuntimeError):
+        torch.ops.torchao.int8_dyn_linear(torch.zeros(1, 128, dtype=torch.bfloat16, device=DEV),
+                                          w, s, None)
+
+
+def test_int8dq_decode_takes_fused_path_and_matches_unfused():
+    """quantize_(Int8DynamicActivationInt8WeightConfig) + one token on the GPU: the LAQT fast
+    path (one launch) equals quantise -> F.linear(AQT x, AQT w), bit for bit, and the
+    prefill-shaped input still takes the reference route."""
+    from torchao.quantization import Int8DynamicActivationInt8WeightConfig, quantize_
+    from torchao.quantization.linear_activation_quantized_tensor import _fused_int8_dyn_decode
+
+    K, N = 4096, 1024
+    m = torch.nn.Linear(K, N, bias=True).to(torch.bfloat16).to(DEV)
+    quantize_(m, Int8DynamicActivationInt8WeightConfig())
+    wt = m.weight
+    for shape in ((1, K), (1, 1, K)):
+        x = torch.randn(*shape, dtype=torch.bfloat16, device=DEV)
+        assert _fused_int8_dyn_decode(x, wt, m.bias) is not None
+        y = m(x)
+        qx = wt.input_quant_func(x, **wt.quant_kwargs)
+        y_ref = torch.nn.functional.linear(qx, wt.original_weight_tensor, m.bias)
+        assert y.shape == y_ref.shape
+        assert torch.equal(y, y_ref)
+    assert _fused_int8_dyn_decode(torch.randn(4, K, dtype=torch.bfloat16, device=DEV), wt,
+                                  None) is None

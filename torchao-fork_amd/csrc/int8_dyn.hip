@@ -4,20 +4,293 @@
 //      which the reference runs as ~6 eager kernels (amin/amax/div/round/clamp/cast);
 //   2. tao_int8_scaled_mm_bf16: int32 MFMA GEMM with the fused two-scale epilogue, replacing
 //      int_scaled_matmul + the weight-scale multiply (torchao/kernel/intmm.py:108-143,
-//      torchao/dtypes/uintx/plain_layout.py:294-315). The GEMM is the Int8Dyn instance of the
-//      shared skinny-GEMM template in gemm_mfma.hip.
+//      torchao/dtypes/uintx/plain_layout.py:294-315). M > 4: the Int8Dyn instance of the
+//      shared skinny-GEMM template in gemm_mfma.hip; M <= 4 (decode): int8dyn_gemv_kernel
+//      below, exact int32 dot products (v_dot4_i32_i8) streamed like the int4 / int8 GEMVs;
+//   3. tao_int8_dyn_linear_bf16 (M == 1): 1 + 2 in one launch — every workgroup quantises the
+//      token into LDS (the per-token kernel's exact arithmetic) while its first weight slice
+//      is in flight, then runs the GEMV on it: one launch per linear instead of two.
+#include <atomic>
+
 #include "tao_common.h"
+#include "tao_reduce.h"
 
 namespace tao {
+
+// Launch shape override of the int8 decode GEMVs (tao_tune_int8_gemv; 0 = heuristic), shared
+// with int8wo_gemv (int8_gemv.hip).
+std::atomic<int> g_i8_rpw{0}, g_i8_wk{0}, g_i8_g{0};
+
 namespace {
 
-// ---- per-token quantisation ------------------------------------------------------------------
-constexpr int kQBlock = 256;
+
+// ---- int8 x int8 GEMV (decode) ------------------------------------------------------------------
+// A slice is 1024 k of one row = 64 lanes x 16 B; a wave owns RPW rows, Wk waves split K inside a
+// workgroup, G row groups share it (int8wo_gemv_kernel's decomposition). Per lane and row:
+// four v_dot4_i32_i8 per 16-B chunk into an int32 accumulator. Every partial sum is an exact
+// integer (|acc| <= 127 * 127 * K < 2^31 for K < 133144), so the cross-lane and cross-wave
+// reduction order cannot change the result: bit-identical to the MFMA path and the reference.
+// Lanes past K read a clamped in-bounds chunk and a zeroed x, adding exactly 0.
+//
+// FQ (M == 1): x is the bf16 token. Each workgroup first issues its first slice's weight loads,
+// then quantises the token into LDS with int8_quant_per_token_kernel's exact arithmetic (below)
+// under their latency, so the per-token quantisation costs no launch of its own.
+struct Int8DynGemvArgs {
+  const void* x;          // int8 q [M][K] (FQ: bf16 token [K])
+  const uint16_t* xs;     // [M] bf16 per-token scales (unused with FQ)
+  const uint4* w;         // [N][K/16]
+  const uint16_t* ws;     // [N]
+  const uint16_t* bias;   // [N] or null
+  uint16_t* y;            // [M][N]
+  int M, N, K, Wk, G, S;
+};
+
+__device__ __forceinline__ int sdot4(uint32_t a, uint32_t b, int c) {
+  return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
+}
+
+// per-token scale and its reciprocal from amax (quant_primitives.py:1548-1554, 449-453)
+__device__ __forceinline__ float token_scale(float amax) {
+  float s = round_bf16(amax / 127.f);
+  const float eps = round_bf16(1e-5f);
+  return s < eps ? eps : s;
+}
+
+// q = clamp(round(bf16(x * r)), -127, 127) for the 8 bf16 of one 16-B piece -> 8 int8 bytes
+__device__ __forceinline__ uint2 quant8(const uint4 v, float r) {
+  const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+  uint32_t packed[2] = {0u, 0u};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float xv = (j & 1) ? bf16hi_to_f32(d[j >> 1]) : bf16lo_to_f32(d[j >> 1]);
+    float t = rintf(round_bf16(xv * r));
+    t = fminf(fmaxf(t, -127.f), 127.f);
+    packed[j >> 2] |= ((uint32_t)(int32_t)t & 0xFFu) << (8 * (j & 3));
+  }
+  return make_uint2(packed[0], packed[1]);
+}
 
 __device__ __forceinline__ float bf16_abs_max2(uint32_t d, float m) {
   m = fmaxf(m, fabsf(bf16lo_to_f32(d)));
   return fmaxf(m, fabsf(bf16hi_to_f32(d)));
 }
+
+template <int MT, int RPW, int NPT>
+__global__ __launch_bounds__(512) void int8dyn_gemv_kernel(Int8DynGemvArgs a) {
+  constexpr bool FQ = NPT > 0;  // NPT: 16-B pieces of the bf16 token per thread (K <= 8 NPT T)
+  static_assert(!FQ || MT == 1, "the fused quantisation is per token, M == 1");
+  constexpr int V = RPW * MT;
+  // [G][Wk][V] int partials | (FQ) [8] wave maxima | (FQ) token q [K] int8
+  extern __shared__ int lds_i[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
+  const int wk = wave % a.Wk;
+  const int rg = wave / a.Wk;
+  const int row0 = (blockIdx.x * a.G + rg) * RPW;
+  const int K = a.K, N = a.N, S = a.S, Wk = a.Wk;
+  const int nchunk = K >> 4;  // 16-B (16-k) chunks per row
+  const int nw = a.G * a.Wk;
+  float* wmax = reinterpret_cast<float*>(lds_i + nw * V);
+  uint4* xl = reinterpret_cast<uint4*>(lds_i + ((nw * V + 8 + 3) & ~3));
+
+  int acc[RPW][MT];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[r][m] = 0;
+
+  uint4 wv[RPW];
+  auto load_w = [&](int s) __attribute__((always_inline)) {
+    const int c = s * 64 + lane;
+    const int cc = c < nchunk ? c : nchunk - 1;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int n = row0 + r;
+      wv[r] = ld_nt_u4(a.w + (size_t)(n < N ? n : N - 1) * nchunk + cc);
+    }
+  };
+
+  float sx[MT];
+  if constexpr (FQ) {
+    // The token's pieces are loaded BEFORE the first slice's weights: vector loads retire in
+    // issue order, so the wait for x does not wait for the weights, and the amax, the two
+    // barriers and the quantisation into LDS run under the weight loads' latency.
+    const uint4* xr = reinterpret_cast<const uint4*>(a.x);
+    const int nvec = K >> 3;
+    uint4 xv[NPT];
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int i = threadIdx.x + u * (int)blockDim.x;
+      xv[u] = xr[i < nvec ? i : nvec - 1];  // clamped, masked below
+    }
+    load_w(wk);  // every wave owns at least one slice (Wk <= S)
+    // amax over K bf16, then quantise into LDS (int8_quant_per_token_kernel's arithmetic)
+    float m = 0.f;
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const bool ok = threadIdx.x + u * (int)blockDim.x < nvec;
+      const uint4 v = ok ? xv[u] : make_uint4(0u, 0u, 0u, 0u);
+      m = bf16_abs_max2(v.x, m);
+      m = bf16_abs_max2(v.y, m);
+      m = bf16_abs_max2(v.z, m);
+      m = bf16_abs_max2(v.w, m);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (lane == 0) wmax[wave] = m;
+    __syncthreads();
+    float amax = wmax[0];
+    for (int w = 1; w < nw; ++w) amax = fmaxf(amax, wmax[w]);
+    const float st = token_scale(amax);
+    const float rs = round_bf16(1.f / st);
+    uint2* xq = reinterpret_cast<uint2*>(xl);
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int i = threadIdx.x + u * (int)blockDim.x;
+      if (i < nvec) xq[i] = quant8(xv[u], rs);
+    }
+    __syncthreads();
+    sx[0] = st;
+  } else {
+    load_w(wk);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) sx[m] = bf16_to_f32(a.xs[m < a.M ? m : a.M - 1]);
+  }
+
+  for (int s = wk; s < S; s += Wk) {
+    if (s != wk) load_w(s);
+    const int c = s * 64 + lane;
+    const bool cval = c < nchunk;
+    const int cc = cval ? c : nchunk - 1;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      uint4 xv;
+      if constexpr (FQ) {
+        xv = xl[cc];
+      } else {
+        const int mm = m < a.M ? m : a.M - 1;
+        xv = reinterpret_cast<const uint4*>(a.x)[(size_t)mm * nchunk + cc];
+      }
+      const uint32_t keep = cval ? ~0u : 0u;  // lanes past K add exactly 0
+      const uint32_t xd[4] = {xv.x & keep, xv.y & keep, xv.z & keep, xv.w & keep};
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        int d = acc[r][m];
+        d = sdot4(xd[0], wv[r].x, d);
+        d = sdot4(xd[1], wv[r].y, d);
+        d = sdot4(xd[2], wv[r].z, d);
+        d = sdot4(xd[3], wv[r].w, d);
+        acc[r][m] = d;
+      }
+    }
+  }
+
+  int v[V];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) v[r * MT + m] = acc[r][m];
+  wave_reduce_scatter<V>(v, lane);
+
+  constexpr int T = Log2<V>::value;
+  const bool owner = (lane & ((64 >> T) - 1)) == 0;
+  const int idx = lane >> (6 - T);
+  int total = v[0];
+  bool writer = owner;
+  int widx = idx;
+  if (Wk > 1) {
+    if (owner) lds_i[(rg * Wk + wk) * V + idx] = v[0];
+    __syncthreads();
+    writer = (wk == 0) && (lane < V);
+    widx = lane;
+    if (writer) {
+      total = 0;
+      for (int kk = 0; kk < Wk; ++kk) total += lds_i[(rg * Wk + kk) * V + widx];
+    }
+  }
+  if (writer) {
+    const int r = widx / MT, m = widx % MT;
+    const int n = row0 + r;
+    if (n < N && m < a.M) {
+      // bf16(c) * x_scale, * w_scale, each rounded (intmm.py:133-137, plain_layout.py:301-315);
+      // the MFMA path's Int8Dyn::epilogue
+      float o = round_bf16(round_bf16((float)total) * sx[m]);
+      o = round_bf16(o * bf16_to_f32(a.ws[n]));
+      if (a.bias != nullptr) o = round_bf16(o + bf16_to_f32(a.bias[n]));
+      a.y[(size_t)m * N + n] = f32_to_bf16(o);
+    }
+  }
+}
+
+
+template <int MT, int RPW, int NPT>
+int launch_dyn_gemv_npt(Int8DynGemvArgs a, int grid, int threads, size_t lds, hipStream_t stream) {
+  launch((int8dyn_gemv_kernel<MT, RPW, NPT>), dim3(grid), dim3(threads), lds, stream, a);
+  return check_launch("int8dyn_gemv_kernel");
+}
+
+template <int MT, int RPW, bool FQ>
+int launch_dyn_gemv(Int8DynGemvArgs a, int wk, int g, hipStream_t stream) {
+  const int nchunk = a.K / 16;
+  a.S = (nchunk + 63) / 64;
+  a.Wk = wk < a.S ? wk : a.S;
+  a.G = g;
+  // FQ: the token must fit the workgroup's registers (K <= 8 x 16 pieces x threads)
+  while (FQ && 64 * a.Wk * a.G * 8 * 16 < a.K && a.Wk * a.G * 2 <= 8) a.G *= 2;
+  const int rows_per_wg = a.G * RPW;
+  const int grid = (a.N + rows_per_wg - 1) / rows_per_wg;
+  const int nw = a.G * a.Wk;
+  const int threads = 64 * nw;
+  if (!FQ) {
+    const size_t lds = (size_t)nw * RPW * MT * sizeof(int);
+    return launch_dyn_gemv_npt<MT, RPW, 0>(a, grid, threads, lds, stream);
+  }
+  if constexpr (FQ) {
+    const size_t lds = (((size_t)nw * RPW * MT + 8 + 3) & ~(size_t)3) * sizeof(int) + (size_t)a.K;
+    const int per = (a.K / 8 + threads - 1) / threads;  // pieces per thread
+    if (per <= 1) return launch_dyn_gemv_npt<MT, RPW, 1>(a, grid, threads, lds, stream);
+    if (per <= 2) return launch_dyn_gemv_npt<MT, RPW, 2>(a, grid, threads, lds, stream);
+    if (per <= 4) return launch_dyn_gemv_npt<MT, RPW, 4>(a, grid, threads, lds, stream);
+    if (per <= 8) return launch_dyn_gemv_npt<MT, RPW, 8>(a, grid, threads, lds, stream);
+    if (per <= 16) return launch_dyn_gemv_npt<MT, RPW, 16>(a, grid, threads, lds, stream);
+    TAO_CHECK_ARG(false, "int8 dyn linear: K (%d) too long for the token prologue", a.K);
+  }
+  return TAO_OK;
+}
+
+// M == 1 shape (experiments/sweep_int8.py, profiles/r1_sweep_int8.jsonl, fused path):
+// K <= 4096: 4 rows per wave, 2 waves along K, 2 row groups (one for the 128256-row head);
+// longer K: 8 rows per wave, 4 waves along K (4096x14336 11.5 us).
+template <bool FQ>
+int dyn_gemv_m1(Int8DynGemvArgs a, hipStream_t stream) {
+  const int S = (a.K / 16 + 63) / 64;
+  int rpw = 4, wk = S < 2 ? S : 2, g = a.N >= 65536 ? 1 : 2;
+  if (S > 4) {
+    rpw = 8;
+    wk = 4;
+    g = 1;
+  }
+  const int trpw = g_i8_rpw.load(std::memory_order_relaxed);
+  const int twk = g_i8_wk.load(std::memory_order_relaxed);
+  const int tg = g_i8_g.load(std::memory_order_relaxed);
+  if (trpw > 0) rpw = trpw;
+  if (twk > 0) wk = twk;
+  if (tg > 0) g = tg;
+  if (rpw == 2) return launch_dyn_gemv<1, 2, FQ>(a, wk, g, stream);
+  if (rpw == 8) return launch_dyn_gemv<1, 8, FQ>(a, wk, g, stream);
+  return launch_dyn_gemv<1, 4, FQ>(a, wk, g, stream);
+}
+
+int int8dyn_gemv(Int8DynGemvArgs a, hipStream_t stream) {
+  const int S = (a.K / 16 + 63) / 64;
+  const int wk = S < 8 ? S : 8, g = (8 / wk) > 0 ? 8 / wk : 1;
+  if (a.M <= 1) return dyn_gemv_m1<false>(a, stream);
+  if (a.M <= 2) return launch_dyn_gemv<2, 4, false>(a, wk, g, stream);
+  return launch_dyn_gemv<4, 2, false>(a, wk, g, stream);
+}
+
+// ---- per-token quantisation ------------------------------------------------------------------
+constexpr int kQBlock = 256;
 
 __global__ __launch_bounds__(kQBlock) void int8_quant_per_token_kernel(
     const uint16_t* __restrict__ x, int8_t* __restrict__ q, uint16_t* __restrict__ scale, int K) {
@@ -43,27 +316,12 @@ __global__ __launch_bounds__(kQBlock) void int8_quant_per_token_kernel(
 
   // scale = clamp(bf16(amax / 127), min = 1e-5) in bf16 (quant_primitives.py:1548-1554 with
   // quant range [-127, 127]); the clamp minimum is compared after bf16 rounding.
-  float s = round_bf16(amax / 127.f);
-  const float eps = round_bf16(1e-5f);
-  s = s < eps ? eps : s;
+  const float s = token_scale(amax);
   if (threadIdx.x == 0) scale[row] = f32_to_bf16(s);
   // q = clamp(round(bf16(x * bf16(1/s))), -127, 127)  (quant_primitives.py:449-453)
   const float r = round_bf16(1.f / s);
   uint2* qr = reinterpret_cast<uint2*>(q + (size_t)row * K);
-  for (int i = threadIdx.x; i < nvec; i += kQBlock) {
-    const uint4 v = xr[i];
-    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-    uint32_t packed[2] = {0u, 0u};
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float xv = (j & 1) ? bf16hi_to_f32(d[j >> 1]) : bf16lo_to_f32(d[j >> 1]);
-      float t = rintf(round_bf16(xv * r));
-      t = fminf(fmaxf(t, -127.f), 127.f);
-      const uint32_t b = (uint32_t)(int32_t)t & 0xFFu;
-      packed[j >> 2] |= b << (8 * (j & 3));
-    }
-    qr[i] = make_uint2(packed[0], packed[1]);
-  }
+  for (int i = threadIdx.x; i < nvec; i += kQBlock) qr[i] = quant8(xr[i], r);
 }
 
 }  // namespace
@@ -102,8 +360,44 @@ int tao_int8_scaled_mm_bf16(const int8_t* xq, const uint16_t* xs, const int8_t* 
   TAO_CHECK_ARG(K > 0, "int8 scaled mm: K must be > 0");
   TAO_CHECK_ALIGN(xq, 16, "xq");
   TAO_CHECK_ALIGN(wq, 16, "wq");
+  if (M <= 4) {
+    Int8DynGemvArgs a{xq, xs, reinterpret_cast<const uint4*>(wq), ws, bias, y,
+                      (int)M, (int)N, (int)K, 0, 0, 0};
+    return int8dyn_gemv(a, as_stream(stream));
+  }
   return int8_scaled_mm_launch(xq, xs, wq, ws, bias, y, (int)M, (int)N, (int)K,
                                as_stream(stream));
+}
+
+int tao_int8_dyn_linear_bf16(const uint16_t* x, const int8_t* wq, const uint16_t* ws,
+                             const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K,
+                             void* stream) {
+  TAO_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "int8 dyn linear: negative size");
+  TAO_CHECK_ARG(M <= 1, "int8 dyn linear: the fused path is one token (M <= 1, got %lld)",
+                (long long)M);
+  TAO_CHECK_ARG(K % 16 == 0, "int8 dyn linear: K (%lld) must be a multiple of 16", (long long)K);
+  TAO_CHECK_ARG(K <= 65536, "int8 dyn linear: K (%lld) must be <= 65536 (token in LDS)",
+                (long long)K);
+  TAO_CHECK_ARG(N < (1LL << 31), "int8 dyn linear: size out of range");
+  if (M == 0 || N == 0) return TAO_OK;
+  TAO_CHECK_ARG(K > 0, "int8 dyn linear: K must be > 0");
+  TAO_CHECK_ALIGN(x, 16, "x");
+  TAO_CHECK_ALIGN(wq, 16, "wq");
+  Int8DynGemvArgs a{x, nullptr, reinterpret_cast<const uint4*>(wq), ws, bias, y,
+                    1, (int)N, (int)K, 0, 0, 0};
+  return dyn_gemv_m1<true>(a, as_stream(stream));
+}
+
+int tao_tune_int8_gemv(int rows_per_wave, int waves_k, int row_groups) {
+  TAO_CHECK_ARG(rows_per_wave == 0 || rows_per_wave == 2 || rows_per_wave == 4 ||
+                    rows_per_wave == 8,
+                "tune: rows_per_wave must be 0 (auto), 2, 4 or 8");
+  TAO_CHECK_ARG(waves_k >= 0 && row_groups >= 0 && waves_k * (row_groups ? row_groups : 1) <= 8,
+                "tune: waves_k * row_groups must be <= 8");
+  g_i8_rpw.store(rows_per_wave);
+  g_i8_wk.store(waves_k);
+  g_i8_g.store(row_groups);
+  return TAO_OK;
 }
 
 }  // extern "C"

@@ -7,10 +7,15 @@
 // a wave owns RPW rows; Wk waves split K inside a workgroup; LDS combines the waves.
 // Per lane: bytes are biased to unsigned (xor 0x80), converted with v_cvt_f32_ubyte{0..3} and
 // FMA'd against x in f32; the bias is removed once per chunk as 128 * sum(x).
+#include <atomic>
+
 #include "tao_common.h"
 #include "tao_reduce.h"
 
 namespace tao {
+
+extern std::atomic<int> g_i8_rpw, g_i8_wk, g_i8_g;  // tao_tune_int8_gemv (int8_dyn.hip)
+
 namespace {
 
 template <int MT, int RPW>
@@ -116,11 +121,13 @@ __global__ __launch_bounds__(512) void int8wo_gemv_kernel(
 
 template <int MT, int RPW>
 int launch_gemv(const uint16_t* x, const int8_t* w, const uint16_t* scale, const uint16_t* bias,
-                uint16_t* y, int M, int N, int K, hipStream_t stream) {
+                uint16_t* y, int M, int N, int K, hipStream_t stream, int wk = 0, int g = 0) {
   const int nchunk = K / 16;
   const int S = (nchunk + 63) / 64;
-  const int Wk = S < 8 ? S : 8;
-  const int G = (8 / Wk) > 0 ? 8 / Wk : 1;
+  int Wk = S < 8 ? S : 8;
+  int G = (8 / Wk) > 0 ? 8 / Wk : 1;
+  if (wk > 0) Wk = wk < S ? wk : S;
+  if (g > 0) G = g;
   const int rows_per_wg = G * RPW;
   const int grid = (N + rows_per_wg - 1) / rows_per_wg;
   const size_t lds = (size_t)G * Wk * RPW * MT * sizeof(float);
@@ -133,7 +140,19 @@ int launch_gemv(const uint16_t* x, const int8_t* w, const uint16_t* scale, const
 
 int int8wo_gemv(const uint16_t* x, const int8_t* w, const uint16_t* scale, const uint16_t* bias,
                 uint16_t* y, int64_t M, int64_t N, int64_t K, hipStream_t stream) {
-  if (M <= 1) return launch_gemv<1, 4>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream);
+  if (M <= 1) {
+    const int rpw = g_i8_rpw.load(std::memory_order_relaxed);
+    // one row group per workgroup at M == 1 (experiments/sweep_int8.py,
+    // profiles/r1_sweep_int8.jsonl: 4 rows per wave, Wk = min(S, 8), G = 1 is within 1% of the
+    // per-shape best on every Llama-3-8B linear; the head 77.8 -> 72.7 us)
+    const int wk = g_i8_wk.load(std::memory_order_relaxed);
+    const int tg = g_i8_g.load(std::memory_order_relaxed), g = tg > 0 ? tg : 1;
+    if (rpw == 2)
+      return launch_gemv<1, 2>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream, wk, g);
+    if (rpw == 8)
+      return launch_gemv<1, 8>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream, wk, g);
+    return launch_gemv<1, 4>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream, wk, g);
+  }
   if (M <= 2) return launch_gemv<2, 4>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream);
   if (M <= 4) return launch_gemv<4, 2>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream);
   return launch_gemv<8, 1>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream);

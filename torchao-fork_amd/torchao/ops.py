@@ -18,6 +18,7 @@ Operators:
   * ``int8_weight_only_linear`` — replaces mm + scale (plain_layout.py:256-266).
   * ``int8_quantize_per_token`` / ``int8_scaled_mm`` — replace the activation quant
     (quant_api.py:1258-1273) and ``int_scaled_matmul`` + weight scale (plain_layout.py:294-315).
+  * ``int8_dyn_linear`` — one token through both in one launch (decode), bit-identical.
   * ``int4_quantize_pack`` / ``int8_quantize_rows`` — the weight quantizers of
     ``from_hp_to_intx`` in one pass each (tinygemm qparams + quantize + row-stream pack;
     symmetric per-row int8), bit-exact to the bf16 torch-op formulation.
@@ -58,6 +59,9 @@ lib.define("int8_quantize_rows(Tensor w, float eps) -> (Tensor, Tensor)")
 lib.define(
     "int8_scaled_mm(Tensor x_int8, Tensor x_scale, Tensor w_int8, Tensor w_scale, "
     "Tensor? bias=None) -> Tensor"
+)
+lib.define(
+    "int8_dyn_linear(Tensor x, Tensor w_int8, Tensor w_scale, Tensor? bias=None) -> Tensor"
 )
 
 _GROUP_SIZES = (32, 64, 128, 256)
@@ -391,6 +395,34 @@ def _int8_scaled_mm_cuda(x_int8, x_scale, w_int8, w_scale, bias=None):
     return y.reshape(_linear_out_shape(x_int8, N))
 
 
+@torch.library.register_fake("torchao::int8_dyn_linear")
+def _(x, w_int8, w_scale, bias=None):
+    N, K = _check_int8_weight(w_int8, w_scale)
+    torch._check(x.numel() == K, lambda: "int8_dyn_linear is one token (x.numel() == K)")
+    return x.new_empty(_linear_out_shape(x, N), dtype=torch.bfloat16)
+
+
+def _int8_dyn_linear_cuda(x, w_int8, w_scale, bias=None):
+    """One token: per-token int8 quant + int8 x int8 GEMV in one launch, bit-identical to
+    int8_quantize_per_token -> int8_scaled_mm."""
+    N, K = _check_int8_weight(w_int8, w_scale)
+    torch._check(x.dtype is torch.bfloat16, lambda: "int8_dyn_linear (HIP) needs bf16 x")
+    torch._check(x.size(-1) == K, lambda: f"x last dim {x.size(-1)} != K {K}")
+    torch._check(x.numel() == K, lambda: "int8_dyn_linear is one token (x.numel() == K)")
+    x2 = x.reshape(1, K)
+    if not x2.is_contiguous() or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    ws = w_scale.reshape(-1).to(torch.bfloat16).contiguous()
+    w_int8 = w_int8.contiguous()
+    if bias is not None:
+        bias = bias.to(torch.bfloat16).contiguous()
+    y = torch.empty((1, N), dtype=torch.bfloat16, device=x.device)
+    with torch.cuda.device(x.device):
+        _lib.call("tao_int8_dyn_linear_bf16", _ptr(x2), _ptr(w_int8), _ptr(ws), _ptr(bias),
+                  _ptr(y), 1, N, K, _stream(x))
+    return y.reshape(_linear_out_shape(x, N))
+
+
 @torch.library.register_fake("torchao::int4_quantize_pack")
 def _(w, group_size, eps):
     torch._check(group_size in _GROUP_SIZES, lambda: "group_size must be 32, 64, 128, or 256")
@@ -458,6 +490,7 @@ for _name, _fn in [
     ("int4_quantize_pack", _int4_quantize_pack_cuda),
     ("int8_quantize_rows", _int8_quantize_rows_cuda),
     ("int8_scaled_mm", _int8_scaled_mm_cuda),
+    ("int8_dyn_linear", _int8_dyn_linear_cuda),
 ]:
     lib.impl(_name, _fn, "CUDA")
 # Host packers (C++ in the same library) so quantize_ works on CPU-resident models.

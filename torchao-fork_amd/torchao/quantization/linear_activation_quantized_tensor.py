@@ -59,6 +59,9 @@ class LinearActivationQuantizedTensor(TorchAOBaseTensor):
     def _quantized_linear_op(input_tensor, weight_tensor, bias):
         if input_tensor.numel() == 0:
             return input_tensor
+        y = _fused_int8_dyn_decode(input_tensor, weight_tensor, bias)
+        if y is not None:
+            return y
         qx = weight_tensor.input_quant_func(input_tensor, **weight_tensor.quant_kwargs)
         return torch.nn.functional.linear(qx, weight_tensor.original_weight_tensor, bias)
 
@@ -79,6 +82,32 @@ class LinearActivationQuantizedTensor(TorchAOBaseTensor):
         return type(self)(
             self.original_weight_tensor.to(**kwargs), self.input_quant_func, self.quant_kwargs
         )
+
+
+def _fused_int8_dyn_decode(x, weight_tensor, bias):
+    """One bf16 token on the GPU with the default Int8DynamicActivationInt8WeightConfig recipe
+    (per-token reduced-range quant, plain int8 per-channel weight): quantise + int8 GEMV in one
+    launch (``torch.ops.torchao.int8_dyn_linear``), bit-identical to quantising the input and
+    dispatching F.linear(AQT x, AQT w) to ``_linear_int8_act_int8_weight_impl``. Any other
+    recipe, shape or device returns None and takes the reference path above."""
+    from torchao.dtypes.affine_quantized_tensor import AffineQuantizedTensor
+    from torchao.dtypes.uintx.plain_layout import PlainLayout, _aqt_is_int8
+    from torchao.quantization.quant_api import _int8_symm_per_token_reduced_range_quant
+
+    if weight_tensor.input_quant_func is not _int8_symm_per_token_reduced_range_quant:
+        return None
+    if weight_tensor.quant_kwargs or not isinstance(x, torch.Tensor) or type(x) is not torch.Tensor:
+        return None
+    K = x.shape[-1]
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and K % 16 == 0 and x.numel() == K):
+        return None
+    w = weight_tensor.original_weight_tensor
+    if not (isinstance(w, AffineQuantizedTensor) and _aqt_is_int8(w) and w.dtype == torch.bfloat16
+            and isinstance(w._layout, PlainLayout) and len(w.shape) == 2 and w.shape[1] == K
+            and w.tensor_impl.int_data.is_cuda):
+        return None
+    impl = w.tensor_impl
+    return torch.ops.torchao.int8_dyn_linear(x, impl.int_data, impl.scale.reshape(-1), bias)
 
 
 implements = LinearActivationQuantizedTensor.implements
