@@ -9,6 +9,7 @@ import torch
 
 from torchao._models.llama.generate import (
     GraphDecoder,
+    GraphPrefill,
     apply_quantization,
     build_model,
     decode_one_token,
@@ -80,6 +81,16 @@ def test_graph_decode_matches_eager_gpu(quant):
     # a second run replays the same graph from a fresh prefill
     again, _, _ = generate(model, prompt, T, dec)
     assert torch.equal(again, eager)
+    # the graph-captured prefill gives the same first token and caches; a second prompt
+    # through the same prefill graph matches its eager run too
+    pre = GraphPrefill(model, (1, P), dev)
+    pre.capture(prompt)
+    both, _, _ = generate(model, prompt, T, dec, pre)
+    assert torch.equal(both, eager)
+    prompt2 = torch.randint(0, model.config.vocab_size, (1, P), generator=gen).to(dev)
+    eager2, _, _ = generate(model, prompt2, T, None)
+    both2, _, _ = generate(model, prompt2, T, dec, pre)
+    assert torch.equal(both2, eager2)
     # single step helper agrees with the graph's first produced token
     tok = prefill(model, prompt, torch.arange(P, device=dev))
     nxt = decode_one_token(model, tok, torch.tensor([P], device=dev))

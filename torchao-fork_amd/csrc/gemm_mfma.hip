@@ -30,6 +30,10 @@
 #ifndef TAO_GEMM_DEBUG
 #define TAO_GEMM_DEBUG 0
 #endif
+// Experiment switch: ring depth override (experiments/gemm_depth.sh; 0 = the policy below).
+#ifndef TAO_GEMM_DEPTH
+#define TAO_GEMM_DEPTH 0
+#endif
 
 namespace tao {
 
@@ -632,7 +636,8 @@ void launch_one(dim3 grid, hipStream_t stream, const uint8_t* xb, const P& pol,
     // ring depth: 4 steps, 3 where the per-stage registers grow (int8-dyn's 64-B pieces,
     // int4's 512-B x rows), 2 at BM >= 64
     constexpr bool big = sizeof(typename P::Chunk) > 32 || P::kABytes * P::kKStep > 256;
-    constexpr int D = BM <= 16 ? 4 : (BM <= 32 ? (big ? 3 : 4) : 2);
+    constexpr int D = TAO_GEMM_DEPTH > 0 ? TAO_GEMM_DEPTH
+                                         : (BM <= 16 ? 4 : (BM <= 32 ? (big ? 3 : 4) : 2));
     launch((gemm_mfma_kernel<BM, D, KG, P>), grid, dim3(256 * KG), 0, stream, xb, pol, bias, y,
            M, N, K, sps, slab, cnt);
   }

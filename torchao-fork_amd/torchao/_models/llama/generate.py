@@ -144,15 +144,49 @@ class GraphDecoder:
         self.graph.replay()
 
 
+class GraphPrefill:
+    """The prefill of a fixed prompt shape captured in a HIP graph over static buffers (the
+    reference compiles it with ``--compile_prefill``, generate.py:865-875): ``prompt`` [B, P]
+    is copied in, the replay writes the KV caches and the first greedy token into ``token``."""
+
+    def __init__(self, model: Transformer, prompt_shape, device):
+        self.model = model
+        self.prompt = torch.zeros(prompt_shape, dtype=torch.int64, device=device)
+        self.pos = torch.arange(prompt_shape[1], device=device)
+        self.token = torch.zeros(prompt_shape[0], 1, dtype=torch.int64, device=device)
+        self.stream = torch.cuda.Stream(device)
+        self.graph = None
+
+    @torch.no_grad()
+    def capture(self, prompt: torch.Tensor):
+        self.prompt.copy_(prompt)
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            self.token.copy_(prefill(self.model, self.prompt, self.pos))  # eager warm-up
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph, stream=self.stream):
+                self.token.copy_(prefill(self.model, self.prompt, self.pos))
+        torch.cuda.current_stream().wait_stream(self.stream)
+        torch.cuda.synchronize()
+
+    def __call__(self, prompt: torch.Tensor) -> torch.Tensor:
+        self.prompt.copy_(prompt)
+        self.graph.replay()
+        return self.token
+
+
 @torch.no_grad()
 def generate(model: Transformer, prompt: torch.Tensor, max_new_tokens: int,
-             decoder: Optional[GraphDecoder] = None):
+             decoder: Optional[GraphDecoder] = None, prefiller: Optional[GraphPrefill] = None):
     """Greedy decode. Returns (tokens [B, P + max_new_tokens], prefill_s, decode_s)."""
     B, P = prompt.shape
     device = prompt.device
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    tok = prefill(model, prompt, torch.arange(P, device=device))
+    if prefiller is not None:
+        tok = prefiller(prompt)
+    else:
+        tok = prefill(model, prompt, torch.arange(P, device=device))
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if decoder is not None:
@@ -215,17 +249,19 @@ def main(argv=None):
     gen = torch.Generator(device="cpu").manual_seed(args.seed + 1)
     prompt = torch.randint(0, model.config.vocab_size, (B, P), generator=gen).to(device)
 
-    decoder = None
+    decoder = prefiller = None
     if not args.no_graph:
         decoder = GraphDecoder(model, B, P + T, device)
         # capture after an eager prefill so every kernel and workspace has been set up
         decoder.reset(prompt, prefill(model, prompt, torch.arange(P, device=device)))
         decoder.capture()
+        prefiller = GraphPrefill(model, (B, P), device)
+        prefiller.capture(prompt)
 
-    generate(model, prompt, min(T, 8), decoder)  # warm-up
+    generate(model, prompt, min(T, 8), decoder, prefiller)  # warm-up
     runs = []
     for _ in range(args.num_samples):
-        tokens, t_pre, t_dec = generate(model, prompt, T, decoder)
+        tokens, t_pre, t_dec = generate(model, prompt, T, decoder, prefiller)
         runs.append((t_pre, t_dec))
     t_pre = sorted(r[0] for r in runs)[len(runs) // 2]
     t_dec = sorted(r[1] for r in runs)[len(runs) // 2]
