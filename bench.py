@@ -36,6 +36,9 @@ Reported (one JSON line, rank 0):
                  committed rocprofv3 FETCH_SIZE pass (profiles/, gfx950 x2 correction)
   cpu_baseline = the reference's CPU "dequant path" (dequantize -> F.linear, bf16) restated in
                  oracle/, timed on this host's cores over a bounded sample (rank 0, N = 1)
+  reference_gpu = the reference's own GPU kernel (PyTorch-ROCm aten._weight_int4pack_mm, which
+                 torchao's TensorCoreTiledLayout calls) on the identical weights and step, one
+                 HIP graph: its GB/s and the max rel. L2 difference from our outputs
   prefill_mfma = BASELINE config 3 (int8 dyn-act int8-weight linear, M = 128, 4096x4096, the
                  int8 MFMA path) and the int4 g32 linear at M = 128 on its bf16 MFMA path:
                  kernel us, TOPS, fraction of the dense MFMA peak, attainable-roofline fraction
@@ -191,6 +194,50 @@ INT8_PEAK_TOPS = 5000.0   # MI355X dense int8 MFMA, 2x the bf16 rate (MI355X_MIC
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA
 
 
+def reference_gpu_step(plan, xs, g, device, steps):
+    """The reference's own GPU kernel on the same step: PyTorch-ROCm's aten._weight_int4pack_mm
+    (what torchao's TensorCoreTiledLayout dispatches to, tensor_core_tiled_layout.py:104) on
+    the identical weights (repacked by aten._convert_weight_to_int4pack from the same nibbles,
+    scales/zeros in its [K/g, N, 2] layout), the 129 calls captured in one HIP graph like ours.
+    Returns its GB/s over the same algorithmic bytes and its max relative difference from our
+    outputs on the step's linears."""
+    packs = []
+    for (_, n_loc, K, packed, sz, y_loc, _y) in plan:
+        q = torch.ops.torchao.int4_unpack(packed)
+        u8 = ((q[:, ::2] << 4) | q[:, 1::2]).to(torch.uint8)
+        del q
+        packs.append((torch.ops.aten._convert_weight_to_int4pack(u8, 8),
+                      sz.transpose(0, 1).contiguous(), K, y_loc))
+        del u8
+    outs = [None] * len(packs)
+
+    def step():
+        for i, (wp, szt, K, _) in enumerate(packs):
+            outs[i] = torch.ops.aten._weight_int4pack_mm(xs[K], wp, g, szt)
+
+    stream = torch.cuda.Stream(device)
+    stream.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(stream):
+        step()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            step()
+        for _ in range(3):
+            graph.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(steps):
+            graph.replay()
+        e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    diff = max(float((o.float().reshape(-1) - y.float()).norm() / y.float().norm().clamp_min(1e-30))
+               for o, (_, _, _, y) in zip(outs, packs))
+    del packs, outs, graph
+    torch.cuda.empty_cache()
+    return ms, diff
+
+
 def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
     """BASELINE config 3 (int8 dynamic-activation int8-weight linear, M = 128, the MFMA int8
     path) and the int4 g32 linear at the same M on its bf16-MFMA path, timed per kernel by the
@@ -326,6 +373,8 @@ def main():
     ap.add_argument("--group-size", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-reference-gpu", action="store_true",
+                    help="skip timing PyTorch-ROCm's aten._weight_int4pack_mm on the same step")
     ap.add_argument("--no-prefill", action="store_true",
                     help="skip the config-3 MFMA prefill measurement (prefill_mfma)")
     ap.add_argument("--shard-policy", default="auto", choices=["auto", "size", "all", "none"],
@@ -514,6 +563,23 @@ def main():
         barrier()
         comm_ms = (time.perf_counter() - tc) / args.steps * 1e3
 
+    ref_gpu = None
+    if P == 1 and not args.no_reference_gpu:
+        try:
+            # our outputs of the last timed replay are in each plan entry's y_loc
+            ref_ms, ref_diff = reference_gpu_step(plan, xs, g, device, args.steps)
+            ref_gpu = {
+                "op": "aten._weight_int4pack_mm (PyTorch-ROCm; the reference's GPU int4 GEMM, "
+                      "tensor_core_tiled_layout.py:104), same weights, same 129-call step in one "
+                      "HIP graph",
+                "value": round(bytes_per_step / (ref_ms * 1e-3) / 1e9, 2),
+                "unit": "GB/s",
+                "ms_per_step": round(ref_ms, 4),
+                "rel_l2_vs_ours_max": round(ref_diff, 5),
+            }
+        except Exception as e:  # the aten op is build dependent: report, never fail the bench
+            ref_gpu = {"op": "aten._weight_int4pack_mm", "error": f"{type(e).__name__}: {e}"[:300]}
+
     prefill = None
     if P == 1 and args.model == "8b" and not args.no_prefill:
         prefill = prefill_mfma(device)
@@ -570,6 +636,10 @@ def main():
             },
             "cpu_baseline": cpu,
         }
+        if ref_gpu is not None:
+            rec["reference_gpu"] = ref_gpu
+            if "value" in ref_gpu:
+                rec["speedup_vs_reference_gpu"] = round(rec["value"] / ref_gpu["value"], 2)
         if prefill is not None:
             rec["prefill_mfma"] = prefill
         if comm_ms is not None:
