@@ -248,38 +248,56 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
     int H, int Hkv, int T, float scale) {
   static_assert(D == 128, "head_dim 128");
-  __shared__ float qs[D];
   __shared__ float wm[NW], wl[NW];
   __shared__ float wo[NW][D];
   const int bh = blockIdx.x;  // b * H + h
   const int b = bh / H, h = bh % H, kvh = h / (H / Hkv);
   const int L = (int)pos[0] + 1;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  if (tid < D) qs[tid] = bf16_to_f32(q[(size_t)bh * D + tid]);
-  __syncthreads();
   const int kq = lane >> 2, p = lane & 3;
-  float qr[32];
-#pragma unroll
-  for (int v = 0; v < 4; ++v)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) qr[v * 8 + e] = qs[v * 32 + p * 8 + e];
   const size_t head = (size_t)(b * Hkv + kvh) * T;
   const uint16_t* kb = kc + head * D + p * 8;
   const uint32_t* vb = reinterpret_cast<const uint32_t*>(vc + head * D) + lane;
 
-  float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
-  for (int t0 = wave * 16; t0 < L; t0 += NW * 16) {
+  // One step = 16 keys of this wave: lane (kq, p) loads 4 x 16 B of key t0 + kq, and the 16
+  // keys' V dim pair `lane`. The first step's K/V loads are issued before q's, so q (fresh from
+  // the wqkv kernel) and the first keys arrive in the same round trip; later steps prefetch the
+  // next step's K/V before computing the current one.
+  uint4 kv[4];
+  uint32_t vv[16];
+  auto load_step = [&](int t0) __attribute__((always_inline)) {
     const int t = t0 + kq;
     const int tc = t < L ? t : L - 1;  // clamped loads, masked below
-    uint4 kv[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) kv[v] = *reinterpret_cast<const uint4*>(kb + (size_t)tc * D + v * 32);
-    uint32_t vv[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int tj = t0 + j < L ? t0 + j : L - 1;
       vv[j] = vb[(size_t)tj * (D / 2)];
     }
+  };
+  load_step(wave * 16);
+  // lane p holds q dims v*32 + 8p + e (e < 8) in registers: 4 x 16 B straight from global
+  float qr[32];
+  {
+    const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bh * D + p * 8);
+    uint4 qv[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) qv[v] = qp[v * 4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const uint32_t w[4] = {qv[v].x, qv[v].y, qv[v].z, qv[v].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        qr[v * 8 + 2 * e] = bf16lo_to_f32(w[e]);
+        qr[v * 8 + 2 * e + 1] = bf16hi_to_f32(w[e]);
+      }
+    }
+  }
+
+  float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
+  for (int t0 = wave * 16; t0 < L; t0 += NW * 16) {
+    const int t = t0 + kq;
     float sc = 0.f;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
@@ -289,6 +307,13 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
         sc = fmaf(qr[v * 8 + 2 * e], bf16lo_to_f32(w[e]),
                   fmaf(qr[v * 8 + 2 * e + 1], bf16hi_to_f32(w[e]), sc));
     }
+    float vf[32];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      vf[2 * j] = bf16lo_to_f32(vv[j]);
+      vf[2 * j + 1] = bf16hi_to_f32(vv[j]);
+    }
+    if (t0 + NW * 16 < L) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
     sc += __shfl_xor(sc, 1, 64);
     sc += __shfl_xor(sc, 2, 64);
     sc = t < L ? sc * scale : -INFINITY;
@@ -307,8 +332,8 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const float pj = __shfl(e, j * 4, 64);
-      o0 = fmaf(pj, bf16lo_to_f32(vv[j]), o0);
-      o1 = fmaf(pj, bf16hi_to_f32(vv[j]), o1);
+      o0 = fmaf(pj, vf[2 * j], o0);
+      o1 = fmaf(pj, vf[2 * j + 1], o1);
     }
     m = mn;
   }
