@@ -80,7 +80,7 @@ struct Int4WO {
   static constexpr int kMfma = 8;
   static constexpr int kMaxBM = 64;  // 512-B x rows: BM 128 would need 64 x VGPRs per stage
   static constexpr int kPrefKG = 2;
-  static constexpr int kMinSlice = 8;  // steps per split-K slice
+  static constexpr int kMinSlice = 4;  // steps per split-K slice (1024 k)
   // Weights in full 128-B lines (8 rows x 128 B per wave instruction: lane l reads row
   // 8 g + l / 8, 16-B chunk l % 8 of the step) regrouped to the MFMA layout through a 2-KiB
   // per-wave LDS stage ([16 rows][8 chunks], XOR-swizzled by row); lane (n, kq) then holds
@@ -185,7 +185,7 @@ struct Int8WO {
   static constexpr int kMfma = 4;
   static constexpr int kMaxBM = 128;
   static constexpr int kPrefKG = 2;
-  static constexpr int kMinSlice = 14;
+  static constexpr int kMinSlice = 8;
   typedef f32x4_t Acc;
   const uint4* w;         // [N][K/16]
   const uint16_t* scale;  // [N]
@@ -255,7 +255,7 @@ struct Int8Dyn {
   static constexpr int kMfma = 4;
   static constexpr int kMaxBM = 128;
   static constexpr int kPrefKG = 1;
-  static constexpr int kMinSlice = 14;
+  static constexpr int kMinSlice = 4;
   typedef i32x4_t Acc;
   const uint4* w;           // [N][K/16]
   const uint16_t* wscale;   // [N]
@@ -504,42 +504,49 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
 
   const int S = gridDim.z;
   if (S > 1) {
+    // Slab hand-off without agent fences (MI355X_MICROARCH.md, "Hand-offs measured with sc1
+    // loads in place of the acquire", first row): every slab byte is stored sc1 (write-through
+    // past the XCD's L2) and read sc1 (L1 bypassed), each storing wave waits for its stores
+    // before the workgroup barrier, one lane adds the tile's ticket, and the last arriver is told
+    // by the value its add returned. The fences this replaces (buffer_wbl2 + buffer_inv, 1.7-6.5
+    // µs each and serialised per CU) made every split slower than no split.
     const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const size_t tile_bytes = (size_t)S * 4 * MT * 64 * sizeof(Acc);
+    const Rsrc srs = make_rsrc(reinterpret_cast<const uint8_t*>(slab) + tile * tile_bytes,
+                               (uint32_t)tile_bytes);
+    const uint32_t lane_off = (uint32_t)((wave * MT * 64 + lane) * sizeof(Acc));
+    constexpr uint32_t kZ = 4 * MT * 64 * sizeof(Acc);  // one slice's slab
     if (kg == 0) {
-      Acc* mine = slab + (((size_t)tile * S + blockIdx.z) * 4 + wave) * MT * 64 + lane;
 #pragma unroll
-      for (int t = 0; t < MT; ++t) mine[t * 64] = acc[t];
+      for (int t = 0; t < MT; ++t)
+        bstore16<kSC1>(srs, lane_off + t * 64 * sizeof(Acc), blockIdx.z * kZ,
+                       __builtin_bit_cast(uint4, acc[t]));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     unsigned* flag = reinterpret_cast<unsigned*>(lds);
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned ticket =
           __hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const bool last = ticket == (unsigned)S - 1;
-      if (last) {
-        __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (last) __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *flag = last ? 1u : 0u;
     }
     __syncthreads();
     if (*flag == 0 || kg != 0) return;
-    const Acc* all = slab + ((size_t)tile * S * 4 + wave) * MT * 64 + lane;
-    const size_t zstride = (size_t)4 * MT * 64;
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = Acc{0, 0, 0, 0};
-    // 4 slabs per round, all loads issued before the first add (clamped, then masked)
+    // 4 slabs per round, all loads issued before the first add (clamped, then masked); slices
+    // summed in slice order whatever the arrival order
     for (int z0 = 0; z0 < S; z0 += 4) {
       Acc part[4][MT];
 #pragma unroll
       for (int zz = 0; zz < 4; ++zz) {
         const int z = z0 + zz < S ? z0 + zz : S - 1;
 #pragma unroll
-        for (int t = 0; t < MT; ++t) part[zz][t] = all[z * zstride + t * 64];
+        for (int t = 0; t < MT; ++t)
+          part[zz][t] = __builtin_bit_cast(
+              Acc, bload16<kSC1>(srs, lane_off + t * 64 * sizeof(Acc), z * kZ));
       }
 #pragma unroll
       for (int zz = 0; zz < 4; ++zz) {
@@ -580,42 +587,36 @@ std::atomic<int> g_tune_bm{0}, g_tune_kg{0}, g_tune_splits{0};
 
 GemmShape choose_shape(int M, int N, int nsteps, int max_bm, int xsb, int pref_kg,
                        int min_slice) {
-  // From the full sweep (experiments/sweep_gemm.py, profiles/r1_sweep_gemm_full*.jsonl):
-  //  * the largest M tile (no 2x padding of M) that gives ~one round of workgroups
-  //    (>= 224 tiles of 256 CUs) unsplit; 128 gives way to 64 while that still fits in two
-  //    rounds (<= 512 tiles);
-  //  * only when even 16-row tiles are too few: split-K with the largest tile that reaches
-  //    the round, <= 256 workgroups and >= min_slice steps per slice (the slab hand-off costs
-  //    microseconds);
+  // From the sweeps with the fence-free split-K hand-off (experiments/sweep_gemm.py,
+  // profiles/r1_sweep_gemm_sc1*.jsonl; the fenced hand-off made every split lose):
+  //  * short K (<= 16 steps): the largest M tile (no 2x padding of M) that gives ~one round of
+  //    workgroups (>= 224 tiles of 256 CUs) unsplit; 128 gives way to 64 while that still fits
+  //    in two rounds (<= 512 tiles);
+  //  * otherwise the M tile that covers M up to 64 rows, and K split until the distinct weight
+  //    slices (N tiles x K slices) reach one round, <= 512 workgroups, slices >= min_slice
+  //    steps (1024 k);
   //  * the policy's preferred k-groups (int4 / int8-WO 2, int8-dyn 1).
   const long nb = (N + kBN - 1) / kBN;
   auto tiles_of = [&](int bm) { return nb * ((M + bm - 1) / bm); };
-  auto splits_of = [&](long tiles) {
-    int s = 1;
-    while (tiles * s * 2 <= 256 && s * 2 <= 8 && nsteps >= min_slice * s * 2) s *= 2;
-    return s;
-  };
   GemmShape sh{16, pref_kg, 1};
   const int cands[4] = {128, 64, 32, 16};
   bool found = false;
-  for (int bm : cands)  // first choice: no split
-    if (bm <= max_bm && (bm < 2 * M || bm == 16) && tiles_of(bm) >= 224) {
-      sh.bm = bm;
-      found = true;
-      break;
-    }
-  if (found && sh.bm == 128 && tiles_of(64) <= 512) sh.bm = 64;
-  if (!found) {  // too few tiles even at 16 rows: split K, with the largest tile that fills
-    sh.splits = splits_of(tiles_of(16));
-    for (int bm : cands) {
-      if (bm > max_bm || (bm >= 2 * M && bm != 16)) continue;
-      const int sp = splits_of(tiles_of(bm));
-      if (tiles_of(bm) * sp >= 224) {
+  if (nsteps <= 16) {
+    for (int bm : cands)
+      if (bm <= max_bm && (bm < 2 * M || bm == 16) && tiles_of(bm) >= 224) {
         sh.bm = bm;
-        sh.splits = sp;
+        found = true;
         break;
       }
-    }
+    if (found && sh.bm == 128 && tiles_of(64) <= 512) sh.bm = 64;
+  }
+  if (!found) {
+    const int cap = max_bm < 64 ? max_bm : 64;
+    while (sh.bm < cap && sh.bm < M) sh.bm *= 2;
+    const long tiles = tiles_of(sh.bm);
+    while (nb * sh.splits < 224 && tiles * sh.splits * 2 <= 512 && sh.splits * 2 <= 8 &&
+           nsteps >= min_slice * sh.splits * 2)
+      sh.splits *= 2;
   }
   const int tb = g_tune_bm.load(std::memory_order_relaxed);
   const int tk = g_tune_kg.load(std::memory_order_relaxed);

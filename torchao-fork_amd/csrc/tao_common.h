@@ -97,7 +97,8 @@ __device__ __forceinline__ uint4 ld_nt_u4(const uint4* p) {
 // no VALU on 64-bit address arithmetic (cdna guide T8/T20). Loads past the descriptor's byte
 // count return 0; callers keep every operand below 4 GiB.
 typedef __amdgpu_buffer_rsrc_t Rsrc;
-constexpr int kNT = 2;  // aux: non-temporal (streamed-once weights)
+constexpr int kNT = 2;    // aux: non-temporal (streamed-once weights)
+constexpr int kSC1 = 16;  // aux: sc1 (device scope: L1 bypassed, stores written through L2)
 
 __device__ __forceinline__ Rsrc make_rsrc(const void* base, uint32_t bytes) {
   // readfirstlane on the inputs makes the descriptor provably uniform (no waterfall loops)
@@ -114,6 +115,12 @@ __device__ __forceinline__ uint4 bload16(Rsrc r, uint32_t voff, uint32_t soff) {
   const u32x4 v =
       __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX));
   return make_uint4(v[0], v[1], v[2], v[3]);
+}
+template <int AUX = 0>
+__device__ __forceinline__ void bstore16(Rsrc r, uint32_t voff, uint32_t soff, uint4 v) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 d = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(d, r, voff, soff, AUX);
 }
 template <int AUX = 0>
 __device__ __forceinline__ uint32_t bload4(Rsrc r, uint32_t voff, uint32_t soff) {
