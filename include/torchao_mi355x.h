@@ -188,12 +188,19 @@ int tao_rope_kv_bf16(const uint16_t* qkv, const float* freqs, const int64_t* pos
                      int64_t H, int64_t Hkv, int64_t D, int64_t T, void* stream);
 
 /* One-query attention over keys 0..pos[0] of the caches, GQA (H % Hkv == 0, H/Hkv <= 8),
- * D == 128: out [B][1][H*D] bf16. partial: fp32 workspace of B*Hkv*ceil(T/64)*(H/Hkv)*(D+2),
- * used only when T > 1024 (shorter caches run one single-pass kernel and may pass NULL).
+ * D == 128: out [B][1][H*D] bf16. partial: fp32 workspace of B*Hkv*ceil(T/64)*(H/Hkv)*(D+2)
+ * for the two-launch split (T > 1024, or tao_tune_attn 1); NULL = the library's per-stream
+ * workspace (as the one-launch split of tao_tune_attn 2/3 uses: run once eagerly before graph
+ * capture). Shorter caches run one single-pass kernel and do not touch it.
  * Replaces F.scaled_dot_product_attention at decode (model.py:441-476). */
 int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
                          const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
                          int64_t Hkv, int64_t D, int64_t T, float scale, void* stream);
+
+/* Process-wide choice of the decode-attention kernel: 0 = single-pass workgroup per query head
+ * for T <= 1024, else the two-launch split (default); 1 = two-launch split; 2 / 3 = one launch
+ * over 32 / 64-key chunks merged by the kv head's last arriving chunk. */
+int tao_tune_attn(int mode);
 
 /* y = bf16(bf16(silu(a)) * b) elementwise over n bf16 (n even). Replaces FeedForward's
  * F.silu(w1(x)) * w3(x) (model.py:485-486). b == NULL: a holds n interleaved (gate, up) pairs

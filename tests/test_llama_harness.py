@@ -170,6 +170,41 @@ def test_fused_kernels_match_torch_ops_gpu():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
+def test_attn_decode_modes_gpu(mode, G):
+    """Every decode-attention kernel (tao_tune_attn: 0 single-pass up to 1024 keys, 1 two-launch
+    split, 2 / 3 one launch over 32 / 64-key chunks merged by the last arriver) against fp32 SDPA, GQA groups 1..8, lengths across chunk edges; the one-launch kernels are also
+    run-to-run identical (chunks merged in chunk order whatever the arrival order) and leave
+    their counters reset (the same workspace serves every call)."""
+    import torch.nn.functional as F
+
+    from torchao import _lib
+    from torchao._models.llama import kernels
+
+    dev = torch.device("cuda")
+    Hkv, D = 8 // G if G < 8 else 2, 128
+    H = Hkv * G
+    _lib.call("tao_tune_attn", mode)
+    try:
+        for T, L in ((64, 1), (64, 31), (64, 32), (64, 33), (328, 129), (328, 328),
+                     (1024, 1000), (1536, 1100)):
+            kc = torch.randn(2, Hkv, T, D, device=dev, dtype=torch.bfloat16)
+            vc = torch.randn_like(kc)
+            q = torch.randn(2, H, 1, D, device=dev, dtype=torch.bfloat16)
+            pos = torch.tensor([L - 1], device=dev)
+            got = kernels.attn_decode(q, kc, vc, pos, 1 / math.sqrt(D))
+            again = kernels.attn_decode(q, kc, vc, pos, 1 / math.sqrt(D))
+            ref = F.scaled_dot_product_attention(q.float(), kc[:, :, :L].float(),
+                                                 vc[:, :, :L].float(), enable_gqa=True)
+            ref = ref.transpose(1, 2).reshape(2, 1, H * D)
+            torch.testing.assert_close(got.float(), ref, rtol=2e-2, atol=2e-2)
+            assert torch.equal(got, again)
+    finally:
+        _lib.call("tao_tune_attn", 0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("quant", [None, "int4wo-32"])
 def test_fused_decode_matches_unfused_gpu(quant):
     dev = torch.device("cuda")

@@ -10,9 +10,13 @@
 //   * attention: one query per (batch, head), keys 0..pos. Caches of <= 1024 rows: one kernel,
 //                a workgroup per query head (online softmax per wave, LDS merge). Longer:
 //                split over 64-key chunks (flash-decoding; GQA: a workgroup serves the G query
-//                heads of one kv head), then a combine kernel merges the chunks' (max, sum, o)
+//                heads of one kv head), then a combine kernel merges the chunks' (max, sum, o).
+//                Opt-in (tao_tune_attn 2/3): the split in one launch, merged by the kv head's
+//                last arriving chunk (measured slower end to end, 672 vs 700 tokens/s)
 //   * SiLU-mul:  y = bf16(bf16(silu(a)) * b)                             (F.silu(w1 x) * w3 x)
 //   * argmax:    greedy next token over bf16 logits, torch.argmax's first-index tie rule
+#include <atomic>
+
 #include "tao_common.h"
 
 #ifndef TAO_ATTN_WAVES
@@ -240,6 +244,9 @@ __global__ __launch_bounds__(64) void attn_combine_kernel(const float* __restric
 // ceil((L - 16 w) / (16 NW)) steps, so at T <= 1024 the chain is <= 4 round trips; longer
 // caches take the two-kernel split above.
 constexpr int kSingleMaxT = 1024;
+// tao_tune_attn: 0 = single-pass for T <= 1024 else the two-launch split (default), 1 = the
+// two-launch split, 2 / 3 = attn_chunk_fused_kernel with 32 / 64-key chunks
+std::atomic<int> g_attn_mode{0};
 constexpr int kSingleWaves = TAO_ATTN_WAVES;
 
 template <int D, int NW>
@@ -358,6 +365,167 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     }
     const float inv = 1.f / ls;
     reinterpret_cast<uint32_t*>(out)[(size_t)bh * (D / 2) + lane] =
+        (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
+  }
+}
+
+// ---- decode attention in one launch, split over key chunks (opt-in, tao_tune_attn 2 / 3) -----
+// Flash-decoding with the merge in the same launch: a workgroup per (batch, kv head, CH-key
+// chunk) serves the G query heads of its kv head (GQA: each K/V byte is read once, not G
+// times), and the chunk's partial (m, l, o) goes to a slab; the chunk whose ticket comes last
+// for its kv head merges all its chunks in chunk order (deterministic) and writes the bf16
+// output. Hand-off as the split-K GEMM's (gemm_mfma.hip): sc1 stores and loads of the partials,
+// every storing wave's vmcnt(0) wait and a workgroup barrier before one lane's agent-scope
+// ticket, no fences. The grid is sized by T; chunks past pos[0] exit without a ticket. Against
+// attn_single_kernel (a workgroup per query head over the whole cache): G x fewer K/V bytes and
+// ~ceil(L / CH) x more workgroups per head, but the hand-off adds three device-scope round trips
+// (sc1 store, ticket, sc1 loads) to a latency-bound launch: Llama-3-8B int4 decode 672 (32-key)
+// / 669 (64-key) vs 700 tokens/s with the single-pass kernel (experiments/ab_attn.py,
+// profiles/r1_ab_attn.jsonl).
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+template <int G, int CH>
+__global__ __launch_bounds__(256) void attn_chunk_fused_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, float* __restrict__ part,
+    unsigned* __restrict__ cnt, uint16_t* __restrict__ out, int Hkv, int T, float scale) {
+  constexpr int D = 128;
+  constexpr int KPT = 256 / CH;       // threads per key in the score phase
+  constexpr int DPT = D / KPT;        // dims per thread
+  constexpr int KL = DPT / 8;         // 16-B K loads per thread
+  constexpr int PS = D + 2;           // floats per (chunk, head) partial: o[D], m, l
+  static_assert(CH == 32 || CH == 64, "chunk of 32 or 64 keys");
+  __shared__ float qs[G][D];
+  __shared__ float ps[G][CH];
+  __shared__ unsigned flag;
+  const int bk = blockIdx.x;  // b * Hkv + kvh
+  const int b = bk / Hkv, kvh = bk % Hkv;
+  const int c = blockIdx.y, NC = gridDim.y;
+  const int L = (int)pos[0] + 1;
+  const int t0 = c * CH;
+  if (t0 >= L) return;  // uniform; not counted
+  const int nact = (L + CH - 1) / CH;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int H = Hkv * G;
+  const size_t head = (size_t)bk * T;
+
+  // every load of the chunk up front: this thread's K piece, then its V column (dim pair
+  // `lane`, all CH keys; rows past L clamped and weighted 0), then q
+  const int j = tid / KPT, pp = tid % KPT;
+  const int kk = t0 + j;
+  uint4 kv[KL];
+  {
+    const uint4* kr = reinterpret_cast<const uint4*>(
+        kc + (head + (kk < L ? kk : L - 1)) * D + pp * DPT);
+#pragma unroll
+    for (int v = 0; v < KL; ++v) kv[v] = kr[v];
+  }
+  uint32_t vv[CH];
+  {
+    const uint32_t* vb = reinterpret_cast<const uint32_t*>(vc + head * D) + lane;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) vv[i] = vb[(size_t)(t0 + i < L ? t0 + i : L - 1) * (D / 2)];
+  }
+  for (int i = tid; i < G * D / 2; i += 256) {
+    const int g = i / (D / 2), d2 = i % (D / 2);
+    const uint32_t w = reinterpret_cast<const uint32_t*>(q)[((size_t)b * H + kvh * G + g) * (D / 2) + d2];
+    qs[g][2 * d2] = bf16lo_to_f32(w);
+    qs[g][2 * d2 + 1] = bf16hi_to_f32(w);
+  }
+  __syncthreads();
+
+  // scores of key j for the G heads: KPT lanes per key, DPT dims each
+  float sc[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) sc[g] = 0.f;
+#pragma unroll
+  for (int v = 0; v < KL; ++v) {
+    const uint32_t w[4] = {kv[v].x, kv[v].y, kv[v].z, kv[v].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int d = pp * DPT + v * 8 + 2 * e;
+      const float k0 = bf16lo_to_f32(w[e]), k1 = bf16hi_to_f32(w[e]);
+#pragma unroll
+      for (int g = 0; g < G; ++g) sc[g] = fmaf(qs[g][d], k0, fmaf(qs[g][d + 1], k1, sc[g]));
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int o = 1; o < KPT; o <<= 1) sc[g] += __shfl_xor(sc[g], o, 64);
+  if (pp == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) ps[g][j] = kk < L ? sc[g] * scale : -INFINITY;
+  }
+  __syncthreads();
+
+  // per head (wave g, g + 4): chunk softmax, then o = sum_j p_j v_j for dim pair `lane`
+  const Rsrc prs = make_rsrc(part + (size_t)bk * NC * G * PS, (uint32_t)(NC * G * PS * 4));
+  for (int g = wave; g < G; g += 4) {
+    const float s = lane < CH ? ps[g][lane] : -INFINITY;
+    float m = s;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));  // finite: key t0 < L
+    const float e = s == -INFINITY ? 0.f : __expf(s - m);
+    float l = e;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o, 64);
+    float o0 = 0.f, o1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const float pj = __shfl(e, i, 64);
+      o0 = fmaf(pj, bf16lo_to_f32(vv[i]), o0);
+      o1 = fmaf(pj, bf16hi_to_f32(vv[i]), o1);
+    }
+    const uint32_t base = (uint32_t)((c * G + g) * PS) * 4;
+    const uint2 ov = make_uint2(__float_as_uint(o0), __float_as_uint(o1));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, ov), prs, base + 8 * lane,
+                                          0, kSC1);
+    if (lane == 0) {
+      const uint2 ml = make_uint2(__float_as_uint(m), __float_as_uint(l));
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, ml), prs, base + 4 * D,
+                                            0, kSC1);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned ticket =
+        __hip_atomic_fetch_add(&cnt[bk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = ticket == (unsigned)nact - 1;
+    if (last) __hip_atomic_store(&cnt[bk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = last ? 1u : 0u;
+  }
+  __syncthreads();
+  if (flag == 0) return;
+
+  // merge the kv head's chunks in chunk order, 8 chunks' loads in flight per round
+  for (int g = wave; g < G; g += 4) {
+    float M = -INFINITY, ls = 0.f, a0 = 0.f, a1 = 0.f;
+    for (int c0 = 0; c0 < nact; c0 += 8) {
+      uint2 ml[8], ov[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int cc = c0 + u < nact ? c0 + u : nact - 1;
+        const uint32_t base = (uint32_t)((cc * G + g) * PS) * 4;
+        ml[u] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(prs, base + 4 * D, 0, kSC1));
+        ov[u] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(prs, base + 8 * lane, 0, kSC1));
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (c0 + u < nact) {
+          const float m = __uint_as_float(ml[u].x), l = __uint_as_float(ml[u].y);
+          const float mn = fmaxf(M, m);
+          const float fo = __expf(M - mn), fn = __expf(m - mn);  // M = -inf first: fo = 0
+          ls = ls * fo + l * fn;
+          a0 = a0 * fo + __uint_as_float(ov[u].x) * fn;
+          a1 = a1 * fo + __uint_as_float(ov[u].y) * fn;
+          M = mn;
+        }
+      }
+    }
+    const float inv = 1.f / ls;
+    reinterpret_cast<uint32_t*>(out)[((size_t)b * H + kvh * G + g) * (D / 2) + lane] =
         (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
   }
 }
@@ -498,7 +666,31 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
   TAO_CHECK_ARG(G == 1 || G == 2 || G == 4 || G == 8, "attn_decode: H / Hkv must be 1, 2, 4 or 8");
   TAO_CHECK_ALIGN(k_cache, 16, "k_cache");
   hipStream_t st = as_stream(stream);
-  if (T <= kSingleMaxT) {  // partial is not touched
+  const int mode = g_attn_mode.load(std::memory_order_relaxed);
+  if (mode == 2 || mode == 3) {  // one launch, key chunks merged by the last arriver
+    const int CH = mode == 2 ? 32 : 64;
+    const int NC = (int)((T + CH - 1) / CH);
+    void* ws = nullptr;
+    unsigned* cnt = nullptr;
+    const size_t bytes = (size_t)B * Hkv * NC * G * (D + 2) * sizeof(float);
+    TAO_CHECK_ARG(bytes / B / Hkv < (1ull << 31), "attn_decode: cache too long");
+    const int rc = split_workspace(st, bytes, (size_t)(B * Hkv), &ws, &cnt);
+    if (rc != TAO_OK) return rc;
+    float* slab = reinterpret_cast<float*>(ws);
+    const dim3 grid((unsigned)(B * Hkv), (unsigned)NC);
+    switch (G * 100 + CH) {
+#define TAO_ATTN_F(GG, CC)                                                                   \
+  case GG * 100 + CC:                                                                        \
+    launch(attn_chunk_fused_kernel<GG, CC>, grid, dim3(256), 0, st, q, k_cache, v_cache, pos, \
+           slab, cnt, out, (int)Hkv, (int)T, scale);                                         \
+    break;
+      TAO_ATTN_F(1, 32) TAO_ATTN_F(2, 32) TAO_ATTN_F(4, 32) TAO_ATTN_F(8, 32)
+      TAO_ATTN_F(1, 64) TAO_ATTN_F(2, 64) TAO_ATTN_F(4, 64) TAO_ATTN_F(8, 64)
+#undef TAO_ATTN_F
+    }
+    return check_launch("attn_chunk_fused_kernel");
+  }
+  if (T <= kSingleMaxT && mode == 0) {  // partial is not touched
     launch((attn_single_kernel<128, kSingleWaves>), dim3((unsigned)(B * H)),
            dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
            (int)T, scale);
@@ -506,6 +698,14 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
   }
   const int NC = (int)((T + kChunk - 1) / kChunk);
   const dim3 g1((unsigned)(B * Hkv), (unsigned)NC), g2((unsigned)(B * H));
+  if (partial == nullptr) {  // the library's workspace
+    void* ws = nullptr;
+    unsigned* cnt = nullptr;
+    const int rc = split_workspace(st, (size_t)B * Hkv * NC * G * (D + 2) * sizeof(float), 1,
+                                   &ws, &cnt);
+    if (rc != TAO_OK) return rc;
+    partial = reinterpret_cast<float*>(ws);
+  }
   switch (G) {
 #define TAO_ATTN(GG)                                                                          \
   case GG:                                                                                    \
@@ -520,6 +720,15 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
 #undef TAO_ATTN
   }
   return check_launch("attn_decode");
+}
+
+int tao_tune_attn(int mode) {
+  TAO_CHECK_ARG(mode >= 0 && mode <= 3,
+                "tune: attention mode must be 0 (auto: single-pass up to 1024 keys, else split), "
+                "1 (two-launch split), 2 (one launch, 32-key chunks) or 3 (one launch, 64-key "
+                "chunks)");
+  g_attn_mode.store(mode);
+  return TAO_OK;
 }
 
 int tao_silu_mul_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t n,

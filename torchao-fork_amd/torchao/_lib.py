@@ -55,6 +55,7 @@ _SIGNATURES = {
     "tao_rope_kv_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p],
     "tao_attn_decode_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
                              ctypes.c_float, _p],
+    "tao_tune_attn": [_int],
     "tao_silu_mul_bf16": [_p, _p, _p, _i64, _p],
     "tao_argmax_bf16": [_p, _p, _i64, _i64, _p],
     "tao_int4_quantize_bf16": [_p, _p, _p, _i64, _i64, _i64, ctypes.c_float, _p],
