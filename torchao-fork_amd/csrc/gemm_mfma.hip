@@ -618,6 +618,9 @@ GemmShape choose_shape(int M, int N, int nsteps, int max_bm, int xsb, int pref_k
            nsteps >= min_slice * sh.splits * 2)
       sh.splits *= 2;
   }
+  // int8-dyn (one k-group by default): two when the launch is unsplit and >= 4 M tiles re-read
+  // each weight tile (M = 128, 4096^2: 11.4 vs 11.9 µs; profiles/r1_sweep_gemm_sc1*.jsonl)
+  if (pref_kg == 1 && sh.splits == 1 && (M + sh.bm - 1) / sh.bm >= 4) sh.kg = 2;
   const int tb = g_tune_bm.load(std::memory_order_relaxed);
   const int tk = g_tune_kg.load(std::memory_order_relaxed);
   const int ts = g_tune_splits.load(std::memory_order_relaxed);
