@@ -83,6 +83,12 @@ int tao_tune_linear_crossover(int max_gemv_m);
  * each. Process-wide. */
 int tao_tune_gemm(int m_tile, int k_groups, int splits);
 
+/* Process-wide choice of the int8 dynamic-activation GEMM kernel (M above the GEMV crossover):
+ * 0 = auto (the LDS-staged int8 kernel when K % 128 == 0, M >= 128 and its 64-row tiles number
+ * >= 192, unsplit; else the per-wave-column MFMA kernel), 1 = always the per-wave-column kernel,
+ * 2 = the LDS-staged kernel whenever K % 128 == 0. tao_tune_gemm's m_tile (64 / 128) and splits also apply to the LDS kernel. */
+int tao_tune_gemm_algo(int algo);
+
 /* packed[N][K/8] <- q[N][K] (int32 values 0..15).
  * Replaces aten._convert_weight_to_int4pack(u8, inner_k_tiles) at
  * torchao/dtypes/uintx/tensor_core_tiled_layout.py:279 (device kernel). K % 8 == 0. */

@@ -193,3 +193,42 @@ def test_int8dq_decode_takes_fused_path_and_matches_unfused():
         assert torch.equal(y, y_ref)
     assert _fused_int8_dyn_decode(torch.randn(4, K, dtype=torch.bfloat16, device=DEV), wt,
                                   None) is None
+
+
+# ---- int8-dyn GEMM at M >= 48: the LDS-staged kernel (gemm_i8_lds_kernel) --------------------
+# Forced on (tao_tune_gemm_algo 2) across ragged M / N, both M tiles and several K splits, with
+# and without bias: bit-exact against the CPU oracle, and identical to the per-wave-column
+# kernel (algo 1) on the same inputs.
+@pytest.mark.parametrize("M,N,K", [(128, 4096, 4096), (48, 330, 1024), (200, 4160, 2048),
+                                   (128, 14336, 4096), (128, 4096, 14336), (5, 64, 128),
+                                   (512, 1024, 3072), (256, 4096, 4096), (128, 6144, 4096)])
+def test_int8_lds_gemm_bit_exact(M, N, K):
+    from torchao import _lib
+
+    w = oracle.make_linear_weight(N, K, seed=N + 7)
+    wq, ws = oracle.int8_dyn_weight(w)
+    x = oracle.make_activation(M, K, seed=M + 3) * 2
+    x[0, K // 5] = 300.0
+    xq, xs = oracle.int8_act_quant(x)
+    bias = oracle.make_activation(1, N, seed=9).reshape(-1)
+    args = [t.to(DEV) for t in (xq, xs, wq, ws)]
+    try:
+        for b in (None, bias):
+            ref = oracle.int8_scaled_mm(xq, xs, wq, ws, b, epilogue="cpu")
+            bd = None if b is None else b.to(DEV)
+            _lib.call("tao_tune_gemm_algo", 1)
+            _lib.call("tao_tune_linear_crossover", 1)
+            old = torch.ops.torchao.int8_scaled_mm(*args, bd).cpu()
+            _lib.call("tao_tune_gemm_algo", 2)
+            for bm, splits in ((0, 0), (64, 1), (128, 1), (64, 3), (128, 8)):
+                _lib.call("tao_tune_gemm", bm, 0, splits)
+                y = torch.ops.torchao.int8_scaled_mm(*args, bd).cpu()
+                assert torch.equal(y, ref), (bm, splits)
+            assert torch.equal(old, ref)
+            _lib.call("tao_tune_gemm", 0, 0, 0)
+            _lib.call("tao_tune_gemm_algo", 0)  # the auto policy's pick for this shape
+            assert torch.equal(torch.ops.torchao.int8_scaled_mm(*args, bd).cpu(), ref)
+    finally:
+        _lib.call("tao_tune_gemm", 0, 0, 0)
+        _lib.call("tao_tune_gemm_algo", 0)
+        _lib.call("tao_tune_linear_crossover", 0)

@@ -683,6 +683,232 @@ int launch_gemm(const void* x, const P& pol, const uint16_t* bias, uint16_t* y, 
   return check_launch("gemm_mfma_kernel");
 }
 
+// ---- int8 x int8 GEMM with both operands staged through LDS (int8-dyn, M >= 48) -------------
+// gemm_mfma_kernel gives each wave 16 columns x all BM rows: every MFMA reads its own 1-KiB A
+// fragment from LDS and every 16-column weight piece is regrouped per wave, ~2 KiB of LDS
+// traffic per MFMA, so at M = 128 the LDS port, not the MFMA or HBM, sets the pace. Here a
+// workgroup tile is BM x 64 with the 4 waves in 2 x 2 (wave (wm, wn): rows wm BM/2 .., columns
+// wn 32 ..), so each A fragment feeds 2 MFMAs and each B fragment BM/32: 0.75 KiB per MFMA at
+// BM = 128. Per 128-k step the workgroup loads x [BM][128 B] and W [64][128 B] in full 128-B
+// lines (8 threads per row) D steps ahead into registers, then stores them to a double-buffered
+// LDS image whose 16-B chunks are XOR-swizzled by (row >> 1) & 7: the 16 lanes of each
+// ds_write_b128 / ds_read_b128 pass (two rows x 8 chunks; 16 consecutive rows at one chunk) hit
+// 16 distinct bank groups. One barrier per step. K is split across workgroups with the same
+// fence-free slab hand-off as gemm_mfma_kernel; the epilogue is Int8Dyn's (bit-exact).
+constexpr int kI8Step = 128;  // k bytes per step of gemm_i8_lds_kernel
+
+__device__ __forceinline__ int i8_swz(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
+
+template <int BM, int D>
+__global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
+    const int8_t* __restrict__ x, const int8_t* __restrict__ w, const uint16_t* __restrict__ xscale,
+    const uint16_t* __restrict__ wscale, const uint16_t* __restrict__ bias,
+    uint16_t* __restrict__ y, int M, int N, int K, int sps, i32x4_t* __restrict__ slab,
+    unsigned* __restrict__ cnt) {
+  constexpr int XL = BM / 32;           // x chunks per thread per step
+  constexpr int WL = 2;                 // W chunks per thread per step (64 rows x 8 chunks)
+  constexpr int MT = BM / 32, NT = 2;   // 16x16 output tiles per wave
+  constexpr int XT = BM * 8, WT = 64 * 8;  // uint4 per image
+  __shared__ uint4 lds[2 * (XT + WT)];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int n_blk = blockIdx.x * 64, m_blk = blockIdx.y * BM;
+  const int nsteps = K / kI8Step;
+  const int s0 = blockIdx.z * sps;
+  const int s1 = s0 + sps < nsteps ? s0 + sps : nsteps;  // launcher: no empty slice
+  const int J = s1 - s0;
+
+  // load slots: row lr + 32 i, 16-B chunk lc; rows past M / N clamped (computed, dropped)
+  const int lr = tid >> 3, lc = tid & 7;
+  const Rsrc xrs = make_rsrc(x, (uint32_t)M * (uint32_t)K);
+  const Rsrc wrs = make_rsrc(w, (uint32_t)N * (uint32_t)K);
+  uint32_t xv[XL], wv[WL];
+  int xo[XL], wo[WL];
+#pragma unroll
+  for (int i = 0; i < XL; ++i) {
+    const int r = lr + 32 * i, gm = m_blk + r < M ? m_blk + r : M - 1;
+    xv[i] = (uint32_t)gm * (uint32_t)K + 16 * lc;
+    xo[i] = i8_swz(r, lc);
+  }
+#pragma unroll
+  for (int i = 0; i < WL; ++i) {
+    const int r = lr + 32 * i, gn = n_blk + r < N ? n_blk + r : N - 1;
+    wv[i] = (uint32_t)gn * (uint32_t)K + 16 * lc;
+    wo[i] = XT + i8_swz(r, lc);
+  }
+
+  i32x4_t acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = i32x4_t{0, 0, 0, 0};
+
+  uint4 xr[D][XL], wr[D][WL];
+  auto load_step = [&](int j, uint4 (&xd)[XL], uint4 (&wd)[WL]) __attribute__((always_inline)) {
+    const int st = s0 + j < s1 ? s0 + j : s1 - 1;  // past the slice: re-read (never predicated)
+#pragma unroll
+    for (int i = 0; i < XL; ++i) xd[i] = bload16(xrs, xv[i], st * kI8Step);
+#pragma unroll
+    for (int i = 0; i < WL; ++i) wd[i] = bload16<kNT>(wrs, wv[i], st * kI8Step);
+  };
+  auto store_step = [&](const uint4 (&xd)[XL], const uint4 (&wd)[WL], int buf)
+      __attribute__((always_inline)) {
+    uint4* img = lds + buf * (XT + WT);
+#pragma unroll
+    for (int i = 0; i < XL; ++i) img[xo[i]] = xd[i];
+#pragma unroll
+    for (int i = 0; i < WL; ++i) img[wo[i]] = wd[i];
+  };
+  const int fr = lane & 15, kq = lane >> 4;
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const uint4* img = lds + buf * (XT + WT);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {  // two 64-k blocks per step: chunks 4 b + kq
+      const int c = 4 * b + kq;
+      i32x4_t bf[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        bf[nt] = __builtin_bit_cast(i32x4_t, img[XT + i8_swz(wn * 32 + nt * 16 + fr, c)]);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const i32x4_t af =
+            __builtin_bit_cast(i32x4_t, img[i8_swz(wm * (BM / 2) + mt * 16 + fr, c)]);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[nt], acc[mt][nt], 0, 0, 0);
+      }
+    }
+  };
+  // slot u holds local step j (j % D == u, compile-time); its registers are free once stored
+  auto body = [&](auto uc, int j) __attribute__((always_inline)) {
+    constexpr int u = decltype(uc)::value;
+    load_step(j + D, xr[u], wr[u]);
+    compute(j & 1);
+    if (j + 1 < J) store_step(xr[(u + 1) % D], wr[(u + 1) % D], (j + 1) & 1);
+    __syncthreads();
+  };
+  static_for<0, D>([&](auto i) __attribute__((always_inline)) {
+    load_step(decltype(i)::value, xr[decltype(i)::value], wr[decltype(i)::value]);
+  });
+  store_step(xr[0], wr[0], 0);
+  __syncthreads();
+  int j = 0;
+  for (; j + D <= J; j += D)
+    static_for<0, D>([&](auto uc) __attribute__((always_inline)) {
+      body(uc, j + decltype(uc)::value);
+    });
+  static_for<0, D - 1>([&](auto uc) __attribute__((always_inline)) {
+    if (j + decltype(uc)::value < J) body(uc, j + decltype(uc)::value);
+  });
+
+  const int S = gridDim.z;
+  if (S > 1) {  // fence-free slab hand-off (see gemm_mfma_kernel)
+    const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
+    constexpr uint32_t kZ = 4 * MT * NT * 64 * sizeof(i32x4_t);  // one slice's slab
+    const Rsrc srs = make_rsrc(reinterpret_cast<const uint8_t*>(slab) + (size_t)tile * S * kZ,
+                               (uint32_t)(S * kZ));
+    const uint32_t lo = (uint32_t)((wave * MT * NT * 64 + lane) * sizeof(i32x4_t));
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+        bstore16<kSC1>(srs, lo + (a * NT + b) * 64 * sizeof(i32x4_t), blockIdx.z * kZ,
+                       __builtin_bit_cast(uint4, acc[a][b]));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* flag = reinterpret_cast<unsigned*>(lds);
+    if (tid == 0) {
+      const unsigned ticket =
+          __hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = ticket == (unsigned)S - 1;
+      if (last) __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last ? 1u : 0u;
+    }
+    __syncthreads();
+    if (*flag == 0) return;
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b) acc[a][b] = i32x4_t{0, 0, 0, 0};
+    for (int z = 0; z < S; ++z) {  // slice order
+      i32x4_t part[MT][NT];
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b)
+          part[a][b] = __builtin_bit_cast(
+              i32x4_t, bload16<kSC1>(srs, lo + (a * NT + b) * 64 * sizeof(i32x4_t), z * kZ));
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) acc[a][b] += part[a][b];
+    }
+  }
+
+  // C/D map: col = lane & 15 (n), row = 4 (lane >> 4) + i (m); Int8Dyn's epilogue
+#pragma unroll
+  for (int b = 0; b < NT; ++b) {
+    const int n = n_blk + wn * 32 + b * 16 + fr;
+    if (n >= N) continue;
+    const float sw = bf16_to_f32(wscale[n]);
+    const float bv = bias != nullptr ? bf16_to_f32(bias[n]) : 0.f;
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m_blk + wm * (BM / 2) + a * 16 + 4 * kq + i;
+        if (m < M) {
+          float v = round_bf16(round_bf16((float)acc[a][b][i]) * bf16_to_f32(xscale[m]));
+          v = round_bf16(v * sw);
+          if (bias != nullptr) v = round_bf16(v + bv);
+          y[(size_t)m * N + n] = f32_to_bf16(v);
+        }
+      }
+  }
+}
+
+// gemm_i8_lds_kernel selection (tao_tune_gemm_algo): 0 = auto, 1 = never, 2 = always (K % 128)
+std::atomic<int> g_gemm_algo{0};
+
+int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uint16_t* ws,
+                  const uint16_t* bias, uint16_t* y, int M, int N, int K, bool auto_mode,
+                  hipStream_t stream) {
+  const int nsteps = K / kI8Step;
+  const long ntile = (N + 63) / 64;
+  // auto (profiles/r1_sweep_i8_lds.jsonl): the M = 128 tile once it alone fills a round of
+  // workgroups, else 64; no split (every winning LDS shape ran unsplit). Forced (algo 2, the
+  // parity tests' mode): split towards one round, slices of >= 4 steps (512 k).
+  int bm = auto_mode ? (ntile * ((M + 127) / 128) >= 224 ? 128 : 64) : (M > 64 ? 128 : 64);
+  const int tb = g_tune_bm.load(std::memory_order_relaxed);
+  if (tb == 64 || tb == 128) bm = tb;
+  const long tiles = ntile * ((M + bm - 1) / bm);
+  int splits = 1;
+  while (!auto_mode && tiles * splits < 224 && splits * 2 <= 16 && nsteps >= 4 * splits * 2)
+    splits *= 2;
+  const int ts = g_tune_splits.load(std::memory_order_relaxed);
+  if (ts) splits = ts < nsteps ? ts : nsteps;
+  const int sps = (nsteps + splits - 1) / splits;
+  const int S = (nsteps + sps - 1) / sps;
+  const dim3 grid((N + 63) / 64, (M + bm - 1) / bm, S);
+  i32x4_t* slab = nullptr;
+  unsigned* cnt = nullptr;
+  if (S > 1) {
+    void* wsp = nullptr;
+    const size_t t = (size_t)grid.x * grid.y;
+    const int rc = split_workspace(stream, t * S * bm * 64 * sizeof(int), t, &wsp, &cnt);
+    if (rc != TAO_OK) return rc;
+    slab = reinterpret_cast<i32x4_t*>(wsp);
+  }
+  if (bm == 128)
+    launch((gemm_i8_lds_kernel<128, 3>), grid, dim3(256), 0, stream, xq, wq, xs, ws, bias, y, M,
+           N, K, sps, slab, cnt);
+  else
+    launch((gemm_i8_lds_kernel<64, 4>), grid, dim3(256), 0, stream, xq, wq, xs, ws, bias, y, M,
+           N, K, sps, slab, cnt);
+  return check_launch("gemm_i8_lds_kernel");
+}
+
 // Largest M served by the GEMV kernels (tao_tune_linear_crossover; 0 = built-in).
 std::atomic<int> g_max_gemv_m{0};
 // Built-in crossover (experiments/bench_paths.py --crossover): the GEMV wins at M <= 2, and at
@@ -708,6 +934,13 @@ int gshift_of(int64_t g) {
 int int8_scaled_mm_launch(const int8_t* xq, const uint16_t* xs, const int8_t* wq,
                           const uint16_t* ws, const uint16_t* bias, uint16_t* y, int M, int N,
                           int K, hipStream_t stream) {
+  // The LDS-staged kernel where its unsplit 64-row tiles fill >= 192 workgroups (M >= 128):
+  // M = 128 N = 6144 14.9 vs 20.0 µs, M = 256 4096^2 14.8 vs 16.5, M = 512 22.5 vs 30.8; ties at
+  // N >= 14336; the per-wave-column kernel keeps M = 64..128 at N = 4096 (11.8 vs 12.6 µs).
+  const int algo = g_gemm_algo.load(std::memory_order_relaxed);
+  const long t64 = (long)((N + 63) / 64) * ((M + 63) / 64);
+  if (K % kI8Step == 0 && (algo == 2 || (algo == 0 && M >= 128 && t64 >= 192)))
+    return launch_i8_lds(xq, xs, wq, ws, bias, y, M, N, K, algo == 0, stream);
   Int8Dyn pol;
   pol.w = reinterpret_cast<const uint4*>(wq);
   pol.wscale = ws;
@@ -758,6 +991,14 @@ extern "C" int tao_int8wo_linear_bf16(const uint16_t* x, const int8_t* w, const 
 extern "C" int tao_tune_linear_crossover(int max_gemv_m) {
   TAO_CHECK_ARG(max_gemv_m >= 0 && max_gemv_m <= 8, "tune: max_gemv_m must be in [0, 8]");
   tao::g_max_gemv_m.store(max_gemv_m);
+  return TAO_OK;
+}
+
+extern "C" int tao_tune_gemm_algo(int algo) {
+  TAO_CHECK_ARG(algo >= 0 && algo <= 2,
+                "tune: gemm algo must be 0 (auto), 1 (per-wave-column kernel only) or 2 (LDS-staged "
+                "int8 kernel whenever K %% 128 == 0)");
+  tao::g_gemm_algo.store(algo);
   return TAO_OK;
 }
 
