@@ -81,4 +81,24 @@ float probe_read(const void* p, int64_t bytes, int block, int L, int nt, void* o
   return ms;
 }
 
+// Plain launch of the streaming read on a stream (graph capture). bytes % (16 * block * L) == 0.
+int probe_read_launch(const void* p, int64_t bytes, int block, int L, int nt, void* out,
+                      void* stream) {
+  const int64_t T = bytes / 16 / L;
+  const int grid = (int)(T / block);
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint32_t* o = reinterpret_cast<uint32_t*>(out);
+  hipStream_t st = (hipStream_t)stream;
+#define RL(LL)                                                                               \
+  if (L == LL) {                                                                             \
+    if (nt)                                                                                  \
+      hipLaunchKernelGGL((read_kernel<LL, true>), dim3(grid), dim3(block), 0, st, q, o, T);   \
+    else                                                                                     \
+      hipLaunchKernelGGL((read_kernel<LL, false>), dim3(grid), dim3(block), 0, st, q, o, T);  \
+  }
+  RL(1) RL(2) RL(4) RL(8) RL(16)
+#undef RL
+  return (int)hipGetLastError();
+}
+
 }  // extern "C"

@@ -2,12 +2,15 @@
 
 For each (N, K): weights rotated over > 300 MB of copies (Infinity Cache defeated), one
 dispatch-event timing per launch (KernelTimer), median over launches; each config's output is
-checked against the default config (rel L2 < 1e-3). Prints JSON lines, best config last."""
+checked against the default config (rel L2 < 1e-3). Prints JSON lines, best config last.
+--graph: time instead by the wall time per launch of R back-to-back launches replayed from one
+HIP graph (how bench.py and the decode harness run them; dispatch events floor at ~4 us and hide
+differences between small shapes)."""
 
-import itertools
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "torchao-fork_amd"))
@@ -25,8 +28,32 @@ def bytes_of(N, K, g=32):
     return N * K // 2 + (K // g) * N * 4 + K * 2 + N * 2
 
 
+def graph_us(fn, R, reps=10):
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+        with torch.cuda.graph(g, stream=s):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    best = 1e9
+    for _ in range(3):
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            g.replay()
+        torch.cuda.synchronize()
+        best = min(best, (time.perf_counter() - t0) / reps / R * 1e6)
+    return best
+
+
 def main():
-    shapes = SHAPES if len(sys.argv) < 2 else [tuple(map(int, s.split("x"))) for s in sys.argv[1:]]
+    args = sys.argv[1:]
+    use_graph = "--graph" in args
+    args = [a for a in args if a != "--graph"]
+    shapes = SHAPES if not args else [tuple(map(int, s.split("x"))) for s in args]
     lib = _lib.lib()
     g = 32
     for (N, K) in shapes:
@@ -64,12 +91,15 @@ def main():
                 continue
             y = torch.ops.torchao.int4_weight_only_linear(x, p, sz, g, None).float()
             err = float((y - ref).norm() / ref.norm())
-            run(4)
-            with _lib.KernelTimer(reps) as kt:
-                run(reps)
-            d = sorted(kt.durations_ms)
-            us = d[len(d) // 2] * 1e3
-            rec = {"N": N, "K": K, "rpw": rpw, "wk": wk, "g": gg, "occ": occ, "us": round(us, 3),
+            if use_graph:
+                us = graph_us(lambda: run(reps), reps)
+            else:
+                run(4)
+                with _lib.KernelTimer(reps) as kt:
+                    run(reps)
+                d = sorted(kt.durations_ms)
+                us = d[len(d) // 2] * 1e3
+            rec = {"timing": "graph" if use_graph else "events", "N": N, "K": K, "rpw": rpw, "wk": wk, "g": gg, "occ": occ, "us": round(us, 3),
                    "GBps": round(bytes_of(N, K) / us / 1e3, 1), "err": round(err, 6)}
             results.append(rec)
             print(json.dumps(rec), flush=True)

@@ -89,6 +89,10 @@ int tao_tune_gemm(int m_tile, int k_groups, int splits);
  * 2 = the LDS-staged kernel whenever K % 128 == 0. tao_tune_gemm's m_tile (64 / 128) and splits also apply to the LDS kernel. */
 int tao_tune_gemm_algo(int algo);
 
+/* Register-ring depth (k steps in flight) of the LDS-staged int8 GEMM: 0 = built-in (3 at M tile
+ * 128, 4 at 64), else 2, 3, 4, 6 or 8 (8 only at M tile 64; 128 takes 6). Process-wide. */
+int tao_tune_gemm_depth(int depth);
+
 /* packed[N][K/8] <- q[N][K] (int32 values 0..15).
  * Replaces aten._convert_weight_to_int4pack(u8, inner_k_tiles) at
  * torchao/dtypes/uintx/tensor_core_tiled_layout.py:279 (device kernel). K % 8 == 0. */

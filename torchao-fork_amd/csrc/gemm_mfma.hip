@@ -870,6 +870,8 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
 
 // gemm_i8_lds_kernel selection (tao_tune_gemm_algo): 0 = auto, 1 = never, 2 = always (K % 128)
 std::atomic<int> g_gemm_algo{0};
+// register-ring depth of gemm_i8_lds_kernel (tao_tune_gemm_depth; 0 = built-in 3 / 4)
+std::atomic<int> g_i8_depth{0};
 
 int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uint16_t* ws,
                   const uint16_t* bias, uint16_t* y, int M, int N, int K, bool auto_mode,
@@ -900,12 +902,23 @@ int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const 
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<i32x4_t*>(wsp);
   }
-  if (bm == 128)
-    launch((gemm_i8_lds_kernel<128, 3>), grid, dim3(256), 0, stream, xq, wq, xs, ws, bias, y, M,
-           N, K, sps, slab, cnt);
-  else
-    launch((gemm_i8_lds_kernel<64, 4>), grid, dim3(256), 0, stream, xq, wq, xs, ws, bias, y, M,
-           N, K, sps, slab, cnt);
+  const int td = g_i8_depth.load(std::memory_order_relaxed);
+  const int d = td ? td : (bm == 128 ? 3 : 4);
+  auto go = [&](auto kern) {
+    launch(kern, grid, dim3(256), 0, stream, xq, wq, xs, ws, bias, y, M, N, K, sps, slab, cnt);
+  };
+  if (bm == 128) {
+    if (d == 2) go(gemm_i8_lds_kernel<128, 2>);
+    else if (d == 3) go(gemm_i8_lds_kernel<128, 3>);
+    else if (d == 4) go(gemm_i8_lds_kernel<128, 4>);
+    else go(gemm_i8_lds_kernel<128, 6>);
+  } else {
+    if (d == 2) go(gemm_i8_lds_kernel<64, 2>);
+    else if (d == 3) go(gemm_i8_lds_kernel<64, 3>);
+    else if (d == 4) go(gemm_i8_lds_kernel<64, 4>);
+    else if (d == 6) go(gemm_i8_lds_kernel<64, 6>);
+    else go(gemm_i8_lds_kernel<64, 8>);
+  }
   return check_launch("gemm_i8_lds_kernel");
 }
 
@@ -999,6 +1012,13 @@ extern "C" int tao_tune_gemm_algo(int algo) {
                 "tune: gemm algo must be 0 (auto), 1 (per-wave-column kernel only) or 2 (LDS-staged "
                 "int8 kernel whenever K %% 128 == 0)");
   tao::g_gemm_algo.store(algo);
+  return TAO_OK;
+}
+
+extern "C" int tao_tune_gemm_depth(int depth) {
+  TAO_CHECK_ARG(depth == 0 || depth == 2 || depth == 3 || depth == 4 || depth == 6 || depth == 8,
+                "tune: LDS int8 GEMM depth must be 0 (built-in), 2, 3, 4, 6 or 8 (8: M tile 64)");
+  tao::g_i8_depth.store(depth);
   return TAO_OK;
 }
 

@@ -20,6 +20,14 @@
 #include "tao_common.h"
 #include "tao_reduce.h"
 
+// Timing-only variant builds (experiments/gemv_debug.sh; never the shipped library):
+// 1 x not loaded (a lane-dependent constant), 2 no dequant/dot arithmetic (the weight words
+// are folded in with one integer add), 3 no (scale, zero) loads, 4 no cross-lane / cross-wave
+// reduction (each wave's lane 0 writes its own partial). Results are wrong in every variant.
+#ifndef TAO_GEMV_DEBUG
+#define TAO_GEMV_DEBUG 0
+#endif
+
 namespace tao {
 namespace {
 
@@ -144,7 +152,11 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
       const int n = row0 + r;
       const int nn = n < N ? n : N - 1;
       wv[r] = ld_nt_u4(wq + (size_t)nn * nchunk + cc);
+#if TAO_GEMV_DEBUG == 3
+      szv[r] = 0x3F803F80u ^ (uint32_t)cc;
+#else
       szv[r] = ld_nt(sz + (size_t)nn * ngroups + (cc >> gshift));
+#endif
     }
   };
   auto do_slice = [&](const uint4 (&wv)[RPW], const uint32_t (&szv)[RPW], int cc, bool cval)
@@ -167,7 +179,12 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
       uint32_t xd[4][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+#if TAO_GEMV_DEBUG == 1
+        const uint4 t4 = make_uint4(0x3F803F80u + cc + j, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+        (void)xp;
+#else
         const uint4 t4 = PRO ? xs[cc * 4 + ((j + (cc >> 2)) & 3)] : xp[j];
+#endif
         xd[j][0] = t4.x;
         xd[j][1] = t4.y;
         xd[j][2] = t4.z;
@@ -182,6 +199,10 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
 #pragma unroll
       for (int r = 0; r < RPW; ++r) {
         const uint32_t wd[4] = {wv[r].x, wv[r].y, wv[r].z, wv[r].w};
+#if TAO_GEMV_DEBUG == 2
+        acc[r][m] += __uint_as_float((wd[0] + wd[1] + wd[2] + wd[3] + xd[0][0] + xd[3][3]) & 0x3FFFFFFFu) + sc[r] + zp[r];
+        continue;
+#endif
         float d = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -244,6 +265,17 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     }
   }
 
+#if TAO_GEMV_DEBUG == 4
+  if constexpr (EPI == kEpiNone && !PRO) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) t += acc[r][m];
+    if (lane == 0 && row0 < N) y[row0] = f32_to_bf16(t);
+    return;
+  }
+#endif
   float v[V];
 #pragma unroll
   for (int r = 0; r < RPW; ++r)
