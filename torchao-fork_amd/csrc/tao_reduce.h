@@ -14,35 +14,66 @@ struct Log2<1> {
   static constexpr int value = 0;
 };
 
+// The value held by a "partner" lane across bit `off` of the lane index, without the LDS pipe
+// (ds_bpermute: ~100+ cycles of latency per step on the reduction's critical path):
+//   off 32 / 16: v_permlane32_swap / v_permlane16_swap (gfx950) -> exactly lane ^ off;
+//   off 8 / 4:   DPP row_mirror / row_half_mirror -> lane ^ 15 / lane ^ 7 (within the row);
+//   off 2 / 1:   DPP quad_perm -> lane ^ 2 / lane ^ 1.
+// Every partner has the opposite bit `off`, and taken from high `off` to low the masks
+// 32, 16, 15, 7, 2, 1 are each outside the span of the ones before, so a high-to-low butterfly
+// over them is still a reduction tree over disjoint lane sets (any fixed order: deterministic).
+template <int OFF, typename T>
+__device__ __forceinline__ T xor_partner(T v, int lane) {
+  static_assert(OFF == 32 || OFF == 16 || OFF == 8 || OFF == 4 || OFF == 2 || OFF == 1, "off");
+  const uint32_t u = __builtin_bit_cast(uint32_t, v);
+  uint32_t r;
+  if constexpr (OFF == 32 || OFF == 16) {
+    const auto sw = OFF == 32 ? __builtin_amdgcn_permlane32_swap(u, u, false, false)
+                              : __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    r = (lane & OFF) ? sw[0] : sw[1];
+  } else {
+    constexpr int kCtl = OFF == 8 ? 0x140 : OFF == 4 ? 0x141 : OFF == 2 ? 0x4E : 0xB1;
+    r = (uint32_t)__builtin_amdgcn_mov_dpp((int)u, kCtl, 0xF, 0xF, false);
+  }
+  return __builtin_bit_cast(T, r);
+}
+
+// One reduce-scatter step at lane bit OFF over the first CUR values: the lanes with the bit
+// keep the upper half, the others the lower half, each adding the partner's copy.
+template <int OFF, int CUR, int V, typename T>
+__device__ __forceinline__ void rs_step(T (&v)[V], int lane) {
+  constexpr int half = CUR >> 1;
+  // select by bit mask on register values (a select between two array elements can be
+  // canonicalised into a dynamically indexed load, which spills the array to scratch)
+  const uint32_t m = (lane & OFF) ? ~0u : 0u;
+#pragma unroll
+  for (int i = 0; i < half; ++i) {
+    const uint32_t a = __builtin_bit_cast(uint32_t, v[i]);
+    const uint32_t b = __builtin_bit_cast(uint32_t, v[i + half]);
+    const T send = __builtin_bit_cast(T, (a & m) | (b & ~m));
+    const T keep = __builtin_bit_cast(T, (b & m) | (a & ~m));
+    v[i] = keep + xor_partner<OFF>(send, lane);
+  }
+  if constexpr (half > 1) rs_step<OFF / 2, half>(v, lane);
+}
+
+template <int OFF, typename T>
+__device__ __forceinline__ void bfly(T& x, int lane) {
+  x += xor_partner<OFF>(x, lane);
+  if constexpr (OFF > 1) bfly<OFF / 2>(x, lane);
+}
+
 // Reduce V values per lane across the 64 lanes of a wave. On return v[0] holds, in every lane
 // of each aligned group of 64>>T lanes (T = log2 V), the wave-wide total of value index
 // lane >> (6 - T). T is float (the bf16/int4 GEMVs) or int (the exact int8 x int8 GEMV).
+// Exchanges go through xor_partner (no LDS pipe).
 template <int V, typename T>
 __device__ __forceinline__ void wave_reduce_scatter(T (&v)[V], int lane) {
   static_assert(sizeof(T) == 4, "32-bit values");
   constexpr int L = Log2<V>::value;
   static_assert((1 << L) == V && L <= 6, "V must be a power of two <= 64");
-  int off = 32;
-#pragma unroll
-  for (int step = 0; step < L; ++step) {
-    const int cur = V >> step;
-    const int half = cur >> 1;
-    const bool up = (lane & off) != 0;
-    // select by bit mask on register values (a select between two array elements can be
-    // canonicalised into a dynamically indexed load, which spills the array to scratch)
-    const uint32_t m = up ? ~0u : 0u;
-#pragma unroll
-    for (int i = 0; i < half; ++i) {
-      const uint32_t a = __builtin_bit_cast(uint32_t, v[i]);
-      const uint32_t b = __builtin_bit_cast(uint32_t, v[i + half]);
-      const T send = __builtin_bit_cast(T, (a & m) | (b & ~m));
-      const T keep = __builtin_bit_cast(T, (b & m) | (a & ~m));
-      v[i] = keep + __shfl_xor(send, off, 64);
-    }
-    off >>= 1;
-  }
-#pragma unroll
-  for (int o = 32 >> L; o > 0; o >>= 1) v[0] += __shfl_xor(v[0], o, 64);
+  if constexpr (V > 1) rs_step<32, V>(v, lane);
+  if constexpr (L < 6) bfly<(32 >> L)>(v[0], lane);
 }
 
 }  // namespace tao
