@@ -18,6 +18,7 @@
 #include <atomic>
 
 #include "tao_common.h"
+#include "tao_reduce.h"
 
 #ifndef TAO_ATTN_WAVES
 #define TAO_ATTN_WAVES 16  // waves per workgroup of the single-pass decode attention
@@ -27,8 +28,7 @@ namespace tao {
 namespace {
 
 __device__ __forceinline__ float block_sum(float v, float* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v = wave_sum(v);
   const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[w] = v;
@@ -156,8 +156,8 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(
   }
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    sc[g] += __shfl_xor(sc[g], 1, 64);
-    sc[g] += __shfl_xor(sc[g], 2, 64);
+    sc[g] += xor_partner<1>(sc[g], lane_id());
+    sc[g] += xor_partner<2>(sc[g], lane_id());
   }
   if (p == 0) {
 #pragma unroll
@@ -170,12 +170,9 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(
   for (int g = wave; g < G; g += 4) {
     const float v = ps[g][lane];
     float m = v;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    m = wave_max(m);
     const float e = lane + t0 < L ? __expf(v - m) : 0.f;
-    float l = e;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o, 64);
+    const float l = wave_sum(e);
     ps[g][lane] = e;
     if (lane == 0) {
       mls[g][0] = m;
@@ -321,18 +318,16 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
       vf[2 * j + 1] = bf16hi_to_f32(vv[j]);
     }
     if (t0 + NW * 16 < L) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
-    sc += __shfl_xor(sc, 1, 64);
-    sc += __shfl_xor(sc, 2, 64);
+    sc += xor_partner<1>(sc, lane_id());
+    sc += xor_partner<2>(sc, lane_id());
     sc = t < L ? sc * scale : -INFINITY;
     float mx = sc;
-#pragma unroll
-    for (int o = 4; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    mx = wave_bfly<4, 64>(mx, lane_id(), [](float a, float b) { return fmaxf(a, b); });
     const float mn = fmaxf(m, mx);  // finite: key t0 < L is valid
     const float corr = __expf(m - mn);
     const float e = t < L ? __expf(sc - mn) : 0.f;
     float es = e;  // each key sits in 4 lanes; the xor 4..32 sum counts it once
-#pragma unroll
-    for (int o = 4; o < 64; o <<= 1) es += __shfl_xor(es, o, 64);
+    es = wave_bfly<4, 64>(es, lane_id(), [](float a, float b) { return a + b; });
     l = fmaf(l, corr, es);
     o0 *= corr;
     o1 *= corr;
@@ -451,8 +446,8 @@ __global__ __launch_bounds__(256) void attn_chunk_fused_kernel(
   }
 #pragma unroll
   for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int o = 1; o < KPT; o <<= 1) sc[g] += __shfl_xor(sc[g], o, 64);
+    if constexpr (KPT > 1)
+      sc[g] = wave_bfly<1, KPT>(sc[g], lane_id(), [](float a, float b) { return a + b; });
   if (pp == 0) {
 #pragma unroll
     for (int g = 0; g < G; ++g) ps[g][j] = kk < L ? sc[g] * scale : -INFINITY;
@@ -464,12 +459,9 @@ __global__ __launch_bounds__(256) void attn_chunk_fused_kernel(
   for (int g = wave; g < G; g += 4) {
     const float s = lane < CH ? ps[g][lane] : -INFINITY;
     float m = s;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));  // finite: key t0 < L
+    m = wave_max(m);  // finite: key t0 < L
     const float e = s == -INFINITY ? 0.f : __expf(s - m);
-    float l = e;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o, 64);
+    const float l = wave_sum(e);
     float o0 = 0.f, o1 = 0.f;
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
@@ -616,8 +608,7 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const uint16_t* __restrict
     const s16x2_t k = argmax_keys(row[i]);
     best = umax64(best, pack_key(k.x, (uint32_t)i));
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) best = umax64(best, __shfl_xor(best, o, 64));
+  best = wave_bfly<1, 64>(best, lane_id(), umax64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
   __syncthreads();
   if (threadIdx.x == 0) {

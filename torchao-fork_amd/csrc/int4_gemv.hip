@@ -118,8 +118,7 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
         ss = fmaf(a, a, fmaf(b, b, ss));
       }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+    ss = wave_sum(ss);
     float* ssr = red + G * Wk * V;
     if (lane == 0) ssr[wave] = ss;
     __syncthreads();

@@ -135,8 +135,7 @@ __global__ __launch_bounds__(512) void int8dyn_gemv_kernel(Int8DynGemvArgs a) {
       m = bf16_abs_max2(v.z, m);
       m = bf16_abs_max2(v.w, m);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    m = wave_max(m);
     if (lane == 0) wmax[wave] = m;
     __syncthreads();
     float amax = wmax[0];
@@ -306,8 +305,7 @@ __global__ __launch_bounds__(kQBlock) void int8_quant_per_token_kernel(
     m = bf16_abs_max2(v.z, m);
     m = bf16_abs_max2(v.w, m);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  m = wave_max(m);
   if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
   __syncthreads();
   float amax = wmax[0];

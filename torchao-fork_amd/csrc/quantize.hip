@@ -17,6 +17,7 @@
 // group reductions are lane shuffles (g / 8 lanes per group), the int8 row reduction a
 // workgroup per row.
 #include "tao_common.h"
+#include "tao_reduce.h"
 
 namespace tao {
 namespace {
@@ -79,8 +80,7 @@ __global__ __launch_bounds__(256) void int8_quantize_rows_kernel(const uint4* __
     for (int j = 0; j < 4; ++j)
       amax = fmaxf(amax, fmaxf(fabsf(bf16lo_to_f32(d[j])), fabsf(bf16hi_to_f32(d[j]))));
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  amax = wave_max(amax);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
   __syncthreads();
   amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));

@@ -23,7 +23,20 @@ struct Log2<1> {
 // 32, 16, 15, 7, 2, 1 are each outside the span of the ones before, so a high-to-low butterfly
 // over them is still a reduction tree over disjoint lane sets (any fixed order: deterministic).
 template <int OFF, typename T>
+__device__ __forceinline__ T xor_partner(T v, int lane);
+
+template <int OFF>
+__device__ __forceinline__ uint64_t xor_partner64(uint64_t v, int lane) {
+  const uint64_t lo = xor_partner<OFF>((uint32_t)v, lane);
+  const uint64_t hi = xor_partner<OFF>((uint32_t)(v >> 32), lane);
+  return lo | (hi << 32);
+}
+
+template <int OFF, typename T>
 __device__ __forceinline__ T xor_partner(T v, int lane) {
+  if constexpr (sizeof(T) == 8) {
+    return xor_partner64<OFF>(v, lane);
+  } else {
   static_assert(OFF == 32 || OFF == 16 || OFF == 8 || OFF == 4 || OFF == 2 || OFF == 1, "off");
   const uint32_t u = __builtin_bit_cast(uint32_t, v);
   uint32_t r;
@@ -36,6 +49,29 @@ __device__ __forceinline__ T xor_partner(T v, int lane) {
     r = (uint32_t)__builtin_amdgcn_mov_dpp((int)u, kCtl, 0xF, 0xF, false);
   }
   return __builtin_bit_cast(T, r);
+  }
+}
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+// All-reduce over lane bits O, 2 O, ... < END (ascending) with a commutative op. Ascending, the
+// lanes are uniform across the lower bits before each mirror step, so DPP row_half_mirror /
+// row_mirror give exactly the values xor 4 / xor 8 would: the result is bit-identical to the
+// __shfl_xor butterfly in the same (ascending) order.
+template <int O, int END, typename T, typename F>
+__device__ __forceinline__ T wave_bfly(T x, int lane, F op) {
+  x = op(x, xor_partner<O>(x, lane));
+  if constexpr (O * 2 < END) return wave_bfly<O * 2, END>(x, lane, op);
+  return x;
+}
+__device__ __forceinline__ float wave_sum(float x) {
+  return wave_bfly<1, 64>(x, (int)__lane_id(), [](float a, float b) { return a + b; });
+}
+__device__ __forceinline__ float wave_max(float x) {
+  return wave_bfly<1, 64>(x, (int)__lane_id(), [](float a, float b) { return fmaxf(a, b); });
+}
+__device__ __forceinline__ float wave_min(float x) {
+  return wave_bfly<1, 64>(x, (int)__lane_id(), [](float a, float b) { return fminf(a, b); });
 }
 
 // One reduce-scatter step at lane bit OFF over the first CUR values: the lanes with the bit
