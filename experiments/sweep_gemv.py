@@ -52,9 +52,11 @@ def graph_us(fn, R, reps=10):
 def main():
     args = sys.argv[1:]
     use_graph = "--graph" in args
-    args = [a for a in args if a != "--graph"]
+    xlds = "--xlds" in args  # x staged in LDS per workgroup (tao_tune_int4_xlds 1)
+    args = [a for a in args if a not in ("--graph", "--xlds")]
     shapes = SHAPES if not args else [tuple(map(int, s.split("x"))) for s in args]
     lib = _lib.lib()
+    lib.tao_tune_int4_xlds(1 if xlds else 0)
     g = 32
     for (N, K) in shapes:
         S = (K // 32 + 63) // 64
@@ -80,7 +82,7 @@ def main():
         ref = torch.ops.torchao.int4_weight_only_linear(x, p, sz, g, None).float()
         results = []
         cands = []
-        for rpw in (1, 2, 4, 8):
+        for rpw in ((2, 4) if xlds else (1, 2, 4, 8)):
             for occ in ((4, 8) if rpw == 4 else (0,)):
                 for wk in sorted({w for w in (1, 2, 3, 4, 7, 8) if w <= S} | {min(S, 8)}):
                     for gg in (1, 2, 4, 8):
@@ -99,7 +101,7 @@ def main():
                     run(reps)
                 d = sorted(kt.durations_ms)
                 us = d[len(d) // 2] * 1e3
-            rec = {"timing": "graph" if use_graph else "events", "N": N, "K": K, "rpw": rpw, "wk": wk, "g": gg, "occ": occ, "us": round(us, 3),
+            rec = {"timing": "graph" if use_graph else "events", "xlds": xlds, "N": N, "K": K, "rpw": rpw, "wk": wk, "g": gg, "occ": occ, "us": round(us, 3),
                    "GBps": round(bytes_of(N, K) / us / 1e3, 1), "err": round(err, 6)}
             results.append(rec)
             print(json.dumps(rec), flush=True)

@@ -93,6 +93,10 @@ int tao_tune_gemm_algo(int algo);
  * 128, 4 at 64), else 2, 3, 4, 6 or 8 (8 only at M tile 64; 128 takes 6). Process-wide. */
 int tao_tune_gemm_depth(int depth);
 
+/* M == 1 int4 linears without bias: 1 = stage x once per workgroup in LDS (the decode RMSNorm
+ * prologue's copy, without the norm), 0 = built-in policy. Process-wide; for sweeps. */
+int tao_tune_int4_xlds(int mode);
+
 /* packed[N][K/8] <- q[N][K] (int32 values 0..15).
  * Replaces aten._convert_weight_to_int4pack(u8, inner_k_tiles) at
  * torchao/dtypes/uintx/tensor_core_tiled_layout.py:279 (device kernel). K % 8 == 0. */

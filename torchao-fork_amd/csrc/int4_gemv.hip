@@ -102,11 +102,23 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
       const int i = threadIdx.x + u * (int)blockDim.x;
       const int ic = i < nx ? i : nx - 1;  // clamped, masked below
       xv[u] = xr[ic];
-      gv[u] = gr[ic];
+      if (fu.norm_w != nullptr) gv[u] = gr[ic];  // wave-uniform
     }
   };
   auto norm_finish = [&]() __attribute__((always_inline)) {
     const int nx = K >> 3;
+    if (fu.norm_w == nullptr) {  // plain x staged in LDS (tao_tune_int4_xlds), no RMSNorm
+#pragma unroll
+      for (int u = 0; u < NPT; ++u) {
+        const int i = threadIdx.x + u * (int)blockDim.x;
+        if (i < nx) {
+          const int c = i >> 2;
+          xs[c * 4 + (((i & 3) + (c >> 2)) & 3)] = xv[u];
+        }
+      }
+      __syncthreads();
+      return;
+    }
     float ss = 0.f;
 #pragma unroll
     for (int u = 0; u < NPT; ++u) {
@@ -490,6 +502,10 @@ int launch_decode(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
 
 }  // namespace
 
+// M == 1 plain linears with x staged once per workgroup in LDS (the RMSNorm prologue's copy,
+// without the norm): 0 = off (built-in), 1 = on. tao_tune_int4_xlds.
+std::atomic<int> g_tune_xlds{0};
+
 // Internal entry (also used by the MFMA dispatcher for small M).
 int int4wo_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
                 const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K,
@@ -498,6 +514,11 @@ int int4wo_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
   const int S = (int)((K / 32 + 63) / 64);
   GemvShape sh = default_shape(S);
   const int iM = (int)M, iN = (int)N, iK = (int)K;
+  if (M <= 1 && bias == nullptr && g_tune_xlds.load(std::memory_order_relaxed) == 1) {
+    GemvFuse fu{};
+    fu.norm_w = nullptr;
+    return launch_decode<true, kEpiNone>(x, packed, sz, y, iN, iK, gs, stream, fu);
+  }
   if (M <= 1) {
     const M1Shape c = m1_shape(iN, S);
     sh = c.sh;
@@ -533,6 +554,12 @@ int int4_check_linear_args(const uint16_t* x, const uint32_t* packed, const uint
 }
 
 }  // namespace tao
+
+extern "C" int tao_tune_int4_xlds(int mode) {
+  TAO_CHECK_ARG(mode == 0 || mode == 1, "tune: xlds mode must be 0 or 1");
+  tao::g_tune_xlds.store(mode);
+  return TAO_OK;
+}
 
 extern "C" int tao_tune_int4_gemv(int rows_per_wave, int waves_k, int row_groups, int occupancy) {
   TAO_CHECK_ARG(rows_per_wave == 0 || rows_per_wave == 1 || rows_per_wave == 2 ||
