@@ -217,3 +217,24 @@ def test_quantize_api_end_to_end_on_gpu():
     quantize_(lin, Int4WeightOnlyConfig(group_size=64))
     lin = lin.to(DEV)
     assert lin(x.to(DEV)).shape == (4, N)
+
+
+# ---- experiment knob tao_tune_int4_xlds (x staged once per workgroup in LDS) ------
+# Off by default; when switched on the plain M = 1 linear takes the decode prologue's LDS copy of
+# x (no norm). Same tolerances as the default path, ragged K and N included; bias falls back.
+@pytest.mark.parametrize("N,K,g", [(4096, 4096, 32), (28672, 4096, 32), (4096, 14336, 32),
+                                   (40, 352, 32), (1000, 11008, 64)])
+def test_xlds_knob_m1(N, K, g):
+    w, q, s, z = _qparams(N, K, g, seed=N + K)
+    x = oracle.make_activation(1, K, seed=7)
+    packed, sz = _gpu_weight(q, s, z)
+    ref = oracle.int4_linear_fp32(x, q, s, z, g)
+    try:
+        _lib.call("tao_tune_int4_xlds", 1)
+        y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, None).cpu()
+        b = oracle.make_activation(1, N, seed=3).reshape(-1)
+        yb = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, b.to(DEV)).cpu()
+    finally:
+        _lib.call("tao_tune_int4_xlds", 0)
+    assert oracle.rel_l2(y, ref) < TOL_FP32
+    assert oracle.rel_l2(yb, ref + b.float()) < TOL_REF
