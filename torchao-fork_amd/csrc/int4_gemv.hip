@@ -23,7 +23,8 @@
 // Timing-only variant builds (experiments/gemv_debug.sh; never the shipped library):
 // 1 x not loaded (a lane-dependent constant), 2 no dequant/dot arithmetic (the weight words
 // are folded in with one integer add), 3 no (scale, zero) loads, 4 no cross-lane / cross-wave
-// reduction (each wave's lane 0 writes its own partial). Results are wrong in every variant.
+// reduction (each wave's lane 0 writes its own partial), 5 = 2 + 4, 6 = 1 + 2 + 3 + 4 (only the
+// weight loads in the GEMV's pattern). Results are wrong in every variant.
 #ifndef TAO_GEMV_DEBUG
 #define TAO_GEMV_DEBUG 0
 #endif
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
       const int n = row0 + r;
       const int nn = n < N ? n : N - 1;
       wv[r] = ld_nt_u4(wq + (size_t)nn * nchunk + cc);
-#if TAO_GEMV_DEBUG == 3
+#if TAO_GEMV_DEBUG == 3 || TAO_GEMV_DEBUG == 6
       szv[r] = 0x3F803F80u ^ (uint32_t)cc;
 #else
       szv[r] = ld_nt(sz + (size_t)nn * ngroups + (cc >> gshift));
@@ -190,7 +191,7 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
       uint32_t xd[4][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-#if TAO_GEMV_DEBUG == 1
+#if TAO_GEMV_DEBUG == 1 || TAO_GEMV_DEBUG == 6
         const uint4 t4 = make_uint4(0x3F803F80u + cc + j, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
         (void)xp;
 #else
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
 #pragma unroll
       for (int r = 0; r < RPW; ++r) {
         const uint32_t wd[4] = {wv[r].x, wv[r].y, wv[r].z, wv[r].w};
-#if TAO_GEMV_DEBUG == 2
+#if TAO_GEMV_DEBUG == 2 || TAO_GEMV_DEBUG >= 5
         acc[r][m] += __uint_as_float((wd[0] + wd[1] + wd[2] + wd[3] + xd[0][0] + xd[3][3]) & 0x3FFFFFFFu) + sc[r] + zp[r];
         continue;
 #endif
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     }
   }
 
-#if TAO_GEMV_DEBUG == 4
+#if TAO_GEMV_DEBUG == 4 || TAO_GEMV_DEBUG >= 5
   if constexpr (EPI == kEpiNone && !PRO) {
     float t = 0.f;
 #pragma unroll
