@@ -32,10 +32,19 @@ __device__ __forceinline__ uint64_t xor_partner64(uint64_t v, int lane) {
   return lo | (hi << 32);
 }
 
+// TAO_REDUCE_BPERMUTE=1 (timing-only variant builds, experiments/ab_gemv.sh): the same
+// exchanges through ds_bpermute (__shfl_xor), the pre-DPP code.
+#ifndef TAO_REDUCE_BPERMUTE
+#define TAO_REDUCE_BPERMUTE 0
+#endif
+
 template <int OFF, typename T>
 __device__ __forceinline__ T xor_partner(T v, int lane) {
   if constexpr (sizeof(T) == 8) {
     return xor_partner64<OFF>(v, lane);
+  } else if constexpr (TAO_REDUCE_BPERMUTE) {
+    (void)lane;
+    return __shfl_xor(v, OFF, 64);
   } else {
   static_assert(OFF == 32 || OFF == 16 || OFF == 8 || OFF == 4 || OFF == 2 || OFF == 1, "off");
   const uint32_t u = __builtin_bit_cast(uint32_t, v);
