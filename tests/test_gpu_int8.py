@@ -220,15 +220,20 @@ def test_int8_lds_gemm_bit_exact(M, N, K):
             _lib.call("tao_tune_linear_crossover", 1)
             old = torch.ops.torchao.int8_scaled_mm(*args, bd).cpu()
             _lib.call("tao_tune_gemm_algo", 2)
-            for bm, splits in ((0, 0), (64, 1), (128, 1), (64, 3), (128, 8)):
+            for bm, splits, depth in ((0, 0, 0), (64, 1, 0), (128, 1, 0), (64, 3, 0),
+                                      (128, 8, 0), (64, 1, 2), (64, 2, 8), (128, 1, 6),
+                                      (128, 3, 2)):
                 _lib.call("tao_tune_gemm", bm, 0, splits)
+                _lib.call("tao_tune_gemm_depth", depth)
                 y = torch.ops.torchao.int8_scaled_mm(*args, bd).cpu()
-                assert torch.equal(y, ref), (bm, splits)
+                assert torch.equal(y, ref), (bm, splits, depth)
+            _lib.call("tao_tune_gemm_depth", 0)
             assert torch.equal(old, ref)
             _lib.call("tao_tune_gemm", 0, 0, 0)
             _lib.call("tao_tune_gemm_algo", 0)  # the auto policy's pick for this shape
             assert torch.equal(torch.ops.torchao.int8_scaled_mm(*args, bd).cpu(), ref)
     finally:
         _lib.call("tao_tune_gemm", 0, 0, 0)
+        _lib.call("tao_tune_gemm_depth", 0)
         _lib.call("tao_tune_gemm_algo", 0)
         _lib.call("tao_tune_linear_crossover", 0)
