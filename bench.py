@@ -42,6 +42,9 @@ Reported (one JSON line, rank 0):
   prefill_mfma = BASELINE config 3 (int8 dyn-act int8-weight linear, M = 128, 4096x4096, the
                  int8 MFMA path) and the int4 g32 linear at M = 128 on its bf16 MFMA path:
                  kernel us, TOPS, fraction of the dense MFMA peak, attainable-roofline fraction
+  e2e_decode   = BASELINE config 4: the e2e decode harness (random-init Llama-3-8B, int4wo-32,
+                 prompt 128, 200 new tokens, bs = 1, HIP-graph decode) in a child process:
+                 decode tokens/s, ms/token, prefill ms (rank 0, N = 1; --no-e2e skips it)
 """
 
 import argparse
@@ -314,6 +317,28 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
     return out
 
 
+def e2e_decode(timeout_s=240):
+    """BASELINE config 4 beside the linears-only step: the e2e decode harness
+    (torchao/_models/llama/generate.py semantics: random-init Llama-3-8B, quantize_ int4wo-32,
+    prompt 128, 200 new tokens, bs=1, greedy, HIP-graph decode) in a child process (its own
+    model and weights; this process only waits). Its JSON line, trimmed."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torchao._models.llama.generate", "-q", "int4wo-32",
+           "--num_samples", "2"]
+    try:
+        out = subprocess.run(cmd, cwd=os.path.join(ROOT, "torchao-fork_amd"), capture_output=True,
+                             text=True, timeout=timeout_s, check=True).stdout
+        d = json.loads(out.strip().splitlines()[-1])
+    except Exception as e:  # reported, never fatal to the bench line
+        return {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+    keep = ("model", "quantization", "weights", "batch_size", "prompt_length", "max_new_tokens",
+            "decode_tokens_per_s", "decode_ms_per_token", "prefill_ms", "tokens_per_s_incl_prefill")
+    rec = {k: d[k] for k in keep if k in d}
+    rec["config"] = "BASELINE config 4: Llama-3-8B quantize_(Int4WeightOnlyConfig(32)), greedy bs=1"
+    return rec
+
+
 def cpu_baseline(cfg, g, budget_s=12.0):
     """The reference CPU dequant path (oracle restatement) on one layer's five linears, M = 1."""
     from oracle import oracle
@@ -377,6 +402,8 @@ def main():
                     help="skip timing PyTorch-ROCm's aten._weight_int4pack_mm on the same step")
     ap.add_argument("--no-prefill", action="store_true",
                     help="skip the config-3 MFMA prefill measurement (prefill_mfma)")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the config-4 e2e decode run (e2e_decode, a child process)")
     ap.add_argument("--shard-policy", default="auto", choices=["auto", "size", "all", "none"],
                     help="P > 1: which linears to column-shard. auto = per (N, K), whichever of "
                          "{whole GEMV on every rank, N/P GEMV + all-gather} measured faster "
@@ -642,6 +669,8 @@ def main():
                 rec["speedup_vs_reference_gpu"] = round(rec["value"] / ref_gpu["value"], 2)
         if prefill is not None:
             rec["prefill_mfma"] = prefill
+        if P == 1 and args.model == "8b" and not args.no_e2e:
+            rec["e2e_decode"] = e2e_decode()
         if comm_ms is not None:
             rec["allgather_ms_per_step"] = round(comm_ms, 4)
         if calib:
