@@ -99,6 +99,14 @@ def main():
 
             res = {"model": args.model, "op": name, "tune": t, "fused_us": round(time_graph(fused, n), 3),
                    "fused_nonorm_us": round(time_graph(lambda i: fused(i, False), n), 3)}
+            # the prologue's LDS staging without the norm (tao_tune_int4_xlds 1): separates
+            # the RMSNorm's own cost from staging x through LDS
+            _lib.call("tao_tune_int4_xlds", 1)
+            res["fused_lds_nonorm_us"] = round(time_graph(lambda i: fused(i, False), n), 3)
+            _lib.call("tao_tune_int4_xlds", 0)
+            _lib.call("tao_tune_int4_norm", 1)  # deferred RMSNorm scale
+            res["fused_deferred_norm_us"] = round(time_graph(fused, n), 3)
+            _lib.call("tao_tune_int4_norm", 0)
             if t == (0, 0, 0, 0):
                 res["unfused_us"] = round(time_graph(unfused, n), 3)
                 res["gemv_only_us"] = round(time_graph(plain, n), 3)

@@ -97,6 +97,11 @@ int tao_tune_gemm_depth(int depth);
  * prologue's copy, without the norm), 0 = built-in policy. Process-wide; for sweeps. */
 int tao_tune_int4_xlds(int mode);
 
+/* RMSNorm prologue of tao_int4wo_decode_bf16: 0 = exact (normalise x with the reference's two
+ * bf16 roundings before the slices; built-in), 1 = deferred (stage bf16(x * norm_weight), scale
+ * each output by rsqrt(mean(x^2) + eps) at the end). Process-wide; for measurement. */
+int tao_tune_int4_norm(int mode);
+
 /* packed[N][K/8] <- q[N][K] (int32 values 0..15).
  * Replaces aten._convert_weight_to_int4pack(u8, inner_k_tiles) at
  * torchao/dtypes/uintx/tensor_core_tiled_layout.py:279 (device kernel). K % 8 == 0. */

@@ -51,7 +51,14 @@ struct GemvFuse {
   uint16_t* k_cache;       // [Hkv][T][D]
   uint16_t* v_cache;
   int H, Hkv, D, T;
+  int norm_deferred;  // PRO: 1 = stage bf16(x * w) and scale the outputs by r (see norm_finish)
 };
+
+__device__ __forceinline__ uint32_t mul_pair_bf16(uint32_t xv, uint32_t wv) {
+  const float lo = bf16lo_to_f32(xv) * bf16lo_to_f32(wv);
+  const float hi = bf16hi_to_f32(xv) * bf16hi_to_f32(wv);
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
 
 __device__ __forceinline__ uint32_t rmsnorm_pair(uint32_t xv, uint32_t wv, float r) {
   const float lo = round_bf16(bf16lo_to_f32(xv) * r) * bf16lo_to_f32(wv);
@@ -134,6 +141,24 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     ss = wave_sum(ss);
     float* ssr = red + G * Wk * V;
     if (lane == 0) ssr[wave] = ss;
+    if (fu.norm_deferred) {
+      // Deferred normalisation (tao_tune_int4_norm 1): r = rsqrt(mean(x^2) + eps) is one scalar
+      // per token, so stage bf16(x * w) now and multiply each output by r at the end. One
+      // barrier, no wait for the cross-wave sum before the slices; one bf16 rounding of the
+      // normalised input instead of the reference's two (bf16(bf16(x * r) * w)).
+#pragma unroll
+      for (int u = 0; u < NPT; ++u) {
+        const int i = threadIdx.x + u * (int)blockDim.x;
+        if (i < nx) {
+          const int c = i >> 2;
+          xs[c * 4 + (((i & 3) + (c >> 2)) & 3)] =
+              make_uint4(mul_pair_bf16(xv[u].x, gv[u].x), mul_pair_bf16(xv[u].y, gv[u].y),
+                         mul_pair_bf16(xv[u].z, gv[u].z), mul_pair_bf16(xv[u].w, gv[u].w));
+        }
+      }
+      __syncthreads();
+      return;
+    }
     __syncthreads();
     float t = 0.f;
     for (int w = 0; w < G * Wk; ++w) t += ssr[w];
@@ -300,6 +325,16 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
   const int idx = lane >> (6 - T);
 
   float total = v[0];
+  if constexpr (PRO) {
+    if (fu.norm_deferred && fu.norm_w != nullptr) {  // the deferred RMSNorm scale (norm_finish)
+      const float* ssr = red + G * Wk * V;
+      float t = 0.f;
+      for (int w = 0; w < G * Wk; ++w) t += ssr[w];
+      const float rn = rsqrtf(t / (float)K + fu.eps);
+      total *= rn;
+      v[0] *= rn;
+    }
+  }
   bool writer = owner;
   int widx = idx;
   if (Wk > 1) {
@@ -506,6 +541,9 @@ int launch_decode(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
 // M == 1 plain linears with x staged once per workgroup in LDS (the RMSNorm prologue's copy,
 // without the norm): 0 = off (built-in), 1 = on. tao_tune_int4_xlds.
 std::atomic<int> g_tune_xlds{0};
+// RMSNorm prologue mode of the decode GEMV: 0 = exact (the reference's two bf16 roundings,
+// normalised before the slices), 1 = deferred (outputs scaled by r). tao_tune_int4_norm.
+std::atomic<int> g_tune_norm{0};
 
 // Internal entry (also used by the MFMA dispatcher for small M).
 int int4wo_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
@@ -556,6 +594,12 @@ int int4_check_linear_args(const uint16_t* x, const uint32_t* packed, const uint
 
 }  // namespace tao
 
+extern "C" int tao_tune_int4_norm(int mode) {
+  TAO_CHECK_ARG(mode == 0 || mode == 1, "tune: norm mode must be 0 (exact) or 1 (deferred)");
+  tao::g_tune_norm.store(mode);
+  return TAO_OK;
+}
+
 extern "C" int tao_tune_int4_xlds(int mode) {
   TAO_CHECK_ARG(mode == 0 || mode == 1, "tune: xlds mode must be 0 or 1");
   tao::g_tune_xlds.store(mode);
@@ -597,6 +641,7 @@ extern "C" int tao_int4wo_decode_bf16(const uint16_t* x, const uint32_t* packed,
   tao::GemvFuse fu{};
   fu.norm_w = norm_weight;
   fu.eps = eps;
+  fu.norm_deferred = tao::g_tune_norm.load(std::memory_order_relaxed);
   if (epilogue == tao::kEpiRopeKV) {
     TAO_CHECK_ARG(n_head > 0 && n_kv_head > 0 && head_dim > 0 && head_dim % 2 == 0 &&
                       max_seq > 0 && N == (n_head + 2 * n_kv_head) * head_dim,
@@ -620,7 +665,10 @@ extern "C" int tao_int4wo_decode_bf16(const uint16_t* x, const uint32_t* packed,
   const int gs = tao::gshift_of(group_size);
   hipStream_t st = tao::as_stream(stream);
   const int iN = (int)N, iK = (int)K;
-  const bool pro = norm_weight != nullptr;
+  // without a norm, tao_tune_int4_xlds 1 still takes the prologue path (x staged raw in LDS):
+  // the experiment that separates the RMSNorm's cost from the LDS staging's
+  const bool pro =
+      norm_weight != nullptr || tao::g_tune_xlds.load(std::memory_order_relaxed) == 1;
 #define TAO_DEC(P, E) \
   return tao::launch_decode<P, E>(x, packed, scales_and_zeros, y, iN, iK, gs, st, fu)
   switch (epilogue) {

@@ -223,11 +223,18 @@ def main(argv=None):
                     help="torch ops for norms / rope / attention / silu (no fused kernels)")
     ap.add_argument("--no_fuse_w13", action="store_true",
                     help="keep w1 and w3 as two linears (the reference module layout)")
+    ap.add_argument("--deferred_norm", action="store_true",
+                    help="fused RMSNorm scales the GEMV outputs by rsqrt(mean(x^2)+eps) instead "
+                         "of normalising x first (one bf16 rounding fewer; tao_tune_int4_norm 1)")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--write_result", type=Path, default=None)
     args = ap.parse_args(argv)
 
+    if args.deferred_norm:
+        from torchao import _lib
+
+        _lib.call("tao_tune_int4_norm", 1)
     device = torch.device(args.device)
     t = time.perf_counter()
     model = build_model(args.model_name, device, checkpoint_path=args.checkpoint_path,
@@ -276,6 +283,7 @@ def main(argv=None):
         "hip_graph": decoder is not None,
         "fused_decode_kernels": model.fused,
         "fused_w13": not args.no_fuse_w13,
+        "deferred_norm": args.deferred_norm,
         "decode_tokens_per_s": round(dec_tok_s, 2),
         "decode_ms_per_token": round(t_dec / (T - 1) * 1e3, 3),
         "prefill_ms": round(t_pre * 1e3, 3),
