@@ -86,12 +86,18 @@ int tao_tune_gemm(int m_tile, int k_groups, int splits);
 /* Process-wide choice of the int8 dynamic-activation GEMM kernel (M above the GEMV crossover):
  * 0 = auto (the LDS-staged int8 kernel when K % 128 == 0, M >= 128 and its 64-row tiles number
  * >= 192, unsplit; else the per-wave-column MFMA kernel), 1 = always the per-wave-column kernel,
- * 2 = the LDS-staged kernel whenever K % 128 == 0. tao_tune_gemm's m_tile (64 / 128) and splits also apply to the LDS kernel. */
+ * 2 = the LDS-staged kernel whenever K % 128 == 0. tao_tune_gemm's m_tile (64 / 128) and
+ * splits also apply to the LDS kernel. */
 int tao_tune_gemm_algo(int algo);
 
 /* Register-ring depth (k steps in flight) of the LDS-staged int8 GEMM: 0 = built-in (3 at M tile
  * 128, 4 at 64), else 2, 3, 4, 6 or 8 (8 only at M tile 64; 128 takes 6). Process-wide. */
 int tao_tune_gemm_depth(int depth);
+
+/* Column tile of the LDS-staged int8 GEMM: 0 = built-in (128 when M >= 256 and 128 x 128 tiles
+ * number >= 256, else 64), 64, or 128 (each wave 2 x 4 16x16 tiles per M half; ring depth 2 or
+ * 3). Process-wide; for sweeps. */
+int tao_tune_gemm_bn(int bn);
 
 /* M == 1 int4 linears without bias: 1 = stage x once per workgroup in LDS (the decode RMSNorm
  * prologue's copy, without the norm), 0 = built-in policy. Process-wide; for sweeps. */

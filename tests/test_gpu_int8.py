@@ -201,7 +201,8 @@ def test_int8dq_decode_takes_fused_path_and_matches_unfused():
 # kernel (algo 1) on the same inputs.
 @pytest.mark.parametrize("M,N,K", [(128, 4096, 4096), (48, 330, 1024), (200, 4160, 2048),
                                    (128, 14336, 4096), (128, 4096, 14336), (5, 64, 128),
-                                   (512, 1024, 3072), (256, 4096, 4096), (128, 6144, 4096)])
+                                   (512, 1024, 3072), (256, 4096, 4096), (128, 6144, 4096),
+                                   (512, 14336, 4096), (300, 4200, 1024)])
 def test_int8_lds_gemm_bit_exact(M, N, K):
     from torchao import _lib
 
@@ -223,11 +224,14 @@ def test_int8_lds_gemm_bit_exact(M, N, K):
             for bm, splits, depth in ((0, 0, 0), (64, 1, 0), (128, 1, 0), (64, 3, 0),
                                       (128, 8, 0), (64, 1, 2), (64, 2, 8), (128, 1, 6),
                                       (128, 3, 2)):
-                _lib.call("tao_tune_gemm", bm, 0, splits)
-                _lib.call("tao_tune_gemm_depth", depth)
-                y = torch.ops.torchao.int8_scaled_mm(*args, bd).cpu()
-                assert torch.equal(y, ref), (bm, splits, depth)
+                for bn in ((64, 128) if depth in (0, 2) else (64,)):
+                    _lib.call("tao_tune_gemm", bm, 0, splits)
+                    _lib.call("tao_tune_gemm_depth", depth)
+                    _lib.call("tao_tune_gemm_bn", bn)
+                    y = torch.ops.torchao.int8_scaled_mm(*args, bd).cpu()
+                    assert torch.equal(y, ref), (bm, splits, depth, bn)
             _lib.call("tao_tune_gemm_depth", 0)
+            _lib.call("tao_tune_gemm_bn", 0)
             assert torch.equal(old, ref)
             _lib.call("tao_tune_gemm", 0, 0, 0)
             _lib.call("tao_tune_gemm_algo", 0)  # the auto policy's pick for this shape
@@ -235,5 +239,6 @@ def test_int8_lds_gemm_bit_exact(M, N, K):
     finally:
         _lib.call("tao_tune_gemm", 0, 0, 0)
         _lib.call("tao_tune_gemm_depth", 0)
+        _lib.call("tao_tune_gemm_bn", 0)
         _lib.call("tao_tune_gemm_algo", 0)
         _lib.call("tao_tune_linear_crossover", 0)

@@ -699,21 +699,21 @@ constexpr int kI8Step = 128;  // k bytes per step of gemm_i8_lds_kernel
 
 __device__ __forceinline__ int i8_swz(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
 
-template <int BM, int D>
+template <int BM, int D, int BN = 64>
 __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
     const int8_t* __restrict__ x, const int8_t* __restrict__ w, const uint16_t* __restrict__ xscale,
     const uint16_t* __restrict__ wscale, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int sps, i32x4_t* __restrict__ slab,
     unsigned* __restrict__ cnt) {
   constexpr int XL = BM / 32;           // x chunks per thread per step
-  constexpr int WL = 2;                 // W chunks per thread per step (64 rows x 8 chunks)
-  constexpr int MT = BM / 32, NT = 2;   // 16x16 output tiles per wave
-  constexpr int XT = BM * 8, WT = 64 * 8;  // uint4 per image
+  constexpr int WL = BN / 32;           // W chunks per thread per step (BN rows x 8 chunks)
+  constexpr int MT = BM / 32, NT = BN / 32;  // 16x16 output tiles per wave
+  constexpr int XT = BM * 8, WT = BN * 8;    // uint4 per image
   __shared__ uint4 lds[2 * (XT + WT)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int n_blk = blockIdx.x * 64, m_blk = blockIdx.y * BM;
+  const int n_blk = blockIdx.x * BN, m_blk = blockIdx.y * BM;
   const int nsteps = K / kI8Step;
   const int s0 = blockIdx.z * sps;
   const int s1 = s0 + sps < nsteps ? s0 + sps : nsteps;  // launcher: no empty slice
@@ -769,7 +769,7 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
       i32x4_t bf[NT];
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
-        bf[nt] = __builtin_bit_cast(i32x4_t, img[XT + i8_swz(wn * 32 + nt * 16 + fr, c)]);
+        bf[nt] = __builtin_bit_cast(i32x4_t, img[XT + i8_swz(wn * (BN / 2) + nt * 16 + fr, c)]);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const i32x4_t af =
@@ -849,7 +849,7 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
   // C/D map: col = lane & 15 (n), row = 4 (lane >> 4) + i (m); Int8Dyn's epilogue
 #pragma unroll
   for (int b = 0; b < NT; ++b) {
-    const int n = n_blk + wn * 32 + b * 16 + fr;
+    const int n = n_blk + wn * (BN / 2) + b * 16 + fr;
     if (n >= N) continue;
     const float sw = bf16_to_f32(wscale[n]);
     const float bv = bias != nullptr ? bf16_to_f32(bias[n]) : 0.f;
@@ -872,16 +872,27 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
 std::atomic<int> g_gemm_algo{0};
 // register-ring depth of gemm_i8_lds_kernel (tao_tune_gemm_depth; 0 = built-in 3 / 4)
 std::atomic<int> g_i8_depth{0};
+// column tile of gemm_i8_lds_kernel (tao_tune_gemm_bn; 0 = built-in 64, or 128)
+std::atomic<int> g_i8_bn{0};
 
 int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uint16_t* ws,
                   const uint16_t* bias, uint16_t* y, int M, int N, int K, bool auto_mode,
                   hipStream_t stream) {
   const int nsteps = K / kI8Step;
-  const long ntile = (N + 63) / 64;
+  // auto: 128-column tiles once 128 x 128 tiles alone number >= 256 (M >= 256;
+  // profiles/r1_sweep_i8_bn.jsonl: M=512 14336x4096 54.6 vs 70.6 us; no gain at M = 128)
+  const int tbn = g_i8_bn.load(std::memory_order_relaxed);
+  const int bn = tbn ? (tbn == 128 ? 128 : 64)
+                     : (auto_mode && M >= 256 &&
+                                (long)((N + 127) / 128) * ((M + 127) / 128) >= 256
+                            ? 128
+                            : 64);
+  const long ntile = (N + bn - 1) / bn;
   // auto (profiles/r1_sweep_i8_lds.jsonl): the M = 128 tile once it alone fills a round of
   // workgroups, else 64; no split (every winning LDS shape ran unsplit). Forced (algo 2, the
   // parity tests' mode): split towards one round, slices of >= 4 steps (512 k).
-  int bm = auto_mode ? (ntile * ((M + 127) / 128) >= 224 ? 128 : 64) : (M > 64 ? 128 : 64);
+  int bm = auto_mode ? (bn == 128 || ntile * ((M + 127) / 128) >= 224 ? 128 : 64)
+                     : (M > 64 ? 128 : 64);
   const int tb = g_tune_bm.load(std::memory_order_relaxed);
   if (tb == 64 || tb == 128) bm = tb;
   const long tiles = ntile * ((M + bm - 1) / bm);
@@ -892,13 +903,13 @@ int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const 
   if (ts) splits = ts < nsteps ? ts : nsteps;
   const int sps = (nsteps + splits - 1) / splits;
   const int S = (nsteps + sps - 1) / sps;
-  const dim3 grid((N + 63) / 64, (M + bm - 1) / bm, S);
+  const dim3 grid((N + bn - 1) / bn, (M + bm - 1) / bm, S);
   i32x4_t* slab = nullptr;
   unsigned* cnt = nullptr;
   if (S > 1) {
     void* wsp = nullptr;
     const size_t t = (size_t)grid.x * grid.y;
-    const int rc = split_workspace(stream, t * S * bm * 64 * sizeof(int), t, &wsp, &cnt);
+    const int rc = split_workspace(stream, t * S * bm * bn * sizeof(int), t, &wsp, &cnt);
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<i32x4_t*>(wsp);
   }
@@ -907,7 +918,15 @@ int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const 
   auto go = [&](auto kern) {
     launch(kern, grid, dim3(256), 0, stream, xq, wq, xs, ws, bias, y, M, N, K, sps, slab, cnt);
   };
-  if (bm == 128) {
+  if (bn == 128) {  // experiment (tao_tune_gemm_bn): ring depth 2 or 3
+    if (bm == 128) {
+      if (d == 2) go(gemm_i8_lds_kernel<128, 2, 128>);
+      else go(gemm_i8_lds_kernel<128, 3, 128>);
+    } else {
+      if (d == 2) go(gemm_i8_lds_kernel<64, 2, 128>);
+      else go(gemm_i8_lds_kernel<64, 3, 128>);
+    }
+  } else if (bm == 128) {
     if (d == 2) go(gemm_i8_lds_kernel<128, 2>);
     else if (d == 3) go(gemm_i8_lds_kernel<128, 3>);
     else if (d == 4) go(gemm_i8_lds_kernel<128, 4>);
@@ -1012,6 +1031,12 @@ extern "C" int tao_tune_gemm_algo(int algo) {
                 "tune: gemm algo must be 0 (auto), 1 (per-wave-column kernel only) or 2 (LDS-staged "
                 "int8 kernel whenever K %% 128 == 0)");
   tao::g_gemm_algo.store(algo);
+  return TAO_OK;
+}
+
+extern "C" int tao_tune_gemm_bn(int bn) {
+  TAO_CHECK_ARG(bn == 0 || bn == 64 || bn == 128, "tune: LDS int8 GEMM bn must be 0, 64 or 128");
+  tao::g_i8_bn.store(bn);
   return TAO_OK;
 }
 

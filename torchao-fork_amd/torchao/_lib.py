@@ -39,6 +39,7 @@ _SIGNATURES = {
     "tao_tune_gemm": [_int, _int, _int],
     "tao_tune_gemm_algo": [_int],
     "tao_tune_gemm_depth": [_int],
+    "tao_tune_gemm_bn": [_int],
     "tao_tune_int4_xlds": [_int],
     "tao_tune_int4_norm": [_int],
     "tao_int4_pack": [_p, _p, _i64, _i64, _p],
