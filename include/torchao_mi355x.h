@@ -66,8 +66,19 @@ int tao_int4wo_linear_bf16(const uint16_t* x, const uint32_t* packed, const uint
                            const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K,
                            int64_t group_size, void* stream);
 
+/* Tuning hooks (tao_tune_*). Every override is THREAD-LOCAL: it re-routes only launches issued
+ * from the thread that set it, never another thread's model. tao_tune_reset() restores every
+ * built-in choice for the calling thread (torchao.kernel.tuning(...) wraps set + reset). */
+int tao_tune_reset(void);
+
+/* Split-K / last-arriver hand-off form for the calling thread: 0 = fence-free sc1 protocol
+ * (built-in; MI355X_MICROARCH.md "Hand-offs measured with sc1 loads in place of the acquire",
+ * first row), 1 = the same plus agent release / acquire fences (the HIP memory-model form).
+ * Both give bit-identical results (tests/test_gpu_gemm_tiles.py). */
+int tao_tune_splitk_fenced(int fenced);
+
 /* Tuning hook (benchmarks / autotuning sweeps): override the M == 1 int4 GEMV launch shape,
- * process-wide. rows_per_wave in {1,2,4,8}; waves_k = waves splitting K inside a workgroup
+ * for the calling thread. rows_per_wave in {1,2,4,8}; waves_k = waves splitting K inside a workgroup
  * (1..8); row_groups = row groups per workgroup; waves_k * row_groups <= 8; occupancy in {4,8}
  * = minimum waves per SIMD the register budget targets (rows_per_wave 4 only).
  * 0 for any field keeps the built-in choice; all zeros restores the defaults. */
@@ -75,15 +86,15 @@ int tao_tune_int4_gemv(int rows_per_wave, int waves_k, int row_groups, int occup
 
 /* Tuning hook: the weight-only linears (int4 and int8) use the GEMV kernels for M <= max_gemv_m
  * and the MFMA skinny GEMM above it. 0 restores the built-in crossover (M <= 2, or M <= 4 for
- * weights of at most 32 Mi elements). Process-wide. */
+ * weights of at most 32 Mi elements). Calling thread only. */
 int tao_tune_linear_crossover(int max_gemv_m);
 
 /* Tuning hook: force the MFMA skinny GEMM's M tile (16/32/64/128), k-groups per workgroup
  * (1/2/4; 4 waves each) and K slices across workgroups (1..64); 0 = the built-in choice for
- * each. Process-wide. */
+ * each. Calling thread only. */
 int tao_tune_gemm(int m_tile, int k_groups, int splits);
 
-/* Process-wide choice of the int8 dynamic-activation GEMM kernel (M above the GEMV crossover):
+/* Calling thread's choice of the int8 dynamic-activation GEMM kernel (M above the GEMV crossover):
  * 0 = auto (the LDS-staged int8 kernel when K % 128 == 0, M >= 128 and its 64-row tiles number
  * >= 192, unsplit; else the per-wave-column MFMA kernel), 1 = always the per-wave-column kernel,
  * 2 = the LDS-staged kernel whenever K % 128 == 0. tao_tune_gemm's m_tile (64 / 128) and
@@ -91,21 +102,21 @@ int tao_tune_gemm(int m_tile, int k_groups, int splits);
 int tao_tune_gemm_algo(int algo);
 
 /* Register-ring depth (k steps in flight) of the LDS-staged int8 GEMM: 0 = built-in (3 at M tile
- * 128, 4 at 64), else 2, 3, 4, 6 or 8 (8 only at M tile 64; 128 takes 6). Process-wide. */
+ * 128, 4 at 64), else 2, 3, 4, 6 or 8 (8 only at M tile 64; 128 takes 6). Calling thread only. */
 int tao_tune_gemm_depth(int depth);
 
 /* Column tile of the LDS-staged int8 GEMM: 0 = built-in (128 when M >= 256 and 128 x 128 tiles
  * number >= 256, else 64), 64, or 128 (each wave 2 x 4 16x16 tiles per M half; ring depth 2 or
- * 3). Process-wide; for sweeps. */
+ * 3). Calling thread only; for sweeps. */
 int tao_tune_gemm_bn(int bn);
 
 /* M == 1 int4 linears without bias: 1 = stage x once per workgroup in LDS (the decode RMSNorm
- * prologue's copy, without the norm), 0 = built-in policy. Process-wide; for sweeps. */
+ * prologue's copy, without the norm), 0 = built-in policy. Calling thread only; for sweeps. */
 int tao_tune_int4_xlds(int mode);
 
 /* RMSNorm prologue of tao_int4wo_decode_bf16: 0 = exact (normalise x with the reference's two
  * bf16 roundings before the slices; built-in), 1 = deferred (stage bf16(x * norm_weight), scale
- * each output by rsqrt(mean(x^2) + eps) at the end). Process-wide; for measurement. */
+ * each output by rsqrt(mean(x^2) + eps) at the end). Calling thread only; for measurement. */
 int tao_tune_int4_norm(int mode);
 
 /* packed[N][K/8] <- q[N][K] (int32 values 0..15).
@@ -192,7 +203,7 @@ int tao_int8_dyn_linear_bf16(const uint16_t* x, const int8_t* wq, const uint16_t
 
 /* Tuning hook: M == 1 launch shape of the int8 decode GEMVs (int8 weight-only and int8 x int8:
  * rows per wave 2/4/8, waves along K, row groups per workgroup; 0 = built-in heuristic).
- * Process-wide; for sweeps (experiments/sweep_int8.py). */
+ * Calling thread only; for sweeps (experiments/sweep_int8.py). */
 int tao_tune_int8_gemv(int rows_per_wave, int waves_k, int row_groups);
 
 /* ---- fused decode-step kernels of the end-to-end harness (torchao/_models/llama) -------------
@@ -222,10 +233,17 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
                          const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
                          int64_t Hkv, int64_t D, int64_t T, float scale, void* stream);
 
-/* Process-wide choice of the decode-attention kernel: 0 = single-pass workgroup per query head
+/* Calling thread's choice of the decode-attention kernel: 0 = single-pass workgroup per query head
  * for T <= 1024, else the two-launch split (default); 1 = two-launch split; 2 / 3 = one launch
  * over 32 / 64-key chunks merged by the kv head's last arriving chunk. */
 int tao_tune_attn(int mode);
+
+/* Device-side faults of the decode kernels since the last call, read and cleared (synchronous:
+ * call outside graph capture). bits & 1: a KV-cache position outside [0, T) reached
+ * tao_rope_kv_bf16 / tao_int4wo_decode_bf16's rope_kv epilogue; those launches wrote no cache
+ * row and tao_attn_decode_bf16 clamped its key count to T. (The reference's index_put KV cache
+ * device-asserts in this case, torchao/_models/llama/model.py KVCache.update.) */
+int tao_decode_status(int* bits);
 
 /* y = bf16(bf16(silu(a)) * b) elementwise over n bf16 (n even). Replaces FeedForward's
  * F.silu(w1(x)) * w3(x) (model.py:485-486). b == NULL: a holds n interleaved (gate, up) pairs

@@ -174,3 +174,111 @@ def test_tune_gemm_rejects_bad_values():
         _lib.call("tao_tune_gemm", 0, 3, 0)
     with pytest.raises(RuntimeError, match="splits"):
         _lib.call("tao_tune_gemm", 0, 0, 65)
+
+
+def _int4_operands(M, N, K, g, seed):
+    w = oracle.make_linear_weight(N, K, seed=seed)
+    s, z = oracle.int4_qparams(w, g)
+    q = oracle.int4_quantize(w, s, z, g)
+    x = oracle.make_activation(M, K, seed=seed + 1)
+    packed = torch.ops.torchao.int4_pack(q.to(DEV))
+    sz = torch.stack([s, z], dim=-1).contiguous().to(DEV)
+    return x, q, s, z, packed, sz
+
+
+def test_split_k_capture_owns_its_workspace():
+    """a captured split-K launch must not share scratch with eager work.
+    Capture at a small split-K shape, then run a LARGER split-K shape eagerly on the capture
+    stream (which grows, and frees, that stream's eager workspace) and on another stream; every
+    later replay must still reproduce the eager result exactly."""
+    from torchao.kernel import tuning
+
+    g = 32
+    x1, q1, s1, z1, p1, sz1 = _int4_operands(16, 512, 2048, g, seed=11)
+    x2, q2, s2, z2, p2, sz2 = _int4_operands(64, 4096, 8192, g, seed=12)
+    x1, x2 = x1.to(DEV), x2.to(DEV)
+    stream = torch.cuda.Stream()
+    with tuning(gemm=(16, 1, 8)):
+        with torch.cuda.stream(stream):
+            ref1 = torch.ops.torchao.int4_weight_only_linear(x1, p1, sz1, g, None)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                out1 = torch.ops.torchao.int4_weight_only_linear(x1, p1, sz1, g, None)
+            ref2 = torch.ops.torchao.int4_weight_only_linear(x2, p2, sz2, g, None)
+        other = torch.cuda.Stream()
+        with torch.cuda.stream(other):
+            ref2b = torch.ops.torchao.int4_weight_only_linear(x2, p2, sz2, g, None)
+        torch.cuda.synchronize()
+        for _ in range(3):
+            out1.zero_()
+            graph.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out1, ref1)
+        # replay concurrently with eager split-K work on another stream: disjoint scratch
+        with torch.cuda.stream(other):
+            again2 = torch.ops.torchao.int4_weight_only_linear(x2, p2, sz2, g, None)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out1, ref1)
+        assert torch.equal(again2, ref2b) and torch.equal(ref2, ref2b)
+    y = ref2.cpu()
+    assert oracle.rel_l2(y, oracle.int4_linear_fp32(x2.cpu(), q2, s2, z2, g)) < TOL_FP32
+
+
+@pytest.mark.parametrize("fmt", ["int4", "int8dyn", "int8dyn_lds"])
+def test_split_k_fenced_equals_fence_free(fmt):
+    """The default sc1 hand-off (no agent fences) and the fenced memory-model form give
+    bit-identical outputs at the maximum split of 8 slices over many tiles."""
+    from torchao.kernel import tuning
+
+    M, N, K, g = 32, 4096, 4096, 32
+    outs = []
+    for fenced in (0, 1, 0):
+        if fmt == "int4":
+            x, q, s, z, packed, sz = _int4_operands(M, N, K, g, seed=21)
+            with tuning(gemm=(16, 1, 8), splitk_fenced=fenced):
+                y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, None)
+        else:
+            w = oracle.make_linear_weight(N, K, seed=22)
+            wq, ws = oracle.int8_dyn_weight(w)
+            xq, xs = oracle.int8_act_quant(oracle.make_activation(M, K, seed=23))
+            knobs = dict(gemm=(64 if fmt == "int8dyn_lds" else 16, 1, 8), splitk_fenced=fenced,
+                         gemm_algo=2 if fmt == "int8dyn_lds" else 1)
+            with tuning(**knobs):
+                y = torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV),
+                                                     ws.to(DEV), None)
+        outs.append(y.cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    if fmt == "int4":
+        assert oracle.rel_l2(outs[0], oracle.int4_linear_fp32(x, q, s, z, g)) < TOL_FP32
+    else:
+        assert torch.equal(outs[0], oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="cpu"))
+
+
+def test_tuning_is_scoped_and_thread_local():
+    """tao_tune_* overrides apply to the calling thread only and tuning() restores defaults."""
+    import threading
+
+    from torchao.kernel import tuning
+
+    with pytest.raises(ValueError):
+        with tuning(no_such_knob=1):
+            pass
+    with pytest.raises(RuntimeError, match="splitk_fenced"):
+        _lib.call("tao_tune_splitk_fenced", 2)
+    _lib.call("tao_tune_reset")
+    # an out-of-range override set on another thread must not reach this thread: the crossover
+    # forced to 8 there would send M = 6 to the GEMV here; the MFMA path's result differs in bits
+    N, K, g = 1024, 2048, 64
+    x, q, s, z, packed, sz = _int4_operands(6, N, K, g, seed=31)
+    xd = x.to(DEV)
+    base = torch.ops.torchao.int4_weight_only_linear(xd, packed, sz, g, None)
+    with tuning(linear_crossover=8):
+        gemv = torch.ops.torchao.int4_weight_only_linear(xd, packed, sz, g, None)
+    t = threading.Thread(target=lambda: _lib.call("tao_tune_linear_crossover", 8))
+    t.start()
+    t.join()
+    after = torch.ops.torchao.int4_weight_only_linear(xd, packed, sz, g, None)
+    assert torch.equal(after, base)
+    for y in (base, gemv):
+        assert oracle.rel_l2(y.cpu(), oracle.int4_linear_fp32(x, q, s, z, g)) < TOL_FP32

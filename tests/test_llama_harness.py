@@ -261,3 +261,36 @@ def test_fuse_w13_gpu(quant):
     one = torch.tensor([8], device=dev)
     a, b = model(prompt[:, -1:], one), ref(prompt[:, -1:], one)
     assert (a - b).norm() / b.norm() < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("quant", [None, "int4wo-32"])
+def test_decode_past_kv_cache_is_reported_gpu(quant):
+    """a decode step at a position past max_seq must not write outside the cache.
+    The fused kernels skip the write and report it; check_decode_status() raises."""
+    from torchao._models.llama import kernels
+
+    dev = torch.device("cuda")
+    model = _tiny(dev, seed=8).fuse_w13()
+    apply_quantization(model, quant)
+    model.setup_caches(1, 16)
+    assert model.enable_fused_kernels()
+    T = model.max_seq
+    prompt = torch.randint(0, 1000, (1, 8), device=dev)
+    model(prompt, torch.arange(8, device=dev))
+    kernels.check_decode_status()  # clean so far
+    one = torch.tensor([T - 1], device=dev)
+    model(prompt[:, -1:], one)  # last valid row
+    kernels.check_decode_status()
+    caches = [(b.attention.kv_cache.k_cache.clone(), b.attention.kv_cache.v_cache.clone())
+              for b in model.layers]
+    canary = torch.full((4096,), 7, dtype=torch.int32, device=dev)  # neighbouring allocation
+    model(prompt[:, -1:], torch.tensor([T], device=dev))  # one past the end
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="past the KV cache"):
+        kernels.check_decode_status()
+    kernels.check_decode_status()  # the read cleared it
+    for b, (kc, vc) in zip(model.layers, caches):
+        assert torch.equal(b.attention.kv_cache.k_cache, kc)
+        assert torch.equal(b.attention.kv_cache.v_cache, vc)
+    assert bool((canary == 7).all())

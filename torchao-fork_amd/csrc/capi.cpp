@@ -57,6 +57,11 @@ static void profile_release() {
   g_prof.active = false;
 }
 
+Tuning& tuning() {
+  static thread_local Tuning t;
+  return t;
+}
+
 // ---- split-K workspace --------------------------------------------------------------------------
 struct Workspace {
   void* slab = nullptr;
@@ -65,33 +70,62 @@ struct Workspace {
   size_t cnt_cap = 0;
 };
 static std::mutex g_ws_mu;
+// eager: one per (device, stream); graphs: one per (device, capture sequence id), never freed
 static std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
+static std::map<std::pair<int, unsigned long long>, Workspace> g_ws_graph;
+
+// Allocate zeroed counters without touching any stream that may be capturing: a private
+// non-blocking stream does the memset (it does not synchronise with the capturing stream).
+static int alloc_counters(unsigned** cnt, size_t n) {
+  if (hipMalloc(reinterpret_cast<void**>(cnt), n * sizeof(unsigned)) != hipSuccess)
+    return set_error(TAO_ERR_HIP, "split-K counter allocation failed");
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+    return set_error(TAO_ERR_HIP, "split-K counter init: stream creation failed");
+  const bool ok = hipMemsetAsync(*cnt, 0, n * sizeof(unsigned), s) == hipSuccess &&
+                  hipStreamSynchronize(s) == hipSuccess;
+  (void)hipStreamDestroy(s);
+  return ok ? TAO_OK : set_error(TAO_ERR_HIP, "split-K counter init failed");
+}
 
 int split_workspace(hipStream_t stream, size_t slab_bytes, size_t counters, void** slab,
                     unsigned** cnt) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return set_error(TAO_ERR_HIP, "hipGetDevice failed");
   std::lock_guard<std::mutex> lock(g_ws_mu);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long cap_id = 0;
+  if (hipStreamGetCaptureInfo(stream, &cs, &cap_id) != hipSuccess)
+    return set_error(TAO_ERR_HIP, "hipStreamGetCaptureInfo failed");
+  if (cs == hipStreamCaptureStatusActive) {
+    // This capture's own workspace. Allocation is not a stream operation; relaxed mode lets
+    // this thread make it while a global-mode capture is open. A larger request later in the
+    // same capture retires the smaller buffers (kept: earlier nodes of this graph use them).
+    Workspace& w = g_ws_graph[{dev, cap_id}];
+    if (w.slab_cap < slab_bytes || w.cnt_cap < counters) {
+      hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+      (void)hipThreadExchangeStreamCaptureMode(&mode);
+      int rc = TAO_OK;
+      Workspace n;
+      n.slab_cap = std::max(slab_bytes, w.slab_cap);
+      n.cnt_cap = std::max(counters, w.cnt_cap);
+      if (hipMalloc(&n.slab, n.slab_cap) != hipSuccess)
+        rc = set_error(TAO_ERR_HIP, "hipMalloc of %zu B split-K slabs (capture) failed",
+                       n.slab_cap);
+      if (rc == TAO_OK) rc = alloc_counters(&n.cnt, n.cnt_cap);
+      (void)hipThreadExchangeStreamCaptureMode(&mode);
+      if (rc != TAO_OK) return rc;
+      w = n;  // the previous buffers are intentionally leaked: the graph references them
+    }
+    *slab = w.slab;
+    *cnt = w.cnt;
+    return TAO_OK;
+  }
+  if (cs != hipStreamCaptureStatusNone)
+    return set_error(TAO_ERR_HIP, "split-K launch on an invalidated capture");
   Workspace& w = g_ws[{dev, stream}];
   if (w.slab_cap < slab_bytes || w.cnt_cap < counters) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
-      // No allocation inside a capture. A warm-up on another stream of this device (the usual
-      // torch.cuda.graph pattern) reserved one: the graph borrows it.
-      for (auto& kv : g_ws) {
-        const Workspace& o = kv.second;
-        if (kv.first.first == dev && o.slab_cap >= slab_bytes && o.cnt_cap >= counters) {
-          *slab = o.slab;
-          *cnt = o.cnt;
-          return TAO_OK;
-        }
-      }
-      return set_error(TAO_ERR_UNSUPPORTED,
-                       "split-K workspace of %zu B not reserved on this device: run the op once "
-                       "at this shape before graph capture",
-                       slab_bytes);
-    }
-    // the old buffers may still be read by work queued on this stream
+    // only work queued on this stream can hold the old buffers (graphs never borrow them)
     if (hipStreamSynchronize(stream) != hipSuccess)
       return set_error(TAO_ERR_HIP, "hipStreamSynchronize failed");
     const size_t sb = std::max(slab_bytes, w.slab_cap);
@@ -108,9 +142,8 @@ int split_workspace(hipStream_t stream, size_t slab_bytes, size_t counters, void
       (void)hipFree(w.cnt);
       w.cnt = nullptr;
       w.cnt_cap = 0;
-      if (hipMalloc(reinterpret_cast<void**>(&w.cnt), nc * sizeof(unsigned)) != hipSuccess ||
-          hipMemset(w.cnt, 0, nc * sizeof(unsigned)) != hipSuccess)
-        return set_error(TAO_ERR_HIP, "split-K counter allocation failed");
+      const int rc = alloc_counters(&w.cnt, nc);
+      if (rc != TAO_OK) return rc;
       w.cnt_cap = nc;
     }
   }
@@ -134,6 +167,17 @@ int tao_device_count(void) {
     return 0;
   }
   return n;
+}
+
+int tao_tune_reset(void) {
+  tao::tuning() = tao::Tuning{};
+  return TAO_OK;
+}
+
+int tao_tune_splitk_fenced(int fenced) {
+  TAO_CHECK_ARG(fenced == 0 || fenced == 1, "tune: splitk_fenced must be 0 or 1");
+  tao::tuning().splitk_fenced = fenced;
+  return TAO_OK;
 }
 
 int tao_profile_begin(int capacity) {

@@ -25,6 +25,10 @@
 #endif
 
 namespace tao {
+
+TAO_DECODE_ERROR_WORD(decode_ops_status)
+int int4gemv_decode_status(unsigned* bits);
+
 namespace {
 
 __device__ __forceinline__ float block_sum(float v, float* red) {
@@ -80,7 +84,12 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(
   const int tok = blockIdx.x;  // b * S + s
   const int b = tok / S, s = tok % S;
   const int half = D / 2;
-  const int64_t p = pos[s];
+  int64_t p = pos[s];
+  const bool pok = p >= 0 && p < T;  // KV cache row inside [0, T)
+  if (!pok) {  // report (tao_decode_status) and write no cache row
+    if (threadIdx.x == 0) flag_decode_error(kDecodeErrKvPos);
+    p = p < 0 ? 0 : T - 1;
+  }
   const uint32_t* row = reinterpret_cast<const uint32_t*>(qkv + (size_t)tok * (H + 2 * Hkv) * D);
   const float2* f = reinterpret_cast<const float2*>(freqs) + (size_t)p * half;  // table row pos
   const int rot_pairs = (H + Hkv) * half;
@@ -94,11 +103,11 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(
       const uint32_t o = (uint32_t)f32_to_bf16(o0) | ((uint32_t)f32_to_bf16(o1) << 16);
       if (head < H) {
         reinterpret_cast<uint32_t*>(q_out)[(((size_t)b * H + head) * S + s) * half + j] = o;
-      } else {
+      } else if (pok) {
         const int kh = head - H;
         reinterpret_cast<uint32_t*>(kc)[(((size_t)b * Hkv + kh) * T + p) * half + j] = o;
       }
-    } else {
+    } else if (pok) {
       const int k = i - rot_pairs;
       const int vh = k / half, j = k % half;
       reinterpret_cast<uint32_t*>(vc)[(((size_t)b * Hkv + vh) * T + p) * half + j] = w;
@@ -121,7 +130,7 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(
   const int bk = blockIdx.x;  // b * Hkv + kvh
   const int b = bk / Hkv, kvh = bk % Hkv;
   const int c = blockIdx.y, NC = gridDim.y;
-  const int L = (int)pos[0] + 1;
+  const int L = attn_len(pos[0], T);
   const int t0 = c * kChunk;
   if (t0 >= L) return;  // uniform: the combine kernel skips this chunk too
   const int tid = threadIdx.x;
@@ -213,7 +222,7 @@ __global__ __launch_bounds__(64) void attn_combine_kernel(const float* __restric
   const int bh = blockIdx.x;  // b * H + h
   const int H = Hkv * G;
   const int b = bh / H, h = bh % H, kvh = h / G, g = h % G;
-  const int L = (int)pos[0] + 1;
+  const int L = attn_len(pos[0], NC * kChunk);
   const int nc = (L + kChunk - 1) / kChunk < NC ? (L + kChunk - 1) / kChunk : NC;
   const float* base = part + ((size_t)(b * Hkv + kvh) * NC * G + g) * (D + 2);
   const size_t cstride = (size_t)G * (D + 2);
@@ -243,7 +252,6 @@ __global__ __launch_bounds__(64) void attn_combine_kernel(const float* __restric
 constexpr int kSingleMaxT = 1024;
 // tao_tune_attn: 0 = single-pass for T <= 1024 else the two-launch split (default), 1 = the
 // two-launch split, 2 / 3 = attn_chunk_fused_kernel with 32 / 64-key chunks
-std::atomic<int> g_attn_mode{0};
 constexpr int kSingleWaves = TAO_ATTN_WAVES;
 
 template <int D, int NW>
@@ -256,7 +264,7 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
   __shared__ float wo[NW][D];
   const int bh = blockIdx.x;  // b * H + h
   const int b = bh / H, h = bh % H, kvh = h / (H / Hkv);
-  const int L = (int)pos[0] + 1;
+  const int L = attn_len(pos[0], T);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int kq = lane >> 2, p = lane & 3;
   const size_t head = (size_t)(b * Hkv + kvh) * T;
@@ -396,7 +404,7 @@ __global__ __launch_bounds__(256) void attn_chunk_fused_kernel(
   const int bk = blockIdx.x;  // b * Hkv + kvh
   const int b = bk / Hkv, kvh = bk % Hkv;
   const int c = blockIdx.y, NC = gridDim.y;
-  const int L = (int)pos[0] + 1;
+  const int L = attn_len(pos[0], T);
   const int t0 = c * CH;
   if (t0 >= L) return;  // uniform; not counted
   const int nact = (L + CH - 1) / CH;
@@ -481,15 +489,7 @@ __global__ __launch_bounds__(256) void attn_chunk_fused_kernel(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) {
-    const unsigned ticket =
-        __hip_atomic_fetch_add(&cnt[bk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = ticket == (unsigned)nact - 1;
-    if (last) __hip_atomic_store(&cnt[bk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag = last ? 1u : 0u;
-  }
-  __syncthreads();
-  if (flag == 0) return;
+  if (!last_arriver(&cnt[bk], (unsigned)nact, &flag, 0)) return;
 
   // merge the kv head's chunks in chunk order, 8 chunks' loads in flight per round
   for (int g = wave; g < G; g += 4) {
@@ -657,7 +657,7 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
   TAO_CHECK_ARG(G == 1 || G == 2 || G == 4 || G == 8, "attn_decode: H / Hkv must be 1, 2, 4 or 8");
   TAO_CHECK_ALIGN(k_cache, 16, "k_cache");
   hipStream_t st = as_stream(stream);
-  const int mode = g_attn_mode.load(std::memory_order_relaxed);
+  const int mode = tao::tuning().attn_mode;
   if (mode == 2 || mode == 3) {  // one launch, key chunks merged by the last arriver
     const int CH = mode == 2 ? 32 : 64;
     const int NC = (int)((T + CH - 1) / CH);
@@ -718,7 +718,7 @@ int tao_tune_attn(int mode) {
                 "tune: attention mode must be 0 (auto: single-pass up to 1024 keys, else split), "
                 "1 (two-launch split), 2 (one launch, 32-key chunks) or 3 (one launch, 64-key "
                 "chunks)");
-  g_attn_mode.store(mode);
+  tao::tuning().attn_mode = mode;
   return TAO_OK;
 }
 
@@ -747,3 +747,12 @@ int tao_argmax_bf16(const uint16_t* x, int64_t* out, int64_t rows, int64_t n, vo
 }
 
 }  // extern "C"
+
+extern "C" int tao_decode_status(int* bits) {
+  TAO_CHECK_ARG(bits != nullptr, "decode status: null output");
+  unsigned v = 0;
+  int rc = tao::decode_ops_status(&v);
+  if (rc == TAO_OK) rc = tao::int4gemv_decode_status(&v);
+  *bits = (int)v;
+  return rc;
+}

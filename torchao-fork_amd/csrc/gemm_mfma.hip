@@ -347,15 +347,16 @@ __device__ __forceinline__ void static_for(F&& f) {
 //    (k-group g: steps s0 + g, s0 + g + KG, ...), each with its own double-buffered x tile;
 //    their accumulators are summed through LDS in k-group order at the end;
 //  * across workgroups (gridDim.z = S slices of `sps` steps): each slice stores its raw
-//    accumulator tile to a slab, and the tile's last arriver (agent-scope counter) sums the S
-//    slabs in slice order and runs the epilogue. Both sums have a fixed order, so results do
-//    not depend on arrival order. Protocol: cdna guide §5 "Projection GEMM at M = 256" item 2
-//    (release fence before the ticket, acquire after it, flag through the one LDS array).
+//    accumulator tile to a slab with sc1 (write-through) stores, and the tile's last arriver
+//    (agent-scope ticket, told by the value its add returned) reads the S slabs with sc1 loads,
+//    sums them in slice order and runs the epilogue. Both sums have a fixed order, so results
+//    do not depend on arrival order. Protocol and its hardware assumption: last_arriver()
+//    (tao_common.h); `fenced` adds the agent release/acquire fences (tao_tune_splitk_fenced).
 template <int BM, int D, int KG, class P>
 __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int sps, typename P::Acc* __restrict__ slab,
-    unsigned* __restrict__ cnt) {
+    unsigned* __restrict__ cnt, int fenced) {
   typedef typename P::Acc Acc;
   constexpr int MT = BM / 16;
   constexpr int XSB = P::kABytes * P::kKStep;  // x bytes per row per step (256 or 512)
@@ -504,12 +505,13 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
 
   const int S = gridDim.z;
   if (S > 1) {
-    // Slab hand-off without agent fences (MI355X_MICROARCH.md, "Hand-offs measured with sc1
-    // loads in place of the acquire", first row): every slab byte is stored sc1 (write-through
+    // Slab hand-off (last_arriver, tao_common.h: MI355X_MICROARCH.md "Hand-offs measured with
+    // sc1 loads in place of the acquire", first row): every slab byte is stored sc1 (write-through
     // past the XCD's L2) and read sc1 (L1 bypassed), each storing wave waits for its stores
     // before the workgroup barrier, one lane adds the tile's ticket, and the last arriver is told
-    // by the value its add returned. The fences this replaces (buffer_wbl2 + buffer_inv, 1.7-6.5
-    // µs each and serialised per CU) made every split slower than no split.
+    // by the value its add returned. The fences this leaves out by default (buffer_wbl2 +
+    // buffer_inv, 1.7-6.5 µs each and serialised per CU) made every split slower than no split;
+    // `fenced` puts them back (tao_tune_splitk_fenced).
     const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
     const size_t tile_bytes = (size_t)S * 4 * MT * 64 * sizeof(Acc);
     const Rsrc srs = make_rsrc(reinterpret_cast<const uint8_t*>(slab) + tile * tile_bytes,
@@ -524,16 +526,9 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    unsigned* flag = reinterpret_cast<unsigned*>(lds);
-    if (tid == 0) {
-      const unsigned ticket =
-          __hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool last = ticket == (unsigned)S - 1;
-      if (last) __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = last ? 1u : 0u;
-    }
-    __syncthreads();
-    if (*flag == 0 || kg != 0) return;
+    const bool last =
+        last_arriver(&cnt[tile], (unsigned)S, reinterpret_cast<unsigned*>(lds), fenced);
+    if (!last || kg != 0) return;
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = Acc{0, 0, 0, 0};
     // 4 slabs per round, all loads issued before the first add (clamped, then masked); slices
@@ -583,7 +578,6 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
 struct GemmShape {
   int bm, kg, splits;
 };
-std::atomic<int> g_tune_bm{0}, g_tune_kg{0}, g_tune_splits{0};
 
 GemmShape choose_shape(int M, int N, int nsteps, int max_bm, int xsb, int pref_kg,
                        int min_slice) {
@@ -621,9 +615,9 @@ GemmShape choose_shape(int M, int N, int nsteps, int max_bm, int xsb, int pref_k
   // int8-dyn (one k-group by default): two when the launch is unsplit and >= 4 M tiles re-read
   // each weight tile (M = 128, 4096^2: 11.4 vs 11.9 µs; profiles/r1_sweep_gemm_sc1*.jsonl)
   if (pref_kg == 1 && sh.splits == 1 && (M + sh.bm - 1) / sh.bm >= 4) sh.kg = 2;
-  const int tb = g_tune_bm.load(std::memory_order_relaxed);
-  const int tk = g_tune_kg.load(std::memory_order_relaxed);
-  const int ts = g_tune_splits.load(std::memory_order_relaxed);
+  const int tb = tao::tuning().bm;
+  const int tk = tao::tuning().kg;
+  const int ts = tao::tuning().splits;
   if (tb) sh.bm = tb < max_bm ? tb : max_bm;
   if (tk) sh.kg = tk;
   if (ts) sh.splits = ts < nsteps ? ts : nsteps;
@@ -643,7 +637,7 @@ void launch_one(dim3 grid, hipStream_t stream, const uint8_t* xb, const P& pol,
     constexpr int D = TAO_GEMM_DEPTH > 0 ? TAO_GEMM_DEPTH
                                          : (BM <= 16 ? 4 : (BM <= 32 ? (big ? 3 : 4) : 2));
     launch((gemm_mfma_kernel<BM, D, KG, P>), grid, dim3(256 * KG), 0, stream, xb, pol, bias, y,
-           M, N, K, sps, slab, cnt);
+           M, N, K, sps, slab, cnt, tuning().splitk_fenced);
   }
 }
 
@@ -704,7 +698,7 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
     const int8_t* __restrict__ x, const int8_t* __restrict__ w, const uint16_t* __restrict__ xscale,
     const uint16_t* __restrict__ wscale, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int sps, i32x4_t* __restrict__ slab,
-    unsigned* __restrict__ cnt) {
+    unsigned* __restrict__ cnt, int fenced) {
   constexpr int XL = BM / 32;           // x chunks per thread per step
   constexpr int WL = BN / 32;           // W chunks per thread per step (BN rows x 8 chunks)
   constexpr int MT = BM / 32, NT = BN / 32;  // 16x16 output tiles per wave
@@ -803,7 +797,7 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
   });
 
   const int S = gridDim.z;
-  if (S > 1) {  // fence-free slab hand-off (see gemm_mfma_kernel)
+  if (S > 1) {  // slab hand-off as in gemm_mfma_kernel (last_arriver, tao_common.h)
     const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
     constexpr uint32_t kZ = 4 * MT * NT * 64 * sizeof(i32x4_t);  // one slice's slab
     const Rsrc srs = make_rsrc(reinterpret_cast<const uint8_t*>(slab) + (size_t)tile * S * kZ,
@@ -817,16 +811,7 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
                        __builtin_bit_cast(uint4, acc[a][b]));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    unsigned* flag = reinterpret_cast<unsigned*>(lds);
-    if (tid == 0) {
-      const unsigned ticket =
-          __hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool last = ticket == (unsigned)S - 1;
-      if (last) __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = last ? 1u : 0u;
-    }
-    __syncthreads();
-    if (*flag == 0) return;
+    if (!last_arriver(&cnt[tile], (unsigned)S, reinterpret_cast<unsigned*>(lds), fenced)) return;
 #pragma unroll
     for (int a = 0; a < MT; ++a)
 #pragma unroll
@@ -869,11 +854,8 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
 }
 
 // gemm_i8_lds_kernel selection (tao_tune_gemm_algo): 0 = auto, 1 = never, 2 = always (K % 128)
-std::atomic<int> g_gemm_algo{0};
 // register-ring depth of gemm_i8_lds_kernel (tao_tune_gemm_depth; 0 = built-in 3 / 4)
-std::atomic<int> g_i8_depth{0};
 // column tile of gemm_i8_lds_kernel (tao_tune_gemm_bn; 0 = built-in 64, or 128)
-std::atomic<int> g_i8_bn{0};
 
 int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uint16_t* ws,
                   const uint16_t* bias, uint16_t* y, int M, int N, int K, bool auto_mode,
@@ -881,7 +863,7 @@ int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const 
   const int nsteps = K / kI8Step;
   // auto: 128-column tiles once 128 x 128 tiles alone number >= 256 (M >= 256;
   // profiles/r1_sweep_i8_bn.jsonl: M=512 14336x4096 54.6 vs 70.6 us; no gain at M = 128)
-  const int tbn = g_i8_bn.load(std::memory_order_relaxed);
+  const int tbn = tao::tuning().i8_bn;
   const int bn = tbn ? (tbn == 128 ? 128 : 64)
                      : (auto_mode && M >= 256 &&
                                 (long)((N + 127) / 128) * ((M + 127) / 128) >= 256
@@ -893,13 +875,13 @@ int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const 
   // parity tests' mode): split towards one round, slices of >= 4 steps (512 k).
   int bm = auto_mode ? (bn == 128 || ntile * ((M + 127) / 128) >= 224 ? 128 : 64)
                      : (M > 64 ? 128 : 64);
-  const int tb = g_tune_bm.load(std::memory_order_relaxed);
+  const int tb = tao::tuning().bm;
   if (tb == 64 || tb == 128) bm = tb;
   const long tiles = ntile * ((M + bm - 1) / bm);
   int splits = 1;
   while (!auto_mode && tiles * splits < 224 && splits * 2 <= 16 && nsteps >= 4 * splits * 2)
     splits *= 2;
-  const int ts = g_tune_splits.load(std::memory_order_relaxed);
+  const int ts = tao::tuning().splits;
   if (ts) splits = ts < nsteps ? ts : nsteps;
   const int sps = (nsteps + splits - 1) / splits;
   const int S = (nsteps + sps - 1) / sps;
@@ -913,10 +895,11 @@ int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const 
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<i32x4_t*>(wsp);
   }
-  const int td = g_i8_depth.load(std::memory_order_relaxed);
+  const int td = tao::tuning().i8_depth;
   const int d = td ? td : (bm == 128 ? 3 : 4);
   auto go = [&](auto kern) {
-    launch(kern, grid, dim3(256), 0, stream, xq, wq, xs, ws, bias, y, M, N, K, sps, slab, cnt);
+    launch(kern, grid, dim3(256), 0, stream, xq, wq, xs, ws, bias, y, M, N, K, sps, slab, cnt,
+           tuning().splitk_fenced);
   };
   if (bn == 128) {  // experiment (tao_tune_gemm_bn): ring depth 2 or 3
     if (bm == 128) {
@@ -942,11 +925,10 @@ int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const 
 }
 
 // Largest M served by the GEMV kernels (tao_tune_linear_crossover; 0 = built-in).
-std::atomic<int> g_max_gemv_m{0};
 // Built-in crossover (experiments/bench_paths.py --crossover): the GEMV wins at M <= 2, and at
 // M <= 4 for small weights; the MFMA kernel's per-M cost is nearly flat.
 bool use_gemv(int64_t M, int64_t N, int64_t K) {
-  const int v = g_max_gemv_m.load(std::memory_order_relaxed);
+  const int v = tao::tuning().max_gemv_m;
   if (v > 0) return M <= v;
   return M <= 2 || (M <= 4 && N * K <= (32LL << 20));
 }
@@ -969,7 +951,7 @@ int int8_scaled_mm_launch(const int8_t* xq, const uint16_t* xs, const int8_t* wq
   // The LDS-staged kernel where its unsplit 64-row tiles fill >= 192 workgroups (M >= 128):
   // M = 128 N = 6144 14.9 vs 20.0 µs, M = 256 4096^2 14.8 vs 16.5, M = 512 22.5 vs 30.8; ties at
   // N >= 14336; the per-wave-column kernel keeps M = 64..128 at N = 4096 (11.8 vs 12.6 µs).
-  const int algo = g_gemm_algo.load(std::memory_order_relaxed);
+  const int algo = tao::tuning().gemm_algo;
   const long t64 = (long)((N + 63) / 64) * ((M + 63) / 64);
   if (K % kI8Step == 0 && (algo == 2 || (algo == 0 && M >= 128 && t64 >= 192)))
     return launch_i8_lds(xq, xs, wq, ws, bias, y, M, N, K, algo == 0, stream);
@@ -1022,7 +1004,7 @@ extern "C" int tao_int8wo_linear_bf16(const uint16_t* x, const int8_t* w, const 
 
 extern "C" int tao_tune_linear_crossover(int max_gemv_m) {
   TAO_CHECK_ARG(max_gemv_m >= 0 && max_gemv_m <= 8, "tune: max_gemv_m must be in [0, 8]");
-  tao::g_max_gemv_m.store(max_gemv_m);
+  tao::tuning().max_gemv_m = max_gemv_m;
   return TAO_OK;
 }
 
@@ -1030,20 +1012,20 @@ extern "C" int tao_tune_gemm_algo(int algo) {
   TAO_CHECK_ARG(algo >= 0 && algo <= 2,
                 "tune: gemm algo must be 0 (auto), 1 (per-wave-column kernel only) or 2 (LDS-staged "
                 "int8 kernel whenever K %% 128 == 0)");
-  tao::g_gemm_algo.store(algo);
+  tao::tuning().gemm_algo = algo;
   return TAO_OK;
 }
 
 extern "C" int tao_tune_gemm_bn(int bn) {
   TAO_CHECK_ARG(bn == 0 || bn == 64 || bn == 128, "tune: LDS int8 GEMM bn must be 0, 64 or 128");
-  tao::g_i8_bn.store(bn);
+  tao::tuning().i8_bn = bn;
   return TAO_OK;
 }
 
 extern "C" int tao_tune_gemm_depth(int depth) {
   TAO_CHECK_ARG(depth == 0 || depth == 2 || depth == 3 || depth == 4 || depth == 6 || depth == 8,
                 "tune: LDS int8 GEMM depth must be 0 (built-in), 2, 3, 4, 6 or 8 (8: M tile 64)");
-  tao::g_i8_depth.store(depth);
+  tao::tuning().i8_depth = depth;
   return TAO_OK;
 }
 
@@ -1053,8 +1035,8 @@ extern "C" int tao_tune_gemm(int m_tile, int k_groups, int splits) {
   TAO_CHECK_ARG(k_groups == 0 || k_groups == 1 || k_groups == 2 || k_groups == 4,
                 "tune: k_groups must be 0 (auto), 1, 2 or 4");
   TAO_CHECK_ARG(splits >= 0 && splits <= 64, "tune: splits must be in [0, 64]");
-  tao::g_tune_bm.store(m_tile);
-  tao::g_tune_kg.store(k_groups);
-  tao::g_tune_splits.store(splits);
+  tao::tuning().bm = m_tile;
+  tao::tuning().kg = k_groups;
+  tao::tuning().splits = splits;
   return TAO_OK;
 }

@@ -30,6 +30,9 @@
 #endif
 
 namespace tao {
+
+TAO_DECODE_ERROR_WORD(int4gemv_decode_status)
+
 namespace {
 
 // Decode-step fusions of the M == 1 GEMV (tao_int4wo_decode_bf16). They fold
@@ -371,7 +374,12 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
         y[n >> 1] = f32_to_bf16(round_bf16(a / (1.f + __expf(-a))) * b);
       } else {
         const int D = fu.D, HD = fu.H * fu.D, KD = fu.Hkv * fu.D;
-        const int64_t p = fu.pos[0];
+        int64_t p = fu.pos[0];
+        const bool pok = p >= 0 && p < fu.T;  // KV cache row inside [0, T)
+        if (!pok) {  // report (tao_decode_status) and write no cache row
+          flag_decode_error(kDecodeErrKvPos);
+          p = p < 0 ? 0 : fu.T - 1;
+        }
         uint32_t ov = (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
         if (n < HD + KD) {
           const float2 cs = reinterpret_cast<const float2*>(fu.freqs)[p * (D >> 1) + ((n % D) >> 1)];
@@ -380,7 +388,7 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
         }
         if (n < HD) {
           reinterpret_cast<uint32_t*>(y)[n >> 1] = ov;
-        } else {
+        } else if (pok) {
           const int nk = n < HD + KD ? n - HD : n - HD - KD;
           uint16_t* cache = n < HD + KD ? fu.k_cache : fu.v_cache;
           const size_t off = ((size_t)(nk / D) * fu.T + p) * D + nk % D;
@@ -439,7 +447,6 @@ int launch_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
 }
 
 // Process-wide override of the M == 1 launch shape (tao_tune_int4_gemv; 0 = heuristic).
-std::atomic<int> g_tune_rpw{0}, g_tune_wk{0}, g_tune_g{0}, g_tune_occ{0};
 
 // M == 1 launch shape. Measured on MI355X (experiments/sweep_gemv.py,
 // profiles/r1_sweep_gemv*.jsonl): the best shapes per (N, K) class, dispatch-event timed over
@@ -477,10 +484,10 @@ M1Shape m1_shape(int N, int S) {
       c.sh = {N <= 4096 ? 2 : (S >= 8 ? 1 : 4), 1};
     }
   }
-  const int trpw = g_tune_rpw.load(std::memory_order_relaxed);
-  const int tocc = g_tune_occ.load(std::memory_order_relaxed);
-  const int twk = g_tune_wk.load(std::memory_order_relaxed);
-  const int tg = g_tune_g.load(std::memory_order_relaxed);
+  const int trpw = tao::tuning().rpw;
+  const int tocc = tao::tuning().occ;
+  const int twk = tao::tuning().wk;
+  const int tg = tao::tuning().g;
   if (trpw > 0) c.rpw = trpw;
   if (tocc > 0) c.occ = tocc;
   if (twk > 0) c.sh.wk = twk;
@@ -521,9 +528,9 @@ int launch_decode(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
     // prologue a workgroup should own whole rows (no K split) and 4 waves of them, so the
     // per-workgroup normalisation is amortised over 8-16 rows; 2 rows per wave below
     // N = 16384 (Llama-3-70B wqkv 10240x8192: 14.0 vs 18.0 µs at 4 rows).
-    if (g_tune_rpw.load(std::memory_order_relaxed) == 0) c.rpw = N < 16384 ? 2 : 4;
-    if (g_tune_wk.load(std::memory_order_relaxed) == 0) c.sh.wk = 1;
-    if (g_tune_g.load(std::memory_order_relaxed) == 0) c.sh.g = 4;
+    if (tao::tuning().rpw == 0) c.rpw = N < 16384 ? 2 : 4;
+    if (tao::tuning().wk == 0) c.sh.wk = 1;
+    if (tao::tuning().g == 0) c.sh.g = 4;
     // enough threads to hold x in the prologue: K <= 8 * NPT * threads, NPT <= kMaxNormPT
     const int wk = c.sh.wk < S ? c.sh.wk : S;
     while (64 * wk * c.sh.g * 8 * kMaxNormPT < K && wk * c.sh.g * 2 <= 8) c.sh.g *= 2;
@@ -540,10 +547,8 @@ int launch_decode(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
 
 // M == 1 plain linears with x staged once per workgroup in LDS (the RMSNorm prologue's copy,
 // without the norm): 0 = off (built-in), 1 = on. tao_tune_int4_xlds.
-std::atomic<int> g_tune_xlds{0};
 // RMSNorm prologue mode of the decode GEMV: 0 = exact (the reference's two bf16 roundings,
 // normalised before the slices), 1 = deferred (outputs scaled by r). tao_tune_int4_norm.
-std::atomic<int> g_tune_norm{0};
 
 // Internal entry (also used by the MFMA dispatcher for small M).
 int int4wo_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
@@ -553,7 +558,7 @@ int int4wo_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
   const int S = (int)((K / 32 + 63) / 64);
   GemvShape sh = default_shape(S);
   const int iM = (int)M, iN = (int)N, iK = (int)K;
-  if (M <= 1 && bias == nullptr && g_tune_xlds.load(std::memory_order_relaxed) == 1) {
+  if (M <= 1 && bias == nullptr && tao::tuning().xlds == 1) {
     GemvFuse fu{};
     fu.norm_w = nullptr;
     return launch_decode<true, kEpiNone>(x, packed, sz, y, iN, iK, gs, stream, fu);
@@ -596,13 +601,13 @@ int int4_check_linear_args(const uint16_t* x, const uint32_t* packed, const uint
 
 extern "C" int tao_tune_int4_norm(int mode) {
   TAO_CHECK_ARG(mode == 0 || mode == 1, "tune: norm mode must be 0 (exact) or 1 (deferred)");
-  tao::g_tune_norm.store(mode);
+  tao::tuning().norm = mode;
   return TAO_OK;
 }
 
 extern "C" int tao_tune_int4_xlds(int mode) {
   TAO_CHECK_ARG(mode == 0 || mode == 1, "tune: xlds mode must be 0 or 1");
-  tao::g_tune_xlds.store(mode);
+  tao::tuning().xlds = mode;
   return TAO_OK;
 }
 
@@ -613,10 +618,10 @@ extern "C" int tao_tune_int4_gemv(int rows_per_wave, int waves_k, int row_groups
   TAO_CHECK_ARG(waves_k >= 0 && row_groups >= 0 && waves_k * (row_groups ? row_groups : 1) <= 8,
                 "tune: waves_k * row_groups must be <= 8");
   TAO_CHECK_ARG(occupancy == 0 || occupancy == 4 || occupancy == 8, "tune: occupancy 0, 4 or 8");
-  tao::g_tune_rpw.store(rows_per_wave);
-  tao::g_tune_wk.store(waves_k);
-  tao::g_tune_g.store(row_groups);
-  tao::g_tune_occ.store(occupancy);
+  tao::tuning().rpw = rows_per_wave;
+  tao::tuning().wk = waves_k;
+  tao::tuning().g = row_groups;
+  tao::tuning().occ = occupancy;
   return TAO_OK;
 }
 
@@ -641,7 +646,7 @@ extern "C" int tao_int4wo_decode_bf16(const uint16_t* x, const uint32_t* packed,
   tao::GemvFuse fu{};
   fu.norm_w = norm_weight;
   fu.eps = eps;
-  fu.norm_deferred = tao::g_tune_norm.load(std::memory_order_relaxed);
+  fu.norm_deferred = tao::tuning().norm;
   if (epilogue == tao::kEpiRopeKV) {
     TAO_CHECK_ARG(n_head > 0 && n_kv_head > 0 && head_dim > 0 && head_dim % 2 == 0 &&
                       max_seq > 0 && N == (n_head + 2 * n_kv_head) * head_dim,
@@ -668,7 +673,7 @@ extern "C" int tao_int4wo_decode_bf16(const uint16_t* x, const uint32_t* packed,
   // without a norm, tao_tune_int4_xlds 1 still takes the prologue path (x staged raw in LDS):
   // the experiment that separates the RMSNorm's cost from the LDS staging's
   const bool pro =
-      norm_weight != nullptr || tao::g_tune_xlds.load(std::memory_order_relaxed) == 1;
+      norm_weight != nullptr || tao::tuning().xlds == 1;
 #define TAO_DEC(P, E) \
   return tao::launch_decode<P, E>(x, packed, scales_and_zeros, y, iN, iK, gs, st, fu)
   switch (epilogue) {

@@ -19,7 +19,6 @@ namespace tao {
 
 // Launch shape override of the int8 decode GEMVs (tao_tune_int8_gemv; 0 = heuristic), shared
 // with int8wo_gemv (int8_gemv.hip).
-std::atomic<int> g_i8_rpw{0}, g_i8_wk{0}, g_i8_g{0};
 
 namespace {
 
@@ -269,9 +268,9 @@ int dyn_gemv_m1(Int8DynGemvArgs a, hipStream_t stream) {
     wk = 4;
     g = 1;
   }
-  const int trpw = g_i8_rpw.load(std::memory_order_relaxed);
-  const int twk = g_i8_wk.load(std::memory_order_relaxed);
-  const int tg = g_i8_g.load(std::memory_order_relaxed);
+  const int trpw = tao::tuning().i8_rpw;
+  const int twk = tao::tuning().i8_wk;
+  const int tg = tao::tuning().i8_g;
   if (trpw > 0) rpw = trpw;
   if (twk > 0) wk = twk;
   if (tg > 0) g = tg;
@@ -392,9 +391,9 @@ int tao_tune_int8_gemv(int rows_per_wave, int waves_k, int row_groups) {
                 "tune: rows_per_wave must be 0 (auto), 2, 4 or 8");
   TAO_CHECK_ARG(waves_k >= 0 && row_groups >= 0 && waves_k * (row_groups ? row_groups : 1) <= 8,
                 "tune: waves_k * row_groups must be <= 8");
-  g_i8_rpw.store(rows_per_wave);
-  g_i8_wk.store(waves_k);
-  g_i8_g.store(row_groups);
+  tao::tuning().i8_rpw = rows_per_wave;
+  tao::tuning().i8_wk = waves_k;
+  tao::tuning().i8_g = row_groups;
   return TAO_OK;
 }
 

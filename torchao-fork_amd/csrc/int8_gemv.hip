@@ -14,7 +14,6 @@
 
 namespace tao {
 
-extern std::atomic<int> g_i8_rpw, g_i8_wk, g_i8_g;  // tao_tune_int8_gemv (int8_dyn.hip)
 
 namespace {
 
@@ -141,12 +140,12 @@ int launch_gemv(const uint16_t* x, const int8_t* w, const uint16_t* scale, const
 int int8wo_gemv(const uint16_t* x, const int8_t* w, const uint16_t* scale, const uint16_t* bias,
                 uint16_t* y, int64_t M, int64_t N, int64_t K, hipStream_t stream) {
   if (M <= 1) {
-    const int rpw = g_i8_rpw.load(std::memory_order_relaxed);
+    const int rpw = tao::tuning().i8_rpw;
     // one row group per workgroup at M == 1 (experiments/sweep_int8.py,
     // profiles/r1_sweep_int8.jsonl: 4 rows per wave, Wk = min(S, 8), G = 1 is within 1% of the
     // per-shape best on every Llama-3-8B linear; the head 77.8 -> 72.7 us)
-    const int wk = g_i8_wk.load(std::memory_order_relaxed);
-    const int tg = g_i8_g.load(std::memory_order_relaxed), g = tg > 0 ? tg : 1;
+    const int wk = tao::tuning().i8_wk;
+    const int tg = tao::tuning().i8_g, g = tg > 0 ? tg : 1;
     if (rpw == 2)
       return launch_gemv<1, 2>(x, w, scale, bias, y, (int)M, (int)N, (int)K, stream, wk, g);
     if (rpw == 8)

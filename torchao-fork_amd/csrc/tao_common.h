@@ -29,12 +29,30 @@ int check_launch(const char* what);
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- split-K workspace (capi.cpp) ------------------------------------------------------------
-// Per (device, stream) scratch for the partial-sum slabs of split-K launches plus a zeroed array
-// of arrival counters (each reset by its tile's last arriver). Grows outside graph capture
-// only: a capture borrows a large-enough workspace reserved on the device by an earlier eager
-// call (on any stream), else it is an error (run the op once at that shape before capturing).
+// Scratch for the partial-sum slabs of split-K launches plus a zeroed array of arrival counters
+// (each reset by its tile's last arriver). Eager calls use one workspace per (device, stream),
+// grown after a synchronisation of that stream (nothing else ever holds its pointers). A graph
+// capture gets a workspace of its own, per capture sequence, allocated during the capture
+// (relaxed capture mode) and never freed: a replay can never share scratch with eager work or
+// with another graph, and no pointer a graph holds is ever released.
 int split_workspace(hipStream_t stream, size_t slab_bytes, size_t counters, void** slab,
                     unsigned** cnt);
+
+// ---- launch-shape overrides (tao_tune_*, tao_tune_reset) --------------------------------------
+// Zero means "built-in choice". Thread-local: a tao_tune_* call re-routes only launches issued
+// from the calling thread, and tao_tune_reset() (torchao.kernel.tuning() on exit) restores the
+// built-in shapes, so sweeps cannot re-route another thread's model.
+struct Tuning {
+  int rpw = 0, wk = 0, g = 0, occ = 0;           // int4 GEMV (tao_tune_int4_gemv)
+  int xlds = 0, norm = 0;                        // int4 GEMV x staging / deferred norm
+  int bm = 0, kg = 0, splits = 0;                // MFMA GEMM (tao_tune_gemm)
+  int gemm_algo = 0, i8_depth = 0, i8_bn = 0;    // int8 LDS GEMM
+  int max_gemv_m = 0;                            // GEMV <-> MFMA crossover
+  int i8_rpw = 0, i8_wk = 0, i8_g = 0;           // int8 GEMVs (tao_tune_int8_gemv)
+  int attn_mode = 0;                             // decode attention (tao_tune_attn)
+  int splitk_fenced = 0;                         // split-K hand-off with agent fences
+};
+Tuning& tuning();
 
 // ---- optional per-kernel timing (tao_profile_begin / tao_profile_end, capi.cpp) ---------------
 // While a profile session is open on this thread, each launch gets a start/stop hipEvent pair
@@ -128,5 +146,73 @@ __device__ __forceinline__ uint32_t bload4(Rsrc r, uint32_t voff, uint32_t soff)
 }
 
 constexpr int kWave = 64;
+
+// ---- decode-step error word ------------------------------------------------------------------
+// Device-side argument faults of the decode kernels (a KV position outside [0, T)) are not
+// trapped: the kernel skips the out-of-range cache write, clamps what it reads, and ORs a bit
+// into a per-translation-unit error word that the host reads and clears with
+// tao_decode_status() (a synchronous read, made outside graph capture; the decode harness does
+// it after every generate()). The reference's index_put KV cache device-asserts instead.
+constexpr unsigned kDecodeErrKvPos = 1u;
+#define TAO_DECODE_ERROR_WORD(reader)                                                        \
+  static __device__ unsigned g_decode_err = 0;                                                \
+  __device__ __forceinline__ void flag_decode_error(unsigned bits) {                          \
+    (void)__hip_atomic_fetch_or(&g_decode_err, bits, __ATOMIC_RELAXED,                        \
+                                __HIP_MEMORY_SCOPE_AGENT);                                    \
+  }                                                                                           \
+  int reader(unsigned* bits) {                                                                \
+    unsigned v = 0, zero = 0;                                                                 \
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_decode_err), sizeof(v)) != hipSuccess ||         \
+        hipMemcpyToSymbol(HIP_SYMBOL(g_decode_err), &zero, sizeof(zero)) != hipSuccess)       \
+      return set_error(TAO_ERR_HIP, "decode status: symbol copy failed");                     \
+    *bits |= v;                                                                               \
+    return TAO_OK;                                                                            \
+  }
+
+// keys attended at query position p of a cache of T rows: p + 1, clamped to [1, T] (a p
+// outside [0, T) was reported by the KV-writing kernel of the same step)
+__device__ __forceinline__ int attn_len(int64_t p, int T) {
+  return p < 0 ? 1 : (p >= T ? T : (int)p + 1);
+}
+
+// ---- last-arriver hand-off (split-K slabs, decode-attention chunks) ------------------------------
+// Call after every storing wave of the workgroup has stored its share of the hand-off (all with
+// kSC1) and run `s_waitcnt vmcnt(0)`, from all threads (contains a workgroup barrier). One lane
+// adds to the tile's arrival counter; every thread learns whether this workgroup arrived last
+// (then the counter is reset for the next launch) and may load the others' bytes with kSC1 loads.
+//
+// fenced == 0 (default): no agent fences. This is MI355X_MICROARCH.md's "Hand-offs measured with
+// sc1 loads in place of the acquire", first row: one lane per storing workgroup signals with an
+// agent-scope atomic add to one unsharded counter, the workgroup whose add came last is told by
+// the value it returned, its other waves load after a workgroup barrier joined behind an LDS
+// word, sc1 stores and sc1 loads of 16 B (and 8 B in decode attention), hipMalloc'd memory. That
+// row is a measured gfx950 / ROCm 7.2 behaviour, not an HIP memory-model guarantee (the guide
+// says so); the fences it removes cost 1.7-6.5 µs each.
+// fenced == 1 (tao_tune_splitk_fenced): the memory-model form on top of the same stores and
+// loads: release fence (buffer_wbl2 sc1 + asm vmcnt(0), the guide's compiler-hazard fix) before
+// the add, acquire fence (buffer_inv sc1 + vmcnt(0)) in the last arriver before the barrier.
+// tests/test_gpu_gemm_tiles.py checks both give bit-identical results.
+__device__ __forceinline__ bool last_arriver(unsigned* counter, unsigned arrivals,
+                                             unsigned* lds_word, int fenced) {
+  if (threadIdx.x == 0 && threadIdx.y == 0) {
+    if (fenced) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const unsigned ticket =
+        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = ticket == arrivals - 1;
+    if (last) {
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (fenced) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    *lds_word = last ? 1u : 0u;
+  }
+  __syncthreads();
+  return *lds_word != 0;
+}
 
 }  // namespace tao

@@ -42,6 +42,8 @@ _SIGNATURES = {
     "tao_tune_gemm_bn": [_int],
     "tao_tune_int4_xlds": [_int],
     "tao_tune_int4_norm": [_int],
+    "tao_tune_reset": [],
+    "tao_tune_splitk_fenced": [_int],
     "tao_int4_pack": [_p, _p, _i64, _i64, _p],
     "tao_int4_pack_u8": [_p, _p, _i64, _i64, _p],
     "tao_int4_unpack": [_p, _p, _i64, _i64, _p],
@@ -61,6 +63,7 @@ _SIGNATURES = {
     "tao_attn_decode_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
                              ctypes.c_float, _p],
     "tao_tune_attn": [_int],
+    "tao_decode_status": [_p],
     "tao_silu_mul_bf16": [_p, _p, _p, _i64, _p],
     "tao_argmax_bf16": [_p, _p, _i64, _i64, _p],
     "tao_int4_quantize_bf16": [_p, _p, _p, _i64, _i64, _i64, ctypes.c_float, _p],

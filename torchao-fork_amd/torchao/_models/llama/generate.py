@@ -195,6 +195,7 @@ def generate(model: Transformer, prompt: torch.Tensor, max_new_tokens: int,
             decoder.step()
         torch.cuda.synchronize()
         t2 = time.perf_counter()
+        _check_status(model)
         return decoder.tokens[:, :P + max_new_tokens].clone(), t1 - t0, t2 - t1
     out = torch.empty(B, P + max_new_tokens, dtype=prompt.dtype, device=device)
     out[:, :P] = prompt
@@ -206,7 +207,15 @@ def generate(model: Transformer, prompt: torch.Tensor, max_new_tokens: int,
         pos += 1
     torch.cuda.synchronize()
     t2 = time.perf_counter()
+    _check_status(model)
     return out, t1 - t0, t2 - t1
+
+
+def _check_status(model: Transformer) -> None:
+    if model.fused:
+        from torchao._models.llama import kernels
+
+        kernels.check_decode_status()
 
 
 def main(argv=None):

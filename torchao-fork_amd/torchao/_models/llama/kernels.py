@@ -6,7 +6,8 @@ import torch
 
 from torchao import _lib
 
-__all__ = ["rmsnorm", "rope_kv", "attn_decode", "silu_mul", "int4_decode", "argmax"]
+__all__ = ["rmsnorm", "rope_kv", "attn_decode", "silu_mul", "int4_decode", "argmax",
+           "check_decode_status"]
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -131,3 +132,17 @@ def argmax(logits: torch.Tensor) -> torch.Tensor:
     _lib.call("tao_argmax_bf16", logits.data_ptr(), out.data_ptr(), logits.numel() // V, V,
               _stream(logits))
     return out
+
+
+def check_decode_status() -> None:
+    """Raise if a decode kernel saw a KV-cache position outside the cache since the last check
+    (tao_decode_status: the kernels skip that write instead of faulting; synchronous, so call it
+    outside graph capture, e.g. after a generate())."""
+    import ctypes
+
+    bits = ctypes.c_int(0)
+    _lib.call("tao_decode_status", ctypes.cast(ctypes.pointer(bits), ctypes.c_void_p))
+    if bits.value & 1:
+        raise RuntimeError("decode step at a position past the KV cache (max_seq_length): "
+                           "no cache row was written; call setup_caches() with a larger "
+                           "max_seq_length")
