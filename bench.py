@@ -133,7 +133,7 @@ def make_int4_weight(N, K, g, seed, device):
     return packed, sz
 
 
-def calibrate_sharding(shapes, P, g, device, rehearsal, reps=20):
+def calibrate_sharding(shapes, P, g, device, rehearsal, reps=20, pairs=None):
     """Per (N, K): time the whole-N GEMV and the N/P GEMV + its all-gather (eager launches on
     the current stream, each shape's weights rotated over copies past the 256 MiB Infinity
     Cache; GPU events; max over ranks so every rank takes the same decision). An M = 1
@@ -179,16 +179,42 @@ def calibrate_sharding(shapes, P, g, device, rehearsal, reps=20):
         e1.synchronize()
         return e0.elapsed_time(e1) * 1e3 / reps
 
+    def allreduce_us(N):
+        y = torch.zeros(N, device=device, dtype=torch.bfloat16)
+        if rehearsal:
+            return 1e9
+        for _ in range(3):
+            dist.all_reduce(y)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            dist.all_reduce(y)
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / reps
+
+    def agree(vals):  # max over ranks so every rank takes the same decision
+        t = torch.tensor(vals, dtype=torch.float64, device="cpu" if rehearsal else device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(v) for v in t.tolist()]
+
     out = {}
     for N, K in shapes:
         if N % P:
             continue
-        t = torch.tensor([gemv_us(N, K), gemv_us(N // P, K), gather_us(N)], dtype=torch.float64,
-                         device="cpu" if rehearsal else device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        whole, part, gather = (float(v) for v in t.tolist())
+        whole, part, gather = agree([gemv_us(N, K), gemv_us(N // P, K), gather_us(N)])
         out[(N, K)] = {"whole_us": round(whole, 2), "shard_us": round(part, 2),
                        "allgather_us": round(gather, 2), "shard": part + gather < 0.95 * whole}
+        torch.cuda.empty_cache()
+    # Megatron pairs (colwise A without a gather -> rowwise B + all-reduce), per distinct pair
+    for (Na, Ka), (Nb, Kb) in pairs or ():
+        if Na % P or Kb % (P * g):
+            continue
+        wa, wb, pa, pb, ar = agree([gemv_us(Na, Ka), gemv_us(Nb, Kb), gemv_us(Na // P, Ka),
+                                    gemv_us(Nb, Kb // P), allreduce_us(Nb)])
+        out[("pair", Na, Ka, Nb, Kb)] = {
+            "whole_us": round(wa + wb, 2), "colwise_us": round(pa, 2), "rowwise_us": round(pb, 2),
+            "allreduce_us": round(ar, 2), "shard": pa + pb + ar < 0.95 * (wa + wb)}
         torch.cuda.empty_cache()
     return out
 
@@ -205,7 +231,7 @@ def reference_gpu_step(plan, xs, g, device, steps):
     Returns its GB/s over the same algorithmic bytes and its max relative difference from our
     outputs on the step's linears."""
     packs = []
-    for (_, n_loc, K, packed, sz, y_loc, _y) in plan:
+    for (_, n_loc, K, packed, sz, y_loc, _y, _k) in plan:
         q = torch.ops.torchao.int4_unpack(packed)
         u8 = ((q[:, ::2] << 4) | q[:, 1::2]).to(torch.uint8)
         del q
@@ -339,11 +365,53 @@ def e2e_decode(timeout_s=240):
     return rec
 
 
+def host_cpu_info():
+    """CPU model, the physical cores this process may run on, and the cgroup CPU quota (the
+    GPU box's share of a large host), read from /proc/cpuinfo and /sys/fs/cgroup."""
+    allowed = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
+    model, cores, cur = None, set(), {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f.read().splitlines() + [""]:
+                if not line.strip():
+                    if cur.get("processor") is not None and (not allowed or int(cur["processor"]) in allowed):
+                        cores.add((cur.get("physical id", "0"), cur.get("core id", cur["processor"])))
+                    cur = {}
+                    continue
+                k, _, v = line.partition(":")
+                cur[k.strip()] = v.strip()
+                if k.strip() == "model name" and model is None:
+                    model = v.strip()
+    except OSError:
+        pass
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+            if path.endswith("cpu.max") and parts and parts[0] != "max":
+                quota = float(parts[0]) / float(parts[1])
+            elif path.endswith("quota_us") and parts and int(parts[0]) > 0:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f2:
+                    quota = int(parts[0]) / int(f2.read().split()[0])
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    physical = len(cores) or len(allowed) or (os.cpu_count() or 1)
+    return {"cpu_model": model, "physical_cores": physical, "logical_cpus": len(allowed) or None,
+            "cgroup_cpu_quota": quota}
+
+
 def cpu_baseline(cfg, g, budget_s=12.0):
-    """The reference CPU dequant path (oracle restatement) on one layer's five linears, M = 1."""
+    """The reference CPU dequant path (oracle restatement) on one layer's five linears, M = 1,
+    plus BASELINE config 1 (one 4096x4096 linear), on every physical core this process may use
+    (capped by the cgroup CPU quota: a thread per core the scheduler actually grants)."""
     from oracle import oracle
 
-    cores = min(16, os.cpu_count() or 1)
+    info = host_cpu_info()
+    cores = info["physical_cores"]
+    if info["cgroup_cpu_quota"]:
+        cores = max(1, min(cores, int(info["cgroup_cpu_quota"])))
     torch.set_num_threads(cores)
     layer = [lin for lin in llama_linears(cfg) if lin[0].startswith("layers.0.")]
     mats = []
@@ -378,10 +446,29 @@ def cpu_baseline(cfg, g, budget_s=12.0):
         tg = sample_bytes * r2 / (time.perf_counter() - t1) / 1e9
     except Exception as e:  # pragma: no cover - depends on the host's torch build
         tg = f"unavailable: {type(e).__name__}"
+    # BASELINE config 1: a single nn.Linear 4096x4096, int4 g32, the same CPU dequant path
+    w1 = oracle.make_linear_weight(4096, 4096, seed=41)
+    s1, z1 = oracle.int4_qparams(w1, g)
+    q1 = oracle.int4_quantize(w1, s1, z1, g)
+    x1 = oracle.make_activation(1, 4096, seed=42)
+    oracle.int4_linear(x1, q1, s1, z1, g)
+    times = []
+    t2 = time.perf_counter()
+    while len(times) < 50 and time.perf_counter() - t2 < 3.0:
+        t3 = time.perf_counter()
+        oracle.int4_linear(x1, q1, s1, z1, g)
+        times.append(time.perf_counter() - t3)
+    c1 = sorted(times)[len(times) // 2]
     return {
         "value": round(sample_bytes * reps / dt / 1e9, 3),
         "unit": "GB/s",
         "cores": cores,
+        "cpu_model": info["cpu_model"],
+        "physical_cores": info["physical_cores"],
+        "cgroup_cpu_quota": info["cgroup_cpu_quota"],
+        "config1_4096x4096": {"ms_median": round(c1 * 1e3, 3),
+                              "GBps": round(int4_alg_bytes(4096, 4096, g) / c1 / 1e9, 3),
+                              "runs": len(times)},
         "kind": "port",
         "sample": (f"reference CPU dequant path (dequantize -> F.linear bf16, oracle/oracle.py) on "
                    f"layer 0's 5 int4 g{g} linears at M=1, {reps} reps in {dt:.1f}s"),
@@ -404,10 +491,13 @@ def main():
                     help="skip the config-3 MFMA prefill measurement (prefill_mfma)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the config-4 e2e decode run (e2e_decode, a child process)")
-    ap.add_argument("--shard-policy", default="auto", choices=["auto", "size", "all", "none"],
-                    help="P > 1: which linears to column-shard. auto = per (N, K), whichever of "
-                         "{whole GEMV on every rank, N/P GEMV + all-gather} measured faster "
-                         "at startup (max over ranks); size = N*K >= --shard-min-elems")
+    ap.add_argument("--shard-policy", default="auto",
+                    choices=["auto", "tp", "size", "all", "none"],
+                    help="P > 1: how to shard. tp = Megatron pairs (wqkv colwise -> wo rowwise + "
+                         "all-reduce, w1||w3 colwise -> w2 rowwise + all-reduce) and the output "
+                         "head colwise + all-gather; all / size = every (large) linear colwise + "
+                         "all-gather; auto = per pair / per head, whichever of {replicated, "
+                         "sharded} measured faster at startup (max over ranks)")
     ap.add_argument("--shard-min-elems", type=int, default=64 << 20,
                     help="--shard-policy size: shard when N*K >= this")
     ap.add_argument("--shard-all", action="store_true", help="= --shard-policy all")
@@ -447,31 +537,62 @@ def main():
     g, P = args.group_size, world
     lins = llama_linears(cfg, fuse_w13=not args.no_fuse_w13)
     policy = "all" if args.shard_all else args.shard_policy
+    # Megatron pairs of a Llama block (colwise -> rowwise): wqkv -> wo, w1||w3 (or w1, w3) -> w2
+    pair_of = {}
+    for i, (name, N, K) in enumerate(lins):
+        if name.endswith("attention.wo"):
+            pair_of[i - 1], pair_of[i] = ("col", i), ("row", i - 1)
+        elif name.endswith("feed_forward.w2"):
+            j = i - 1
+            while j >= 0 and lins[j][0].rsplit(".", 1)[0] == name.rsplit(".", 1)[0]:
+                pair_of[j] = ("col", i)
+                j -= 1
+            pair_of[i] = ("row", j + 1)
     calib = {}
     if P > 1 and policy == "auto":
+        pairs = sorted({((lins[i][1], lins[i][2]), (lins[j][1], lins[j][2]))
+                        for i, (kind, j) in pair_of.items() if kind == "col"})
         calib = calibrate_sharding(sorted({(N, K) for _, N, K in lins}), P, g, device,
-                                   rehearsal)
+                                   rehearsal, pairs=pairs)
+
+    def pair_sharded(i):
+        kind, j = pair_of[i]
+        a, b = (i, j) if kind == "col" else (j, i)
+        (_, Na, Ka), (_, Nb, Kb) = lins[a], lins[b]
+        if Na % P or Kb % (P * g):
+            return False
+        if policy == "tp":
+            return True
+        return bool(calib.get(("pair", Na, Ka, Nb, Kb), {}).get("shard"))
 
     # ---- build the sharded weights, inputs and outputs (all resident in HBM) ----
+    # kinds: whole (replicated), gather (colwise + all-gather), local (colwise, output consumed
+    # by its rowwise partner), reduce (rowwise on K/P + all-reduce)
     plan, bytes_per_step = [], 0
-    xs = {K: torch.randn(1, K, device=device, dtype=torch.bfloat16) for K in {K for _, _, K in lins}}
+    xs = {}
     n_sharded = 0
     for i, (name, N, K) in enumerate(lins):
-        # column-shard the large linears (north star); a small one is cheaper to run whole on
-        # every rank than to shard and gather (an M = 1 gather costs more than its GEMV)
-        if P == 1 or N % P or policy == "none":
-            shard = False
-        elif policy == "auto":
-            shard = calib[(N, K)]["shard"]
-        else:
-            shard = policy == "all" or N * K >= args.shard_min_elems
-        n_sharded += shard
-        n_loc = N // P if shard else N
-        packed, sz = make_int4_weight(n_loc, K, g, seed=1000 * i + (rank if shard else 0),
+        kind = "whole"
+        if P > 1 and policy != "none":
+            if i in pair_of and policy in ("tp", "auto") and pair_sharded(i):
+                kind = "local" if pair_of[i][0] == "col" else "reduce"
+            elif policy == "auto" and i not in pair_of and N % P == 0:
+                kind = "gather" if calib[(N, K)]["shard"] else "whole"
+            elif policy in ("all", "size") and N % P == 0:
+                kind = "gather" if policy == "all" or N * K >= args.shard_min_elems else "whole"
+            elif policy == "tp" and i not in pair_of and N % P == 0:
+                kind = "gather"
+        n_sharded += kind != "whole"
+        n_loc = N // P if kind in ("gather", "local") else N
+        k_loc = K // P if kind == "reduce" else K
+        packed, sz = make_int4_weight(n_loc, k_loc, g,
+                                      seed=1000 * i + (rank if kind != "whole" else 0),
                                       device=device)
+        if k_loc not in xs:
+            xs[k_loc] = torch.randn(1, k_loc, device=device, dtype=torch.bfloat16)
         y_loc = torch.empty(n_loc, device=device, dtype=torch.bfloat16)  # M = 1 row
-        y_full = torch.empty(N, device=device, dtype=torch.bfloat16) if shard else y_loc
-        plan.append((name, n_loc, K, packed, sz, y_loc, y_full))
+        y_full = torch.empty(N, device=device, dtype=torch.bfloat16) if kind == "gather" else y_loc
+        plan.append((name, n_loc, k_loc, packed, sz, y_loc, y_full, kind))
         bytes_per_step += int4_alg_bytes(N, K, g)
     torch.cuda.synchronize()
 
@@ -480,19 +601,27 @@ def main():
 
     def step(do_gemv=True, do_comm=True):
         sp = torch.cuda.current_stream(device).cuda_stream
-        for (_, n_loc, K, packed, sz, y_loc, y_full) in plan:
+        for (_, n_loc, K, packed, sz, y_loc, y_full, kind) in plan:
             if do_gemv:
                 rc = lib.tao_int4wo_linear_bf16(xs[K].data_ptr(), packed.data_ptr(), sz.data_ptr(),
                                                 None, y_loc.data_ptr(), 1, n_loc, K, g, sp)
                 if rc:
                     raise RuntimeError(lib.tao_last_error().decode())
-            if do_comm and y_full is not y_loc:
+            if not do_comm or kind in ("whole", "local"):
+                continue
+            if kind == "gather":
                 if rehearsal:
                     parts = [torch.empty_like(y_loc, device="cpu") for _ in range(P)]
                     dist.all_gather(parts, y_loc.cpu())
                     y_full.copy_(torch.cat(parts))
                 else:
                     dist.all_gather_into_tensor(y_full, y_loc)
+            elif rehearsal:  # reduce
+                t = y_loc.cpu()
+                dist.all_reduce(t)
+                y_loc.copy_(t)
+            else:
+                dist.all_reduce(y_loc)
 
     def capture(**kw):
         graph = torch.cuda.CUDAGraph()
@@ -640,8 +769,12 @@ def main():
                 "seq_len": 1,
                 "group_size": g,
                 "bytes_per_step": bytes_per_step,
-                "parallelism": (f"colwise-tp{P} + RCCL all-gather on {n_sharded} of {len(plan)} "
-                                f"linears (shard policy {policy}), rest replicated"
+                "parallelism": (f"tp{P} (shard policy {policy}): "
+                                + ", ".join(f"{sum(e[7] == k for e in plan)} {k}" for k in
+                                            ("local", "reduce", "gather", "whole"))
+                                + " of " + str(len(plan)) + " linears (local = colwise feeding "
+                                "its rowwise partner, reduce = rowwise + RCCL all-reduce, gather = "
+                                "colwise + RCCL all-gather, whole = replicated)"
                                 if P > 1 else "single-gpu"),
                 "hip_graph": graph is not None,
             },
@@ -672,9 +805,11 @@ def main():
         if P == 1 and args.model == "8b" and not args.no_e2e:
             rec["e2e_decode"] = e2e_decode()
         if comm_ms is not None:
-            rec["allgather_ms_per_step"] = round(comm_ms, 4)
+            rec["collectives_ms_per_step"] = round(comm_ms, 4)
         if calib:
-            rec["shard_calibration_us"] = {f"{N}x{K}": v for (N, K), v in calib.items()}
+            rec["shard_calibration_us"] = {
+                ("x".join(str(v) for v in key[1:3]) + "->" + "x".join(str(v) for v in key[3:])
+                 if key[0] == "pair" else f"{key[0]}x{key[1]}"): v for key, v in calib.items()}
         if cpu is not None:
             rec["speedup_vs_cpu_baseline"] = round(rec["value"] / cpu["value"], 1)
         print(json.dumps(rec), flush=True)

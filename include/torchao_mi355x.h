@@ -148,11 +148,25 @@ int tao_int4_unpack_host(const uint32_t* packed, int32_t* q, int64_t N, int64_t 
 
 /* ---- reference tile-format compat (torchao::*_tensor_core_tiled_layout) ------------------- */
 
-/* out[N][K] int32 <- tile-format packed_w [N/8][K/(ikt*16)][32][ikt/2] (int32).
+/* The reference tile format: int32 [N/8][K/(ikt*16)][32][ikt/2], inner_k_tiles (ikt) in {2,4,8}.
+ * Two nibble maps share that shape (tile_format):
+ *   0 = CUDA: the semantics of the reference's own kernels (tensor_core_tiled_layout.cu:131-215),
+ *       i.e. what aten._convert_weight_to_int4pack writes on CUDA builds of PyTorch;
+ *   1 = ROCm: what aten._convert_weight_to_int4pack writes on PyTorch-ROCm (gfx950, measured:
+ *       experiments/probe_aten_tile_map.py, tests/golden/aten_tile_map_rocm.npz), the bytes seen
+ *       flat as [N/16][K/(ikt*16)][64][ikt/2] for wave64 lanes; needs N % 16 == 0.
+ * A checkpoint saved by torchao holds whichever format its producing build wrote. */
+
+/* out[N][K] int32 <- tile-format packed_w.
  * Replaces torchao::unpack_tensor_core_tiled_layout (torchao/ops.py:255-296,
- * tensor_core_tiled_layout.cu:320-368). inner_k_tiles in {2,4,8}. */
+ * tensor_core_tiled_layout.cu:320-368). */
 int tao_unpack_tensor_core_tiled_layout(const int32_t* packed_w, int32_t* out, int64_t N,
-                                        int64_t K, int64_t inner_k_tiles, void* stream);
+                                        int64_t K, int64_t inner_k_tiles, int tile_format,
+                                        void* stream);
+
+/* The same on the host (checkpoint conversion of CPU-resident state dicts). */
+int tao_unpack_tensor_core_tiled_layout_host(const int32_t* packed_w, int32_t* out, int64_t N,
+                                             int64_t K, int64_t inner_k_tiles, int tile_format);
 
 /* out[N][K] bf16 <- fma(q-8, s, z) with scales_and_zeros [K/g][N][2] bf16 (tinygemm packing,
  * torchao/quantization/utils.py:395-409). Replaces torchao::dequantize_tensor_core_tiled_layout
@@ -160,13 +174,14 @@ int tao_unpack_tensor_core_tiled_layout(const int32_t* packed_w, int32_t* out, i
 int tao_dequantize_tensor_core_tiled_layout(const int32_t* packed_w,
                                             const uint16_t* scales_and_zeros, uint16_t* out,
                                             int64_t N, int64_t K, int64_t group_size,
-                                            int64_t inner_k_tiles, void* stream);
+                                            int64_t inner_k_tiles, int tile_format,
+                                            void* stream);
 
-/* Tile-format packer (the inverse of the unpack above): packed_w <- q[N][K] int32.
- * Equivalent of aten._convert_weight_to_int4pack's output format as described by the reference
- * unpack kernel (tensor_core_tiled_layout.cu:131-215). N % 8 == 0, K % (ikt*16) == 0. */
+/* Tile-format packer (the inverse of the unpack above): packed_w <- q[N][K] int32; with
+ * tile_format 1 bit-identical to PyTorch-ROCm's aten._convert_weight_to_int4pack (the call at
+ * torchao/dtypes/uintx/tensor_core_tiled_layout.py:279). K % (ikt*16) == 0. */
 int tao_pack_tensor_core_tiled_layout(const int32_t* q, int32_t* packed_w, int64_t N, int64_t K,
-                                      int64_t inner_k_tiles, void* stream);
+                                      int64_t inner_k_tiles, int tile_format, void* stream);
 
 /* ---- int8 weight-only ---------------------------------------------------------------------- */
 

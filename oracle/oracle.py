@@ -25,13 +25,16 @@ What it restates (CPU, torch ops in bf16 with the reference's op order; numpy fo
     pack_row_stream / unpack_row_stream  <- the gfx950 layout of include/torchao_mi355x.h
     pack_tile / unpack_tile              <- reference tile format, semantics of
                                             csrc/cuda/tensor_core_tiled_layout/tensor_core_tiled_layout.cu:131-215
+                                            (fmt "cuda"), or PyTorch-ROCm's aten producer (fmt "rocm")
 
 Pinning: every float function here is checked bit-exactly (torch.equal) against fixtures the
 reference itself produced in the build container (oracle/gen_golden.py -> tests/golden/*.npz).
 The tile format cannot be produced by the reference on CPU (aten._convert_weight_to_int4pack
-has no CPU kernel); pack_tile/unpack_tile are pinned to the reference unpack kernel's index
-math (round trip + hand-checked vectors), i.e. parity for the tile format is pinned to the
-reference source, not to a run of the reference.
+has no CPU kernel). pack_tile(fmt="cuda") is pinned to the reference unpack kernel's index math
+(round trip + hand-checked vectors: pinned to source); pack_tile(fmt="rocm") is pinned to the
+nibble map PyTorch-ROCm's aten._convert_weight_to_int4pack produced on the MI355X
+(tests/golden/aten_tile_map_rocm.npz, every nibble of 15 (N, K, ikt) cases: pinned to a run),
+and the GPU tests compare the HIP pack with that aten op directly.
 """
 
 from typing import Optional, Tuple
@@ -190,9 +193,23 @@ def unpack_row_stream(p: np.ndarray) -> np.ndarray:
     return out.reshape(N, KD * 8)
 
 
-def _tile_index(N: int, K: int, ikt: int):
-    """For every element of the tile tensor [N/8][K/(ikt*16)][32][ikt/2]: (n, ks[4])."""
+def _tile_index(N: int, K: int, ikt: int, fmt: str = "cuda"):
+    """For every element of the tile tensor [N/8][K/(ikt*16)][32][ikt/2]: (n, ks[4]).
+
+    fmt "cuda": tensor_core_tiled_layout.cu:131-215 (the reference's own kernels).
+    fmt "rocm": PyTorch-ROCm's aten._convert_weight_to_int4pack on gfx950, recovered on the box
+    (experiments/probe_aten_tile_map.py) and pinned by tests/golden/aten_tile_map_rocm.npz: the
+    same bytes seen flat as [N/16][K/(ikt*16)][64][ikt/2]; lane l: n = 16 nb + l % 16,
+    b = kb*ikt*16 + 32 j + 4 (l // 16), ks = {b, b+2, b+16, b+18}."""
     KT = K // (ikt * 16)
+    if fmt == "rocm":
+        nb, kb, l, j = np.meshgrid(np.arange(N // 16), np.arange(KT), np.arange(64),
+                                   np.arange(ikt // 2), indexing="ij")
+        n = nb * 16 + l % 16
+        b = kb * ikt * 16 + 32 * j + 4 * (l // 16)
+        ks = np.stack([b, b + 2, b + 16, b + 18], -1)
+        shape = (N // 8, KT, 32, ikt // 2)
+        return n.reshape(shape), ks.reshape(*shape, 4)
     nt, kt, t, j = np.meshgrid(
         np.arange(N // 8), np.arange(KT), np.arange(32), np.arange(ikt // 2), indexing="ij"
     )
@@ -203,11 +220,11 @@ def _tile_index(N: int, K: int, ikt: int):
     return n, ks
 
 
-def pack_tile(q: np.ndarray, ikt: int) -> np.ndarray:
+def pack_tile(q: np.ndarray, ikt: int, fmt: str = "cuda") -> np.ndarray:
     """int [N, K] -> int32 tile tensor; bits 4i = q[n][ks_i], bits 16+4i = q[n][ks_i + 1]."""
     q = np.asarray(q, dtype=np.uint32)
     N, K = q.shape
-    n, ks = _tile_index(N, K, ikt)
+    n, ks = _tile_index(N, K, ikt, fmt)
     out = np.zeros(n.shape, dtype=np.uint32)
     for i in range(4):
         out |= q[n, ks[..., i]] << np.uint32(4 * i)
@@ -215,11 +232,11 @@ def pack_tile(q: np.ndarray, ikt: int) -> np.ndarray:
     return out.view(np.int32)
 
 
-def unpack_tile(p: np.ndarray, ikt: int) -> np.ndarray:
+def unpack_tile(p: np.ndarray, ikt: int, fmt: str = "cuda") -> np.ndarray:
     p = np.asarray(p).view(np.uint32)
     N = p.shape[0] * 8
     K = p.shape[1] * ikt * 16
-    n, ks = _tile_index(N, K, ikt)
+    n, ks = _tile_index(N, K, ikt, fmt)
     out = np.zeros((N, K), dtype=np.int32)
     for i in range(4):
         out[n, ks[..., i]] = (p >> np.uint32(4 * i)) & 0xF

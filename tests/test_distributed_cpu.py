@@ -91,3 +91,141 @@ def test_colwise_sharded_linear_gloo(world):
         assert ok_plain is True, f"rank {rank}: plain sharded forward mismatch ({ok_plain})"
         assert ok_q, f"rank {rank}: shard-then-quantize differs from quantize-then-slice"
         assert ok_int4, f"rank {rank}: sharded int4 forward differs from the unsharded oracle"
+
+
+def _tp_worker(rank, world, port, q, use_gpu):
+    """Megatron pairing on a SwiGLU MLP: w1 / w3 colwise (no gather) -> silu(a) * b on the local
+    columns -> w2 rowwise + all-reduce (reference test_affine_quantized_tensor_parallel.py:
+    65-80, 120-122). Local compute: the HIP kernels on cuda:0 (use_gpu) or the CPU oracle.
+    The gloo collectives run on CPU tensors."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "torchao-fork_amd"))
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import copy
+
+        import torch.nn.functional as F
+
+        from oracle import oracle
+        from torchao.distributed import (
+            ColwiseShardedLinear,
+            RowwiseShardedLinear,
+            shard_linear_colwise,
+            shard_linear_rowwise,
+            shard_wqkv_by_heads,
+        )
+        from torchao.quantization import Int4WeightOnlyConfig, quantize_
+
+        dev = torch.device("cuda", 0) if use_gpu else torch.device("cpu")
+        g, D, I = 32, 256, 512
+        torch.manual_seed(0)  # identical full weights on every rank
+        w1 = torch.nn.Linear(D, I, bias=False).to(torch.bfloat16)
+        w3 = torch.nn.Linear(D, I, bias=False).to(torch.bfloat16)
+        w2 = torch.nn.Linear(I, D, bias=True).to(torch.bfloat16)
+        x = torch.randn(1, D, dtype=torch.bfloat16)
+
+        # 1) plain bf16: pairing == unsharded up to the bf16 rounding of the partial sums
+        c1 = ColwiseShardedLinear(shard_linear_colwise(w1, rank, world), I, gather=False)
+        c3 = ColwiseShardedLinear(shard_linear_colwise(w3, rank, world), I, gather=False)
+        r2 = RowwiseShardedLinear(shard_linear_rowwise(w2, rank, world, g), I, w2.bias)
+        y_tp = r2(F.silu(c1(x)) * c3(x))
+        y_ref = w2(F.silu(w1(x)) * w3(x))
+        ok_plain = float((y_tp.float() - y_ref.float()).norm() / y_ref.float().norm()) < 1e-2
+
+        # 2) shard-then-quantize == quantize-then-slice, rowwise (groups along K align)
+        qfull = copy.deepcopy(w2)
+        quantize_(qfull, Int4WeightOnlyConfig(group_size=g))
+        qsh = shard_linear_rowwise(w2, rank, world, g)
+        quantize_(qsh, Int4WeightOnlyConfig(group_size=g))
+        k = I // world
+        fa, fb = qsh.weight.tensor_impl, qfull.weight.tensor_impl
+        ok_q = (torch.equal(fa.packed_weight, fb.packed_weight[:, rank * k // 8:(rank + 1) * k // 8])
+                and torch.equal(fa.scale_and_zero, fb.scale_and_zero[:, rank * k // g:(rank + 1) * k // g]))
+
+        # 3) int4 forward of the pair: local linears on the HIP kernels (or the oracle), the
+        # reduction exact against the sum of the gathered partials
+        mods = {}
+        for name, lin, mk in (("w1", w1, "col"), ("w3", w3, "col"), ("w2", w2, "row")):
+            sh = (shard_linear_colwise(lin, rank, world) if mk == "col"
+                  else shard_linear_rowwise(lin, rank, world, g))
+            quantize_(sh, Int4WeightOnlyConfig(group_size=g))
+            mods[name] = sh.to(dev)
+
+        def lin(m, t):
+            if use_gpu:
+                return F.linear(t.to(dev), m.weight).cpu()
+            qq, ss, zz = m.weight.tensor_impl.get_plain()
+            return oracle.int4_linear(t, qq, ss, zz, g)
+
+        a, b = lin(mods["w1"], x), lin(mods["w3"], x)
+        h = (F.silu(a.float()) * b.float()).to(torch.bfloat16)
+        part = lin(mods["w2"], h)
+        parts = [torch.empty_like(part) for _ in range(world)]
+        dist.all_gather(parts, part)
+        red = part.clone()
+        dist.all_reduce(red)
+        manual = parts[0].clone()
+        for p_ in parts[1:]:
+            manual = manual + p_
+        ok_reduce = torch.equal(red, manual)
+        # against the unsharded int4 MLP through the oracle (the CPU dequant path)
+        full = {}
+        for name, lin_ in (("w1", w1), ("w3", w3), ("w2", w2)):
+            m = copy.deepcopy(lin_)
+            quantize_(m, Int4WeightOnlyConfig(group_size=g))
+            full[name] = m.weight.tensor_impl.get_plain()
+        fa_ = oracle.int4_linear(x, *full["w1"], g)
+        fb_ = oracle.int4_linear(x, *full["w3"], g)
+        yref = oracle.int4_linear((F.silu(fa_.float()) * fb_.float()).to(torch.bfloat16),
+                                  *full["w2"], g)
+        ok_int4 = float((red.float() - yref.float()).norm() / yref.float().norm()) < 2e-2
+
+        # 4) head-wise wqkv shard: rank r holds its q, k and v heads
+        H, Hkv, hd = 4, 2, 16
+        wqkv = torch.nn.Linear(64, (H + 2 * Hkv) * hd, bias=False)
+        sq = shard_wqkv_by_heads(wqkv, H, Hkv, hd, rank, world)
+        hq, hk = H // world, Hkv // world
+        W = wqkv.weight.detach()
+        want = torch.cat([W[rank * hq * hd:(rank + 1) * hq * hd],
+                          W[H * hd + rank * hk * hd:H * hd + (rank + 1) * hk * hd],
+                          W[(H + Hkv) * hd + rank * hk * hd:(H + Hkv) * hd + (rank + 1) * hk * hd]])
+        ok_heads = torch.equal(sq.weight, want)
+        q.put((rank, ok_plain, ok_q, ok_reduce and ok_int4, ok_heads))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()[-800:], False, False, False))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_tp(world, use_gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q, use_gpu)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok_plain, ok_q, ok_int4, ok_heads in sorted(results, key=lambda r: r[0]):
+        assert ok_plain is True, f"rank {rank}: bf16 colwise->rowwise pairing ({ok_plain})"
+        assert ok_q, f"rank {rank}: rowwise shard-then-quantize != quantize-then-slice"
+        assert ok_int4, f"rank {rank}: int4 pair forward / reduction mismatch"
+        assert ok_heads, f"rank {rank}: head-wise wqkv shard rows"
+
+
+def test_tp_colwise_rowwise_pairing_gloo():
+    _run_tp(2, use_gpu=False)
+
+
+@pytest.mark.gpu
+def test_tp_pairing_hip_local_compute_gloo():
+    """The same pairing with each rank's local linears on the HIP kernels (both ranks on the one
+    GPU of the box, gloo collectives on host copies)."""
+    _run_tp(2, use_gpu=True)

@@ -316,3 +316,82 @@ def test_fake_impl_rejects_bad_group_size():
         sz = torch.empty(512, 64, 2, dtype=torch.bfloat16, device="cuda")
         with pytest.raises(Exception, match="qGroupSize"):
             torch.ops.torchao.int4_weight_only_linear(x, pw, sz, 48, None)
+
+
+def _reference_tile_state(N, K, g, ikt, fmt, seed):
+    """A state dict as the reference's TensorCoreTiledLayout writes it (same class paths): the
+    weight padded to K -> 1024, N -> 8 (tensor_core_tiled_layout.py:127-188), nibbles in the
+    tile format of `fmt`, scales/zeros in tinygemm [Kp/g, Np, 2] order (quantization/
+    utils.py:395-409). Padding rows / k hold arbitrary nibbles (dropped on load)."""
+    from torchao.dtypes import AffineQuantizedTensor
+    from torchao.dtypes.uintx.tensor_core_tiled_layout import (
+        TensorCoreTiledAQTTensorImpl,
+        TensorCoreTiledLayout,
+    )
+    from torchao.quantization.quant_primitives import ZeroPointDomain
+
+    w = oracle.make_linear_weight(N, K, seed=seed)
+    s, z = oracle.int4_qparams(w, g)
+    q = oracle.int4_quantize(w, s, z, g)
+    Kp = -(-K // 1024) * 1024
+    Np = -(-N // (16 if fmt == "rocm" else 8)) * (16 if fmt == "rocm" else 8)
+    rng = np.random.default_rng(seed)
+    qp = rng.integers(0, 16, size=(Np, Kp), dtype=np.int32)
+    qp[:N, :K] = q.numpy()
+    sp = torch.ones(Np, Kp // g, dtype=torch.bfloat16)
+    zp = torch.zeros(Np, Kp // g, dtype=torch.bfloat16)
+    sp[:N, :K // g], zp[:N, :K // g] = s, z
+    tile = torch.from_numpy(oracle.pack_tile(qp, ikt, fmt))
+    sz_tiny = torch.stack([sp, zp], -1).transpose(0, 1).contiguous()
+    impl = TensorCoreTiledAQTTensorImpl(tile, sz_tiny, False, TensorCoreTiledLayout(ikt))
+    aqt = AffineQuantizedTensor(impl, (1, g), torch.Size([N, K]), 0, 15, ZeroPointDomain.FLOAT,
+                                dtype=torch.bfloat16)
+    return {"weight": aqt}, w, q, s, z
+
+
+@pytest.mark.parametrize("fmt,N,K,g,ikt", [("cuda", 40, 352, 32, 8), ("rocm", 48, 352, 32, 8),
+                                           ("cuda", 64, 2048, 64, 4), ("rocm", 64, 2048, 128, 2)])
+def test_reference_tile_checkpoint_loads_bit_exact(fmt, N, K, g, ikt):
+    """F1 / ADVICE r1: a torchao TensorCoreTiledLayout state dict (tile-format nibbles, [Kp/g,
+    Np, 2] scales) loads with torch.load(weights_only=True) + load_state_dict(assign=True) into
+    the gfx950 layout bit-exactly, un-padded to the logical [N, K]."""
+    import torchao.ops as tops
+
+    sd, w, q, s, z = _reference_tile_state(N, K, g, ikt, fmt, seed=N + K)
+    buf = io.BytesIO()
+    torch.save(sd, buf)
+    buf.seek(0)
+    prev = tops.default_tile_format()
+    tops.set_default_tile_format(fmt)
+    try:
+        loaded = torch.load(buf, weights_only=True)
+    finally:
+        tops.set_default_tile_format(prev)
+    lin = torch.nn.Linear(K, N, bias=False, dtype=torch.bfloat16)
+    quantize_(lin, Int4WeightOnlyConfig(group_size=g))
+    lin.load_state_dict(loaded, assign=True)
+    impl = lin.weight.tensor_impl
+    assert tuple(impl.packed_weight.shape) == (N, K // 8)
+    assert tuple(impl.scale_and_zero.shape) == (N, K // g, 2)
+    qq, ss, zz = impl.get_plain()
+    assert torch.equal(qq, q) and torch.equal(ss, s) and torch.equal(zz, z)
+    assert torch.equal(lin.weight.dequantize(), oracle.int4_dequantize(q, s, z, g))
+    # the same checkpoint into an existing quantized weight through copy_ (no assign)
+    lin2 = torch.nn.Linear(K, N, bias=False, dtype=torch.bfloat16)
+    quantize_(lin2, Int4WeightOnlyConfig(group_size=g))
+    lin2.load_state_dict(loaded)
+    assert torch.equal(lin2.weight.tensor_impl.packed_weight, impl.packed_weight)
+
+
+def test_reference_tile_checkpoint_wrong_map_is_not_silent():
+    """Reading a CUDA-written checkpoint with the ROCm map scrambles nibbles: the maps differ, so
+    the format must be chosen (torchao.ops.set_default_tile_format), never guessed."""
+    sd, w, q, s, z = _reference_tile_state(48, 1024, 32, 8, "cuda", seed=5)
+    from torchao.dtypes.uintx.tensor_core_tiled_layout import convert_from_tensor_core_tiled
+
+    impl = sd["weight"].tensor_impl
+    good, _ = convert_from_tensor_core_tiled(impl.packed_weight, impl.scale_and_zero, 8,
+                                             (48, 1024), "cuda")
+    bad, _ = convert_from_tensor_core_tiled(impl.packed_weight, impl.scale_and_zero, 8,
+                                            (48, 1024), "rocm")
+    assert torch.equal(good, torch.ops.torchao.int4_pack(q)) and not torch.equal(good, bad)

@@ -99,3 +99,51 @@ def test_tile_layout_index_math_hand_checked():
     p = oracle.pack_tile(q, 2).view(np.uint32)
     # bits 4i = q[ks_i], bits 16+4i = q[ks_i + 1]
     assert int(p[0, 0, 5, 0]) == (1 | 3 << 4 | 5 << 8 | 7 << 12 | 2 << 16 | 4 << 20 | 6 << 24 | 8 << 28)
+
+
+def test_rocm_tile_map_matches_aten_fixture():
+    """oracle.pack_tile(fmt="rocm") against the nibble map PyTorch-ROCm's
+    aten._convert_weight_to_int4pack produced on the MI355X (experiments/probe_aten_tile_map.py
+    -> tests/golden/aten_tile_map_rocm.npz): every nibble of 15 (N, K, inner_k_tiles) cases."""
+    m = load_golden("aten_tile_map_rocm.npz")
+    assert len(m.files) == 15
+    for key in m.files:
+        N = int(key.split("_")[0][1:])
+        K = int(key.split("_")[1][1:])
+        ikt = int(key.split("ikt")[1])
+        idx = np.arange(N * K, dtype=np.int64).reshape(N, K)
+        # pack the flat index 4 bits at a time, exactly as the probe did, and rebuild the map
+        got = np.zeros(m[key].shape, dtype=np.int64)
+        for p4 in range((int(N * K - 1).bit_length() + 3) // 4):
+            packed = oracle.pack_tile((idx >> (4 * p4)) & 0xF, ikt, "rocm").view(np.uint32)
+            nib = np.stack([(packed >> np.uint32(4 * i)) & 0xF for i in range(8)], -1)
+            got |= nib.astype(np.int64) << (4 * p4)
+        np.testing.assert_array_equal(got, m[key].astype(np.int64), err_msg=key)
+
+
+@pytest.mark.parametrize("ikt", [2, 4, 8])
+def test_rocm_tile_roundtrip(ikt):
+    rng = np.random.default_rng(ikt + 100)
+    N, K = 48, ikt * 16 * 3
+    q = rng.integers(0, 16, size=(N, K), dtype=np.int32)
+    p = oracle.pack_tile(q, ikt, "rocm")
+    assert p.shape == (N // 8, K // (ikt * 16), 32, ikt // 2)
+    np.testing.assert_array_equal(oracle.unpack_tile(p, ikt, "rocm"), q)
+    assert not np.array_equal(p, oracle.pack_tile(q, ikt, "cuda"))
+
+
+def test_llama_oracle_matches_reference_model():
+    """oracle/llama_ref.py (the config-4 tolerance anchor) against the reference gpt-fast
+    Transformer's own fp32 logits (oracle/gen_golden_llama.py): a 10-token prefill and two KV-
+    cache decode steps of a 2-layer GQA model."""
+    from oracle import llama_ref
+
+    rec = load_golden("llama_tiny_fp32.npz")
+    W = {k[2:]: bf16(rec[k]).float() for k in rec.files if k.startswith("w:")}
+    n_layer, n_head, n_kv, base = rec["config"]
+    tokens = torch.from_numpy(rec["tokens"]).long()
+    logits = llama_ref.llama_forward_fp32(W, int(n_layer), int(n_head), int(n_kv), float(base),
+                                          1e-5, tokens)
+    ref = torch.from_numpy(rec["logits"])
+    assert logits.shape == ref.shape
+    torch.testing.assert_close(logits, ref, rtol=2e-5, atol=2e-5)

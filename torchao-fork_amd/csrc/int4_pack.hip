@@ -101,35 +101,55 @@ __global__ void int4_dequant_kernel(const uint32_t* __restrict__ packed,
   }
 }
 
-// ---- reference tile format [N/8][K/(ikt*16)][32][ikt/2] ------------------------------------
-// For P[nt][kt][t][j]: n = 8nt + t/4; kb0 = (kt*ikt + 2j)*16; ks = {kb0+2(t%4), +8,
-// kb0+16+2(t%4), +8}; bits 4i hold q[n][ks_i], bits 16+4i hold q[n][ks_i + 1]
-// (semantics of tensor_core_tiled_layout.cu:131-215).
-__device__ __forceinline__ void tile_coords(int64_t idx, int ikt, int64_t KT, int64_t K,
-                                            int64_t* n, int64_t* kb, int* t4) {
+// ---- reference tile format: [N/8][K/(ikt*16)][32][ikt/2] int32, two nibble maps --------------
+// fmt 0 (kTileCuda), the semantics of the reference's unpack kernel
+//   (tensor_core_tiled_layout.cu:131-215): P[nt][kt][t][j]: n = 8nt + t/4;
+//   kb0 = (kt*ikt + 2j)*16; ks = {kb0+2(t%4), +8, kb0+16+2(t%4), +8}.
+// fmt 1 (kTileRocm), what PyTorch-ROCm's aten._convert_weight_to_int4pack writes on gfx950
+//   (recovered on the box by experiments/probe_aten_tile_map.py, pinned by
+//   tests/golden/aten_tile_map_rocm.npz): the same bytes seen flat as [N/16][K/(ikt*16)][64][ikt/2]
+//   for wave64 lanes l: n = 16nb + l%16; b = kb*ikt*16 + 32j + 4(l/16); ks = {b, b+2, b+16, b+18}.
+// Both: bits 4i hold q[n][ks_i], bits 16+4i hold q[n][ks_i + 1].
+constexpr int kTileCuda = 0, kTileRocm = 1;
+
+__device__ __host__ __forceinline__ void tile_coords(int64_t idx, int ikt, int64_t KT, int fmt,
+                                                     int64_t* n, int64_t ks[4]) {
   const int half = ikt / 2;
   const int j = (int)(idx % half);
   int64_t r = idx / half;
-  const int t = (int)(r % 32);
-  r /= 32;
-  const int64_t kt = r % KT;
-  const int64_t nt = r / KT;
-  *n = nt * 8 + t / 4;
-  *kb = (kt * ikt + 2 * j) * 16;
-  *t4 = t % 4;
+  if (fmt == kTileRocm) {
+    const int l = (int)(r % 64);
+    r /= 64;
+    const int64_t kb = r % KT, nb = r / KT;
+    *n = nb * 16 + l % 16;
+    const int64_t b = kb * ikt * 16 + 32 * j + 4 * (l / 16);
+    ks[0] = b;
+    ks[1] = b + 2;
+    ks[2] = b + 16;
+    ks[3] = b + 18;
+  } else {
+    const int t = (int)(r % 32);
+    r /= 32;
+    const int64_t kt = r % KT, nt = r / KT;
+    *n = nt * 8 + t / 4;
+    const int64_t kb = (kt * ikt + 2 * j) * 16;
+    const int t4 = t % 4;
+    ks[0] = kb + 2 * t4;
+    ks[1] = kb + 2 * t4 + 8;
+    ks[2] = kb + 16 + 2 * t4;
+    ks[3] = kb + 16 + 2 * t4 + 8;
+  }
 }
 
 template <int OUT>  // 0: int32 unpack, 1: bf16 dequant
 __global__ void tile_unpack_kernel(const int32_t* __restrict__ in, void* __restrict__ out,
                                    const uint16_t* __restrict__ sz, int64_t total, int ikt,
-                                   int64_t KT, int64_t N, int64_t K, int g) {
+                                   int64_t KT, int64_t N, int64_t K, int g, int fmt) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t n, kb;
-    int t4;
-    tile_coords(i, ikt, KT, K, &n, &kb, &t4);
+    int64_t n, ks[4];
+    tile_coords(i, ikt, KT, fmt, &n, ks);
     const uint32_t p = (uint32_t)in[i];
-    int64_t ks[4] = {kb + 2 * t4, kb + 2 * t4 + 8, kb + 16 + 2 * t4, kb + 16 + 2 * t4 + 8};
     if (OUT == 0) {
       int32_t* o = reinterpret_cast<int32_t*>(out) + n * K;
 #pragma unroll
@@ -138,7 +158,7 @@ __global__ void tile_unpack_kernel(const int32_t* __restrict__ in, void* __restr
             make_int2((p >> (4 * q)) & 0xF, (p >> (16 + 4 * q)) & 0xF);
       }
     } else {
-      const int64_t grp = ks[0] / g;  // one group covers the 32 k of this pair of k-tiles
+      const int64_t grp = ks[0] / g;  // the 4 pairs lie in one 32-k window: one group
       const uint16_t* psz = sz + (grp * N + n) * 2;
       const float s = bf16_to_f32(psz[0]), z = bf16_to_f32(psz[1]);
       uint16_t* o = reinterpret_cast<uint16_t*>(out) + n * K;
@@ -153,14 +173,12 @@ __global__ void tile_unpack_kernel(const int32_t* __restrict__ in, void* __restr
 }
 
 __global__ void tile_pack_kernel(const int32_t* __restrict__ q, int32_t* __restrict__ out,
-                                 int64_t total, int ikt, int64_t KT, int64_t K) {
+                                 int64_t total, int ikt, int64_t KT, int64_t K, int fmt) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t n, kb;
-    int t4;
-    tile_coords(i, ikt, KT, K, &n, &kb, &t4);
+    int64_t n, ks[4];
+    tile_coords(i, ikt, KT, fmt, &n, ks);
     const int32_t* row = q + n * K;
-    int64_t ks[4] = {kb + 2 * t4, kb + 2 * t4 + 8, kb + 16 + 2 * t4, kb + 16 + 2 * t4 + 8};
     uint32_t p = 0;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -247,55 +265,82 @@ int tao_int4_dequant(const uint32_t* packed, const uint16_t* sz, uint16_t* w, in
   return check_launch("int4_dequant_kernel");
 }
 
-static int check_tile_args(int64_t N, int64_t K, int64_t ikt, const char* who) {
+static int check_tile_args(int64_t N, int64_t K, int64_t ikt, int fmt, const char* who) {
   TAO_CHECK_ARG(ikt == 2 || ikt == 4 || ikt == 8, "%s: inner_k_tiles must be 2, 4, or 8", who);
-  TAO_CHECK_ARG(N >= 0 && N % 8 == 0, "%s: N (%lld) must be a multiple of 8", who, (long long)N);
+  TAO_CHECK_ARG(fmt == kTileCuda || fmt == kTileRocm, "%s: tile_format must be 0 or 1", who);
+  const int nm = fmt == kTileRocm ? 16 : 8;
+  TAO_CHECK_ARG(N >= 0 && N % nm == 0, "%s: N (%lld) must be a multiple of %d", who, (long long)N,
+                nm);
   TAO_CHECK_ARG(K >= 0 && K % (ikt * 16) == 0, "%s: K (%lld) must be a multiple of %lld", who,
                 (long long)K, (long long)(ikt * 16));
   return TAO_OK;
 }
 
 int tao_unpack_tensor_core_tiled_layout(const int32_t* packed_w, int32_t* out, int64_t N,
-                                        int64_t K, int64_t inner_k_tiles, void* stream) {
-  int rc = check_tile_args(N, K, inner_k_tiles, "unpack_tensor_core_tiled_layout");
+                                        int64_t K, int64_t inner_k_tiles, int tile_format,
+                                        void* stream) {
+  int rc = check_tile_args(N, K, inner_k_tiles, tile_format, "unpack_tensor_core_tiled_layout");
   if (rc) return rc;
   if (N * K == 0) return TAO_OK;
   const int64_t KT = K / (inner_k_tiles * 16);
-  const int64_t total = (N / 8) * KT * 32 * (inner_k_tiles / 2);
-  launch(tile_unpack_kernel<0>, dim3(grid_for(total)), dim3(kBlock), 0,
-                     as_stream(stream), packed_w, (void*)out, (const uint16_t*)nullptr, total,
-                     (int)inner_k_tiles, KT, N, K, 32);
+  const int64_t total = N * K / 8;
+  launch(tile_unpack_kernel<0>, dim3(grid_for(total)), dim3(kBlock), 0, as_stream(stream),
+         packed_w, (void*)out, (const uint16_t*)nullptr, total, (int)inner_k_tiles, KT, N, K, 32,
+         tile_format);
   return check_launch("tile_unpack_kernel");
 }
 
 int tao_dequantize_tensor_core_tiled_layout(const int32_t* packed_w,
                                             const uint16_t* scales_and_zeros, uint16_t* out,
                                             int64_t N, int64_t K, int64_t group_size,
-                                            int64_t inner_k_tiles, void* stream) {
-  int rc = check_tile_args(N, K, inner_k_tiles, "dequantize_tensor_core_tiled_layout");
+                                            int64_t inner_k_tiles, int tile_format,
+                                            void* stream) {
+  int rc = check_tile_args(N, K, inner_k_tiles, tile_format,
+                           "dequantize_tensor_core_tiled_layout");
   if (rc) return rc;
   TAO_CHECK_ARG(gshift_of(group_size) > 0,
                 "dequantize_tensor_core_tiled_layout: qGroupSize must be 32, 64, 128, or 256");
   TAO_CHECK_ARG(K % group_size == 0, "dequantize_tensor_core_tiled_layout: K %% group_size != 0");
   if (N * K == 0) return TAO_OK;
   const int64_t KT = K / (inner_k_tiles * 16);
-  const int64_t total = (N / 8) * KT * 32 * (inner_k_tiles / 2);
-  launch(tile_unpack_kernel<1>, dim3(grid_for(total)), dim3(kBlock), 0,
-                     as_stream(stream), packed_w, (void*)out, scales_and_zeros, total,
-                     (int)inner_k_tiles, KT, N, K, (int)group_size);
+  const int64_t total = N * K / 8;
+  launch(tile_unpack_kernel<1>, dim3(grid_for(total)), dim3(kBlock), 0, as_stream(stream),
+         packed_w, (void*)out, scales_and_zeros, total, (int)inner_k_tiles, KT, N, K,
+         (int)group_size, tile_format);
   return check_launch("tile_dequant_kernel");
 }
 
 int tao_pack_tensor_core_tiled_layout(const int32_t* q, int32_t* packed_w, int64_t N, int64_t K,
-                                      int64_t inner_k_tiles, void* stream) {
-  int rc = check_tile_args(N, K, inner_k_tiles, "pack_tensor_core_tiled_layout");
+                                      int64_t inner_k_tiles, int tile_format, void* stream) {
+  int rc = check_tile_args(N, K, inner_k_tiles, tile_format, "pack_tensor_core_tiled_layout");
   if (rc) return rc;
   if (N * K == 0) return TAO_OK;
   const int64_t KT = K / (inner_k_tiles * 16);
-  const int64_t total = (N / 8) * KT * 32 * (inner_k_tiles / 2);
-  launch(tile_pack_kernel, dim3(grid_for(total)), dim3(kBlock), 0, as_stream(stream),
-                     q, packed_w, total, (int)inner_k_tiles, KT, K);
+  const int64_t total = N * K / 8;
+  launch(tile_pack_kernel, dim3(grid_for(total)), dim3(kBlock), 0, as_stream(stream), q,
+         packed_w, total, (int)inner_k_tiles, KT, K, tile_format);
   return check_launch("tile_pack_kernel");
+}
+
+// Host unpack of either tile format (checkpoints loaded on the CPU, tensor_core_tiled_layout.py)
+int tao_unpack_tensor_core_tiled_layout_host(const int32_t* packed_w, int32_t* out, int64_t N,
+                                             int64_t K, int64_t inner_k_tiles,
+                                             int tile_format) {
+  int rc = check_tile_args(N, K, inner_k_tiles, tile_format,
+                           "unpack_tensor_core_tiled_layout (host)");
+  if (rc) return rc;
+  const int64_t KT = K / (inner_k_tiles * 16);
+  const int64_t total = N * K / 8;
+  for (int64_t i = 0; i < total; ++i) {
+    int64_t n, ks[4];
+    tile_coords(i, (int)inner_k_tiles, KT, tile_format, &n, ks);
+    const uint32_t p = (uint32_t)packed_w[i];
+    for (int q = 0; q < 4; ++q) {
+      out[n * K + ks[q]] = (int32_t)((p >> (4 * q)) & 0xF);
+      out[n * K + ks[q] + 1] = (int32_t)((p >> (16 + 4 * q)) & 0xF);
+    }
+  }
+  return TAO_OK;
 }
 
 }  // extern "C"

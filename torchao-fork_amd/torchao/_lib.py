@@ -50,9 +50,10 @@ _SIGNATURES = {
     "tao_int4_dequant": [_p, _p, _p, _i64, _i64, _i64, _int, _p],
     "tao_int4_pack_host": [_p, _p, _i64, _i64],
     "tao_int4_unpack_host": [_p, _p, _i64, _i64],
-    "tao_unpack_tensor_core_tiled_layout": [_p, _p, _i64, _i64, _i64, _p],
-    "tao_dequantize_tensor_core_tiled_layout": [_p, _p, _p, _i64, _i64, _i64, _i64, _p],
-    "tao_pack_tensor_core_tiled_layout": [_p, _p, _i64, _i64, _i64, _p],
+    "tao_unpack_tensor_core_tiled_layout": [_p, _p, _i64, _i64, _i64, _int, _p],
+    "tao_unpack_tensor_core_tiled_layout_host": [_p, _p, _i64, _i64, _i64, _int],
+    "tao_dequantize_tensor_core_tiled_layout": [_p, _p, _p, _i64, _i64, _i64, _i64, _int, _p],
+    "tao_pack_tensor_core_tiled_layout": [_p, _p, _i64, _i64, _i64, _int, _p],
     "tao_int8wo_linear_bf16": [_p, _p, _p, _p, _p, _i64, _i64, _i64, _p],
     "tao_int8_quant_per_token": [_p, _p, _p, _i64, _i64, _p],
     "tao_int8_scaled_mm_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p],

@@ -10,8 +10,12 @@ replicated input, c10d all-gather). Here it is explicit and graph-capturable:
   rank only ever materialises its own shard);
 * forward: local linear (the gfx950 int4/int8 kernels via the AQT dispatch), then one
   ``all_gather_into_tensor`` of the bf16 output over the group (RCCL over xGMI with backend
-  "nccl"; gloo for CPU tests). The result is bit-identical to the unsharded linear because
-  the reduction order of a column does not depend on P.
+  "nccl"; gloo for CPU tests), or no gather (``gather=False``) when a rowwise linear consumes
+  the local columns (rowwise.py). Each output column is one row's dot product, computed by the
+  same kernel math whatever P is, but the GEMV picks its launch shape (waves along K, rows per
+  wave) from the local N, which can re-associate a column's fp32 sum: the gathered result
+  agrees with the unsharded linear to one bf16 rounding (tests/test_gpu_configs.py, config 5),
+  and is bit-identical wherever the shard's launch shape equals the full one.
 """
 
 from typing import Callable, Optional
@@ -49,19 +53,20 @@ class ColwiseShardedLinear(nn.Module):
     """Wraps this rank's shard (``self.local``, an nn.Linear whose weight may be quantized)."""
 
     def __init__(self, local: nn.Linear, out_features: int, group=None,
-                 local_fn: Optional[Callable] = None):
+                 local_fn: Optional[Callable] = None, gather: bool = True):
         super().__init__()
         self.local = local
         self.out_features = out_features
         self.in_features = local.in_features
         self.group = group
+        self.gather = gather
         # local_fn(x, weight, bias) -> y_local; default F.linear (AQT dispatch -> HIP kernels)
         self.local_fn = local_fn or F.linear
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         y = self.local_fn(x, self.local.weight, self.local.bias)
         _, world = _group_info(self.group)
-        if world == 1:
+        if world == 1 or not self.gather:
             return y
         return all_gather_columns(y, self.out_features, self.group)
 

@@ -96,6 +96,13 @@ def _fused_weight_quant(x, mapping_type, block_size, target_dtype, quant_min, qu
     return None
 
 
+def _adopt_loaded_impl(impl, shape):
+    """A layout impl may recognise storage written by another build and convert it
+    (``_adopt(shape)``, e.g. the reference's int4 tile format); others pass through."""
+    adopt = getattr(type(impl), "_adopt", None)
+    return impl if adopt is None else adopt(impl, tuple(shape))
+
+
 class AffineQuantizedTensor(TorchAOBaseTensor):
     """float_tensor ~= dequantize(tensor_impl) with qparams shared over ``block_size`` blocks.
 
@@ -203,8 +210,10 @@ class AffineQuantizedTensor(TorchAOBaseTensor):
     @classmethod
     def __tensor_unflatten__(cls, tensor_data_dict, tensor_attributes, outer_size, outer_stride):
         block_size, shape, quant_min, quant_max, zero_point_domain, dtype = tensor_attributes
+        impl = _adopt_loaded_impl(tensor_data_dict["tensor_impl"],
+                                  shape if outer_size is None else outer_size)
         return cls(
-            tensor_data_dict["tensor_impl"],
+            impl,
             block_size,
             shape if outer_size is None else outer_size,
             quant_min,
@@ -213,6 +222,13 @@ class AffineQuantizedTensor(TorchAOBaseTensor):
             dtype=dtype,
             strides=outer_stride,
         )
+
+    def __setstate__(self, state):
+        """Unpickling (torch.load): restore the fields, then let the layout adopt storage that
+        another build wrote (a reference TensorCoreTiledLayout checkpoint holds the tile format;
+        tensor_core_tiled_layout.convert_from_tensor_core_tiled)."""
+        torch._utils._set_obj_state(self, state)
+        self.tensor_impl = _adopt_loaded_impl(self.tensor_impl, self.shape)
 
     @classmethod
     def from_hp_to_intx(

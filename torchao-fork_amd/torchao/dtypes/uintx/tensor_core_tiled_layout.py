@@ -37,7 +37,8 @@ from torchao.utils import fill_defaults
 
 aten = torch.ops.aten
 
-__all__ = ["TensorCoreTiledLayout", "TensorCoreTiledAQTTensorImpl"]
+__all__ = ["TensorCoreTiledLayout", "TensorCoreTiledAQTTensorImpl",
+           "convert_from_tensor_core_tiled"]
 
 
 def _aqt_is_tensor_core_tile_uint4(aqt) -> bool:
@@ -78,6 +79,53 @@ def _linear_bf16_act_uint4_weight_impl(input_tensor, weight_tensor, bias):
         bias,
     )
     return y.to(orig_dtype)
+
+
+def _is_tile_storage(packed_weight: torch.Tensor) -> bool:
+    """The reference's storage: int32 [(E,) N/8, K/(ikt*16), 32, ikt/2] (tensor_core_tiled_layout.py
+    docstring, :191-211); the gfx950 row-stream storage is [(E,) N, K/8]."""
+    return packed_weight.dim() in (4, 5) and packed_weight.shape[-2] == 32
+
+
+def convert_from_tensor_core_tiled(
+    packed_weight: torch.Tensor,
+    scale_and_zero: torch.Tensor,
+    inner_k_tiles: int,
+    shape: Optional[Tuple[int, ...]] = None,
+    tile_format=-1,
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Reference ``TensorCoreTiledAQTTensorImpl`` storage -> this layout's storage.
+
+    ``packed_weight`` int32 [(E,) Np/8, Kp/(ikt*16), 32, ikt/2] in the tile format (``tile_format``:
+    "cuda" for a checkpoint written by a CUDA build, "rocm" for one written by PyTorch-ROCm; -1 =
+    ``torchao.ops.default_tile_format()``), ``scale_and_zero`` bf16 [(E,) Kp/g, Np, 2] (tinygemm
+    packing, reference quantization/utils.py:395-409). Returns row-stream ``packed_weight``
+    [(E,) N, K/8] and ``scale_and_zero`` [(E,) N, K/g, 2], un-padded to ``shape``'s trailing
+    (N, K) (the reference pads K to 1024 and N to 8, tensor_core_tiled_layout.py:127-188).
+    Bit-exact: nibbles are moved, scales and zeros copied. Runs on the tensors' device (HIP
+    kernels on GPU, host C++ on CPU)."""
+    from torchao.ops import unpack_tensor_core_tiled_layout
+
+    lead = packed_weight.shape[:-4]
+    Np = packed_weight.shape[-4] * 8
+    Kp = packed_weight.shape[-3] * inner_k_tiles * 16
+    N, K = (Np, Kp) if shape is None else (int(shape[-2]), int(shape[-1]))
+    if N > Np or K > Kp:
+        raise ValueError(f"tile storage [{Np}, {Kp}] smaller than the logical shape {(N, K)}")
+    if scale_and_zero.shape[-3:-1] != (scale_and_zero.shape[-3], Np) or scale_and_zero.shape[-1] != 2:
+        raise ValueError(f"scale_and_zero {tuple(scale_and_zero.shape)} is not [Kp/g, {Np}, 2]")
+    groups_p = scale_and_zero.shape[-3]
+    g = Kp // groups_p
+    if g * groups_p != Kp or K % g:
+        raise ValueError(f"group size {Kp}/{groups_p} does not divide K={K}")
+    pw = packed_weight.reshape(-1, *packed_weight.shape[-4:])
+    rows = []
+    for e in range(pw.shape[0]):
+        q = unpack_tensor_core_tiled_layout(pw[e].contiguous(), inner_k_tiles, tile_format)
+        rows.append(torch.ops.torchao.int4_pack(q[:N, :K].contiguous()))
+    packed = torch.stack(rows).reshape(*lead, N, K // 8)
+    sz = scale_and_zero.transpose(-3, -2)[..., :N, : K // g, :].contiguous()
+    return packed, sz
 
 
 @dataclass(frozen=True)
@@ -131,6 +179,18 @@ class TensorCoreTiledAQTTensorImpl(AQTTensorImpl):
 
     def __tensor_flatten__(self):
         return ["packed_weight", "scale_and_zero"], [self.transposed, self._layout]
+
+    @classmethod
+    def _adopt(cls, impl, shape):
+        """Called when an AQT is unpickled / unflattened with this impl (AffineQuantizedTensor
+        .__setstate__): storage in the reference tile format (a torchao checkpoint) is converted
+        to the gfx950 row-stream layout, un-padded to the AQT's logical ``shape``; storage of
+        this layout is returned as is."""
+        if not _is_tile_storage(impl.packed_weight):
+            return impl
+        packed, sz = convert_from_tensor_core_tiled(
+            impl.packed_weight, impl.scale_and_zero, impl._layout.inner_k_tiles, shape)
+        return cls(packed, sz, impl.transposed, impl._layout)
 
     @classmethod
     def __tensor_unflatten__(cls, tensor_data_dict, tensor_attributes, outer_size, outer_stride):

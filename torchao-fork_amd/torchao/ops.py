@@ -9,9 +9,11 @@ allocator), no host synchronisation, so every op is hipGraph-capturable.
 
 Operators:
   * ``unpack_tensor_core_tiled_layout`` / ``dequantize_tensor_core_tiled_layout`` — the
-    reference schemas (ops.py:16-21), on the reference tile format.
-  * ``pack_tensor_core_tiled_layout`` — inverse of the unpack (the tile format that
-    ``aten._convert_weight_to_int4pack`` produces), for checkpoint interchange.
+    reference schemas (ops.py:16-21) on the reference tile format, with an optional
+    ``tile_format``: the CUDA nibble map of the reference's .cu kernels, or the one PyTorch-ROCm's
+    ``aten._convert_weight_to_int4pack`` writes (the default on ROCm builds).
+  * ``pack_tensor_core_tiled_layout`` — inverse of the unpack (bit-identical to
+    ``aten._convert_weight_to_int4pack`` in the ROCm map), for checkpoint interchange.
   * ``int4_pack`` / ``int4_unpack`` / ``int4_dequantize`` / ``int4_weight_only_linear`` — the
     gfx950 row-stream int4 layout; ``int4_weight_only_linear`` replaces
     ``aten._weight_int4pack_mm`` (tensor_core_tiled_layout.py:104).
@@ -33,12 +35,20 @@ from torch import Tensor
 from torchao import _lib
 
 lib = torch.library.Library("torchao", "FRAGMENT")
-lib.define("unpack_tensor_core_tiled_layout(Tensor packed_w, int inner_k_tiles) -> Tensor")
+# The reference schemas (ops.py:16-21) plus an optional trailing tile_format (-1 = this
+# platform's aten format, see default_tile_format), so the reference's positional calls bind.
+lib.define(
+    "unpack_tensor_core_tiled_layout(Tensor packed_w, int inner_k_tiles, int tile_format=-1) "
+    "-> Tensor"
+)
 lib.define(
     "dequantize_tensor_core_tiled_layout(Tensor packed_w, Tensor scales_and_zeros, "
-    "int group_size, int inner_k_tiles) -> Tensor"
+    "int group_size, int inner_k_tiles, int tile_format=-1) -> Tensor"
 )
-lib.define("pack_tensor_core_tiled_layout(Tensor int_data, int inner_k_tiles) -> Tensor")
+lib.define(
+    "pack_tensor_core_tiled_layout(Tensor int_data, int inner_k_tiles, int tile_format=-1) "
+    "-> Tensor"
+)
 lib.define("int4_pack(Tensor int_data) -> Tensor")
 lib.define("int4_pack_u8(Tensor int_data_u8) -> Tensor")
 lib.define("int4_unpack(Tensor packed_w) -> Tensor")
@@ -82,6 +92,39 @@ def _require_contig(t: Tensor, name: str):
 # ---------------------------------------------------------------------------------------------
 # reference tile format (torchao/ops.py:255-377)
 # ---------------------------------------------------------------------------------------------
+TILE_FORMAT_CUDA = 0  # tensor_core_tiled_layout.cu:131-215 (aten on CUDA builds)
+TILE_FORMAT_ROCM = 1  # aten._convert_weight_to_int4pack on PyTorch-ROCm (wave64 lanes)
+_default_tile_format = TILE_FORMAT_ROCM if torch.version.hip else TILE_FORMAT_CUDA
+
+
+def default_tile_format() -> int:
+    """The nibble map ``aten._convert_weight_to_int4pack`` writes on this PyTorch build (both
+    share the tile tensor's shape; include/torchao_mi355x.h documents the two maps)."""
+    return _default_tile_format
+
+
+def set_default_tile_format(fmt) -> None:
+    """Select the map that tile_format=-1 means: "cuda" / 0 to read a TensorCoreTiledLayout
+    checkpoint written by a CUDA build of torchao, "rocm" / 1 for one written on ROCm."""
+    global _default_tile_format
+    _default_tile_format = _tile_format(fmt)
+
+
+def _tile_format(fmt) -> int:
+    if isinstance(fmt, str):
+        fmt = {"cuda": TILE_FORMAT_CUDA, "rocm": TILE_FORMAT_ROCM}.get(fmt.lower(), -2)
+    if fmt == -1:
+        return _default_tile_format
+    torch._check(fmt in (TILE_FORMAT_CUDA, TILE_FORMAT_ROCM),
+                 lambda: f"tile_format must be 'cuda' (0), 'rocm' (1) or -1, got {fmt}")
+    return int(fmt)
+
+
+def _check_tile_n(N: int, fmt: int):
+    if fmt == TILE_FORMAT_ROCM:
+        torch._check(N % 16 == 0, lambda: f"ROCm tile format needs N % 16 == 0, got N={N}")
+
+
 def _check_tile(packed_w: Tensor, inner_k_tiles: int):
     torch._check(
         packed_w.dim() == 4, lambda: f"packed weight should be a 4d tensor, got {packed_w.dim()}D"
@@ -110,37 +153,56 @@ def _check_tile_sz(sz: Tensor, group_size: int, N: int, K: int):
 
 
 @torch.library.register_fake("torchao::unpack_tensor_core_tiled_layout")
-def _(packed_w: Tensor, inner_k_tiles: int) -> Tensor:
+def _(packed_w: Tensor, inner_k_tiles: int, tile_format: int = -1) -> Tensor:
     N, K = _check_tile(packed_w, inner_k_tiles)
+    _check_tile_n(N, _tile_format(tile_format))
     return packed_w.new_empty((N, K), dtype=torch.int32)
 
 
-def _unpack_tile_cuda(packed_w: Tensor, inner_k_tiles: int) -> Tensor:
+def _unpack_tile_cuda(packed_w: Tensor, inner_k_tiles: int, tile_format: int = -1) -> Tensor:
     N, K = _check_tile(packed_w, inner_k_tiles)
+    fmt = _tile_format(tile_format)
+    _check_tile_n(N, fmt)
     _require_contig(packed_w, "packed_w")
     out = torch.empty((N, K), dtype=torch.int32, device=packed_w.device)
     with torch.cuda.device(packed_w.device):
         _lib.call("tao_unpack_tensor_core_tiled_layout", _ptr(packed_w), _ptr(out), N, K,
-                  inner_k_tiles, _stream(packed_w))
+                  inner_k_tiles, fmt, _stream(packed_w))
+    return out
+
+
+def _unpack_tile_cpu(packed_w: Tensor, inner_k_tiles: int, tile_format: int = -1) -> Tensor:
+    """Host C++ unpack (tao_unpack_tensor_core_tiled_layout_host) for CPU-resident checkpoints."""
+    N, K = _check_tile(packed_w, inner_k_tiles)
+    fmt = _tile_format(tile_format)
+    _check_tile_n(N, fmt)
+    packed_w = packed_w.contiguous()
+    out = torch.empty((N, K), dtype=torch.int32)
+    _lib.call("tao_unpack_tensor_core_tiled_layout_host", _ptr(packed_w), _ptr(out), N, K,
+              inner_k_tiles, fmt)
     return out
 
 
 @torch.library.register_fake("torchao::dequantize_tensor_core_tiled_layout")
-def _(packed_w: Tensor, scales_and_zeros: Tensor, group_size: int, inner_k_tiles: int) -> Tensor:
+def _(packed_w: Tensor, scales_and_zeros: Tensor, group_size: int, inner_k_tiles: int,
+      tile_format: int = -1) -> Tensor:
     N, K = _check_tile(packed_w, inner_k_tiles)
+    _check_tile_n(N, _tile_format(tile_format))
     _check_tile_sz(scales_and_zeros, group_size, N, K)
     return packed_w.new_empty((N, K), dtype=torch.bfloat16)
 
 
-def _dequant_tile_cuda(packed_w, scales_and_zeros, group_size, inner_k_tiles):
+def _dequant_tile_cuda(packed_w, scales_and_zeros, group_size, inner_k_tiles, tile_format=-1):
     N, K = _check_tile(packed_w, inner_k_tiles)
+    fmt = _tile_format(tile_format)
+    _check_tile_n(N, fmt)
     _check_tile_sz(scales_and_zeros, group_size, N, K)
     _require_contig(packed_w, "packed_w")
     _require_contig(scales_and_zeros, "scales_and_zeros")
     out = torch.empty((N, K), dtype=torch.bfloat16, device=packed_w.device)
     with torch.cuda.device(packed_w.device):
         _lib.call("tao_dequantize_tensor_core_tiled_layout", _ptr(packed_w),
-                  _ptr(scales_and_zeros), _ptr(out), N, K, group_size, inner_k_tiles,
+                  _ptr(scales_and_zeros), _ptr(out), N, K, group_size, inner_k_tiles, fmt,
                   _stream(packed_w))
     return out
 
@@ -157,21 +219,24 @@ def _check_pack_tile(int_data: Tensor, inner_k_tiles: int):
 
 
 @torch.library.register_fake("torchao::pack_tensor_core_tiled_layout")
-def _(int_data: Tensor, inner_k_tiles: int) -> Tensor:
+def _(int_data: Tensor, inner_k_tiles: int, tile_format: int = -1) -> Tensor:
     N, K = _check_pack_tile(int_data, inner_k_tiles)
+    _check_tile_n(N, _tile_format(tile_format))
     return int_data.new_empty(
         (N // 8, K // (inner_k_tiles * 16), 32, inner_k_tiles // 2), dtype=torch.int32
     )
 
 
-def _pack_tile_cuda(int_data: Tensor, inner_k_tiles: int) -> Tensor:
+def _pack_tile_cuda(int_data: Tensor, inner_k_tiles: int, tile_format: int = -1) -> Tensor:
     N, K = _check_pack_tile(int_data, inner_k_tiles)
+    fmt = _tile_format(tile_format)
+    _check_tile_n(N, fmt)
     _require_contig(int_data, "int_data")
     out = torch.empty((N // 8, K // (inner_k_tiles * 16), 32, inner_k_tiles // 2),
                       dtype=torch.int32, device=int_data.device)
     with torch.cuda.device(int_data.device):
         _lib.call("tao_pack_tensor_core_tiled_layout", _ptr(int_data), _ptr(out), N, K,
-                  inner_k_tiles, _stream(int_data))
+                  inner_k_tiles, fmt, _stream(int_data))
     return out
 
 
@@ -496,25 +561,33 @@ for _name, _fn in [
 # Host packers (C++ in the same library) so quantize_ works on CPU-resident models.
 lib.impl("int4_pack", _int4_pack_cpu, "CPU")
 lib.impl("int4_unpack", _int4_unpack_cpu, "CPU")
+lib.impl("unpack_tensor_core_tiled_layout", _unpack_tile_cpu, "CPU")
 
 
 # ---- Python-level wrappers with the reference names (ops.py:255-377) ------------------------
-def unpack_tensor_core_tiled_layout(packed_w: Tensor, inner_k_tiles: int) -> Tensor:
+def unpack_tensor_core_tiled_layout(packed_w: Tensor, inner_k_tiles: int,
+                                    tile_format=-1) -> Tensor:
     """Tile-format int4 weight [N/8][K/(ikt*16)][32][ikt/2] -> int32 [N, K]."""
-    return torch.ops.torchao.unpack_tensor_core_tiled_layout.default(packed_w, inner_k_tiles)
+    return torch.ops.torchao.unpack_tensor_core_tiled_layout.default(
+        packed_w, inner_k_tiles, _tile_format(tile_format))
 
 
 def dequantize_tensor_core_tiled_layout(
-    packed_w: Tensor, scales_and_zeros: Tensor, group_size: int, inner_k_tiles: int
+    packed_w: Tensor, scales_and_zeros: Tensor, group_size: int, inner_k_tiles: int,
+    tile_format=-1,
 ) -> Tensor:
     """Tile-format int4 weight + [K/g, N, 2] scales/zeros -> bf16 [N, K]."""
     return torch.ops.torchao.dequantize_tensor_core_tiled_layout.default(
-        packed_w, scales_and_zeros, group_size, inner_k_tiles
+        packed_w, scales_and_zeros, group_size, inner_k_tiles, _tile_format(tile_format)
     )
 
 
-def pack_tensor_core_tiled_layout(int_data: Tensor, inner_k_tiles: int) -> Tensor:
-    return torch.ops.torchao.pack_tensor_core_tiled_layout.default(int_data, inner_k_tiles)
+def pack_tensor_core_tiled_layout(int_data: Tensor, inner_k_tiles: int,
+                                  tile_format=-1) -> Tensor:
+    """int32 [N, K] -> the tile format (tile_format 1 == PyTorch-ROCm's
+    aten._convert_weight_to_int4pack of the same nibbles, bit for bit)."""
+    return torch.ops.torchao.pack_tensor_core_tiled_layout.default(
+        int_data, inner_k_tiles, _tile_format(tile_format))
 
 
 def int4_weight_only_linear(x, packed_w, scales_and_zeros, group_size, bias=None):
