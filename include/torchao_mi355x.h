@@ -183,6 +183,50 @@ int tao_dequantize_tensor_core_tiled_layout(const int32_t* packed_w,
 int tao_pack_tensor_core_tiled_layout(const int32_t* q, int32_t* packed_w, int64_t N, int64_t K,
                                       int64_t inner_k_tiles, int tile_format, void* stream);
 
+/* ---- persistent decode chain (csrc/decode_chain.hip) ----------------------------------------
+ * A sequence of dependent M = 1 int4 weight-only linears run by ONE launch (one workgroup per
+ * CU, flag-chained phases; each workgroup issues its share of phase p+1's weight loads before
+ * it waits for phase p's output). Phase p computes
+ *     y = epilogue( [RMSNorm(x) if norm_w] @ dequant(packed, sz)^T ) [+ residual]
+ * with the bf16 roundings of the unfused ops (tao_rmsnorm_bf16 -> tao_int4wo_linear_bf16 with
+ * the residual as bias; epilogue 1 = SwiGLU over row pairs (2i, 2i+1) as tao_silu_mul_bf16).
+ * x_phase names the earlier phase that writes x (its y buffer), or -1 for a vector written
+ * before the launch. Replaces, for a Llama decode step, the per-linear
+ * aten._weight_int4pack_mm calls (torchao/dtypes/uintx/tensor_core_tiled_layout.py:104) the
+ * reference's model issues layer by layer (torchao/_models/llama/model.py:397-486). */
+typedef struct TaoChainPhase {
+  const uint32_t* packed;   /* [N][K/8] gfx950 row-stream int4 */
+  const uint16_t* sz;       /* [N][K/g][2] bf16 (scale, zero) */
+  const uint16_t* x;        /* [K] bf16 input (16-B aligned) */
+  const uint16_t* norm_w;   /* [K] RMSNorm weight, or NULL */
+  const uint16_t* residual; /* [N] (epilogue 1: [N/2]) bf16 added to the output, or NULL */
+  uint16_t* y;              /* [N] (epilogue 1: [N/2]) bf16 output (8-B aligned) */
+  int64_t N;                /* multiple of 4 */
+  int64_t K;                /* multiple of group_size, <= 32768 */
+  int64_t group_size;       /* 32, 64, 128, 256 */
+  int32_t x_phase;          /* earlier phase producing x, or -1 */
+  int32_t epilogue;         /* 0 = none, 1 = SwiGLU */
+  float eps;                /* RMSNorm epsilon */
+  int32_t reserved;
+} TaoChainPhase;
+
+/* Validate the phases, copy them to the device and allocate the chain's counters. The buffers
+ * the phases name must outlive the handle; the handle is bound to the current device. */
+int tao_chain_create(const TaoChainPhase* phases, int n_phases, void** handle);
+/* Enqueue one run of the whole chain on `stream` (graph-capturable; no host sync). */
+int tao_chain_run(void* handle, void* stream);
+/* Synchronous status: aborted_phase = 0 if no wait timed out, else the phase index + 1 whose
+ * input never arrived (the run's outputs are then invalid; call tao_chain_reset). launches =
+ * runs completed. */
+int tao_chain_status(void* handle, int* aborted_phase, unsigned* launches);
+/* Device synchronise and zero the counters (after an abort). */
+int tao_chain_reset(void* handle);
+int tao_chain_destroy(void* handle);
+/* Measurement: later runs write per (phase, workgroup) wall-clock stamps (100 MHz) into the
+ * device buffer `stamps` [n_phases][grid][4] = {phase start, input ready, tasks done,
+ * signalled}; NULL turns it off. *grid receives the workgroup count. */
+int tao_chain_profile(void* handle, uint64_t* stamps, int* grid);
+
 /* ---- int8 weight-only ---------------------------------------------------------------------- */
 
 /* y[M][N] = bf16( bf16(x @ w^T) * scale[n] ) (+ bias), w int8 [N][K], scale bf16 [N].

@@ -65,6 +65,12 @@ _SIGNATURES = {
                              ctypes.c_float, _p],
     "tao_tune_attn": [_int],
     "tao_decode_status": [_p],
+    "tao_chain_create": [_p, _int, _p],
+    "tao_chain_run": [_p, _p],
+    "tao_chain_status": [_p, _p, _p],
+    "tao_chain_reset": [_p],
+    "tao_chain_destroy": [_p],
+    "tao_chain_profile": [_p, _p, _p],
     "tao_silu_mul_bf16": [_p, _p, _p, _i64, _p],
     "tao_argmax_bf16": [_p, _p, _i64, _i64, _p],
     "tao_int4_quantize_bf16": [_p, _p, _p, _i64, _i64, _i64, ctypes.c_float, _p],
