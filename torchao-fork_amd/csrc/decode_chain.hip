@@ -94,19 +94,17 @@ __device__ __forceinline__ bool poll_phase(const unsigned* cnt, ChainCtl* ctl, i
   }
 }
 
-// Roles: waves 0..14 stream weights and compute (kCompute); wave 15 is the control wave. It
-// holds no weight loads, so its in-order vmcnt waits see only its own hand-off traffic: it
-// polls the input's counters, gathers the input vector (sc1 loads) into the LDS image with the
-// RMSNorm, runs the epilogue of the previous phase's partial sums, stores and signals — while
-// the compute waves already have the next phase's weights in flight.
-//   compute waves:  prefetch(p) | A(p) | tasks(p) -> partials | B(p) | prefetch(p+1) | A(p+1) ...
-//   control wave:   poll(p) + stage x(p) | A(p) | .......... | B(p) | epilogue(p) + signal(p) |
-//                   poll(p+1) + stage x(p+1) | A(p+1) ...
-// LDS: the x image is written by the control wave only between B(p-1) and A(p) and read by
-// the compute waves only between A(p) and B(p); the partials are written between A(p) and B(p)
-// and read by the control wave between B(p) and A(p+1).
+// Roles: waves 0..14 stream weights and compute (kCompute); wave 15 (the poller) issues no
+// weight loads, so its in-order vmcnt waits see only its own polls: it alone waits for the input
+// phase's counters while the compute waves' first weight loads are in flight. Then every wave
+// gathers its share of the input (sc1 loads) and the RMSNorm runs across the workgroup; the
+// norm weights and the residual rows (complete since an earlier phase) are loaded at phase
+// start, off the critical path.
+//   all:      [norm_w, residual -> regs/LDS] [compute waves: first weights in flight]
+//   poller:   poll(p) | A0 |  all: gather x(p) (+ norm) -> LDS | A | compute: tasks -> partials
+//   | B | all: epilogue + sc1 stores, vmcnt(0) | C | one lane signals
 constexpr int kCompute = kChainWaves - 1;
-constexpr int kCtlBatch = 8;   // 16-B x pieces per lane per gather batch
+constexpr int kXPT = 4;  // 16-B x pieces per thread (K <= 8 x 4 x 1024)
 
 __global__ __launch_bounds__(kChainThreads, 1) void chain_kernel(const DevPhase* __restrict__ phases,
                                                                  int nph, unsigned* cnt,
@@ -114,9 +112,11 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_kernel(const DevPhase*
                                                                  uint64_t* prof) {
   extern __shared__ uint4 smem[];  // x image [Kmax/8] uint4, then partials [tasks][4] floats
   __shared__ unsigned s_epoch, s_abort;
+  __shared__ float s_ss[kChainWaves];
+  __shared__ uint32_t s_res[kChainThreads * 2];  // residual rows of this workgroup (<= 4096)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool control = wave == kCompute;
+  const bool poller = wave == kCompute;
   const int G = gridDim.x, b = blockIdx.x;
   if (tid == 0) {
     s_epoch = ld_sc1_u32(&ctl->epoch);
@@ -125,14 +125,12 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_kernel(const DevPhase*
   __syncthreads();
   const unsigned epoch = s_epoch;
 
-  // prof (tao_chain_profile): per (phase, workgroup) wall-clock stamps [start, input ready,
-  // tasks done, signalled], written by the control wave's lane 0 (plain vector stores)
   auto stamp = [&](int p, int k) __attribute__((always_inline)) {
-    if (prof != nullptr && control && lane == 0)
-      prof[((size_t)p * G + b) * 4 + k] = wall_clock64();
+    if (prof != nullptr && tid == 0) prof[((size_t)p * G + b) * 4 + k] = wall_clock64();
   };
 
   for (int p = 0; p < nph; ++p) {
+    stamp(p, 0);
     const DevPhase P = phases[p];
     const int N = P.N, K = P.K, gshift = P.gshift;
     const int nchunk = K >> 5, ngroups = K >> (5 + gshift);
@@ -143,8 +141,24 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_kernel(const DevPhase*
     int KP = nrg >= kCompute ? 1 : kCompute / (nrg > 0 ? nrg : 1);
     KP = KP < S ? KP : S;
     const int ntask = nrg * KP;
+    const int nx = K >> 3;
     uint4* xs = smem;
-    float* part = reinterpret_cast<float*>(smem + (K >> 3));
+    uint4* gs = smem + (K >> 3);  // norm weight image (same element order as the x pieces)
+    float* part = reinterpret_cast<float*>(smem + 2 * (K >> 3));
+
+    // ---- phase start, poller wave: static operands (norm weights, residual rows) -> LDS -----
+    if (poller) {
+      if (P.norm_w != nullptr) {
+        const uint4* gw = reinterpret_cast<const uint4*>(P.norm_w);
+        for (int i = lane; i < nx; i += 64) gs[i] = gw[i];
+      }
+      const int rwords = (P.epi == 1 ? R : 2 * R) >> 2;  // residual dwords of this workgroup
+      if (P.res != nullptr) {
+        const Rsrc rr = make_rsrc(P.res, (uint32_t)(P.epi == 1 ? N : 2 * N));
+        const uint32_t base = (uint32_t)(P.epi == 1 ? r0 : 2 * r0);
+        for (int i = lane; i < rwords; i += 64) s_res[i] = bload4<kSC1>(rr, base + i * 4u, 0);
+      }
+    }
 
     uint4 wv[2][kRPW];
     uint32_t szv[2][kRPW];
@@ -162,73 +176,70 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_kernel(const DevPhase*
         szv[u][r] = ld_nt(P.sz + (size_t)nn * ngroups + (ccs[u] >> gshift));
       }
     };
-
-    if (control) {
-      // ---- control: wait for the input, gather it into the LDS image (+ RMSNorm) ----------
-      stamp(p, 0);
-      bool ok = true;
-      if (P.x_phase >= 0) ok = poll_phase(cnt, ctl, P.x_phase, epoch, G, timeout, lane);
-      if (!ok) {
-        if (lane == 0) s_abort = 1u;
-      } else {
-        const Rsrc xr = make_rsrc(P.x, (uint32_t)K * 2u);
-        const int nx = K >> 3;
-        float ss = 0.f;
-        for (int i0 = 0; i0 < nx; i0 += 64 * kCtlBatch) {
-          uint4 xv[kCtlBatch];
-#pragma unroll
-          for (int u = 0; u < kCtlBatch; ++u) {
-            const int i = i0 + u * 64 + lane;
-            xv[u] = i < nx ? bload16<kSC1>(xr, (uint32_t)i * 16u, 0) : make_uint4(0, 0, 0, 0);
-          }
-#pragma unroll
-          for (int u = 0; u < kCtlBatch; ++u) {
-            const int i = i0 + u * 64 + lane;
-            if (P.norm_w != nullptr) {
-              const uint32_t d[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                const float a = bf16lo_to_f32(d[j]), c = bf16hi_to_f32(d[j]);
-                ss = fmaf(a, a, fmaf(c, c, ss));
-              }
-            }
-            if (i < nx) {
-              const int c = i >> 2;
-              xs[c * 4 + (((i & 3) + (c >> 2)) & 3)] = xv[u];
-            }
-          }
-        }
-        if (P.norm_w != nullptr) {  // second pass over the LDS image: bf16(bf16(x r) w)
-          const float rn = rsqrtf(wave_sum(ss) / (float)K + P.eps);
-          const uint4* gw = reinterpret_cast<const uint4*>(P.norm_w);
-          for (int i = lane; i < nx; i += 64) {
-            const int c = i >> 2;
-            uint4& slot = xs[c * 4 + (((i & 3) + (c >> 2)) & 3)];
-            const uint4 xv = slot, gv = gw[i];
-            const uint32_t xd[4] = {xv.x, xv.y, xv.z, xv.w};
-            const uint32_t gd[4] = {gv.x, gv.y, gv.z, gv.w};
-            uint32_t o[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float lo = round_bf16(bf16lo_to_f32(xd[j]) * rn) * bf16lo_to_f32(gd[j]);
-              const float hi = round_bf16(bf16hi_to_f32(xd[j]) * rn) * bf16hi_to_f32(gd[j]);
-              o[j] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
-            }
-            slot = make_uint4(o[0], o[1], o[2], o[3]);
-          }
-        }
-      }
-      stamp(p, 1);
-    } else if (wave < ntask) {
-      // ---- compute: the first task's first slice pair in flight before the input is ready -
+    if (!poller && wave < ntask) {  // the first task's first slice pair in flight
       const int rg = wave / KP, kp = wave % KP;
       load_slice(0, r0 + rg * kRPW, kp);
       load_slice(1, r0 + rg * kRPW, kp + KP);
     }
-    __syncthreads();  // A(p): x image ready
-    if (s_abort) break;
 
-    if (!control) {
+    // ---- wait for the input (the poller), then gather it across the workgroup ----------------
+    if (poller && P.x_phase >= 0) {
+      if (!poll_phase(cnt, ctl, P.x_phase, epoch, G, timeout, lane) && lane == 0) s_abort = 1u;
+    }
+    __syncthreads();  // A0
+    if (s_abort) break;
+    stamp(p, 1);
+    {
+      // raw x -> LDS image (sc1 loads, all issued before the first use), sum of squares
+      const Rsrc xr = make_rsrc(P.x, (uint32_t)K * 2u);
+      uint4 xv[kXPT];
+#pragma unroll
+      for (int u = 0; u < kXPT; ++u) {
+        const int i = tid + u * kChainThreads;
+        xv[u] = i < nx ? bload16<kSC1>(xr, (uint32_t)i * 16u, 0) : make_uint4(0, 0, 0, 0);
+      }
+      float ss = 0.f;
+#pragma unroll
+      for (int u = 0; u < kXPT; ++u) {
+        const int i = tid + u * kChainThreads;
+        const uint32_t d[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float a = bf16lo_to_f32(d[j]), c = bf16hi_to_f32(d[j]);
+          ss = fmaf(a, a, fmaf(c, c, ss));
+        }
+        if (i < nx) {
+          const int c = i >> 2;
+          xs[c * 4 + (((i & 3) + (c >> 2)) & 3)] = xv[u];
+        }
+      }
+      if (P.norm_w != nullptr) {  // in place over the image: bf16(bf16(x r) w)
+        ss = wave_sum(ss);
+        if (lane == 0) s_ss[wave] = ss;
+        __syncthreads();
+        float t = 0.f;
+        for (int w = 0; w < kChainWaves; ++w) t += s_ss[w];
+        const float rn = rsqrtf(t / (float)K + P.eps);
+        for (int i = tid; i < nx; i += kChainThreads) {
+          const int c = i >> 2;
+          uint4& slot = xs[c * 4 + (((i & 3) + (c >> 2)) & 3)];
+          const uint4 xq = slot, gv = gs[i];
+          const uint32_t xd[4] = {xq.x, xq.y, xq.z, xq.w};
+          const uint32_t gd[4] = {gv.x, gv.y, gv.z, gv.w};
+          uint32_t o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float lo = round_bf16(bf16lo_to_f32(xd[j]) * rn) * bf16lo_to_f32(gd[j]);
+            const float hi = round_bf16(bf16hi_to_f32(xd[j]) * rn) * bf16hi_to_f32(gd[j]);
+            o[j] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+          }
+          slot = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+      }
+    }
+    __syncthreads();  // A: x image ready
+
+    if (!poller) {
       auto do_slice = [&](int u, float (&acc)[kRPW], int rowb) __attribute__((always_inline)) {
         const int cc = ccs[u];
         float sc[kRPW], zp[kRPW];
@@ -283,15 +294,13 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_kernel(const DevPhase*
         if ((lane & 15) == 0) part[t * kRPW + (lane >> 4)] = acc[0];
       }
     }
-    __syncthreads();  // B(p): partials complete
-    if (!control) continue;
-
-    // ---- control: epilogue, 4 rows per lane, k-parts summed in order, sc1 stores, signal ----
+    __syncthreads();  // B: partials complete
     stamp(p, 2);
+
+    // ---- epilogue: 4 rows per thread, k-parts summed in order, sc1 stores ----------------------
     const int nq = R >> 2;
     const Rsrc yr = make_rsrc(P.y, (uint32_t)(P.epi == 1 ? N : 2 * N));
-    const Rsrc rr = make_rsrc(P.res, P.res ? (uint32_t)(P.epi == 1 ? N : 2 * N) : 0u);
-    for (int i = lane; i < nq; i += 64) {
+    for (int i = tid; i < nq; i += kChainThreads) {
       float tot[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -308,7 +317,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_kernel(const DevPhase*
         uint32_t o = (uint32_t)f32_to_bf16(silu_bf16(a0) * b0) |
                      ((uint32_t)f32_to_bf16(silu_bf16(a1) * b1) << 16);
         if (P.res != nullptr) {
-          const uint32_t rv = bload4<kSC1>(rr, (uint32_t)n0, 0);
+          const uint32_t rv = s_res[i];
           o = (uint32_t)f32_to_bf16(bf16lo_to_f32(o) + bf16lo_to_f32(rv)) |
               ((uint32_t)f32_to_bf16(bf16hi_to_f32(o) + bf16hi_to_f32(rv)) << 16);
         }
@@ -318,8 +327,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_kernel(const DevPhase*
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] = f32_to_bf16(tot[q]);
         if (P.res != nullptr) {
-          const uint32_t rv0 = bload4<kSC1>(rr, (uint32_t)n0 * 2u, 0);
-          const uint32_t rv1 = bload4<kSC1>(rr, (uint32_t)n0 * 2u + 4u, 0);
+          const uint32_t rv0 = s_res[2 * i], rv1 = s_res[2 * i + 1];
           const uint32_t rv[4] = {rv0 & 0xFFFFu, rv0 >> 16, rv1 & 0xFFFFu, rv1 >> 16};
 #pragma unroll
           for (int q = 0; q < 4; ++q)
@@ -330,9 +338,9 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_kernel(const DevPhase*
         __builtin_amdgcn_raw_buffer_store_b64(d, yr, (uint32_t)n0 * 2u, 0, kSC1);
       }
     }
-    // the control wave is the only storing wave: its own drain, then one lane signals
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0)
+    __syncthreads();  // C: every storing wave has drained its sc1 stores
+    if (tid == 0)
       __hip_atomic_fetch_add(cnt + p * kShards + (b & (kShards - 1)), 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
     stamp(p, 3);
@@ -389,9 +397,11 @@ int tao_chain_create(const TaoChainPhase* phases, int n, void** handle) {
     TAO_CHECK_ARG(gs >= 0, "chain phase %d: group_size must be 32/64/128/256", p);
     TAO_CHECK_ARG(s.N > 0 && s.N % 4 == 0 && s.N < (1 << 30),
                   "chain phase %d: N (%lld) must be a positive multiple of 4", p, (long long)s.N);
-    TAO_CHECK_ARG(s.K > 0 && s.K % s.group_size == 0 && s.K <= 65536,
-                  "chain phase %d: K (%lld) must be a multiple of the group and <= 65536", p,
-                  (long long)s.K);
+    TAO_CHECK_ARG(s.K > 0 && s.K % s.group_size == 0 && s.K <= 8 * 4 * kChainThreads,
+                  "chain phase %d: K (%lld) must be a multiple of the group and <= %d", p,
+                  (long long)s.K, 8 * 4 * kChainThreads);
+    TAO_CHECK_ARG(s.residual == nullptr || (s.N + 255) / 256 * 4 * 2 <= 4 * 2 * kChainThreads,
+                  "chain phase %d: too many rows per workgroup for the residual stage", p);
     TAO_CHECK_ARG(s.epilogue == 0 || s.epilogue == 1, "chain phase %d: epilogue 0 or 1", p);
     TAO_CHECK_ARG(s.x_phase >= -1 && s.x_phase < p,
                   "chain phase %d: x_phase must name an earlier phase or be -1", p);
@@ -434,7 +444,7 @@ int tao_chain_create(const TaoChainPhase* phases, int n, void** handle) {
     const int64_t tasks = ((rows + kRPW - 1) / kRPW) * kCompute;
     lds_part = tasks * kRPW * 4 > lds_part ? tasks * kRPW * 4 : lds_part;
   }
-  c->lds = (size_t)(kmax * 2 + lds_part);
+  c->lds = (size_t)(kmax * 4 + lds_part);
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, chain_kernel, kChainThreads, c->lds) !=
           hipSuccess ||
