@@ -11,6 +11,7 @@ cd /tmp
 for cfg in "int8dyn 128 4096 4096" "int8dyn 128 28672 4096" "int4 128 4096 4096" "int4 128 28672 4096"; do
   set -- $cfg
   tag=$1_$2_$3_$4
+  mkdir -p "$OUT/$tag"
   timeout -k 10 120 rocprofv3 -d "$OUT/$tag/p1" -o p1 --output-format csv \
     --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS \
     -- python3 "$R/experiments/prof_gemm.py" $1 $2 $3 $4 0 0 0 20 > "$OUT/$tag/p1.log" 2>&1

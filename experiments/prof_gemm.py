@@ -19,13 +19,17 @@ from sweep_gemm import kernel_us, make_int4, make_int8dyn, make_int8wo  # noqa: 
 def main():
     path, M, N, K, bm, kg, sp = sys.argv[1], *map(int, sys.argv[2:8])
     reps = int(sys.argv[8]) if len(sys.argv) > 8 else 50
+    if len(sys.argv) > 9:  # MFMA GEMM workgroup order (tao_tune_gemm_order)
+        _lib.call("tao_tune_gemm_order", int(sys.argv[9]))
     mk = {"int4": make_int4, "int8wo": make_int8wo, "int8dyn": make_int8dyn}[path]
     _lib.call("tao_tune_linear_crossover", 1)
     _lib.call("tao_tune_gemm", bm, kg, sp)
     run, launches = mk(M, N, K)
     us = kernel_us(run, launches, reps)
     torch.cuda.synchronize()
-    print(f"{path} M={M} N={N} K={K} bm={bm} kg={kg} splits={sp}: {us:.2f} us", flush=True)
+    order = sys.argv[9] if len(sys.argv) > 9 else "0"
+    print(f"{path} M={M} N={N} K={K} bm={bm} kg={kg} splits={sp} order={order}: {us:.2f} us",
+          flush=True)
 
 
 if __name__ == "__main__":

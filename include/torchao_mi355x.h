@@ -110,6 +110,11 @@ int tao_tune_gemm_depth(int depth);
  * 3). Calling thread only; for sweeps. */
 int tao_tune_gemm_bn(int bn);
 
+/* Workgroup order of the MFMA GEMMs: 0 = plain grid order (built-in), 1 = the M tiles that share
+ * a weight tile back to back on one XCD (its L2 serves the re-reads: fewer HBM bytes, measured
+ * no faster). Calling thread only; for A/B measurement. */
+int tao_tune_gemm_order(int order);
+
 /* M == 1 int4 linears without bias: 1 = stage x once per workgroup in LDS (the decode RMSNorm
  * prologue's copy, without the norm), 0 = built-in policy. Calling thread only; for sweeps. */
 int tao_tune_int4_xlds(int mode);
@@ -330,6 +335,13 @@ int tao_int8_quantize_rows_bf16(const uint16_t* w, int8_t* q, uint16_t* scale, i
  * counts as the maximum, as in torch.argmax) as int64. Replaces logits.argmax(dim=-1) of the greedy decode
  * (generate.py:111-142, sample with temperature 0). */
 int tao_argmax_bf16(const uint16_t* x, int64_t* out, int64_t rows, int64_t n, void* stream);
+
+/* One decode step's greedy bookkeeping in one launch (batch 1): cur[0] = argmax of x[n] (the
+ * rule of tao_argmax_bf16), then tokens[pos[0] + 1] = cur[0] (when inside [0, max_len)) and
+ * pos[0] += 1. Replaces the harness's argmax + pos.add_ + tokens.index_copy_ + cur.copy_
+ * (torchao/_models/llama/generate.py decode loop, reference generate.py:111-142). */
+int tao_argmax_advance_bf16(const uint16_t* x, int64_t n, int64_t* cur, int64_t* pos,
+                            int64_t* tokens, int64_t max_len, void* stream);
 
 /* Decode-step fused int4 linear, M = 1: y = epilogue(rmsnorm(x) W^T) in one launch, with the
  * operands of tao_int4wo_linear_bf16 (x [K] bf16, packed [N][K/8], scales_and_zeros [N][K/g]).

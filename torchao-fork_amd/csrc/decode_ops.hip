@@ -565,8 +565,14 @@ __device__ __forceinline__ uint64_t pack_key(int k, uint32_t idx) {
 
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 
+// With `pos` set (one row): also the decode loop's bookkeeping in the same launch: out (the
+// graph's current-token buffer) = the argmax, tokens[pos + 1] = it, pos += 1 (GraphDecoder's
+// pos.add_ / tokens.index_copy_ / cur.copy_, three launches, torchao/_models/llama/generate.py).
 __global__ __launch_bounds__(1024) void argmax_kernel(const uint16_t* __restrict__ x,
-                                                      int64_t* __restrict__ out, int64_t n) {
+                                                      int64_t* __restrict__ out, int64_t n,
+                                                      int64_t* __restrict__ pos,
+                                                      int64_t* __restrict__ tokens,
+                                                      int64_t max_len) {
   __shared__ uint64_t red[16];
   const uint16_t* row = x + (size_t)blockIdx.x * n;
   uint64_t best = 0;
@@ -613,7 +619,13 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const uint16_t* __restrict
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = umax64(best, red[w]);
-    out[blockIdx.x] = (int64_t)(uint32_t)~(uint32_t)best;
+    const int64_t idx = (int64_t)(uint32_t)~(uint32_t)best;
+    out[blockIdx.x] = idx;
+    if (pos != nullptr) {
+      const int64_t p = pos[0] + 1;
+      if (p >= 0 && p < max_len) tokens[p] = idx;
+      pos[0] = p;
+    }
   }
 }
 
@@ -742,11 +754,21 @@ int tao_argmax_bf16(const uint16_t* x, int64_t* out, int64_t rows, int64_t n, vo
                 (long long)n);
   if (rows == 0) return TAO_OK;
   TAO_CHECK_ALIGN(x, 2, "x");
-  launch(argmax_kernel, dim3((unsigned)rows), dim3(1024), 0, as_stream(stream), x, out, n);
+  launch(argmax_kernel, dim3((unsigned)rows), dim3(1024), 0, as_stream(stream), x, out, n,
+         (int64_t*)nullptr, (int64_t*)nullptr, (int64_t)0);
   return check_launch("argmax_kernel");
 }
 
 }  // extern "C"
+
+extern "C" int tao_argmax_advance_bf16(const uint16_t* x, int64_t n, int64_t* cur, int64_t* pos,
+                                       int64_t* tokens, int64_t max_len, void* stream) {
+  TAO_CHECK_ARG(x && cur && pos && tokens && n > 0 && n < (1LL << 31) && max_len > 0,
+                "argmax_advance: bad arguments");
+  launch(argmax_kernel, dim3(1), dim3(1024), 0, as_stream(stream), x, cur, n, pos, tokens,
+         max_len);
+  return check_launch("argmax_kernel (advance)");
+}
 
 extern "C" int tao_decode_status(int* bits) {
   TAO_CHECK_ARG(bits != nullptr, "decode status: null output");

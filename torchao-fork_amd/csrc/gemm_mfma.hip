@@ -67,6 +67,39 @@ __device__ __forceinline__ bf16x8_t as_bf16x8(uint32_t a, uint32_t b, uint32_t c
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// Per-wave weight stage of 16 rows x 8 16-B slots (Int4WO, Int8WO). A ds_*_b128 pass is 16
+// lanes of 16 B: conflict-free iff the 16 slots land in 16 distinct 16-B bank groups (slot index
+// mod 16). The write passes cover rows {2i, 2i+1} x 8 slots; the read passes cover rows 0..15 at
+// one slot. Swizzling the slot by (row >> 1) & 7 serves both (the row's parity supplies bit 3);
+// the previous row & 7 gave rows n and n + 8 the same bank group on every read pass
+// (SQ_LDS_BANK_CONFLICT 1.24-1.33 extra cycles per LDS cycle, profiles/r2_pmc_prefill.jsonl).
+__device__ __forceinline__ int stage_slot(int row, int slot) {
+  return row * 8 + (slot ^ ((row >> 1) & 7));
+}
+
+// Optional XCD-grouped workgroup order (tao_tune_gemm_order 1). Workgroups are dealt
+// round-robin over the 8 XCDs (blocks b, b + 8, ... share one L2; which XCD is not fixed:
+// MI355X_MICROARCH.md "Workgroup dispatch"). The M tiles of one (column tile, K slice) read the
+// same weight bytes; grouped, those ny workgroups run back to back on one XCD and its L2 serves
+// the re-reads. Measured (profiles/r2_pmc_prefill*.jsonl, r2_prefill_order_ab.txt): at M = 128,
+// N = 28672 it cuts FETCH_SIZE from 2.2x to 1.26x the algorithmic bytes but runs 76 -> 80 us,
+// and ties elsewhere: these GEMMs are bound by per-CU ingest, not HBM. So the plain grid order
+// is the default. Speed only: any order is correct. Identity unless the grid divides into whole
+// groups of 8 x ny.
+struct TileId {
+  int n, m, z;
+};
+__device__ __forceinline__ TileId xcd_tile(int order) {
+  const int nx = gridDim.x, ny = gridDim.y, nz = gridDim.z;
+  const int L = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  const int T = nx * ny * nz;
+  if (order != 1 || ny == 1 || T % (8 * ny) != 0)
+    return TileId{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+  const int xcd = L & 7, slot = L >> 3;
+  const int gi = (slot / ny) * 8 + xcd;
+  return TileId{gi % nx, slot % ny, gi / nx};
+}
+
 // ---- policies -------------------------------------------------------------------------------
 // setup(): per-lane state for lane (n, kq) — descriptors and voffsets (once per launch).
 // load(): the raw bytes of the lane's weight piece for step `st` (wave-uniform, clamped to the
@@ -128,11 +161,11 @@ struct Int4WO {
   }
   __device__ __forceinline__ Prep prep(const Chunk& ch, uint4* stage, int lane) const {
     const int r = lane >> 3, c = lane & 7;
-    stage[r * 8 + (c ^ r)] = ch.a;
-    stage[(r + 8) * 8 + (c ^ r)] = ch.b;
+    stage[stage_slot(r, c)] = ch.a;
+    stage[stage_slot(r + 8, c)] = ch.b;
     const int n = lane & 15, kq = lane >> 4;
-    const uint4 p0 = stage[n * 8 + (kq ^ (n & 7))];
-    const uint4 p1 = stage[n * 8 + ((4 + kq) ^ (n & 7))];
+    const uint4 p0 = stage[stage_slot(n, kq)];
+    const uint4 p1 = stage[stage_slot(n, 4 + kq)];
     Prep p;
     p.w[0] = p0.x;
     p.w[1] = p0.y;
@@ -220,12 +253,12 @@ struct Int8WO {
   // stage: write the two full-line pieces, read back lane (n, kq)'s bytes 16 kq and 64 + 16 kq
   __device__ __forceinline__ Prep prep(const Chunk& ch, uint4* stage, int lane) const {
     const int r = lane >> 3, c = lane & 7;
-    stage[r * 8 + (c ^ r)] = ch.a;
-    stage[(r + 8) * 8 + (c ^ r)] = ch.b;
+    stage[stage_slot(r, c)] = ch.a;
+    stage[stage_slot(r + 8, c)] = ch.b;
     const int n = lane & 15, kq = lane >> 4;
     Prep p;
-    p.a = stage[n * 8 + (kq ^ (n & 7))];
-    p.b = stage[n * 8 + ((4 + kq) ^ (n & 7))];
+    p.a = stage[stage_slot(n, kq)];
+    p.b = stage[stage_slot(n, 4 + kq)];
     return p;
   }
   // int8 -> bf16 is exact: (q ^ 0x80) is q + 128 as an unsigned byte (one v_cvt_f32_ubyteN),
@@ -356,7 +389,7 @@ template <int BM, int D, int KG, class P>
 __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int sps, typename P::Acc* __restrict__ slab,
-    unsigned* __restrict__ cnt, int fenced) {
+    unsigned* __restrict__ cnt, int fenced, int order) {
   typedef typename P::Acc Acc;
   constexpr int MT = BM / 16;
   constexpr int XSB = P::kABytes * P::kKStep;  // x bytes per row per step (256 or 512)
@@ -374,10 +407,11 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
   const int kg = __builtin_amdgcn_readfirstlane(tid >> 8);
   const int wave = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
   const int ktid = tid & 255;
-  const int n_blk = blockIdx.x * kBN;
-  const int m_blk = blockIdx.y * BM;
+  const TileId tid3 = xcd_tile(order);
+  const int n_blk = tid3.n * kBN;
+  const int m_blk = tid3.m * BM;
   const int nsteps = (K + P::kKStep - 1) / P::kKStep;
-  const int s0 = blockIdx.z * sps;
+  const int s0 = tid3.z * sps;
   const int s1 = s0 + sps < nsteps ? s0 + sps : nsteps;  // launcher: no empty slice
   const int J = (s1 - s0 + KG - 1) / KG;                 // steps per k-group (all k-groups)
   const int row_bytes = K * P::kABytes;
@@ -512,7 +546,7 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
     // by the value its add returned. The fences this leaves out by default (buffer_wbl2 +
     // buffer_inv, 1.7-6.5 µs each and serialised per CU) made every split slower than no split;
     // `fenced` puts them back (tao_tune_splitk_fenced).
-    const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned tile = tid3.m * gridDim.x + tid3.n;
     const size_t tile_bytes = (size_t)S * 4 * MT * 64 * sizeof(Acc);
     const Rsrc srs = make_rsrc(reinterpret_cast<const uint8_t*>(slab) + tile * tile_bytes,
                                (uint32_t)tile_bytes);
@@ -521,7 +555,7 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
     if (kg == 0) {
 #pragma unroll
       for (int t = 0; t < MT; ++t)
-        bstore16<kSC1>(srs, lane_off + t * 64 * sizeof(Acc), blockIdx.z * kZ,
+        bstore16<kSC1>(srs, lane_off + t * 64 * sizeof(Acc), tid3.z * kZ,
                        __builtin_bit_cast(uint4, acc[t]));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -637,7 +671,7 @@ void launch_one(dim3 grid, hipStream_t stream, const uint8_t* xb, const P& pol,
     constexpr int D = TAO_GEMM_DEPTH > 0 ? TAO_GEMM_DEPTH
                                          : (BM <= 16 ? 4 : (BM <= 32 ? (big ? 3 : 4) : 2));
     launch((gemm_mfma_kernel<BM, D, KG, P>), grid, dim3(256 * KG), 0, stream, xb, pol, bias, y,
-           M, N, K, sps, slab, cnt, tuning().splitk_fenced);
+           M, N, K, sps, slab, cnt, tuning().splitk_fenced, tuning().gemm_order);
   }
 }
 
@@ -698,7 +732,7 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
     const int8_t* __restrict__ x, const int8_t* __restrict__ w, const uint16_t* __restrict__ xscale,
     const uint16_t* __restrict__ wscale, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int sps, i32x4_t* __restrict__ slab,
-    unsigned* __restrict__ cnt, int fenced) {
+    unsigned* __restrict__ cnt, int fenced, int order) {
   constexpr int XL = BM / 32;           // x chunks per thread per step
   constexpr int WL = BN / 32;           // W chunks per thread per step (BN rows x 8 chunks)
   constexpr int MT = BM / 32, NT = BN / 32;  // 16x16 output tiles per wave
@@ -707,9 +741,10 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int n_blk = blockIdx.x * BN, m_blk = blockIdx.y * BM;
+  const TileId tid3 = xcd_tile(order);
+  const int n_blk = tid3.n * BN, m_blk = tid3.m * BM;
   const int nsteps = K / kI8Step;
-  const int s0 = blockIdx.z * sps;
+  const int s0 = tid3.z * sps;
   const int s1 = s0 + sps < nsteps ? s0 + sps : nsteps;  // launcher: no empty slice
   const int J = s1 - s0;
 
@@ -798,7 +833,7 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
 
   const int S = gridDim.z;
   if (S > 1) {  // slab hand-off as in gemm_mfma_kernel (last_arriver, tao_common.h)
-    const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned tile = tid3.m * gridDim.x + tid3.n;
     constexpr uint32_t kZ = 4 * MT * NT * 64 * sizeof(i32x4_t);  // one slice's slab
     const Rsrc srs = make_rsrc(reinterpret_cast<const uint8_t*>(slab) + (size_t)tile * S * kZ,
                                (uint32_t)(S * kZ));
@@ -807,7 +842,7 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
     for (int a = 0; a < MT; ++a)
 #pragma unroll
       for (int b = 0; b < NT; ++b)
-        bstore16<kSC1>(srs, lo + (a * NT + b) * 64 * sizeof(i32x4_t), blockIdx.z * kZ,
+        bstore16<kSC1>(srs, lo + (a * NT + b) * 64 * sizeof(i32x4_t), tid3.z * kZ,
                        __builtin_bit_cast(uint4, acc[a][b]));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -899,7 +934,7 @@ int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const 
   const int d = td ? td : (bm == 128 ? 3 : 4);
   auto go = [&](auto kern) {
     launch(kern, grid, dim3(256), 0, stream, xq, wq, xs, ws, bias, y, M, N, K, sps, slab, cnt,
-           tuning().splitk_fenced);
+           tuning().splitk_fenced, tuning().gemm_order);
   };
   if (bn == 128) {  // experiment (tao_tune_gemm_bn): ring depth 2 or 3
     if (bm == 128) {
@@ -1013,6 +1048,13 @@ extern "C" int tao_tune_gemm_algo(int algo) {
                 "tune: gemm algo must be 0 (auto), 1 (per-wave-column kernel only) or 2 (LDS-staged "
                 "int8 kernel whenever K %% 128 == 0)");
   tao::tuning().gemm_algo = algo;
+  return TAO_OK;
+}
+
+extern "C" int tao_tune_gemm_order(int order) {
+  TAO_CHECK_ARG(order == 0 || order == 1,
+                "tune: gemm order must be 0 (plain grid order) or 1 (XCD-grouped M tiles)");
+  tao::tuning().gemm_order = order;
   return TAO_OK;
 }
 

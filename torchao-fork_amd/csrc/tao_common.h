@@ -51,6 +51,7 @@ struct Tuning {
   int i8_rpw = 0, i8_wk = 0, i8_g = 0;           // int8 GEMVs (tao_tune_int8_gemv)
   int attn_mode = 0;                             // decode attention (tao_tune_attn)
   int splitk_fenced = 0;                         // split-K hand-off with agent fences
+  int gemm_order = 0;                            // MFMA GEMM tile order: 0 plain, 1 XCD-grouped
 };
 Tuning& tuning();
 

@@ -40,6 +40,7 @@ _SIGNATURES = {
     "tao_tune_gemm_algo": [_int],
     "tao_tune_gemm_depth": [_int],
     "tao_tune_gemm_bn": [_int],
+    "tao_tune_gemm_order": [_int],
     "tao_tune_int4_xlds": [_int],
     "tao_tune_int4_norm": [_int],
     "tao_tune_reset": [],
@@ -73,6 +74,7 @@ _SIGNATURES = {
     "tao_chain_profile": [_p, _p, _p],
     "tao_silu_mul_bf16": [_p, _p, _p, _i64, _p],
     "tao_argmax_bf16": [_p, _p, _i64, _i64, _p],
+    "tao_argmax_advance_bf16": [_p, _i64, _p, _p, _p, _i64, _p],
     "tao_int4_quantize_bf16": [_p, _p, _p, _i64, _i64, _i64, ctypes.c_float, _p],
     "tao_int8_quantize_rows_bf16": [_p, _p, _p, _i64, _i64, ctypes.c_float, _p],
     "tao_int4wo_decode_bf16": [_p, _p, _p, _i64, _i64, _i64, _p, ctypes.c_float, _int, _p, _p,

@@ -111,6 +111,8 @@ class GraphDecoder:
 
     @torch.no_grad()
     def _step(self):
+        if self.model.decode_advance(self.cur, self.pos, self.tokens):
+            return  # fused path, batch 1: argmax + bookkeeping in one kernel
         nxt = decode_one_token(self.model, self.cur, self.pos)
         self.pos.add_(1)
         self.tokens.index_copy_(1, self.pos, nxt)

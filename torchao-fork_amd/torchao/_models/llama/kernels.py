@@ -7,7 +7,7 @@ import torch
 from torchao import _lib
 
 __all__ = ["rmsnorm", "rope_kv", "attn_decode", "silu_mul", "int4_decode", "argmax",
-           "check_decode_status"]
+           "argmax_advance", "check_decode_status"]
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -132,6 +132,20 @@ def argmax(logits: torch.Tensor) -> torch.Tensor:
     _lib.call("tao_argmax_bf16", logits.data_ptr(), out.data_ptr(), logits.numel() // V, V,
               _stream(logits))
     return out
+
+
+def argmax_advance(logits: torch.Tensor, cur: torch.Tensor, pos: torch.Tensor,
+                   tokens: torch.Tensor) -> None:
+    """Batch 1: cur[0, 0] = argmax(logits), tokens[0, pos + 1] = it, pos += 1, in one launch
+    (tao_argmax_advance_bf16)."""
+    _check(logits, torch.bfloat16, "argmax_advance logits")
+    for t, n in ((cur, "cur"), (pos, "pos"), (tokens, "tokens")):
+        _check(t, torch.int64, f"argmax_advance {n}")
+    if cur.numel() != 1 or tokens.shape[0] != 1:
+        raise RuntimeError("argmax_advance is batch 1")
+    V = logits.shape[-1]
+    _lib.call("tao_argmax_advance_bf16", logits.data_ptr(), V, cur.data_ptr(), pos.data_ptr(),
+              tokens.data_ptr(), tokens.shape[1], _stream(logits))
 
 
 def check_decode_status() -> None:

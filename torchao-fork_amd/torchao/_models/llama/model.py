@@ -346,6 +346,17 @@ class Transformer(nn.Module):
             return kernels.argmax(self._forward_fused(idx, input_pos)[:, -1]).to(idx.dtype)
         return self(idx, input_pos)[:, -1].argmax(dim=-1, keepdim=True).to(idx.dtype)
 
+    def decode_advance(self, cur: torch.Tensor, pos: torch.Tensor, tokens: torch.Tensor) -> bool:
+        """Graph decode step for batch 1 on the fused path: the token in ``cur`` at position
+        ``pos`` through the model, then one kernel takes the greedy next token into ``cur`` and
+        ``tokens[0, pos + 1]`` and advances ``pos``. Returns False (nothing done) off that path."""
+        if not (self.fused and cur.shape == (1, 1) and tokens.shape[0] == 1):
+            return False
+        from torchao._models.llama import kernels
+
+        kernels.argmax_advance(self._forward_fused(cur, pos)[:, -1], cur, pos, tokens)
+        return True
+
     def forward(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
         """idx [B, S] token ids at positions input_pos [S] -> logits [B, S, vocab] (fp32)."""
         assert self.max_seq > 0, "call setup_caches() first"
