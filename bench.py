@@ -27,7 +27,10 @@ headline workload is the 8B.
 
 Reported (one JSON line, rank 0):
   value        = algorithmic bytes per step x steps / wall time  (GB/s, whole job)
-  tokens_per_s = steps / wall time
+  linear_steps_per_s = steps / wall time (linears only; the model's decode rate is e2e_decode)
+  north_star   = BASELINE's per-launch target shape (int4 g32 M=1 4096x4096, wo at 8B): us per
+                 launch inside a replayed graph of that shape's launches, and its fraction of
+                 8 TB/s (target 0.70); roofline.per_shape_graph / per_shape_frac hold every shape
   roofline     = the GEMV kernel: algorithmic bytes per step / GPU time per step of the
                  GEMV-only graph replayed back to back (HIP events on the replay stream, i.e. the
                  sum of the step's kernel durations in the timed regime), against the MI355X
@@ -599,9 +602,11 @@ def main():
     stream = torch.cuda.Stream(device)
     lib = _lib.lib()
 
-    def step(do_gemv=True, do_comm=True):
+    def step(do_gemv=True, do_comm=True, only=None):
         sp = torch.cuda.current_stream(device).cuda_stream
         for (_, n_loc, K, packed, sz, y_loc, y_full, kind) in plan:
+            if only is not None and (n_loc, K) != only:
+                continue
             if do_gemv:
                 rc = lib.tao_int4wo_linear_bf16(xs[K].data_ptr(), packed.data_ptr(), sz.data_ptr(),
                                                 None, y_loc.data_ptr(), 1, n_loc, K, g, sp)
@@ -698,6 +703,30 @@ def main():
         e["us"] = round(e["us"] / e["launches"], 3)
         e["GBps"] = round(e["bytes"] / (e["us"] * 1e-6) / 1e9, 1)
 
+    # per-shape cost inside a replayed graph: each shape's launches (its distinct weights, in
+    # step order) captured alone and replayed back to back; µs per launch from HIP events on
+    # the replay stream. This is the in-step number the north-star target is stated on.
+    per_shape_graph = {}
+    if graph is not None and P == 1:
+        for (n_loc, K) in sorted({(e[1], e[2]) for e in plan}):
+            gs_ = capture(do_comm=False, only=(n_loc, K))
+            cnt = sum(1 for e in plan if (e[1], e[2]) == (n_loc, K))
+            reps = max(args.steps, 10)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(stream):
+                gs_.replay()
+                e0.record(stream)
+                for _ in range(reps):
+                    gs_.replay()
+                e1.record(stream)
+            e1.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / reps / cnt
+            b = int4_alg_bytes(n_loc, K, g)
+            per_shape_graph[f"{n_loc}x{K}"] = {
+                "launches": cnt, "us": round(us, 3), "GBps": round(b / (us * 1e-6) / 1e9, 1),
+                "frac": round(b / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)}
+            del gs_
+
     # HBM traffic from the committed counter pass (rocprofv3 --pmc FETCH_SIZE of this bench,
     # P = 1 shapes): bytes per step, to set against the algorithmic bytes
     traffic = None
@@ -750,7 +779,9 @@ def main():
             "metric": f"int4 WO linear GB/s + tokens/s vs CPU dequant path, {model_name} shapes M=1",
             "value": round(bytes_per_step * args.steps / elapsed / 1e9, 2),
             "unit": "GB/s",
-            "tokens_per_s": round(args.steps / elapsed, 2),
+            # linears only (one step = every int4 linear of one decoded token); the model's
+            # real decode rate (attention, norms, argmax included) is e2e_decode's
+            "linear_steps_per_s": round(args.steps / elapsed, 2),
             "n_gpus": P,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -793,9 +824,19 @@ def main():
                 "kernel_ms_per_step": round(kernel_ms, 4),
                 "eager_kernel_ms_per_step": round(sum(durs), 4),
                 "per_shape_eager": per_shape,
+                "per_shape_graph": per_shape_graph or None,
+                "per_shape_frac": ({k: v["frac"] for k, v in per_shape_graph.items()}
+                                   if per_shape_graph else None),
             },
             "cpu_baseline": cpu,
         }
+        ns = per_shape_graph.get("4096x4096") if per_shape_graph else None
+        if ns is not None:
+            # north_star (BASELINE.json): int4 g32 M=1 4096x4096 at >= 70% of HBM peak per
+            # launch; the graph-replayed in-step number (wo's shape at 8B)
+            rec["north_star"] = {"shape": f"4096x4096 int4 g{g} M=1",
+                                 "us_per_launch": ns["us"], "GBps": ns["GBps"],
+                                 "frac": ns["frac"], "target_frac": 0.70}
         if ref_gpu is not None:
             rec["reference_gpu"] = ref_gpu
             if "value" in ref_gpu:

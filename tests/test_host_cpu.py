@@ -395,3 +395,21 @@ def test_reference_tile_checkpoint_wrong_map_is_not_silent():
     bad, _ = convert_from_tensor_core_tiled(impl.packed_weight, impl.scale_and_zero, 8,
                                             (48, 1024), "rocm")
     assert torch.equal(good, torch.ops.torchao.int4_pack(q)) and not torch.equal(good, bad)
+
+
+def test_per_linear_ops_dispatch_to_cpp_kernels():
+    """The per-linear ops' CUDA kernels are the C++ ones of libtorchao_ops.so (no Python frame per
+    call); the rest keep their Python impls. Checked on the dispatcher's own table."""
+    import torch
+    from torchao import ops
+
+    served = ops.native_dispatch()
+    assert served == {"int4_weight_only_linear", "int8_weight_only_linear",
+                      "int8_quantize_per_token", "int8_scaled_mm", "int8_dyn_linear"}, ops._native_error
+    for name in served:
+        table = torch._C._dispatch_dump(f"torchao::{name}")
+        cuda = [ln for ln in table.splitlines() if ln.startswith("CUDA:")]
+        assert cuda and "torch_ops.cpp" in cuda[0], table
+        assert any(ln.startswith("Meta:") for ln in table.splitlines()), table
+    table = torch._C._dispatch_dump("torchao::int4_dequantize")
+    assert "ops.py" in [ln for ln in table.splitlines() if ln.startswith("CUDA:")][0]

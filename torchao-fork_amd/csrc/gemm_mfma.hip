@@ -74,7 +74,11 @@ __device__ __forceinline__ bf16x8_t as_bf16x8(uint32_t a, uint32_t b, uint32_t c
 // the previous row & 7 gave rows n and n + 8 the same bank group on every read pass
 // (SQ_LDS_BANK_CONFLICT 1.24-1.33 extra cycles per LDS cycle, profiles/r2_pmc_prefill.jsonl).
 __device__ __forceinline__ int stage_slot(int row, int slot) {
+#if TAO_STAGE_OLD
+  return row * 8 + (slot ^ (row & 7));  // timing A/B only
+#else
   return row * 8 + (slot ^ ((row >> 1) & 7));
+#endif
 }
 
 // Optional XCD-grouped workgroup order (tao_tune_gemm_order 1). Workgroups are dealt

@@ -28,6 +28,10 @@
 #ifndef TAO_GEMV_DEBUG
 #define TAO_GEMV_DEBUG 0
 #endif
+// TAO_NORM_DEBUG 1 (timing only): the RMSNorm prologue skips its cross-wave exchange.
+#ifndef TAO_NORM_DEBUG
+#define TAO_NORM_DEBUG 0
+#endif
 
 namespace tao {
 
@@ -142,6 +146,24 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
       }
     }
     ss = wave_sum(ss);
+#if TAO_NORM_DEBUG == 1
+    // timing only: this wave's own sum stands in for the workgroup's (no exchange, no barrier)
+    {
+      const float r = rsqrtf(ss * (float)(G * Wk) / (float)K + fu.eps);
+#pragma unroll
+      for (int u = 0; u < NPT; ++u) {
+        const int i = threadIdx.x + u * (int)blockDim.x;
+        if (i < nx) {
+          const int c = i >> 2;
+          xs[c * 4 + (((i & 3) + (c >> 2)) & 3)] =
+              make_uint4(rmsnorm_pair(xv[u].x, gv[u].x, r), rmsnorm_pair(xv[u].y, gv[u].y, r),
+                         rmsnorm_pair(xv[u].z, gv[u].z, r), rmsnorm_pair(xv[u].w, gv[u].w, r));
+        }
+      }
+      __syncthreads();
+      return;
+    }
+#endif
     float* ssr = red + G * Wk * V;
     if (lane == 0) ssr[wave] = ss;
     if (fu.norm_deferred) {

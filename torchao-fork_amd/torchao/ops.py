@@ -27,6 +27,7 @@ Operators:
 """
 
 import ctypes
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -541,6 +542,31 @@ def _int8_quantize_rows_cuda(w: Tensor, eps: float):
 
 
 # ---- register device impls ------------------------------------------------------------------
+# The per-linear ops take their CUDA kernels from libtorchao_ops.so (csrc/torch_ops.cpp: the
+# same checks, then the C-ABI, with no Python frame: ~19 -> ~7 µs of host time per call at
+# M = 1, profiles/r2_eager_overhead*.json). The Python impls below serve the rest, and these
+# too when that library cannot load or an experiment points TORCHAO_MI355X_LIB at a variant
+# build (the C++ kernels are linked to the in-tree library).
+_OPS_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtorchao_ops.so")
+_native_served: frozenset = frozenset()
+_native_error: Optional[str] = None
+if os.environ.get("TORCHAO_MI355X_LIB"):
+    _native_error = "TORCHAO_MI355X_LIB is set (variant build): Python impls"
+else:
+    try:
+        torch.ops.load_library(_OPS_LIB)
+        _served = ctypes.CDLL(_OPS_LIB).tao_torch_ops_served
+        _served.restype = ctypes.c_char_p
+        _native_served = frozenset(_served().decode().split(","))
+    except (OSError, RuntimeError, AttributeError) as e:
+        _native_error = f"{type(e).__name__}: {e}"
+
+
+def native_dispatch() -> frozenset:
+    """The ``torch.ops.torchao`` ops whose CUDA kernel is C++ (libtorchao_ops.so)."""
+    return _native_served
+
+
 for _name, _fn in [
     ("unpack_tensor_core_tiled_layout", _unpack_tile_cuda),
     ("dequantize_tensor_core_tiled_layout", _dequant_tile_cuda),
@@ -557,7 +583,8 @@ for _name, _fn in [
     ("int8_scaled_mm", _int8_scaled_mm_cuda),
     ("int8_dyn_linear", _int8_dyn_linear_cuda),
 ]:
-    lib.impl(_name, _fn, "CUDA")
+    if _name not in _native_served:
+        lib.impl(_name, _fn, "CUDA")
 # Host packers (C++ in the same library) so quantize_ works on CPU-resident models.
 lib.impl("int4_pack", _int4_pack_cpu, "CPU")
 lib.impl("int4_unpack", _int4_unpack_cpu, "CPU")
