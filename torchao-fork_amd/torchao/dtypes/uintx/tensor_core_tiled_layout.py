@@ -71,14 +71,11 @@ def _linear_bf16_act_uint4_weight_impl(input_tensor, weight_tensor, bias):
     orig_dtype = input_tensor.dtype
     if input_tensor.numel() == 0:
         return input_tensor.new_empty((*input_tensor.shape[:-1], weight_tensor.shape[0]))
+    x = input_tensor if orig_dtype is torch.bfloat16 else input_tensor.to(torch.bfloat16)
     y = torch.ops.torchao.int4_weight_only_linear(
-        input_tensor.to(torch.bfloat16),
-        impl.packed_weight,
-        impl.scale_and_zero,
-        weight_tensor.block_size[-1],
-        bias,
+        x, impl.packed_weight, impl.scale_and_zero, weight_tensor.block_size[-1], bias
     )
-    return y.to(orig_dtype)
+    return y if orig_dtype is torch.bfloat16 else y.to(orig_dtype)
 
 
 def _is_tile_storage(packed_weight: torch.Tensor) -> bool:
