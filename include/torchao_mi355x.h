@@ -114,6 +114,13 @@ int tao_tune_gemm_bn(int bn);
  * a weight tile back to back on one XCD (its L2 serves the re-reads: fewer HBM bytes, measured
  * no faster). Calling thread only; for A/B measurement. */
 int tao_tune_gemm_order(int order);
+/* Columns per wave of the MFMA GEMMs: 0 = built-in, 1 = 16, 2 = 32 (one A-fragment LDS read
+ * feeds two MFMAs; the workgroup tile is 128 columns wide). Calling thread only; for A/B
+ * measurement. */
+int tao_tune_gemm_nw(int nw);
+/* The MFMA GEMMs' measured launch-shape table for the Llama-3 linears (csrc/gemm_table.inc):
+ * 0 = used (built-in), 1 = off (heuristic only). Calling thread only; for A/B measurement. */
+int tao_tune_gemm_table(int off);
 
 /* M == 1 int4 linears without bias: 1 = stage x once per workgroup in LDS (the decode RMSNorm
  * prologue's copy, without the norm), 0 = built-in policy. Calling thread only; for sweeps. */

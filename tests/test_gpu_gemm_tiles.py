@@ -282,3 +282,90 @@ def test_tuning_is_scoped_and_thread_local():
     assert torch.equal(after, base)
     for y in (base, gemv):
         assert oracle.rel_l2(y.cpu(), oracle.int4_linear_fp32(x, q, s, z, g)) < TOL_FP32
+
+
+@pytest.fixture
+def gemm_nw():
+    yield lambda nw: _lib.call("tao_tune_gemm_nw", nw)
+    _lib.call("tao_tune_gemm_nw", 0)
+    _lib.call("tao_tune_gemm", 0, 0, 0)
+
+
+# 32 columns per wave (tao_tune_gemm_nw 2): every instantiated (bm, kg) with and without split-K,
+# ragged N (not a multiple of the 128-column tile) and K tails; the per-element accumulation
+# order does not depend on nw, so the outputs equal the 16-column kernel's bit for bit
+@pytest.mark.parametrize("bm,kg,splits", [(16, 1, 1), (16, 2, 3), (32, 1, 2), (32, 2, 1),
+                                          (64, 1, 4), (64, 2, 1)])
+def test_two_column_blocks_per_wave_equal_one(gemm_nw, bm, kg, splits):
+    M, N, K, g = 70, 328, 1056, 32
+    w = oracle.make_linear_weight(N, K, seed=bm * kg + splits)
+    s, z = oracle.int4_qparams(w, g)
+    q = oracle.int4_quantize(w, s, z, g)
+    x = oracle.make_activation(M, K, seed=splits + 1)
+    bias = oracle.make_activation(1, N, seed=6).reshape(N)
+    packed = torch.ops.torchao.int4_pack(q.to(DEV))
+    sz = torch.stack([s, z], dim=-1).contiguous().to(DEV)
+    xd, bd = x.to(DEV), bias.to(DEV)
+    s8 = oracle.int8_weight_qparams(w)
+    q8 = oracle.int8_weight_quantize(w, s8)
+    wq, ws = oracle.int8_dyn_weight(w)
+    xq, xs = oracle.int8_act_quant(x)
+    _lib.call("tao_tune_gemm", bm, kg, splits)
+    _lib.call("tao_tune_gemm_algo", 1)  # int8-dyn on the template kernel
+    try:
+        outs = {}
+        for nw in (1, 2):
+            gemm_nw(nw)
+            outs[nw] = (
+                torch.ops.torchao.int4_weight_only_linear(xd, packed, sz, g, bd).cpu(),
+                torch.ops.torchao.int8_weight_only_linear(xd, q8.to(DEV), s8.to(DEV), bd).cpu(),
+                torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV),
+                                                 bd).cpu(),
+            )
+    finally:
+        _lib.call("tao_tune_gemm_algo", 0)
+    for a, b in zip(outs[1], outs[2]):
+        assert torch.equal(a, b)
+    assert oracle.rel_l2(outs[2][0], oracle.int4_linear_fp32(x, q, s, z, g, bias)) < TOL_FP32
+    assert oracle.rel_l2(outs[2][1], oracle.int8wo_linear(x, q8, s8, bias)) < TOL_REF
+    assert torch.equal(outs[2][2], oracle.int8_scaled_mm(xq, xs, wq, ws, bias, epilogue="cpu"))
+
+
+# entries of the measured shape table (gemm_table.inc) against the heuristic shape and the
+# oracle: int4 M=64 6144x4096 (64, 1, 4), int8-wo M=128 28672x4096 (nw 2), int8-dyn M=64
+# 6144x4096 (the template kernel in place of the heuristic's), int4 M=100 -> the M=128 bucket
+@pytest.mark.parametrize("path,M,N,K", [("int4", 64, 6144, 4096), ("int8wo", 128, 28672, 4096),
+                                        ("int8dyn", 64, 6144, 4096), ("int4", 100, 6144, 4096)])
+def test_tuned_shape_table(path, M, N, K):
+    g = 32
+    w = oracle.make_linear_weight(N, K, seed=N + M)
+    x = oracle.make_activation(M, K, seed=M)
+    xd = x.to(DEV)
+    if path == "int4":
+        s, z = oracle.int4_qparams(w, g)
+        q = oracle.int4_quantize(w, s, z, g)
+        packed = torch.ops.torchao.int4_pack(q.to(DEV))
+        sz = torch.stack([s, z], dim=-1).contiguous().to(DEV)
+        run = lambda: torch.ops.torchao.int4_weight_only_linear(xd, packed, sz, g, None).cpu()  # noqa: E731
+        ref = oracle.int4_linear_fp32(x, q, s, z, g)
+    elif path == "int8wo":
+        s8 = oracle.int8_weight_qparams(w)
+        q8 = oracle.int8_weight_quantize(w, s8)
+        run = lambda: torch.ops.torchao.int8_weight_only_linear(xd, q8.to(DEV), s8.to(DEV), None).cpu()  # noqa: E731
+        ref = (x.double() @ q8.double().t()) * s8.double()
+    else:
+        wq, ws = oracle.int8_dyn_weight(w)
+        xq, xs = oracle.int8_act_quant(x)
+        run = lambda: torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), None).cpu()  # noqa: E731
+        ref = oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="cpu")
+    y_table = run()
+    _lib.call("tao_tune_gemm_table", 1)
+    try:
+        y_heur = run()
+    finally:
+        _lib.call("tao_tune_gemm_table", 0)
+    if path == "int8dyn":
+        assert torch.equal(y_table, ref) and torch.equal(y_heur, ref)
+    else:
+        assert oracle.rel_l2(y_table, ref) < TOL_FP32
+        assert oracle.rel_l2(y_table, y_heur) < TOL_FP32

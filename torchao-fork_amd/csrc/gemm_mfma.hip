@@ -26,7 +26,8 @@
 #include "tao_common.h"
 
 // Experiment switch (experiments/gemm_debug.sh builds variants; 0 in the product):
-// 1 = no x global loads, 2 = no weight global loads, 3 = no x LDS traffic, 4 = no step barrier.
+// 1 = no x global loads, 2 = no weight global loads, 3 = no x LDS traffic, 4 = no step barrier,
+// 5 = no global loads at all.
 #ifndef TAO_GEMM_DEBUG
 #define TAO_GEMM_DEBUG 0
 #endif
@@ -112,6 +113,7 @@ __device__ __forceinline__ TileId xcd_tile(int order) {
 // columns past N (clamped to row N - 1) are computed and dropped, and a K tail reads the next
 // row's finite weights against x that the LDS store zeroes. prep()/frag(): B fragments.
 struct Int4WO {
+  static constexpr int kPathId = 0;   // gemm_table.inc
   static constexpr int kABytes = 2;   // bf16 x
   static constexpr int kKStep = 256;  // 128 B of nibbles per row per step: one full line
   static constexpr int kMfma = 8;
@@ -217,6 +219,7 @@ struct Int4WO {
 };
 
 struct Int8WO {
+  static constexpr int kPathId = 1;
   static constexpr int kABytes = 2;
   static constexpr int kKStep = 128;
   static constexpr int kMfma = 4;
@@ -287,6 +290,7 @@ struct Int8WO {
 };
 
 struct Int8Dyn {
+  static constexpr int kPathId = 2;
   static constexpr int kABytes = 1;  // int8 x
   static constexpr int kKStep = 256;
   static constexpr int kMfma = 4;
@@ -389,7 +393,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 //    sums them in slice order and runs the epilogue. Both sums have a fixed order, so results
 //    do not depend on arrival order. Protocol and its hardware assumption: last_arriver()
 //    (tao_common.h); `fenced` adds the agent release/acquire fences (tao_tune_splitk_fenced).
-template <int BM, int D, int KG, class P>
+template <int BM, int D, int KG, int NW, class P>
 __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int sps, typename P::Acc* __restrict__ slab,
@@ -401,10 +405,11 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
   constexpr int RPP = 256 / SLOTS;              // x rows loaded per 256-thread pass
   constexpr int XLOADS = BM * SLOTS / 256;      // 16-B x pieces per thread per step
   constexpr int TILE = BM * SLOTS;              // uint4 per x tile
-  static_assert((KG - 1) * 4 * MT * 64 <= KG * 2 * TILE, "k-group reduction must fit in LDS");
+  constexpr int NA = MT * NW;                   // accumulator tiles per wave
+  static_assert((KG - 1) * 4 * NA * 64 <= KG * 2 * TILE, "k-group reduction must fit in LDS");
   // one LDS array (a second __shared__ object can de-pipeline the loop, cdna guide §5 item 4a):
-  // [KG][2][x tile] then the per-wave weight stages
-  __shared__ uint4 lds[KG * 2 * TILE + KG * 4 * P::kStage + (P::kStage == 0)];
+  // [KG][2][x tile] then the per-wave weight stages (NW per wave)
+  __shared__ uint4 lds[KG * 2 * TILE + KG * 4 * NW * P::kStage + (P::kStage == 0)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -412,7 +417,7 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
   const int wave = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
   const int ktid = tid & 255;
   const TileId tid3 = xcd_tile(order);
-  const int n_blk = tid3.n * kBN;
+  const int n_blk = tid3.n * kBN * NW;
   const int m_blk = tid3.m * BM;
   const int nsteps = (K + P::kKStep - 1) / P::kKStep;
   const int s0 = tid3.z * sps;
@@ -421,11 +426,16 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
   const int row_bytes = K * P::kABytes;
   uint4* xs = lds + kg * 2 * TILE;
 
-  const int bn = n_blk + wave * 16 + (lane & 15);
-  const bool nok = bn < N;
+  // the wave's NW 16-column blocks: columns n_blk + 16 (NW wave + c) + (lane & 15)
+  int bn[NW];
+  typename P::Lane wl[NW];
+#pragma unroll
+  for (int c = 0; c < NW; ++c) {
+    bn[c] = n_blk + (wave * NW + c) * 16 + (lane & 15);
+    wl[c] = pol.setup(bn[c], lane, N, K);
+  }
   const int kq = lane >> 4;
-  const typename P::Lane wl = pol.setup(bn, lane, N, K);
-  uint4* wstage = lds + KG * 2 * TILE + (kg * 4 + wave) * P::kStage;
+  uint4* wstage = lds + KG * 2 * TILE + (kg * 4 + wave) * NW * P::kStage;
 
   // this thread's x pieces: rows row0 + RPP i (i < XLOADS), 16-B slot xslot of each; rows
   // past M are clamped to M - 1 (computed and dropped). A k tail past the row end reads the
@@ -443,31 +453,34 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
   }
   const bool ragged = (row_bytes % XSB) != 0;
 
-  Acc acc[MT];
+  Acc acc[NA];  // [t][c]
 #pragma unroll
-  for (int t = 0; t < MT; ++t) acc[t] = Acc{0, 0, 0, 0};
+  for (int t = 0; t < NA; ++t) acc[t] = Acc{0, 0, 0, 0};
 
   uint4 xr[D][XLOADS];
-  typename P::Chunk wr[D];
+  typename P::Chunk wr[D][NW];
 
   // local step j of this k-group -> absolute step (may be >= s1: then inactive)
   auto abs_step = [&](int j) __attribute__((always_inline)) { return s0 + kg + j * KG; };
-  auto load_step = [&](int j, uint4 (&xdst)[XLOADS], typename P::Chunk& wdst)
+  auto load_step = [&](int j, uint4 (&xdst)[XLOADS], typename P::Chunk (&wdst)[NW])
       __attribute__((always_inline)) {
     const int st0 = abs_step(j);
     const int st = st0 < s1 ? st0 : s1 - 1;
-    if (TAO_GEMM_DEBUG != 1) {
+    if (TAO_GEMM_DEBUG != 1 && TAO_GEMM_DEBUG != 5) {
 #pragma unroll
       for (int i = 0; i < XLOADS; ++i) xdst[i] = bload16(xrs, xv[i], st * XSB);
     } else {
 #pragma unroll
       for (int i = 0; i < XLOADS; ++i) xdst[i] = make_uint4(st, i, 0x3c003c00u, 0);
     }
-    if (TAO_GEMM_DEBUG != 2) {
-      wdst = pol.load(wl, st);
-    } else {
-      wdst = typename P::Chunk{};
-      reinterpret_cast<uint32_t*>(&wdst)[0] = st * 0x01010101u;
+#pragma unroll
+    for (int c = 0; c < NW; ++c) {
+      if (TAO_GEMM_DEBUG != 2 && TAO_GEMM_DEBUG != 5) {
+        wdst[c] = pol.load(wl[c], st);
+      } else {
+        wdst[c] = typename P::Chunk{};
+        reinterpret_cast<uint32_t*>(&wdst[c])[0] = st * 0x01010101u;
+      }
     }
   };
   auto store_x = [&](const uint4 (&src)[XLOADS], int j) __attribute__((always_inline)) {
@@ -491,17 +504,23 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
     constexpr int u = decltype(uc)::value;
     load_step(j + D - 1, xr[(u + D - 1) % D], wr[(u + D - 1) % D]);
     if (abs_step(j) < s1) {  // uniform: a k-group's idle tail iterations skip the math
-      const typename P::Prep pw = pol.prep(wr[u], wstage, lane);
+      typename P::Prep pw[NW];
+#pragma unroll
+      for (int c = 0; c < NW; ++c) pw[c] = pol.prep(wr[u][c], wstage + c * P::kStage, lane);
       const uint4* xb = xs + (j & 1) * TILE;
 #pragma unroll
       for (int s = 0; s < P::kMfma; ++s) {
-        const auto bfrag = pol.frag(pw, s);
+        decltype(pol.frag(pw[0], s)) bfrag[NW];
+#pragma unroll
+        for (int c = 0; c < NW; ++c) bfrag[c] = pol.frag(pw[c], s);
         const int slot = P::slot(s, kq);
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
           const int row = t * 16 + (lane & 15);
+          // one A fragment read from LDS feeds the wave's NW column blocks
           const uint4 a = TAO_GEMM_DEBUG == 3 ? xr[u][0] : xb[lds_slot<SLOTS>(row, slot)];
-          acc[t] = P::mfma(a, bfrag, acc[t]);
+#pragma unroll
+          for (int c = 0; c < NW; ++c) acc[t * NW + c] = P::mfma(a, bfrag[c], acc[t * NW + c]);
         }
       }
     }
@@ -529,13 +548,13 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
     Acc* red = reinterpret_cast<Acc*>(lds);
     if (kg > 0) {
 #pragma unroll
-      for (int t = 0; t < MT; ++t) red[(((kg - 1) * 4 + wave) * MT + t) * 64 + lane] = acc[t];
+      for (int t = 0; t < NA; ++t) red[(((kg - 1) * 4 + wave) * NA + t) * 64 + lane] = acc[t];
     }
     __syncthreads();
     if (kg == 0) {
       for (int g = 1; g < KG; ++g) {
 #pragma unroll
-        for (int t = 0; t < MT; ++t) acc[t] += red[(((g - 1) * 4 + wave) * MT + t) * 64 + lane];
+        for (int t = 0; t < NA; ++t) acc[t] += red[(((g - 1) * 4 + wave) * NA + t) * 64 + lane];
       }
     }
     __syncthreads();  // LDS free again (the split-K flag below reuses it)
@@ -551,14 +570,14 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
     // buffer_inv, 1.7-6.5 µs each and serialised per CU) made every split slower than no split;
     // `fenced` puts them back (tao_tune_splitk_fenced).
     const unsigned tile = tid3.m * gridDim.x + tid3.n;
-    const size_t tile_bytes = (size_t)S * 4 * MT * 64 * sizeof(Acc);
+    const size_t tile_bytes = (size_t)S * 4 * NA * 64 * sizeof(Acc);
     const Rsrc srs = make_rsrc(reinterpret_cast<const uint8_t*>(slab) + tile * tile_bytes,
                                (uint32_t)tile_bytes);
-    const uint32_t lane_off = (uint32_t)((wave * MT * 64 + lane) * sizeof(Acc));
-    constexpr uint32_t kZ = 4 * MT * 64 * sizeof(Acc);  // one slice's slab
+    const uint32_t lane_off = (uint32_t)((wave * NA * 64 + lane) * sizeof(Acc));
+    constexpr uint32_t kZ = 4 * NA * 64 * sizeof(Acc);  // one slice's slab
     if (kg == 0) {
 #pragma unroll
-      for (int t = 0; t < MT; ++t)
+      for (int t = 0; t < NA; ++t)
         bstore16<kSC1>(srs, lane_off + t * 64 * sizeof(Acc), tid3.z * kZ,
                        __builtin_bit_cast(uint4, acc[t]));
     }
@@ -568,16 +587,16 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
         last_arriver(&cnt[tile], (unsigned)S, reinterpret_cast<unsigned*>(lds), fenced);
     if (!last || kg != 0) return;
 #pragma unroll
-    for (int t = 0; t < MT; ++t) acc[t] = Acc{0, 0, 0, 0};
+    for (int t = 0; t < NA; ++t) acc[t] = Acc{0, 0, 0, 0};
     // 4 slabs per round, all loads issued before the first add (clamped, then masked); slices
     // summed in slice order whatever the arrival order
     for (int z0 = 0; z0 < S; z0 += 4) {
-      Acc part[4][MT];
+      Acc part[4][NA];
 #pragma unroll
       for (int zz = 0; zz < 4; ++zz) {
         const int z = z0 + zz < S ? z0 + zz : S - 1;
 #pragma unroll
-        for (int t = 0; t < MT; ++t)
+        for (int t = 0; t < NA; ++t)
           part[zz][t] = __builtin_bit_cast(
               Acc, bload16<kSC1>(srs, lane_off + t * 64 * sizeof(Acc), z * kZ));
       }
@@ -585,7 +604,7 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
       for (int zz = 0; zz < 4; ++zz) {
         if (z0 + zz < S) {
 #pragma unroll
-          for (int t = 0; t < MT; ++t) acc[t] += part[zz][t];
+          for (int t = 0; t < NA; ++t) acc[t] += part[zz][t];
         }
       }
     }
@@ -594,17 +613,20 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
   }
 
   // C/D map: col = lane & 15 (n), row = 4*(lane >> 4) + i (m).
-  if (nok) {
-    const float bv = bias != nullptr ? bf16_to_f32(bias[bn]) : 0.f;
 #pragma unroll
-    for (int t = 0; t < MT; ++t) {
+  for (int c = 0; c < NW; ++c) {
+    if (bn[c] < N) {
+      const float bv = bias != nullptr ? bf16_to_f32(bias[bn[c]]) : 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = m_blk + t * 16 + 4 * (lane >> 4) + i;
-        if (m < M) {
-          float v = pol.epilogue(acc[t][i], m, bn);
-          if (bias != nullptr) v = round_bf16(v + bv);
-          y[(size_t)m * N + bn] = f32_to_bf16(v);
+      for (int t = 0; t < MT; ++t) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m_blk + t * 16 + 4 * (lane >> 4) + i;
+          if (m < M) {
+            float v = pol.epilogue(acc[t * NW + c][i], m, bn[c]);
+            if (bias != nullptr) v = round_bf16(v + bv);
+            y[(size_t)m * N + bn[c]] = f32_to_bf16(v);
+          }
         }
       }
     }
@@ -614,11 +636,11 @@ __global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
 // Launch shape: M tile, k-groups per workgroup and K slices. Per-workgroup time is set by its
 // load latency chain, so the grid should put several waves on every SIMD.
 struct GemmShape {
-  int bm, kg, splits;
+  int bm, kg, splits, nw;
 };
 
 GemmShape choose_shape(int M, int N, int nsteps, int max_bm, int xsb, int pref_kg,
-                       int min_slice) {
+                       int min_slice, int nw) {
   // From the sweeps with the fence-free split-K hand-off (experiments/sweep_gemm.py,
   // profiles/r1_sweep_gemm_sc1*.jsonl; the fenced hand-off made every split lose):
   //  * short K (<= 16 steps): the largest M tile (no 2x padding of M) that gives ~one round of
@@ -628,9 +650,9 @@ GemmShape choose_shape(int M, int N, int nsteps, int max_bm, int xsb, int pref_k
   //    slices (N tiles x K slices) reach one round, <= 512 workgroups, slices >= min_slice
   //    steps (1024 k);
   //  * the policy's preferred k-groups (int4 / int8-WO 2, int8-dyn 1).
-  const long nb = (N + kBN - 1) / kBN;
+  const long nb = (N + kBN * nw - 1) / (kBN * nw);
   auto tiles_of = [&](int bm) { return nb * ((M + bm - 1) / bm); };
-  GemmShape sh{16, pref_kg, 1};
+  GemmShape sh{16, pref_kg, 1, nw};
   const int cands[4] = {128, 64, 32, 16};
   bool found = false;
   if (nsteps <= 16) {
@@ -664,7 +686,31 @@ GemmShape choose_shape(int M, int N, int nsteps, int max_bm, int xsb, int pref_k
   return sh;
 }
 
-template <int BM, int KG, class P>
+// Measured launch shapes for the Llama-3 8B / 70B linears (experiments/sweep_nw.py ->
+// experiments/gen_gemm_table.py; profiles/r2_sweep_nw_wide*.jsonl): where a swept shape beat
+// choose_shape (and, for int8-dyn, the LDS-kernel choice) by >= 7% on the box. M is bucketed up
+// to 16 / 32 / ... / 512; other shapes and M > 512 keep the heuristic. Any shape is correct and
+// deterministic; a table shape only changes speed (and, through kg / splits, the fixed fp32
+// summation order).
+struct TunedShape {
+  int path, m, n, k, bm, kg, splits, nw;
+};
+constexpr TunedShape kTuned[] = {
+#include "gemm_table.inc"
+};
+
+const TunedShape* tuned_shape(int path, int M, int N, int K) {
+  if (tuning().gemm_table == 1 || tuning().bm || tuning().kg || tuning().splits ||
+      tuning().gemm_nw || M > 512)
+    return nullptr;
+  int mb = 16;
+  while (mb < M) mb *= 2;
+  for (const TunedShape& t : kTuned)
+    if (t.path == path && t.m == mb && t.n == N && t.k == K) return &t;
+  return nullptr;
+}
+
+template <int BM, int KG, int NW, class P>
 void launch_one(dim3 grid, hipStream_t stream, const uint8_t* xb, const P& pol,
                 const uint16_t* bias, uint16_t* y, int M, int N, int K, int sps,
                 typename P::Acc* slab, unsigned* cnt) {
@@ -674,7 +720,7 @@ void launch_one(dim3 grid, hipStream_t stream, const uint8_t* xb, const P& pol,
     constexpr bool big = sizeof(typename P::Chunk) > 32 || P::kABytes * P::kKStep > 256;
     constexpr int D = TAO_GEMM_DEPTH > 0 ? TAO_GEMM_DEPTH
                                          : (BM <= 16 ? 4 : (BM <= 32 ? (big ? 3 : 4) : 2));
-    launch((gemm_mfma_kernel<BM, D, KG, P>), grid, dim3(256 * KG), 0, stream, xb, pol, bias, y,
+    launch((gemm_mfma_kernel<BM, D, KG, NW, P>), grid, dim3(256 * KG), 0, stream, xb, pol, bias, y,
            M, N, K, sps, slab, cnt, tuning().splitk_fenced, tuning().gemm_order);
   }
 }
@@ -683,17 +729,31 @@ template <class P>
 int launch_gemm(const void* x, const P& pol, const uint16_t* bias, uint16_t* y, int M, int N,
                 int K, hipStream_t stream) {
   const int nsteps = (K + P::kKStep - 1) / P::kKStep;
-  GemmShape sh = choose_shape(M, N, nsteps, P::kMaxBM, P::kABytes * P::kKStep, P::kPrefKG,
-                              P::kMinSlice);
+  const int nw = tuning().gemm_nw == 2 ? 2 : 1;
+  GemmShape sh;
+  if (const TunedShape* t = tuned_shape(P::kPathId, M, N, K)) {
+    sh = GemmShape{t->bm < P::kMaxBM ? t->bm : P::kMaxBM, t->kg,
+                   t->splits < nsteps ? t->splits : nsteps, t->nw};
+    // as choose_shape's overrides were applied when the table was measured
+    while (sh.kg > 1 && sh.kg * sh.bm * P::kABytes * P::kKStep > 32768) sh.kg >>= 1;
+  } else {
+    sh = choose_shape(M, N, nsteps, P::kMaxBM, P::kABytes * P::kKStep, P::kPrefKG, P::kMinSlice,
+                      nw);
+  }
+  if (sh.nw == 2) {  // instantiated: BM <= 64, KG <= 2 (registers)
+    if (sh.bm > 64) sh.bm = 64;
+    if (sh.kg > 2) sh.kg = 2;
+  }
   const int sps = (nsteps + sh.splits - 1) / sh.splits;
   const int S = (nsteps + sps - 1) / sps;  // no empty slice
-  dim3 grid((N + kBN - 1) / kBN, (M + sh.bm - 1) / sh.bm, S);
+  const int bnw = kBN * sh.nw;
+  dim3 grid((N + bnw - 1) / bnw, (M + sh.bm - 1) / sh.bm, S);
   typename P::Acc* slab = nullptr;
   unsigned* cnt = nullptr;
   if (S > 1) {
     const size_t tiles = (size_t)grid.x * grid.y;
     void* ws = nullptr;
-    const int rc = split_workspace(stream, tiles * S * sh.bm * kBN * sizeof(float), tiles, &ws,
+    const int rc = split_workspace(stream, tiles * S * sh.bm * bnw * sizeof(float), tiles, &ws,
                                    &cnt);
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<typename P::Acc*>(ws);
@@ -701,16 +761,27 @@ int launch_gemm(const void* x, const P& pol, const uint16_t* bias, uint16_t* y, 
   const uint8_t* xb = reinterpret_cast<const uint8_t*>(x);
   const auto args = std::make_tuple(grid, stream, xb, pol, bias, y, M, N, K, sps, slab, cnt);
   auto go = [&](auto fn) { std::apply(fn, args); };
+  if (sh.nw == 2) {  // 32 columns per wave: each A fragment read feeds two MFMAs
+    switch (sh.bm * 8 + sh.kg) {
+      case 16 * 8 + 1: go(launch_one<16, 1, 2, P>); break;
+      case 16 * 8 + 2: go(launch_one<16, 2, 2, P>); break;
+      case 32 * 8 + 1: go(launch_one<32, 1, 2, P>); break;
+      case 32 * 8 + 2: go(launch_one<32, 2, 2, P>); break;
+      case 64 * 8 + 1: go(launch_one<64, 1, 2, P>); break;
+      default: go(launch_one<64, 2, 2, P>); break;
+    }
+    return check_launch("gemm_mfma_kernel");
+  }
   switch (sh.bm * 8 + sh.kg) {
-    case 16 * 8 + 1: go(launch_one<16, 1, P>); break;
-    case 16 * 8 + 2: go(launch_one<16, 2, P>); break;
-    case 16 * 8 + 4: go(launch_one<16, 4, P>); break;
-    case 32 * 8 + 1: go(launch_one<32, 1, P>); break;
-    case 32 * 8 + 2: go(launch_one<32, 2, P>); break;
-    case 32 * 8 + 4: go(launch_one<32, 4, P>); break;
-    case 64 * 8 + 1: go(launch_one<64, 1, P>); break;
-    case 64 * 8 + 2: go(launch_one<64, 2, P>); break;
-    default: go(launch_one<128, 1, P>); break;
+    case 16 * 8 + 1: go(launch_one<16, 1, 1, P>); break;
+    case 16 * 8 + 2: go(launch_one<16, 2, 1, P>); break;
+    case 16 * 8 + 4: go(launch_one<16, 4, 1, P>); break;
+    case 32 * 8 + 1: go(launch_one<32, 1, 1, P>); break;
+    case 32 * 8 + 2: go(launch_one<32, 2, 1, P>); break;
+    case 32 * 8 + 4: go(launch_one<32, 4, 1, P>); break;
+    case 64 * 8 + 1: go(launch_one<64, 1, 1, P>); break;
+    case 64 * 8 + 2: go(launch_one<64, 2, 1, P>); break;
+    default: go(launch_one<128, 1, 1, P>); break;
   }
   return check_launch("gemm_mfma_kernel");
 }
@@ -992,7 +1063,8 @@ int int8_scaled_mm_launch(const int8_t* xq, const uint16_t* xs, const int8_t* wq
   // N >= 14336; the per-wave-column kernel keeps M = 64..128 at N = 4096 (11.8 vs 12.6 µs).
   const int algo = tao::tuning().gemm_algo;
   const long t64 = (long)((N + 63) / 64) * ((M + 63) / 64);
-  if (K % kI8Step == 0 && (algo == 2 || (algo == 0 && M >= 128 && t64 >= 192)))
+  const bool tuned = algo == 0 && tuned_shape(Int8Dyn::kPathId, M, N, K) != nullptr;
+  if (K % kI8Step == 0 && !tuned && (algo == 2 || (algo == 0 && M >= 128 && t64 >= 192)))
     return launch_i8_lds(xq, xs, wq, ws, bias, y, M, N, K, algo == 0, stream);
   Int8Dyn pol;
   pol.w = reinterpret_cast<const uint4*>(wq);
@@ -1059,6 +1131,22 @@ extern "C" int tao_tune_gemm_order(int order) {
   TAO_CHECK_ARG(order == 0 || order == 1,
                 "tune: gemm order must be 0 (plain grid order) or 1 (XCD-grouped M tiles)");
   tao::tuning().gemm_order = order;
+  return TAO_OK;
+}
+
+// Columns per wave of the MFMA GEMMs: 0 = built-in, 1 = 16, 2 = 32 (each A fragment read from
+// LDS feeds two MFMAs). Calling thread only; for A/B measurement.
+extern "C" int tao_tune_gemm_nw(int nw) {
+  TAO_CHECK_ARG(nw >= 0 && nw <= 2, "tune: gemm nw must be 0 (auto), 1 or 2");
+  tao::tuning().gemm_nw = nw;
+  return TAO_OK;
+}
+
+// The measured shape table (gemm_table.inc): 0 = used (built-in), 1 = off (heuristic only).
+// Calling thread only; for A/B measurement.
+extern "C" int tao_tune_gemm_table(int off) {
+  TAO_CHECK_ARG(off == 0 || off == 1, "tune: gemm table must be 0 (on) or 1 (off)");
+  tao::tuning().gemm_table = off;
   return TAO_OK;
 }
 

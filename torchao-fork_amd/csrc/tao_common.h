@@ -52,6 +52,8 @@ struct Tuning {
   int attn_mode = 0;                             // decode attention (tao_tune_attn)
   int splitk_fenced = 0;                         // split-K hand-off with agent fences
   int gemm_order = 0;                            // MFMA GEMM tile order: 0 plain, 1 XCD-grouped
+  int gemm_nw = 0;                               // MFMA GEMM 16-col blocks per wave: 0 auto, 1, 2
+  int gemm_table = 0;                            // MFMA GEMM measured-shape table: 0 on, 1 off
 };
 Tuning& tuning();
 
