@@ -3,9 +3,10 @@
 For every configuration and every (bm, kg, splits), the 16-column (nw 1) and the 32-column
 (nw 2) kernel are timed (dispatch events, weights rotated past the MALL) and their outputs
 compared: the per-element accumulation order does not depend on nw, so they must be equal.
-One JSON line per configuration: auto time, best per nw, and every point.
+One JSON line per configuration: auto time, best per nw, and every point. For int4 the
+32x32x16 kernel (tao_tune_int4_mfma32) is swept too, recorded with nw = 32.
 
-    python experiments/sweep_nw.py [--quick] [--wide | --wide70]
+    python experiments/sweep_nw.py [--quick] [--wide | --wide70 | --int4]
     (--wide: 3 paths x 6 M x the Llama-3-8B linears; --wide70: the 70B linears and heads, plus
     int8-dyn at the 8B shapes with the product path's own kernel choice as "auto")
 """
@@ -31,13 +32,15 @@ LLAMA70B = ((10240, 8192), (8192, 8192), (57344, 8192), (8192, 28672), (128256, 
             (128256, 8192))
 MS = (16, 32, 64, 128, 256, 512)
 WIDE = [(p, M, N, K) for p in ("int4", "int8wo", "int8dyn") for M in MS for (N, K) in LLAMA8B]
+INT4 = [("int4", M, N, K) for M in MS for (N, K) in LLAMA8B + LLAMA70B]
 WIDE70 = ([(p, M, N, K) for p in ("int4", "int8wo", "int8dyn") for M in MS for (N, K) in LLAMA70B]
           + [("int8dyn", M, N, K) for M in MS for (N, K) in LLAMA8B])
 
 
 def main():
     quick = "--quick" in sys.argv
-    configs = WIDE if "--wide" in sys.argv else WIDE70 if "--wide70" in sys.argv else CONFIGS
+    configs = (WIDE if "--wide" in sys.argv else WIDE70 if "--wide70" in sys.argv
+               else INT4 if "--int4" in sys.argv else CONFIGS)
     mk = {"int4": make_int4, "int8wo": make_int8wo, "int8dyn": make_int8dyn}
     _lib.call("tao_tune_linear_crossover", 1)
     for path, M, N, K in configs[:4] if quick else configs:
@@ -66,6 +69,13 @@ def main():
                     best[nw] = (round(us, 2), [bm, kg, sp])
             if 2 in outs and not torch.equal(outs[1], outs[2]):
                 mismatches.append([bm, kg, sp])
+        if path == "int4":  # the 32x32x16 kernel, recorded as nw 32
+            _lib.call("tao_tune_gemm_nw", 0)
+            _lib.call("tao_tune_int4_mfma32", 1)
+            for bm, sp in itertools.product((32, 64), (1, 2, 4, 8)):
+                _lib.call("tao_tune_gemm", bm, 0, sp)
+                pts.append([bm, 1, sp, 32, round(kernel_us(run, launches), 2)])
+            _lib.call("tao_tune_int4_mfma32", 0)
         _lib.call("tao_tune_gemm", 0, 0, 0)
         _lib.call("tao_tune_gemm_nw", 0)
         _lib.call("tao_tune_gemm_algo", 0)

@@ -121,6 +121,9 @@ int tao_tune_gemm_nw(int nw);
 /* The MFMA GEMMs' measured launch-shape table for the Llama-3 linears (csrc/gemm_table.inc):
  * 0 = used (built-in), 1 = off (heuristic only). Calling thread only; for A/B measurement. */
 int tao_tune_gemm_table(int off);
+/* int4 MFMA GEMM kernel: 0 = built-in, 1 = the 32x32x16-MFMA kernel (gemm32_int4_kernel).
+ * Calling thread only; for A/B measurement. */
+int tao_tune_int4_mfma32(int on);
 
 /* M == 1 int4 linears without bias: 1 = stage x once per workgroup in LDS (the decode RMSNorm
  * prologue's copy, without the norm), 0 = built-in policy. Calling thread only; for sweeps. */

@@ -369,3 +369,31 @@ def test_tuned_shape_table(path, M, N, K):
     else:
         assert oracle.rel_l2(y_table, ref) < TOL_FP32
         assert oracle.rel_l2(y_table, y_heur) < TOL_FP32
+
+
+# the int4 GEMM on 32x32x16 MFMAs (tao_tune_int4_mfma32 1): M tiles 32 / 64, split-K, ragged
+# N / M / K, every group size, bias; against the oracle's fp32 accumulation of the same weights
+@pytest.mark.parametrize("M,N,K,g,bm,splits", [
+    (5, 328, 1056, 32, 0, 0), (48, 4096, 1024, 64, 0, 0), (70, 328, 1056, 32, 64, 3),
+    (129, 200, 352, 32, 32, 1), (300, 1024, 2048, 128, 64, 2), (128, 4096, 4096, 32, 0, 0),
+    (40, 72, 32, 32, 32, 1), (64, 640, 4096, 256, 32, 4)])
+def test_int4_mfma32_kernel(M, N, K, g, bm, splits):
+    w = oracle.make_linear_weight(N, K, seed=M + K)
+    s, z = oracle.int4_qparams(w, g)
+    q = oracle.int4_quantize(w, s, z, g)
+    x = oracle.make_activation(M, K, seed=M + 1)
+    bias = oracle.make_activation(1, N, seed=9).reshape(N)
+    packed = torch.ops.torchao.int4_pack(q.to(DEV))
+    sz = torch.stack([s, z], dim=-1).contiguous().to(DEV)
+    xd, bd = x.to(DEV), bias.to(DEV)
+    _lib.call("tao_tune_linear_crossover", 1)
+    _lib.call("tao_tune_int4_mfma32", 1)
+    _lib.call("tao_tune_gemm", bm, 0, splits)
+    try:
+        y = torch.ops.torchao.int4_weight_only_linear(xd, packed, sz, g, bd)
+        y2 = torch.ops.torchao.int4_weight_only_linear(xd, packed, sz, g, bd)
+    finally:
+        _lib.call("tao_tune_reset")
+    assert torch.equal(y, y2)
+    assert oracle.rel_l2(y.cpu(), oracle.int4_linear_fp32(x, q, s, z, g, bias)) < TOL_FP32
+    assert oracle.rel_l2(y.cpu(), oracle.int4_linear(x, q, s, z, g, bias)) < TOL_REF

@@ -691,7 +691,7 @@ GemmShape choose_shape(int M, int N, int nsteps, int max_bm, int xsb, int pref_k
 // choose_shape (and, for int8-dyn, the LDS-kernel choice) by >= 7% on the box. M is bucketed up
 // to 16 / 32 / ... / 512; other shapes and M > 512 keep the heuristic. Any shape is correct and
 // deterministic; a table shape only changes speed (and, through kg / splits, the fixed fp32
-// summation order).
+// summation order). nw 32 (int4 only) names gemm32_int4_kernel with that (bm, splits).
 struct TunedShape {
   int path, m, n, k, bm, kg, splits, nw;
 };
@@ -740,6 +740,7 @@ int launch_gemm(const void* x, const P& pol, const uint16_t* bias, uint16_t* y, 
     sh = choose_shape(M, N, nsteps, P::kMaxBM, P::kABytes * P::kKStep, P::kPrefKG, P::kMinSlice,
                       nw);
   }
+  if (sh.nw == 32) sh.nw = 1;  // (the 32x32x16 kernel's entries are dispatched before this)
   if (sh.nw == 2) {  // instantiated: BM <= 64, KG <= 2 (registers)
     if (sh.bm > 64) sh.bm = 64;
     if (sh.kg > 2) sh.kg = 2;
@@ -1034,6 +1035,289 @@ int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const 
   return check_launch("gemm_i8_lds_kernel");
 }
 
+// ---- int4 weight-only GEMM on 32x32x16 MFMAs (gemm32_int4_kernel) -----------------------------
+// §4.2's variants put the int4 GEMM's time on the per-wave work around each MFMA: an A-fragment
+// LDS read (1 KiB) and a B-fragment dequant (8 weights per lane) per 8 K MACs of
+// v_mfma_f32_16x16x32_bf16. v_mfma_f32_32x32x16_bf16 does 16 K MACs with the same two fragment
+// sizes (cdna guide §MFMA operand maps: lane (r = l & 31, h = l >> 5) holds A[r][8h + j] and
+// B[8h + j][r]), so per MAC both halve.
+// * Workgroup: 4 waves x 32 columns (128 columns) x BM rows (MT = BM / 32 tiles per wave).
+// * Step = 256 k. The k order inside a step is permuted identically for A and B: lane half h
+//   owns physical k [128 h, 128 h + 128) of the step, and MFMA s (0..15) takes k 128 h + 8 s + j
+//   from each half. So a lane's B operand for the whole step is 64 contiguous nibble bytes of
+//   its column (16 dwords, dword s -> MFMA s, already in k order for the fp8 dequant), and its A
+//   operand for MFMA s is 16 contiguous bytes of the x image (slot 16 h + s).
+// * Weights: full 128-B lines (lane l of load i: row 8 i + l / 8, 16-B chunk l % 8), regrouped
+//   through a 4-KiB per-wave LDS stage ([32 rows][8 chunks], stage_slot swizzle: conflict-free
+//   for the 2-row write passes and the 16-row read passes).
+// * x: the double-buffered [BM][32 slots] image of gemm_mfma_kernel (lds_slot swizzle), one
+//   barrier per step; (scale, zero): the lane's 4 groups of 32 k (one 16-B load at g = 32).
+// * Split-K over gridDim.z with gemm_mfma_kernel's slab hand-off (last_arriver); bf16(acc)
+//   (+ bias, rounded) as the Int4WO epilogue: results within fp32 re-association of it.
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+template <int BM, int D, bool G32>
+__global__ __launch_bounds__(256) void gemm32_int4_kernel(
+    const uint8_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
+    int gshift, const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K,
+    int sps, f32x16_t* __restrict__ slab, unsigned* __restrict__ cnt, int fenced) {
+  constexpr int MT = BM / 32;
+  constexpr int SLOTS = 32;                  // 16-B x slots per row per step (512 B)
+  constexpr int RPP = 256 / SLOTS;           // x rows per 256-thread pass
+  constexpr int XLOADS = BM * SLOTS / 256;   // x pieces per thread per step
+  constexpr int TILE = BM * SLOTS;           // uint4 per x image
+  constexpr int STAGE = 256;                 // uint4 per wave weight stage (32 rows x 8 chunks)
+  static_assert(BM == 32 || BM == 64, "BM 32 or 64");
+  __shared__ uint4 lds[2 * TILE + 4 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int n_blk = blockIdx.x * 128, m_blk = blockIdx.y * BM;
+  const int nw0 = n_blk + wave * 32;
+  const int nsteps = (K + 255) / 256;
+  const int s0 = blockIdx.z * sps;
+  const int s1 = s0 + sps < nsteps ? s0 + sps : nsteps;  // launcher: no empty slice
+  const int J = s1 - s0;
+  const int row_bytes = K * 2;
+  uint4* xs = lds;
+  uint4* wstage = lds + 2 * TILE + wave * STAGE;
+
+  // weights: 4 full-line pieces per lane per step; (scale, zero): lane (r, h)'s 4 groups
+  const uint32_t wrow = (uint32_t)(K >> 1);
+  const Rsrc wrs = make_rsrc(wq, (uint32_t)N * wrow);
+  uint32_t wv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = nw0 + 8 * i + (lane >> 3);
+    wv[i] = (uint32_t)(n < N ? n : N - 1) * wrow + 16 * (lane & 7);
+  }
+  const uint32_t zrow = (uint32_t)(K >> 5 >> gshift);  // (scale, zero) dwords per row
+  const Rsrc zrs = make_rsrc(sz, (uint32_t)N * zrow * 4u);
+  const int ncol = nw0 + r;
+  const uint32_t zv = (uint32_t)(ncol < N ? ncol : N - 1) * zrow * 4u;
+
+  // x pieces: rows row0 + RPP i, slot xslot (rows past M clamped, k tail masked at the store)
+  const int row0 = tid / SLOTS, xslot = tid % SLOTS;
+  const Rsrc xrs = make_rsrc(x, (uint32_t)M * (uint32_t)row_bytes);
+  uint32_t xv[XLOADS];
+  int xl[XLOADS];
+#pragma unroll
+  for (int i = 0; i < XLOADS; ++i) {
+    const int gm = m_blk + row0 + RPP * i;
+    xv[i] = (uint32_t)(gm < M ? gm : M - 1) * (uint32_t)row_bytes + xslot * 16;
+    xl[i] = lds_slot<SLOTS>(row0 + RPP * i, xslot);
+  }
+  const bool ragged = (row_bytes % 512) != 0;
+
+  struct WChunk {
+    uint4 p[4];
+    uint32_t z[4];
+  };
+  uint4 xr[D][XLOADS];
+  WChunk wr[D];
+  f32x16_t acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+
+  auto load_step = [&](int j, uint4 (&xd)[XLOADS], WChunk& wd) __attribute__((always_inline)) {
+    const int st0 = s0 + j;
+    const int st = st0 < s1 ? st0 : s1 - 1;
+#pragma unroll
+    for (int i = 0; i < XLOADS; ++i) xd[i] = bload16(xrs, xv[i], st * 512);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wd.p[i] = bload16<kNT>(wrs, wv[i], st * 128);
+    if constexpr (G32) {  // groups 8 st + 4 h .. + 3: one 16-B load
+      const uint4 z4 = bload16<kNT>(zrs, zv + 16 * h, st * 32);
+      wd.z[0] = z4.x;
+      wd.z[1] = z4.y;
+      wd.z[2] = z4.z;
+      wd.z[3] = z4.w;
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        wd.z[c] = bload4<kNT>(zrs, zv, (uint32_t)(((8 * st + 4 * h + c) >> gshift) * 4));
+    }
+  };
+  auto store_x = [&](const uint4 (&src)[XLOADS], int j) __attribute__((always_inline)) {
+    const int st = s0 + j;
+    uint4* dst = xs + (j & 1) * TILE;
+    if (!ragged && st < s1) {
+#pragma unroll
+      for (int i = 0; i < XLOADS; ++i) dst[xl[i]] = src[i];
+    } else {
+      const uint32_t keep = st < s1 && st * 512 + xslot * 16 < row_bytes ? ~0u : 0u;
+#pragma unroll
+      for (int i = 0; i < XLOADS; ++i)
+        dst[xl[i]] =
+            make_uint4(src[i].x & keep, src[i].y & keep, src[i].z & keep, src[i].w & keep);
+    }
+  };
+  auto body = [&](auto uc, int j) __attribute__((always_inline)) {
+    constexpr int u = decltype(uc)::value;
+    load_step(j + D - 1, xr[(u + D - 1) % D], wr[(u + D - 1) % D]);
+    {
+      const WChunk& wc = wr[u];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) wstage[stage_slot(8 * i + (lane >> 3), lane & 7)] = wc.p[i];
+      uint32_t w[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = wstage[stage_slot(r, 4 * h + q)];
+        w[4 * q] = v.x;
+        w[4 * q + 1] = v.y;
+        w[4 * q + 2] = v.z;
+        w[4 * q + 3] = v.w;
+      }
+      float sc[4], zc[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        sc[c] = bf16lo_to_f32(wc.z[c]);
+        zc[c] = bf16hi_to_f32(wc.z[c]) - 8.f * sc[c];  // q*s + zc == (q-8)*s + z
+      }
+      const uint4* xb = xs + (j & 1) * TILE;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const uint32_t wd = w[s];
+        const float scl = sc[s >> 2], zcl = zc[s >> 2];
+        const uint32_t lo = wd & 0x0F0F0F0Fu, hi = (wd >> 4) & 0x0F0F0F0Fu;
+        const f32x2_t q04 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(lo, 512.f, false);
+        const f32x2_t q15 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(lo, 512.f, true);
+        const f32x2_t q26 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, false);
+        const f32x2_t q37 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, true);
+        const f32x2_t sv = {scl, scl}, zvv = {zcl, zcl};
+        const f32x2_t w04 = q04 * sv + zvv, w15 = q15 * sv + zvv;
+        const f32x2_t w26 = q26 * sv + zvv, w37 = q37 * sv + zvv;
+        const bf16x8_t b = as_bf16x8(pack_bf16x2(w04[0], w15[0]), pack_bf16x2(w26[0], w37[0]),
+                                     pack_bf16x2(w04[1], w15[1]), pack_bf16x2(w26[1], w37[1]));
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          const uint4 a = xb[lds_slot<SLOTS>(32 * t + r, 16 * h + s)];
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), b,
+                                                           acc[t], 0, 0, 0);
+        }
+      }
+    }
+    if (j + 1 < J) store_x(xr[(u + 1) % D], j + 1);
+    __syncthreads();
+  };
+
+  static_for<0, D - 1>([&](auto i) __attribute__((always_inline)) {
+    load_step(decltype(i)::value, xr[decltype(i)::value], wr[decltype(i)::value]);
+  });
+  store_x(xr[0], 0);
+  __syncthreads();
+  int j = 0;
+  for (; j + D <= J; j += D)
+    static_for<0, D>([&](auto uc) __attribute__((always_inline)) {
+      body(uc, j + decltype(uc)::value);
+    });
+  static_for<0, D - 1>([&](auto uc) __attribute__((always_inline)) {
+    if (j + decltype(uc)::value < J) body(uc, j + decltype(uc)::value);
+  });
+
+  const int S = gridDim.z;
+  if (S > 1) {  // gemm_mfma_kernel's slab hand-off, 64-B accumulators
+    const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const size_t tile_bytes = (size_t)S * 4 * MT * 64 * sizeof(f32x16_t);
+    const Rsrc srs = make_rsrc(reinterpret_cast<const uint8_t*>(slab) + tile * tile_bytes,
+                               (uint32_t)tile_bytes);
+    const uint32_t lane_off = (uint32_t)((wave * MT * 64 + lane) * sizeof(f32x16_t));
+    constexpr uint32_t kZ = 4 * MT * 64 * sizeof(f32x16_t);
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        bstore16<kSC1>(srs, lane_off + t * 64 * sizeof(f32x16_t) + 16 * q, blockIdx.z * kZ,
+                       make_uint4(__float_as_uint(acc[t][4 * q]), __float_as_uint(acc[t][4 * q + 1]),
+                                  __float_as_uint(acc[t][4 * q + 2]),
+                                  __float_as_uint(acc[t][4 * q + 3])));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bool last =
+        last_arriver(&cnt[tile], (unsigned)S, reinterpret_cast<unsigned*>(lds), fenced);
+    if (!last) return;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    for (int z = 0; z < S; ++z) {  // slices summed in slice order
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint4 v =
+              bload16<kSC1>(srs, lane_off + t * 64 * sizeof(f32x16_t) + 16 * q, z * kZ);
+          acc[t][4 * q] += __uint_as_float(v.x);
+          acc[t][4 * q + 1] += __uint_as_float(v.y);
+          acc[t][4 * q + 2] += __uint_as_float(v.z);
+          acc[t][4 * q + 3] += __uint_as_float(v.w);
+        }
+    }
+  }
+
+  // C/D map (32x32x16): col = lane & 31, row = (i & 3) + 8 (i >> 2) + 4 h
+  if (ncol < N) {
+    const float bv = bias != nullptr ? bf16_to_f32(bias[ncol]) : 0.f;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = m_blk + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (m < M) {
+          float v = round_bf16(acc[t][i]);
+          if (bias != nullptr) v = round_bf16(v + bv);
+          y[(size_t)m * N + ncol] = f32_to_bf16(v);
+        }
+      }
+  }
+}
+
+// Launch shape of gemm32_int4_kernel: BM 64 where it gives >= 96 tiles of 128 columns, else 32;
+// K split until the grid reaches ~256 workgroups with slices of >= 4 steps (1024 k).
+int launch_gemm32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int gshift,
+                       const uint16_t* bias, uint16_t* y, int M, int N, int K,
+                       hipStream_t stream, int tbm = 0, int tsplits = 0) {
+  const int nsteps = (K + 255) / 256;
+  const long nb = (N + 127) / 128;
+  int bm = (M > 32 && nb * ((M + 63) / 64) >= 96) ? 64 : 32;
+  int splits = 1;
+  const long tiles = nb * ((M + bm - 1) / bm);
+  while (tiles * splits * 2 <= 320 && nsteps >= 4 * splits * 2 && splits < 8) splits *= 2;
+  const int tb = tbm ? tbm : tuning().bm, ts = tsplits ? tsplits : tuning().splits;
+  if (tb == 32 || tb == 64) bm = tb;
+  if (ts) splits = ts < nsteps ? ts : nsteps;
+  const int sps = (nsteps + splits - 1) / splits;
+  const int S = (nsteps + sps - 1) / sps;
+  const dim3 grid((unsigned)nb, (unsigned)((M + bm - 1) / bm), (unsigned)S);
+  f32x16_t* slab = nullptr;
+  unsigned* cnt = nullptr;
+  if (S > 1) {
+    void* ws = nullptr;
+    const size_t t = (size_t)grid.x * grid.y;
+    const int rc = split_workspace(stream, t * S * bm * 128 * sizeof(float), t, &ws, &cnt);
+    if (rc != TAO_OK) return rc;
+    slab = reinterpret_cast<f32x16_t*>(ws);
+  }
+  const uint8_t* xb = reinterpret_cast<const uint8_t*>(x);
+  const uint4* w = reinterpret_cast<const uint4*>(packed);
+  const uint32_t* z = reinterpret_cast<const uint32_t*>(sz);
+  auto go = [&](auto kern) {
+    launch(kern, grid, dim3(256), 0, stream, xb, w, z, gshift, bias, y, M, N, K, sps, slab, cnt,
+           tuning().splitk_fenced);
+  };
+  if (bm == 64) {
+    if (gshift == 0) go(gemm32_int4_kernel<64, 2, true>);
+    else go(gemm32_int4_kernel<64, 2, false>);
+  } else {
+    if (gshift == 0) go(gemm32_int4_kernel<32, 3, true>);
+    else go(gemm32_int4_kernel<32, 3, false>);
+  }
+  return check_launch("gemm32_int4_kernel");
+}
+
 // Largest M served by the GEMV kernels (tao_tune_linear_crossover; 0 = built-in).
 // Built-in crossover (experiments/bench_paths.py --crossover): the GEMV wins at M <= 2, and at
 // M <= 4 for small weights; the MFMA kernel's per-M cost is nearly flat.
@@ -1085,6 +1369,14 @@ extern "C" int tao_int4wo_linear_bf16(const uint16_t* x, const uint32_t* packed,
   hipStream_t st = tao::as_stream(stream);
   if (tao::use_gemv(M, N, K))
     return tao::int4wo_gemv(x, packed, sz, bias, y, M, N, K, group_size, st);
+  if (tao::tuning().int4_mfma32 == 1)  // 32x32x16 MFMA kernel (tao_tune_int4_mfma32)
+    return tao::launch_gemm32_int4(x, packed, sz, tao::gshift_of(group_size), bias, y, (int)M,
+                                   (int)N, (int)K, st);
+  // measured table entries with nw 32 name the 32x32x16 kernel and its (bm, splits)
+  if (const tao::TunedShape* t = tao::tuned_shape(tao::Int4WO::kPathId, (int)M, (int)N, (int)K))
+    if (t->nw == 32)
+      return tao::launch_gemm32_int4(x, packed, sz, tao::gshift_of(group_size), bias, y, (int)M,
+                                     (int)N, (int)K, st, t->bm, t->splits);
   tao::Int4WO pol;
   pol.wq = reinterpret_cast<const uint4*>(packed);
   pol.sz = reinterpret_cast<const uint32_t*>(sz);
@@ -1147,6 +1439,14 @@ extern "C" int tao_tune_gemm_nw(int nw) {
 extern "C" int tao_tune_gemm_table(int off) {
   TAO_CHECK_ARG(off == 0 || off == 1, "tune: gemm table must be 0 (on) or 1 (off)");
   tao::tuning().gemm_table = off;
+  return TAO_OK;
+}
+
+// int4 MFMA GEMM kernel: 0 = built-in (gemm_mfma_kernel), 1 = gemm32_int4_kernel (32x32x16).
+// Calling thread only; for A/B measurement.
+extern "C" int tao_tune_int4_mfma32(int on) {
+  TAO_CHECK_ARG(on == 0 || on == 1, "tune: int4 mfma32 must be 0 or 1");
+  tao::tuning().int4_mfma32 = on;
   return TAO_OK;
 }
 

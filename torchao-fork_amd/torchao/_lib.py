@@ -43,6 +43,7 @@ _SIGNATURES = {
     "tao_tune_gemm_order": [_int],
     "tao_tune_gemm_nw": [_int],
     "tao_tune_gemm_table": [_int],
+    "tao_tune_int4_mfma32": [_int],
     "tao_tune_int4_xlds": [_int],
     "tao_tune_int4_norm": [_int],
     "tao_tune_reset": [],

@@ -24,6 +24,7 @@ _KNOBS = {
     "gemm_order": ("tao_tune_gemm_order", 1),
     "gemm_nw": ("tao_tune_gemm_nw", 1),
     "gemm_table": ("tao_tune_gemm_table", 1),
+    "int4_mfma32": ("tao_tune_int4_mfma32", 1),
     "int4_xlds": ("tao_tune_int4_xlds", 1),
     "int4_norm": ("tao_tune_int4_norm", 1),
     "int8_gemv": ("tao_tune_int8_gemv", 3),
