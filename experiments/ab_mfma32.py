@@ -23,7 +23,7 @@ def main():
         _lib.call("tao_tune_int4_mfma32", 1)
         rec["mfma32_auto_us"] = round(kernel_us(run, launches, reps=30), 2)
         pts = []
-        for bm in (32, 64):
+        for bm in (32, 64, 128):
             for sp in (1, 2, 4, 8):
                 _lib.call("tao_tune_gemm", bm, 0, sp)
                 pts.append([bm, sp, round(kernel_us(run, launches, reps=30), 2)])

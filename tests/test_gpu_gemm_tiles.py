@@ -333,9 +333,11 @@ def test_two_column_blocks_per_wave_equal_one(gemm_nw, bm, kg, splits):
 
 # entries of the measured shape table (gemm_table.inc) against the heuristic shape and the
 # oracle: int4 M=64 6144x4096 (64, 1, 4), int8-wo M=128 28672x4096 (nw 2), int8-dyn M=64
-# 6144x4096 (the template kernel in place of the heuristic's), int4 M=100 -> the M=128 bucket
+# 6144x4096 (the template kernel in place of the heuristic's), int4 M=100 -> the M=128 bucket,
+# int4 M=128 28672x4096 (nw 32: the 32x32x16-MFMA kernel)
 @pytest.mark.parametrize("path,M,N,K", [("int4", 64, 6144, 4096), ("int8wo", 128, 28672, 4096),
-                                        ("int8dyn", 64, 6144, 4096), ("int4", 100, 6144, 4096)])
+                                        ("int8dyn", 64, 6144, 4096), ("int4", 100, 6144, 4096),
+                                        ("int4", 128, 28672, 4096)])
 def test_tuned_shape_table(path, M, N, K):
     g = 32
     w = oracle.make_linear_weight(N, K, seed=N + M)

@@ -1067,7 +1067,7 @@ __global__ __launch_bounds__(256) void gemm32_int4_kernel(
   constexpr int XLOADS = BM * SLOTS / 256;   // x pieces per thread per step
   constexpr int TILE = BM * SLOTS;           // uint4 per x image
   constexpr int STAGE = 256;                 // uint4 per wave weight stage (32 rows x 8 chunks)
-  static_assert(BM == 32 || BM == 64, "BM 32 or 64");
+  static_assert(BM == 32 || BM == 64 || BM == 128, "BM 32, 64 or 128");
   __shared__ uint4 lds[2 * TILE + 4 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1287,7 +1287,7 @@ int launch_gemm32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t
   const long tiles = nb * ((M + bm - 1) / bm);
   while (tiles * splits * 2 <= 320 && nsteps >= 4 * splits * 2 && splits < 8) splits *= 2;
   const int tb = tbm ? tbm : tuning().bm, ts = tsplits ? tsplits : tuning().splits;
-  if (tb == 32 || tb == 64) bm = tb;
+  if (tb == 32 || tb == 64 || tb == 128) bm = tb;
   if (ts) splits = ts < nsteps ? ts : nsteps;
   const int sps = (nsteps + splits - 1) / splits;
   const int S = (nsteps + sps - 1) / sps;
@@ -1308,7 +1308,10 @@ int launch_gemm32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t
     launch(kern, grid, dim3(256), 0, stream, xb, w, z, gshift, bias, y, M, N, K, sps, slab, cnt,
            tuning().splitk_fenced);
   };
-  if (bm == 64) {
+  if (bm == 128) {  // x ring: one step in flight (2 stages, one live)
+    if (gshift == 0) go(gemm32_int4_kernel<128, 2, true>);
+    else go(gemm32_int4_kernel<128, 2, false>);
+  } else if (bm == 64) {
     if (gshift == 0) go(gemm32_int4_kernel<64, 2, true>);
     else go(gemm32_int4_kernel<64, 2, false>);
   } else {
