@@ -42,6 +42,8 @@ Reported (one JSON line, rank 0):
   reference_gpu = the reference's own GPU kernel (PyTorch-ROCm aten._weight_int4pack_mm, which
                  torchao's TensorCoreTiledLayout calls) on the identical weights and step, one
                  HIP graph: its GB/s and the max rel. L2 difference from our outputs
+  config2_shapes = BASELINE config 2's shapes (4096x4096, 11008x4096, 4096x11008; int4 g32,
+                 M = 1): us per launch in a graph of 32 distinct weights, GB/s, fraction of 8 TB/s
   prefill_mfma = BASELINE config 3 (int8 dyn-act int8-weight linear, M = 128, 4096x4096, the
                  int8 MFMA path) and the int4 g32 linear at M = 128 on its bf16 MFMA path:
                  kernel us, TOPS, fraction of the dense MFMA peak, attainable-roofline fraction
@@ -268,6 +270,49 @@ def reference_gpu_step(plan, xs, g, device, steps):
     del packs, outs, graph
     torch.cuda.empty_cache()
     return ms, diff
+
+
+def config2_shapes(device, g=32, copies=32, reps=20):
+    """BASELINE config 2's named shapes (int4 g32 WO linear, M = 1: 4096x4096, 11008x4096 and
+    4096x11008, the 7B-class FFN width): us per launch inside a HIP graph of `copies` launches
+    over distinct weights (rotated past the 256 MiB MALL), HIP events on the replay stream."""
+    from torchao import _lib
+
+    lib = _lib.lib()
+    out = {}
+    for (N, K) in ((4096, 4096), (11008, 4096), (4096, 11008)):
+        ws = [make_int4_weight(N, K, g, seed=7 * i + N, device=device) for i in range(copies)]
+        x = torch.randn(1, K, device=device, dtype=torch.bfloat16)
+        y = torch.empty(N, device=device, dtype=torch.bfloat16)
+        stream = torch.cuda.Stream(device)
+
+        def run():
+            sp = torch.cuda.current_stream(device).cuda_stream
+            for packed, sz in ws:
+                rc = lib.tao_int4wo_linear_bf16(x.data_ptr(), packed.data_ptr(), sz.data_ptr(),
+                                                None, y.data_ptr(), 1, N, K, g, sp)
+                if rc:
+                    raise RuntimeError(lib.tao_last_error().decode())
+
+        stream.wait_stream(torch.cuda.current_stream(device))
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(stream):
+            run()
+            with torch.cuda.graph(graph, stream=stream):
+                run()
+            graph.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                graph.replay()
+            e1.record(stream)
+        e1.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps / copies
+        b = int4_alg_bytes(N, K, g)
+        out[f"{N}x{K}"] = {"us": round(us, 3), "GBps": round(b / (us * 1e-6) / 1e9, 1),
+                           "frac": round(b / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)}
+        del graph, ws
+    return out
 
 
 def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
@@ -768,6 +813,7 @@ def main():
     prefill = None
     if P == 1 and args.model == "8b" and not args.no_prefill:
         prefill = prefill_mfma(device)
+    config2 = config2_shapes(device) if P == 1 and args.model == "8b" else None
 
     cpu = None
     if rank == 0 and P == 1 and not args.no_cpu_baseline and args.model == "8b":
@@ -843,6 +889,8 @@ def main():
                 rec["speedup_vs_reference_gpu"] = round(rec["value"] / ref_gpu["value"], 2)
         if prefill is not None:
             rec["prefill_mfma"] = prefill
+        if config2 is not None:
+            rec["config2_shapes"] = config2
         if P == 1 and args.model == "8b" and not args.no_e2e:
             rec["e2e_decode"] = e2e_decode()
         if comm_ms is not None:
