@@ -483,6 +483,11 @@ M1Shape m1_shape(int N, int S) {
   if (S <= 2) {  // K <= 4096
     if (N >= 32768) {
       c.sh = {2, 2};
+    } else if (N > 8192 && N < 16384) {  // 11008 (7B-class FFN, BASELINE config 2), 14336:
+      // 2 rows per wave, 2 waves along K, 2 row groups (profiles/r2_sweep_gemv_midN.jsonl:
+      // 11008x4096 6.91 vs 7.49 µs, 14336x4096 8.12 vs 8.40)
+      c.rpw = 2;
+      c.sh = {2, 2};
     } else if (N >= 8192) {  // one wave walks both slices of 4 rows (PAIR)
       c.occ = 4;
       c.sh = {1, N >= 16384 ? 4 : 1};
