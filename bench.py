@@ -272,6 +272,24 @@ def reference_gpu_step(plan, xs, g, device, steps):
     return ms, diff
 
 
+def hbm_copy_gbps(device, nbytes=1 << 30, reps=10):
+    """a copy kernel measured on the box beside the 8 TB/s spec peak (torch's
+    device copy of 1 GiB: read + write bytes / time, HIP events)."""
+    a = torch.empty(nbytes // 4, dtype=torch.int32, device=device).fill_(1)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    gbps = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return round(gbps, 1)
+
+
 def config2_shapes(device, g=32, copies=32, reps=20):
     """BASELINE config 2's named shapes (int4 g32 WO linear, M = 1: 4096x4096, 11008x4096 and
     4096x11008, the 7B-class FFN width): us per launch inside a HIP graph of `copies` launches
@@ -814,6 +832,7 @@ def main():
     if P == 1 and args.model == "8b" and not args.no_prefill:
         prefill = prefill_mfma(device)
     config2 = config2_shapes(device) if P == 1 and args.model == "8b" else None
+    copy_gbps = hbm_copy_gbps(device) if P == 1 else None
 
     cpu = None
     if rank == 0 and P == 1 and not args.no_cpu_baseline and args.model == "8b":
@@ -861,6 +880,7 @@ def main():
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
+                "measured_copy_GBps": copy_gbps,  # 1 GiB device copy on this box (read+write)
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
                 "traffic_unit": f"HBM bytes per step ({len(plan)} launches)",
