@@ -393,8 +393,18 @@ __device__ __forceinline__ void static_for(F&& f) {
 //    sums them in slice order and runs the epilogue. Both sums have a fixed order, so results
 //    do not depend on arrival order. Protocol and its hardware assumption: last_arriver()
 //    (tao_common.h); `fenced` adds the agent release/acquire fences (tao_tune_splitk_fenced).
+// Experiment switch (timing A/B only): minimum waves per SIMD the register allocation must
+// allow (amdgpu_waves_per_eu); 0 = the compiler's choice (the product).
+#ifndef TAO_GEMM_WPE
+#define TAO_GEMM_WPE 0
+#endif
+#if TAO_GEMM_WPE > 0
+#define TAO_GEMM_WPE_ATTR __attribute__((amdgpu_waves_per_eu(TAO_GEMM_WPE)))
+#else
+#define TAO_GEMM_WPE_ATTR
+#endif
 template <int BM, int D, int KG, int NW, class P>
-__global__ __launch_bounds__(256 * KG) void gemm_mfma_kernel(
+__global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int sps, typename P::Acc* __restrict__ slab,
     unsigned* __restrict__ cnt, int fenced, int order) {
