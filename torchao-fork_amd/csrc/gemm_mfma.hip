@@ -215,7 +215,10 @@ struct Int4WO {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), b, c, 0, 0, 0);
   }
   // int4 output: bf16(acc) (+ bias added by the caller, tensor_core_tiled_layout.py:104-114)
-  __device__ __forceinline__ float epilogue(float acc, int, int) const { return round_bf16(acc); }
+  static constexpr bool kRowF = false, kColF = false;  // no per-row / per-column factor
+  __device__ __forceinline__ const uint16_t* row_factor() const { return nullptr; }
+  __device__ __forceinline__ const uint16_t* col_factor() const { return nullptr; }
+  __device__ __forceinline__ float epi(float acc, float, float) const { return round_bf16(acc); }
 };
 
 struct Int8WO {
@@ -284,8 +287,11 @@ struct Int8WO {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), b, c, 0, 0, 0);
   }
   // bf16 mm output, then * scale (plain_layout.py:258-262)
-  __device__ __forceinline__ float epilogue(float acc, int, int n) const {
-    return round_bf16(round_bf16(acc) * bf16_to_f32(scale[n]));
+  static constexpr bool kRowF = false, kColF = true;
+  __device__ __forceinline__ const uint16_t* row_factor() const { return nullptr; }
+  __device__ __forceinline__ const uint16_t* col_factor() const { return scale; }
+  __device__ __forceinline__ float epi(float acc, float, float sc) const {
+    return round_bf16(round_bf16(acc) * sc);
   }
 };
 
@@ -355,9 +361,12 @@ struct Int8Dyn {
     return __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4_t, a), b, c, 0, 0, 0);
   }
   // bf16(c) * x_scale, * w_scale, each rounded (intmm.py:133-137, plain_layout.py:301-315)
-  __device__ __forceinline__ float epilogue(int acc, int m, int n) const {
-    const float v = round_bf16(round_bf16((float)acc) * bf16_to_f32(xscale[m]));
-    return round_bf16(v * bf16_to_f32(wscale[n]));
+  static constexpr bool kRowF = true, kColF = true;
+  __device__ __forceinline__ const uint16_t* row_factor() const { return xscale; }
+  __device__ __forceinline__ const uint16_t* col_factor() const { return wscale; }
+  __device__ __forceinline__ float epi(int acc, float xs, float ws) const {
+    const float v = round_bf16(round_bf16((float)acc) * xs);
+    return round_bf16(v * ws);
   }
 };
 
@@ -393,6 +402,16 @@ __device__ __forceinline__ void static_for(F&& f) {
 //    sums them in slice order and runs the epilogue. Both sums have a fixed order, so results
 //    do not depend on arrival order. Protocol and its hardware assumption: last_arriver()
 //    (tao_common.h); `fenced` adds the agent release/acquire fences (tao_tune_splitk_fenced).
+// Experiment switch (timing only, experiments/gemm_stamps.py): per-workgroup wall-clock stamps
+// (s_memrealtime, 100 MHz) of gemm_mfma_kernel's phases: setup done, prologue done (first
+// barrier), k loop done, k-group reduction done, end; slot 5 = 1 for a split-K last arriver,
+// slot 6 = the kernel's first instruction. Never in the product library.
+#ifndef TAO_GEMM_STAMPS
+#define TAO_GEMM_STAMPS 0
+#endif
+#if TAO_GEMM_STAMPS
+__device__ unsigned long long g_gemm_stamps[16384 * 8];
+#endif
 // Experiment switch (timing A/B only): minimum waves per SIMD the register allocation must
 // allow (amdgpu_waves_per_eu); 0 = the compiler's choice (the product).
 #ifndef TAO_GEMM_WPE
@@ -408,6 +427,9 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int sps, typename P::Acc* __restrict__ slab,
     unsigned* __restrict__ cnt, int fenced, int order) {
+#if TAO_GEMM_STAMPS
+  const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();  // before any setup
+#endif
   typedef typename P::Acc Acc;
   constexpr int MT = BM / 16;
   constexpr int XSB = P::kABytes * P::kKStep;  // x bytes per row per step (256 or 512)
@@ -538,11 +560,62 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
     if (TAO_GEMM_DEBUG != 4) __syncthreads();
   };
 
+#if TAO_GEMM_STAMPS
+  unsigned long long stamp[6] = {0, 0, 0, 0, 0, t_entry};
+  auto mark = [&](int i) __attribute__((always_inline)) {
+    if (tid == 0) stamp[i] = __builtin_amdgcn_s_memrealtime();
+  };
+  auto flush = [&](int last) __attribute__((always_inline)) {
+    if (tid < 64) {  // wave 0: lane i stores slot i (vector stores)
+      unsigned long long v = (unsigned long long)last;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const unsigned lo = __shfl((unsigned)stamp[i], 0), hi = __shfl((unsigned)(stamp[i] >> 32), 0);
+        if (lane == (i < 5 ? i : 6)) v = ((unsigned long long)hi << 32) | lo;
+      }
+      const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+      if (lane < 7 && b < 16384) g_gemm_stamps[b * 8 + lane] = v;
+    }
+  };
+#else
+  auto mark = [](int) {};
+  auto flush = [](int) {};
+#endif
+  // Epilogue operands loaded now, ahead of the weights: loaded in the epilogue, their round
+  // trip sat in every workgroup's tail (~1 µs of the int8-dyn M = 128 4096² kernel;
+  // experiments/gemm_stamps.py). Per lane: the row factor of its 4 rows per M tile (rows
+  // clamped to M - 1, kept as bf16 pairs), the column factor and bias of its NW columns.
+  // (the int4 policy has neither factor; its bias stays an epilogue load: prefetching that too
+  // measured 1.3 µs slower at M = 128, 4096², profiles/r2_ab_epi.txt)
+  constexpr bool kPre = P::kRowF || P::kColF;
+  uint2 rowf[P::kRowF ? MT : 1];
+  float colf[NW], biasf[NW];
+  if constexpr (P::kRowF) {
+    const uint16_t* rp = pol.row_factor();
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      uint32_t h[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m_blk + t * 16 + 4 * (lane >> 4) + i;
+        h[i] = rp[m < M ? m : M - 1];
+      }
+      rowf[t] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NW; ++c) {
+    const int nn = bn[c] < N ? bn[c] : N - 1;
+    colf[c] = P::kColF ? bf16_to_f32(pol.col_factor()[nn]) : 1.f;
+    biasf[c] = (kPre && bias != nullptr) ? bf16_to_f32(bias[nn]) : 0.f;
+  }
+  mark(0);
   static_for<0, D - 1>([&](auto i) __attribute__((always_inline)) {
     load_step(decltype(i)::value, xr[decltype(i)::value], wr[decltype(i)::value]);
   });
   store_x(xr[0], 0);
   __syncthreads();
+  mark(1);
 
   int j = 0;
   for (; j + D <= J; j += D)
@@ -552,6 +625,7 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
   static_for<0, D - 1>([&](auto uc) __attribute__((always_inline)) {
     if (j + decltype(uc)::value < J) body(uc, j + decltype(uc)::value);
   });
+  mark(2);
 
   // k-groups 1..KG-1 hand their accumulators to k-group 0 through LDS (summed in order)
   if constexpr (KG > 1) {
@@ -569,6 +643,7 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
     }
     __syncthreads();  // LDS free again (the split-K flag below reuses it)
   }
+  mark(3);
 
   const int S = gridDim.z;
   if (S > 1) {
@@ -595,7 +670,11 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
     __syncthreads();
     const bool last =
         last_arriver(&cnt[tile], (unsigned)S, reinterpret_cast<unsigned*>(lds), fenced);
-    if (!last || kg != 0) return;
+    if (!last || kg != 0) {
+      mark(4);
+      flush(0);
+      return;
+    }
 #pragma unroll
     for (int t = 0; t < NA; ++t) acc[t] = Acc{0, 0, 0, 0};
     // 4 slabs per round, all loads issued before the first add (clamped, then masked); slices
@@ -626,21 +705,28 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
 #pragma unroll
   for (int c = 0; c < NW; ++c) {
     if (bn[c] < N) {
-      const float bv = bias != nullptr ? bf16_to_f32(bias[bn[c]]) : 0.f;
+      if constexpr (!kPre) biasf[c] = bias != nullptr ? bf16_to_f32(bias[bn[c]]) : 0.f;
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int m = m_blk + t * 16 + 4 * (lane >> 4) + i;
           if (m < M) {
-            float v = pol.epilogue(acc[t * NW + c][i], m, bn[c]);
-            if (bias != nullptr) v = round_bf16(v + bv);
+            float rf = 1.f;
+            if constexpr (P::kRowF) {
+              const uint32_t w = (i < 2) ? rowf[t].x : rowf[t].y;
+              rf = (i & 1) ? bf16hi_to_f32(w) : bf16lo_to_f32(w);
+            }
+            float v = pol.epi(acc[t * NW + c][i], rf, colf[c]);
+            if (bias != nullptr) v = round_bf16(v + biasf[c]);
             y[(size_t)m * N + bn[c]] = f32_to_bf16(v);
           }
         }
       }
     }
   }
+  mark(4);
+  flush(S > 1 ? 1 : 0);
 }
 
 // Launch shape: M tile, k-groups per workgroup and K slices. Per-workgroup time is set by its
@@ -859,6 +945,31 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
 #pragma unroll
     for (int b = 0; b < NT; ++b) acc[a][b] = i32x4_t{0, 0, 0, 0};
 
+  // Epilogue operands loaded up front (gemm_mfma_kernel's reason): the x scales of this lane's
+  // 4 rows per M tile as bf16 pairs (rows clamped), the w scale and bias of its NT columns.
+  uint2 xsf[MT];
+  float wsf[NT], bsf[NT];
+  {
+    const int q = (lane >> 4) & 3, c16 = lane & 15;
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+      uint32_t hh[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m_blk + wm * (BM / 2) + a * 16 + 4 * q + i;
+        hh[i] = xscale[m < M ? m : M - 1];
+      }
+      xsf[a] = make_uint2(hh[0] | (hh[1] << 16), hh[2] | (hh[3] << 16));
+    }
+#pragma unroll
+    for (int b = 0; b < NT; ++b) {
+      const int n = n_blk + wn * (BN / 2) + b * 16 + c16;
+      const int nn = n < N ? n : N - 1;
+      wsf[b] = bf16_to_f32(wscale[nn]);
+      bsf[b] = bias != nullptr ? bf16_to_f32(bias[nn]) : 0.f;
+    }
+  }
+
   uint4 xr[D][XL], wr[D][WL];
   auto load_step = [&](int j, uint4 (&xd)[XL], uint4 (&wd)[WL]) __attribute__((always_inline)) {
     const int st = s0 + j < s1 ? s0 + j : s1 - 1;  // past the slice: re-read (never predicated)
@@ -957,15 +1068,17 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
   for (int b = 0; b < NT; ++b) {
     const int n = n_blk + wn * (BN / 2) + b * 16 + fr;
     if (n >= N) continue;
-    const float sw = bf16_to_f32(wscale[n]);
-    const float bv = bias != nullptr ? bf16_to_f32(bias[n]) : 0.f;
+    const float sw = wsf[b];
+    const float bv = bsf[b];
 #pragma unroll
     for (int a = 0; a < MT; ++a)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = m_blk + wm * (BM / 2) + a * 16 + 4 * kq + i;
         if (m < M) {
-          float v = round_bf16(round_bf16((float)acc[a][b][i]) * bf16_to_f32(xscale[m]));
+          const uint32_t xw = (i < 2) ? xsf[a].x : xsf[a].y;
+          const float xsc = (i & 1) ? bf16hi_to_f32(xw) : bf16lo_to_f32(xw);
+          float v = round_bf16(round_bf16((float)acc[a][b][i]) * xsc);
           v = round_bf16(v * sw);
           if (bias != nullptr) v = round_bf16(v + bv);
           y[(size_t)m * N + n] = f32_to_bf16(v);
@@ -1457,6 +1570,17 @@ extern "C" int tao_tune_gemm_table(int off) {
 
 // int4 MFMA GEMM kernel: 0 = built-in (gemm_mfma_kernel), 1 = gemm32_int4_kernel (32x32x16).
 // Calling thread only; for A/B measurement.
+#if TAO_GEMM_STAMPS
+// timing builds only: copy the per-workgroup stamps (8 u64 per workgroup) and clear them
+extern "C" int tao_debug_gemm_stamps(unsigned long long* out, int n) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tao::g_gemm_stamps), (size_t)n * 8 * 8) != hipSuccess)
+    return TAO_ERR_HIP;
+  static unsigned long long zero[16384 * 8];
+  return hipMemcpyToSymbol(HIP_SYMBOL(tao::g_gemm_stamps), zero, sizeof(zero)) == hipSuccess
+             ? TAO_OK : TAO_ERR_HIP;
+}
+#endif
+
 extern "C" int tao_tune_int4_mfma32(int on) {
   TAO_CHECK_ARG(on == 0 || on == 1, "tune: int4 mfma32 must be 0 or 1");
   tao::tuning().int4_mfma32 = on;
