@@ -28,6 +28,11 @@
 #ifndef TAO_GEMV_DEBUG
 #define TAO_GEMV_DEBUG 0
 #endif
+// TAO_GEMV_STAMPS 1 (timing only, experiments/gemv_stamps.py): per-workgroup s_memrealtime
+// stamps of the plain M = 1 path: first instruction, slices done, end (wave 0 of each group).
+#ifndef TAO_GEMV_STAMPS
+#define TAO_GEMV_STAMPS 0
+#endif
 // TAO_NORM_DEBUG 1 (timing only): the RMSNorm prologue skips its cross-wave exchange.
 #ifndef TAO_NORM_DEBUG
 #define TAO_NORM_DEBUG 0
@@ -36,6 +41,9 @@
 namespace tao {
 
 TAO_DECODE_ERROR_WORD(int4gemv_decode_status)
+#if TAO_GEMV_STAMPS
+__device__ unsigned long long g_gemv_stamps[65536 * 4];
+#endif
 
 namespace {
 
@@ -85,6 +93,9 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
   static_assert(!(PRO || EPI) || (MT == 1 && RPW % 2 == 0), "fusions are M == 1, row pairs");
   constexpr int V = RPW * MT;
   extern __shared__ float red[];  // [G][Wk][V] (PRO: + [8] partial sums, + normalised x [K])
+#if TAO_GEMV_STAMPS
+  const unsigned long long st_entry = __builtin_amdgcn_s_memrealtime();
+#endif
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int wk = wave % Wk;
@@ -327,6 +338,9 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     }
   }
 
+#if TAO_GEMV_STAMPS
+  const unsigned long long st_loop = __builtin_amdgcn_s_memrealtime();
+#endif
 #if TAO_GEMV_DEBUG == 4 || TAO_GEMV_DEBUG >= 5
   if constexpr (EPI == kEpiNone && !PRO) {
     float t = 0.f;
@@ -382,6 +396,13 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
         y[(size_t)m * N + n] = out;
       }
     }
+#if TAO_GEMV_STAMPS
+    if (threadIdx.x < 64 && blockIdx.x < 65536) {  // wave 0: lane i stores stamp i
+      const unsigned long long st_end = __builtin_amdgcn_s_memrealtime();
+      const unsigned long long v = lane == 0 ? st_entry : lane == 1 ? st_loop : st_end;
+      if (lane < 3) g_gemv_stamps[blockIdx.x * 4 + lane] = v;
+    }
+#endif
   } else {
     // Row pair (2p, 2p+1) meets in lane p of the writing wave. Row r's total sits in lane r
     // (Wk > 1) or in owner lane r << (6 - T) (Wk == 1); every lane takes part in the shuffles.
@@ -625,6 +646,16 @@ int int4_check_linear_args(const uint16_t* x, const uint32_t* packed, const uint
 }
 
 }  // namespace tao
+
+#if TAO_GEMV_STAMPS
+extern "C" int tao_debug_gemv_stamps(unsigned long long* out, int n) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tao::g_gemv_stamps), (size_t)n * 4 * 8) != hipSuccess)
+    return TAO_ERR_HIP;
+  static unsigned long long zero[65536 * 4];
+  return hipMemcpyToSymbol(HIP_SYMBOL(tao::g_gemv_stamps), zero, sizeof(zero)) == hipSuccess
+             ? TAO_OK : TAO_ERR_HIP;
+}
+#endif
 
 extern "C" int tao_tune_int4_norm(int mode) {
   TAO_CHECK_ARG(mode == 0 || mode == 1, "tune: norm mode must be 0 (exact) or 1 (deferred)");
