@@ -555,6 +555,9 @@ def main():
                     help="skip timing PyTorch-ROCm's aten._weight_int4pack_mm on the same step")
     ap.add_argument("--no-prefill", action="store_true",
                     help="skip the config-3 MFMA prefill measurement (prefill_mfma)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip config2_shapes and the copy-bandwidth probe (profiler passes that "
+                         "attribute every launch to the step use this)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the config-4 e2e decode run (e2e_decode, a child process)")
     ap.add_argument("--shard-policy", default="auto",
@@ -831,8 +834,9 @@ def main():
     prefill = None
     if P == 1 and args.model == "8b" and not args.no_prefill:
         prefill = prefill_mfma(device)
-    config2 = config2_shapes(device) if P == 1 and args.model == "8b" else None
-    copy_gbps = hbm_copy_gbps(device) if P == 1 else None
+    extras = P == 1 and not args.no_extras
+    config2 = config2_shapes(device) if extras and args.model == "8b" else None
+    copy_gbps = hbm_copy_gbps(device) if extras else None
 
     cpu = None
     if rank == 0 and P == 1 and not args.no_cpu_baseline and args.model == "8b":
