@@ -23,10 +23,19 @@
 #ifndef TAO_ATTN_WAVES
 #define TAO_ATTN_WAVES 16  // waves per workgroup of the single-pass decode attention
 #endif
+// TAO_ATTN_STAMPS 1 (timing only, experiments/attn_stamps.py): per-workgroup s_memrealtime
+// stamps of attn_single_kernel: first instruction, q in registers, key loop done (per wave 0),
+// end. Never in the product library.
+#ifndef TAO_ATTN_STAMPS
+#define TAO_ATTN_STAMPS 0
+#endif
 
 namespace tao {
 
 TAO_DECODE_ERROR_WORD(decode_ops_status)
+#if TAO_ATTN_STAMPS
+__device__ unsigned long long g_attn_stamps[1024 * 4];
+#endif
 int int4gemv_decode_status(unsigned* bits);
 
 namespace {
@@ -259,6 +268,9 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
     int H, int Hkv, int T, float scale) {
+#if TAO_ATTN_STAMPS
+  const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
+#endif
   static_assert(D == 128, "head_dim 128");
   __shared__ float wm[NW], wl[NW];
   __shared__ float wo[NW][D];
@@ -307,6 +319,12 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     }
   }
 
+#if TAO_ATTN_STAMPS
+  float qsum = 0.f;  // forces the q loads to land before the stamp
+#pragma unroll
+  for (int i = 0; i < 32; ++i) qsum += qr[i];
+  const unsigned long long st1 = __builtin_amdgcn_s_memrealtime() + (qsum == 12345.f ? 1 : 0);
+#endif
   float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
   for (int t0 = wave * 16; t0 < L; t0 += NW * 16) {
     const int t = t0 + kq;
@@ -349,6 +367,9 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
   }
   if (lane == 0) {
     wm[wave] = m;
+#if TAO_ATTN_STAMPS
+    if (wave == 0) g_attn_stamps[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
     wl[wave] = l;
   }
   wo[wave][2 * lane] = o0;
@@ -369,6 +390,11 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     const float inv = 1.f / ls;
     reinterpret_cast<uint32_t*>(out)[(size_t)bh * (D / 2) + lane] =
         (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
+#if TAO_ATTN_STAMPS
+    const unsigned long long st3 = __builtin_amdgcn_s_memrealtime();
+    if (lane < 4 && lane != 2 && blockIdx.x < 1024)
+      g_attn_stamps[blockIdx.x * 4 + lane] = lane == 0 ? st0 : lane == 1 ? st1 : st3;
+#endif
   }
 }
 
@@ -724,6 +750,13 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
   }
   return check_launch("attn_decode");
 }
+#if TAO_ATTN_STAMPS
+extern "C" int tao_debug_attn_stamps(unsigned long long* out, int n) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tao::g_attn_stamps), (size_t)n * 4 * 8) != hipSuccess)
+    return TAO_ERR_HIP;
+  return TAO_OK;
+}
+#endif
 
 int tao_tune_attn(int mode) {
   TAO_CHECK_ARG(mode >= 0 && mode <= 3,
