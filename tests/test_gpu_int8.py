@@ -67,6 +67,37 @@ def test_int8dyn_vs_reference_fixtures(fname):
         assert torch.equal(y, bf16(rec[f"y_M{M}"]))
 
 
+def test_int8_empty_and_batched_shapes():
+    """Zero rows and leading batch dims, as torch.nn.functional.linear takes them: the int8
+    weight-only op, the per-token quant and the int8 x int8 op keep the batch shape and give
+    what the oracle gives row by row (zero rows launch nothing)."""
+    N, K = 96, 512
+    w = oracle.make_linear_weight(N, K, seed=5)
+    s8 = oracle.int8_weight_qparams(w)
+    q8 = oracle.int8_weight_quantize(w, s8)
+    wq, ws = oracle.int8_dyn_weight(w)
+    bias = oracle.make_activation(1, N, seed=6).reshape(N)
+    x0 = torch.empty(0, K, dtype=torch.bfloat16, device=DEV)
+    assert torch.ops.torchao.int8_weight_only_linear(x0, q8.to(DEV), s8.to(DEV), None).shape == (0, N)
+    q0, s0 = torch.ops.torchao.int8_quantize_per_token(x0)
+    assert q0.shape == (0, K) and s0.shape == (0, 1)
+    assert torch.ops.torchao.int8_scaled_mm(q0, s0, wq.to(DEV), ws.to(DEV), None).shape == (0, N)
+
+    x = oracle.make_activation(6, K, seed=8)
+    xd = x.reshape(2, 3, K).to(DEV)
+    y = torch.ops.torchao.int8_weight_only_linear(xd, q8.to(DEV), s8.to(DEV), bias.to(DEV))
+    assert y.shape == (2, 3, N)
+    assert oracle.rel_l2(y.cpu().reshape(6, N), oracle.int8wo_linear(x, q8, s8, bias)) < TOL_REF
+    q, s = torch.ops.torchao.int8_quantize_per_token(xd)
+    assert q.shape == (2, 3, K) and s.shape == (2, 3, 1)
+    q_ref, s_ref = oracle.int8_act_quant(x)
+    assert torch.equal(q.cpu().reshape(6, K), q_ref) and torch.equal(s.cpu().reshape(6, 1), s_ref)
+    yd = torch.ops.torchao.int8_scaled_mm(q, s, wq.to(DEV), ws.to(DEV), bias.to(DEV))
+    assert yd.shape == (2, 3, N)
+    ref = oracle.int8_scaled_mm(q_ref, s_ref, wq, ws, bias, epilogue="cpu")
+    assert torch.equal(yd.cpu().reshape(6, N), ref)
+
+
 @pytest.mark.parametrize("M,N,K", [(128, 4096, 4096), (16, 512, 1024), (200, 320, 2048), (1, 256, 256)])
 def test_int8_scaled_mm_exact_epilogue(M, N, K):
     w = oracle.make_linear_weight(N, K, seed=N)
