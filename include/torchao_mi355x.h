@@ -279,6 +279,9 @@ int tao_int8_dyn_linear_bf16(const uint16_t* x, const int8_t* wq, const uint16_t
  * rows per wave 2/4/8, waves along K, row groups per workgroup; 0 = built-in heuristic).
  * Calling thread only; for sweeps (experiments/sweep_int8.py). */
 int tao_tune_int8_gemv(int rows_per_wave, int waves_k, int row_groups);
+/* Per-token int8 quantisation kernel (A/B only): 0 = one wave per token, the token held in
+ * registers (default, K <= 8192); 1 = one 256-thread workgroup per token. Bit-identical. */
+int tao_tune_int8_quant(int block);
 
 /* ---- fused decode-step kernels of the end-to-end harness (torchao/_models/llama) -------------
  * Not on the int4 path: the fusions the reference gets from torch.compile in its gpt-fast

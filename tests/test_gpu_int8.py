@@ -39,7 +39,8 @@ def test_int8wo_all_m_paths(M):
     assert oracle.rel_l2(y, exact) < 4e-3
 
 
-@pytest.mark.parametrize("M,K", [(1, 4096), (7, 1024), (128, 4096), (33, 14336), (64, 16)])
+@pytest.mark.parametrize("M,K", [(1, 4096), (7, 1024), (128, 4096), (33, 14336), (64, 16),
+                                 (130, 8192), (3, 2064), (5, 8208)])
 def test_int8_act_quant_bit_exact(M, K):
     x = oracle.make_activation(M, K, seed=K + M) * 3
     x[0] = 0.0
@@ -49,6 +50,19 @@ def test_int8_act_quant_bit_exact(M, K):
     q_ref, s_ref = oracle.int8_act_quant(x)
     assert torch.equal(s.cpu(), s_ref)
     assert torch.equal(q.cpu(), q_ref)
+
+
+@pytest.mark.parametrize("M,K", [(128, 4096), (9, 2064), (4, 16)])
+def test_int8_act_quant_wave_and_block_kernels_identical(M, K):
+    """The one-wave-per-token kernel (token held in registers, the default for K <= 8192) and
+    the 256-thread block kernel give the same bits."""
+    from torchao.kernel import tuning
+
+    x = (oracle.make_activation(M, K, seed=M * 7 + K) * 5).to(DEV)
+    q0, s0 = torch.ops.torchao.int8_quantize_per_token(x)
+    with tuning(int8_quant=1):
+        q1, s1 = torch.ops.torchao.int8_quantize_per_token(x)
+    assert torch.equal(q0, q1) and torch.equal(s0, s1)
 
 
 @pytest.mark.parametrize("fname", golden_files("int8dyn_"))

@@ -321,6 +321,74 @@ __global__ __launch_bounds__(kQBlock) void int8_quant_per_token_kernel(
   for (int i = threadIdx.x; i < nvec; i += kQBlock) qr[i] = quant8(xr[i], r);
 }
 
+// One wave per token for K <= 64 * 8 * NV (the prefill shapes): the wave's 16-B pieces of the
+// token stay in registers between the amax and the quantisation, so the token is read once
+// (the block kernel above re-reads it after its barrier: a second dependent round trip) and the
+// amax is a DPP wave reduction with no LDS barrier. Same arithmetic, bit-identical output.
+// 4 tokens per 256-thread workgroup.
+constexpr int kQWaves = 4;
+template <int NV>
+__global__ __launch_bounds__(64 * kQWaves) void int8_quant_per_token_wave_kernel(
+    const uint16_t* __restrict__ x, int8_t* __restrict__ q, uint16_t* __restrict__ scale, int M,
+    int K) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kQWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (row >= M) return;  // wave-uniform
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * K);
+  const int nvec = K / 8;
+  uint4 v[NV];
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int i = lane + 64 * u;
+    v[u] = xr[i < nvec ? i : nvec - 1];  // clamped duplicates do not change the max
+  }
+  float m = 0.f;
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    m = bf16_abs_max2(v[u].x, m);
+    m = bf16_abs_max2(v[u].y, m);
+    m = bf16_abs_max2(v[u].z, m);
+    m = bf16_abs_max2(v[u].w, m);
+  }
+  m = wave_max(m);
+  const float s = token_scale(m);
+  if (lane == 0) scale[row] = f32_to_bf16(s);
+  const float r = round_bf16(1.f / s);
+  uint2* qr = reinterpret_cast<uint2*>(q + (size_t)row * K);
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int i = lane + 64 * u;
+    if (i < nvec) qr[i] = quant8(v[u], r);
+  }
+}
+
+int launch_quant_per_token(const uint16_t* x, int8_t* q, uint16_t* scale, int M, int K,
+                           hipStream_t stream) {
+  const int nv = (K / 8 + 63) / 64;
+  const dim3 grid((unsigned)((M + kQWaves - 1) / kQWaves)), block(64 * kQWaves);
+  if (tuning().quant_block == 0) {
+    if (nv <= 2) {
+      launch(int8_quant_per_token_wave_kernel<2>, grid, block, 0, stream, x, q, scale, M, K);
+      return check_launch("int8_quant_per_token_wave_kernel");
+    }
+    if (nv <= 4) {
+      launch(int8_quant_per_token_wave_kernel<4>, grid, block, 0, stream, x, q, scale, M, K);
+      return check_launch("int8_quant_per_token_wave_kernel");
+    }
+    if (nv <= 8) {
+      launch(int8_quant_per_token_wave_kernel<8>, grid, block, 0, stream, x, q, scale, M, K);
+      return check_launch("int8_quant_per_token_wave_kernel");
+    }
+    if (nv <= 16) {
+      launch(int8_quant_per_token_wave_kernel<16>, grid, block, 0, stream, x, q, scale, M, K);
+      return check_launch("int8_quant_per_token_wave_kernel");
+    }
+  }
+  launch(int8_quant_per_token_kernel, dim3((unsigned)M), dim3(kQBlock), 0, stream, x, q, scale,
+         K);
+  return check_launch("int8_quant_per_token_kernel");
+}
+
 }  // namespace
 
 int int8_scaled_mm_launch(const int8_t* xq, const uint16_t* xs, const int8_t* wq,
@@ -341,9 +409,15 @@ int tao_int8_quant_per_token(const uint16_t* x, int8_t* q, uint16_t* scale, int6
   if (M == 0 || K == 0) return TAO_OK;
   TAO_CHECK_ALIGN(x, 16, "x");
   TAO_CHECK_ALIGN(q, 8, "q");
-  launch(int8_quant_per_token_kernel, dim3((unsigned)M), dim3(kQBlock), 0,
-                     as_stream(stream), x, q, scale, (int)K);
-  return check_launch("int8_quant_per_token_kernel");
+  return launch_quant_per_token(x, q, scale, (int)M, (int)K, as_stream(stream));
+}
+
+// per-token quant kernel choice (A/B only): 0 = one wave per token (default), 1 = the
+// 256-thread block kernel
+int tao_tune_int8_quant(int block) {
+  TAO_CHECK_ARG(block == 0 || block == 1, "tune: int8 quant block must be 0 or 1");
+  tuning().quant_block = block;
+  return TAO_OK;
 }
 
 int tao_int8_scaled_mm_bf16(const int8_t* xq, const uint16_t* xs, const int8_t* wq,

@@ -55,6 +55,7 @@ struct Tuning {
   int gemm_nw = 0;                               // MFMA GEMM 16-col blocks per wave: 0 auto, 1, 2
   int gemm_table = 0;                            // MFMA GEMM measured-shape table: 0 on, 1 off
   int int4_mfma32 = 0;                           // int4 GEMM on 32x32x16 MFMAs: 0 off, 1 on
+  int quant_block = 0;                           // per-token int8 quant: 0 wave kernel, 1 block
 };
 Tuning& tuning();
 

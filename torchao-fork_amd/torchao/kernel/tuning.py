@@ -28,6 +28,7 @@ _KNOBS = {
     "int4_xlds": ("tao_tune_int4_xlds", 1),
     "int4_norm": ("tao_tune_int4_norm", 1),
     "int8_gemv": ("tao_tune_int8_gemv", 3),
+    "int8_quant": ("tao_tune_int8_quant", 1),
     "attn": ("tao_tune_attn", 1),
     "splitk_fenced": ("tao_tune_splitk_fenced", 1),
 }
