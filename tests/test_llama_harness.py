@@ -219,7 +219,7 @@ def test_fused_decode_matches_unfused_gpu(quant):
     ref = [model(prompt[:, -1:], torch.tensor([P], device=dev))]
     model.setup_caches(1, P + T)
     assert model.enable_fused_kernels()
-    model(prompt, pos)  # prefill stays on torch ops
+    model(prompt, pos)  # fused prefill (rmsnorm / rope_kv / silu_mul kernels)
     got = [model(prompt[:, -1:], torch.tensor([P], device=dev))]
     rel = (got[0] - ref[0]).norm() / ref[0].norm()
     assert rel < 2e-2, float(rel)
@@ -230,6 +230,43 @@ def test_fused_decode_matches_unfused_gpu(quant):
     dec.capture()
     graphed, _, _ = generate(model, prompt, T, dec)
     assert torch.equal(graphed, eager)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("quant,fuse", [(None, True), ("int4wo-32", True), ("int4wo-32", False)])
+def test_fused_prefill_matches_torch_ops_gpu(quant, fuse):
+    """S > 1 tokens on the fused kernels (RMSNorm, RoPE + KV write, SiLU-mul) track the torch-op
+    forward: all positions' logits and the KV caches; prefill_next (head at the last position
+    only) takes the same greedy token wherever the top-2 margin decides it."""
+    dev = torch.device("cuda")
+    model = _tiny(dev, seed=7)
+    if fuse:
+        model.fuse_w13()
+    apply_quantization(model, quant)
+    P = 37
+    model.setup_caches(2, P + 3)
+    prompt = torch.randint(0, 1000, (2, P), device=dev)
+    pos = torch.arange(P, device=dev)
+    with torch.no_grad():
+        ref = model(prompt, pos)
+        kref = [blk.attention.kv_cache.k_cache.clone() for blk in model.layers]
+        assert model.enable_fused_kernels()
+        for blk in model.layers:
+            blk.attention.kv_cache.k_cache.zero_()
+            blk.attention.kv_cache.v_cache.zero_()
+        got = model(prompt, pos)
+        nxt = model.prefill_next(prompt, pos)
+    assert got.shape == ref.shape
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 2e-2, rel
+    for blk, k0 in zip(model.layers, kref):
+        k1 = blk.attention.kv_cache.k_cache
+        assert float((k1 - k0).float().norm() / k0.float().norm()) < 2e-2
+    last = ref[:, -1]
+    top2 = last.topk(2, dim=-1).values
+    for b in range(last.shape[0]):
+        if float(top2[b, 0] - top2[b, 1]) > 3e-2 * float(last[b].abs().max()):
+            assert int(nxt[b, 0]) == int(last[b].argmax())
 
 
 def test_fuse_w13_is_exact_cpu():

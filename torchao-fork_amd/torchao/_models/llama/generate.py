@@ -85,8 +85,7 @@ def apply_quantization(model: nn.Module, quantization: Optional[str]) -> nn.Modu
 @torch.no_grad()
 def prefill(model: Transformer, prompt: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
     """prompt [B, P] at positions input_pos [P] -> greedy next token [B, 1]."""
-    logits = model(prompt, input_pos)
-    return logits[:, -1].argmax(dim=-1, keepdim=True).to(prompt.dtype)
+    return model.prefill_next(prompt, input_pos)
 
 
 @torch.no_grad()

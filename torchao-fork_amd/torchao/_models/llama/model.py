@@ -16,8 +16,11 @@ Decode-time structure for one process per GPU and HIP graphs (no tracing compile
     (bf16(x + bf16(W a)) is exactly the bias epilogue at M = 1); with int4 weights the norms,
     RoPE + KV write and SwiGLU ride inside the wqkv / w13 / output GEMVs
     (tao_int4wo_decode_bf16) — 6 launches per layer;
-  * otherwise (prefill, CPU): torch ops, ``index_copy_`` into the caches, a causal-mask row
-    gathered by ``input_pos``, ``F.scaled_dot_product_attention(enable_gqa=True)``;
+  * fused prefill (S > 1 tokens): the linears on the MFMA GEMMs, RMSNorm, RoPE + KV-cache write
+    and SiLU-mul on the same kernels (S rows each), ``F.scaled_dot_product_attention`` over the
+    caches; ``prefill_next`` runs the output head at the last position only;
+  * otherwise (CPU, or fused kernels off): torch ops, ``index_copy_`` into the caches, a
+    causal-mask row gathered by ``input_pos``, ``F.scaled_dot_product_attention(enable_gqa=True)``;
   * rotary tables precomputed once (Llama-3.1 frequency scaling where configured).
 """
 
@@ -152,6 +155,12 @@ def _apply_rope(x: torch.Tensor, freqs: torch.Tensor) -> torch.Tensor:
     return out.flatten(3).type_as(x)
 
 
+def kernels_rmsnorm(x: torch.Tensor, norm: "RMSNorm") -> torch.Tensor:
+    from torchao._models.llama import kernels
+
+    return kernels.rmsnorm(x, norm.weight, norm.eps)
+
+
 def _linear_plus(x: torch.Tensor, lin: nn.Linear, residual: torch.Tensor) -> torch.Tensor:
     """residual + lin(x); at one token the add rides on the linear's bias epilogue."""
     if x.numel() == x.shape[-1]:
@@ -192,6 +201,19 @@ class Attention(nn.Module):
             k, v = self.kv_cache.update(input_pos, k, v)
         y = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, enable_gqa=True)
         return self.wo(y.transpose(1, 2).reshape(B, S, q_sz))
+
+    def forward_prefill(self, x, freqs_table, mask, input_pos):
+        """S > 1 tokens on the gfx950 kernels: wqkv (MFMA GEMM), RoPE + KV-cache write in one
+        launch, then F.scaled_dot_product_attention over the caches (forward's math)."""
+        from torchao._models.llama import kernels
+
+        B, S, _ = x.shape
+        kv = self.kv_cache
+        q = kernels.rope_kv(self.wqkv(x), freqs_table, input_pos, kv.k_cache, kv.v_cache,
+                            self.n_head)
+        y = F.scaled_dot_product_attention(q, kv.k_cache, kv.v_cache, attn_mask=mask,
+                                           enable_gqa=True)
+        return self.wo(y.transpose(1, 2).reshape(B, S, self.n_head * self.head_dim))
 
     def forward_fused(self, x, freqs_table, input_pos, residual, norm=None):
         from torchao._models.llama import kernels
@@ -278,6 +300,20 @@ class TransformerBlock(nn.Module):
         h = self.attention.forward_fused(x, freqs_table, input_pos, x, self.attention_norm)
         return self.feed_forward.forward_fused(h, h, self.ffn_norm)
 
+    def forward_prefill(self, x, freqs_table, mask, input_pos):
+        """forward() for S > 1 tokens with the norms, RoPE + KV write and SiLU-mul on the
+        gfx950 kernels (one launch each instead of ~8, ~20 and 2 eager torch ops)."""
+        from torchao._models.llama import kernels
+
+        an, fn = self.attention_norm, self.ffn_norm
+        h = x + self.attention.forward_prefill(kernels.rmsnorm(x, an.weight, an.eps), freqs_table,
+                                               mask, input_pos)
+        ff = self.feed_forward
+        xn = kernels.rmsnorm(h, fn.weight, fn.eps)
+        g = kernels.silu_mul(ff.w13(xn)) if ff.w13 is not None else kernels.silu_mul(ff.w1(xn),
+                                                                                     ff.w3(xn))
+        return h + ff.w2(g)
+
 
 class Transformer(nn.Module):
     def __init__(self, cfg: ModelArgs):
@@ -332,10 +368,33 @@ class Transformer(nn.Module):
         x = self.tok_embeddings(idx)
         for blk in self.layers:
             x = blk.forward_fused(x, self.freqs, input_pos)
+        return self._head_fused(x)
+
+    def _head_fused(self, x: torch.Tensor) -> torch.Tensor:
+        from torchao._models.llama import kernels
+
         head = _int4_parts(self.output) if x.numel() == x.shape[-1] else None
         if head is not None:  # final RMSNorm inside the head GEMV
             return kernels.int4_decode(x, *head, norm_weight=self.norm.weight, eps=self.norm.eps)
         return self.output(kernels.rmsnorm(x, self.norm.weight, self.norm.eps))
+
+    def _layers_prefill(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
+        mask = self.causal_mask[None, None, input_pos]  # [1, 1, S, T]
+        x = self.tok_embeddings(idx)
+        for blk in self.layers:
+            x = blk.forward_prefill(x, self.freqs, mask, input_pos)
+        return x
+
+    def prefill_next(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
+        """Greedy next token [B, 1] after the prompt ``idx`` [B, S] (the reference's prefill:
+        logits[:, -1].argmax). On the fused path only the last position goes through the output
+        head (one M = 1 launch per row instead of an M = S GEMM over the 128K vocabulary)."""
+        if not (self.fused and idx.shape[1] > 1):
+            return self(idx, input_pos)[:, -1].argmax(dim=-1, keepdim=True).to(idx.dtype)
+        from torchao._models.llama import kernels
+
+        x = self._layers_prefill(idx, input_pos)[:, -1:].contiguous()  # [B, 1, dim]
+        return kernels.argmax(self._head_fused(x)[:, -1]).to(idx.dtype)
 
     def decode_next(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
         """Greedy next token [B, 1] for one token per sequence; on the fused path the argmax
@@ -362,6 +421,9 @@ class Transformer(nn.Module):
         assert self.max_seq > 0, "call setup_caches() first"
         if self.fused and idx.shape[1] == 1:
             return self._forward_fused(idx, input_pos).float()
+        if self.fused:
+            x = self._layers_prefill(idx, input_pos)
+            return self.output(kernels_rmsnorm(x, self.norm)).float()
         mask = self.causal_mask[None, None, input_pos]  # [1, 1, S, T]
         freqs = self.freqs[input_pos]
         x = self.tok_embeddings(idx)
