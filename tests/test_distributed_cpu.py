@@ -93,6 +93,80 @@ def test_colwise_sharded_linear_gloo(world):
         assert ok_int4, f"rank {rank}: sharded int4 forward differs from the unsharded oracle"
 
 
+def _colwise_gpu_worker(rank, world, port, q):
+    """Column-sharded int4 forward with each rank's local linear on the HIP kernels (cuda:0) and
+    the all-gather over gloo on host copies: equals the unsharded HIP forward within one bf16
+    rounding per layer (a shard's launch shape follows its own N) and the oracle within 1e-2."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "torchao-fork_amd"))
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import copy
+
+        import torch.nn.functional as F
+
+        from oracle import oracle
+        from torchao.distributed import parallelize_colwise_
+        from torchao.quantization import Int4WeightOnlyConfig, quantize_
+
+        dev = torch.device("cuda", 0)
+        torch.manual_seed(0)
+        full = torch.nn.Sequential(torch.nn.Linear(512, 192), torch.nn.Linear(192, 128)).to(torch.bfloat16)
+        xs = [torch.randn(1, 512, dtype=torch.bfloat16), torch.randn(5, 512, dtype=torch.bfloat16)]
+        qfull = copy.deepcopy(full)
+        quantize_(qfull, Int4WeightOnlyConfig(group_size=32))
+        qsh = parallelize_colwise_(copy.deepcopy(full))
+        quantize_(qsh, Int4WeightOnlyConfig(group_size=32))
+
+        def hip_linear(x, w, b):
+            return F.linear(x.to(dev), w.to(dev), None if b is None else b.to(dev)).cpu()
+
+        for m in qsh:
+            m.local_fn = hip_linear
+        ok = True
+        worst = 0.0
+        for x in xs:
+            y_sh = qsh(x)
+            h = hip_linear(x, qfull[0].weight, qfull[0].bias)
+            y_full = hip_linear(h, qfull[1].weight, qfull[1].bias)
+            q0, s0, z0 = qfull[0].weight.tensor_impl.get_plain()
+            q1, s1, z1 = qfull[1].weight.tensor_impl.get_plain()
+            y_ref = oracle.int4_linear(oracle.int4_linear(x, q0, s0, z0, 32, qfull[0].bias),
+                                       q1, s1, z1, 32, qfull[1].bias)
+            r_full = float((y_sh.float() - y_full.float()).norm() / y_full.float().norm())
+            r_ref = float((y_sh.float() - y_ref.float()).norm() / y_ref.float().norm())
+            worst = max(worst, r_full, r_ref)
+            ok = ok and y_sh.shape == y_full.shape and r_full < 1e-2 and r_ref < 1e-2
+        q.put((rank, ok, worst))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, False, repr(e) + traceback.format_exc()[-800:]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_colwise_gather_hip_local_compute_gloo():
+    """BASELINE config 5's pattern (colwise shards + all-gather of the outputs) with the local
+    linears on the HIP kernels; both ranks share the box's one GPU."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_colwise_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, info in sorted(results, key=lambda r: r[0]):
+        assert ok is True, f"rank {rank}: sharded HIP forward mismatch ({info})"
+
+
 def _tp_worker(rank, world, port, q, use_gpu):
     """Megatron pairing on a SwiGLU MLP: w1 / w3 colwise (no gather) -> silu(a) * b on the local
     columns -> w2 rowwise + all-reduce (reference test_affine_quantized_tensor_parallel.py:
