@@ -356,6 +356,23 @@ int tao_argmax_bf16(const uint16_t* x, int64_t* out, int64_t rows, int64_t n, vo
 int tao_argmax_advance_bf16(const uint16_t* x, int64_t n, int64_t* cur, int64_t* pos,
                             int64_t* tokens, int64_t max_len, void* stream);
 
+/* One token through an int8 weight-only linear with its decode-step neighbours fused (the
+ * int8 counterpart of tao_int4wo_decode_bf16; csrc/int8_gemv.hip). Operands of
+ * tao_int8wo_linear_bf16 at M == 1 (x [K] bf16, w [N][K] int8, scale [N] bf16, no bias).
+ *   norm_weight  NULL: x as is; else [K] bf16, x -> bf16(bf16(x * rsqrt(mean(x^2) + eps)) * w).
+ *   epilogue 0: y [N] = the linear; 1 (swiglu): rows (2i, 2i+1) = (w1_i, w3_i), y [N/2] =
+ *   bf16(bf16(silu(a)) * b); 2 (rope_kv): rows [q | k | v] heads, y [n_head * head_dim] = rotated
+ *   q, rotated k and v written to k_cache / v_cache [n_kv_head][max_seq][head_dim] at pos[0]
+ *   (outside [0, max_seq): no cache row written, reported by tao_decode_status).
+ * Each result equals rmsnorm -> tao_int8wo_linear_bf16 -> silu_mul / rope_kv. Replaces, at
+ * decode, the RMSNorm / SiLU-mul / RoPE + KVCache.update ops around the reference's int8
+ * weight-only linears (torchao/_models/llama/model.py). */
+int tao_int8wo_decode_bf16(const uint16_t* x, const int8_t* w, const uint16_t* scale, int64_t N,
+                           int64_t K, const uint16_t* norm_weight, float eps, int epilogue,
+                           uint16_t* y, const float* freqs, const int64_t* pos, uint16_t* k_cache,
+                           uint16_t* v_cache, int64_t n_head, int64_t n_kv_head, int64_t head_dim,
+                           int64_t max_seq, void* stream);
+
 /* Decode-step fused int4 linear, M = 1: y = epilogue(rmsnorm(x) W^T) in one launch, with the
  * operands of tao_int4wo_linear_bf16 (x [K] bf16, packed [N][K/8], scales_and_zeros [N][K/g]).
  *   norm_weight  NULL: x is used as is; else [K] bf16 and x -> bf16(bf16(x * rsqrt(mean(x^2) +

@@ -6,7 +6,7 @@ import torch
 
 from torchao import _lib
 
-__all__ = ["rmsnorm", "rope_kv", "attn_decode", "silu_mul", "int4_decode", "argmax",
+__all__ = ["rmsnorm", "rope_kv", "attn_decode", "silu_mul", "int4_decode", "int8wo_decode", "argmax",
            "argmax_advance", "check_decode_status"]
 
 
@@ -121,6 +121,37 @@ def int4_decode(x: torch.Tensor, packed: torch.Tensor, scale_and_zero: torch.Ten
     _lib.call("tao_int4wo_decode_bf16", x.data_ptr(), packed.data_ptr(), scale_and_zero.data_ptr(),
               N, K, int(group_size), ptr(norm_weight), float(eps), epi, y.data_ptr(), ptr(freqs),
               ptr(pos), ptr(kc), ptr(vc), H, Hkv, D, T, _stream(x))
+    return y
+
+
+def int8wo_decode(x: torch.Tensor, w: torch.Tensor, scale: torch.Tensor, norm_weight=None,
+                  eps: float = 0.0, epilogue: str = "none", rope=None) -> torch.Tensor:
+    """One token through an int8 weight-only linear (w [N, K] int8, scale [N] bf16) with the
+    int4_decode fusions (tao_int8wo_decode_bf16): optional RMSNorm of x; epilogue "none",
+    "swiglu" or "rope_kv" as in int4_decode."""
+    _check(x, torch.bfloat16, "int8wo_decode x")
+    _check(w, torch.int8, "int8wo_decode w")
+    N, K = w.shape
+    if x.numel() != K:
+        raise RuntimeError(f"int8wo_decode takes one token, got x of shape {tuple(x.shape)}")
+    scale = scale.reshape(-1).contiguous()
+    if norm_weight is not None:
+        _check(norm_weight, torch.bfloat16, "int8wo_decode norm_weight")
+    epi = _EPILOGUES[epilogue]
+    freqs = pos = kc = vc = None
+    H = Hkv = D = T = 0
+    if epi == 2:
+        freqs, pos, kc, vc, H = rope
+        _, Hkv, T, D = kc.shape
+        y = torch.empty(1, H, 1, D, dtype=x.dtype, device=x.device)
+    elif epi == 1:
+        y = torch.empty(*x.shape[:-1], N // 2, dtype=x.dtype, device=x.device)
+    else:
+        y = torch.empty(*x.shape[:-1], N, dtype=x.dtype, device=x.device)
+    ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    _lib.call("tao_int8wo_decode_bf16", x.data_ptr(), w.data_ptr(), scale.data_ptr(), N, K,
+              ptr(norm_weight), float(eps), epi, y.data_ptr(), ptr(freqs), ptr(pos), ptr(kc),
+              ptr(vc), H, Hkv, D, T, _stream(x))
     return y
 
 

@@ -180,6 +180,38 @@ def _int4_parts(lin: Optional[nn.Linear]):
     return packed, impl.scale_and_zero, w.block_size[-1]
 
 
+def _int8wo_parts(lin: Optional[nn.Linear]):
+    """(int_data [N, K] int8, scale [N]) of an int8 weight-only linear (Int8WeightOnlyConfig,
+    PlainLayout) on the GPU, else None: the fused int8 decode kernels read those operands."""
+    w = getattr(lin, "weight", None)
+    if w is None or lin.bias is not None or not w.is_cuda:
+        return None
+    from torchao.dtypes.uintx.plain_layout import _linear_fp_act_int8_weight_check
+
+    if not _linear_fp_act_int8_weight_check(torch.empty(0, dtype=torch.bfloat16), w, None):
+        return None
+    impl = w.tensor_impl
+    return impl.int_data, impl.scale.reshape(-1)
+
+
+def _fused_decode(x, lin, norm=None, epilogue="none", rope=None):
+    """One token through ``lin`` with the decode fusions, on whichever fused kernel its weight
+    format has (int4 weight-only, int8 weight-only); None if neither applies."""
+    from torchao._models.llama import kernels
+
+    if x.numel() != x.shape[-1]:
+        return None
+    nw = None if norm is None else norm.weight
+    eps = 0.0 if norm is None else norm.eps
+    p4 = _int4_parts(lin)
+    if p4 is not None:
+        return kernels.int4_decode(x, *p4, norm_weight=nw, eps=eps, epilogue=epilogue, rope=rope)
+    p8 = _int8wo_parts(lin)
+    if p8 is not None:
+        return kernels.int8wo_decode(x, *p8, norm_weight=nw, eps=eps, epilogue=epilogue, rope=rope)
+    return None
+
+
 class Attention(nn.Module):
     def __init__(self, cfg: ModelArgs):
         super().__init__()
@@ -219,14 +251,11 @@ class Attention(nn.Module):
         from torchao._models.llama import kernels
 
         kv = self.kv_cache
-        wqkv = _int4_parts(self.wqkv) if norm is not None else None
-        if wqkv is not None and x.numel() == x.shape[-1]:
-            # RMSNorm -> wqkv -> RoPE + KV-cache write in one launch
-            q = kernels.int4_decode(x, *wqkv, norm_weight=norm.weight, eps=norm.eps,
-                                    epilogue="rope_kv",
-                                    rope=(freqs_table, input_pos, kv.k_cache, kv.v_cache,
-                                          self.n_head))
-        else:
+        # RMSNorm -> wqkv -> RoPE + KV-cache write in one launch (int4 / int8 weight-only)
+        q = None if norm is None else _fused_decode(
+            x, self.wqkv, norm, "rope_kv", (freqs_table, input_pos, kv.k_cache, kv.v_cache,
+                                            self.n_head))
+        if q is None:
             if norm is not None:
                 x = kernels.rmsnorm(x, norm.weight, norm.eps)
             q = kernels.rope_kv(self.wqkv(x), freqs_table, input_pos, kv.k_cache, kv.v_cache,
@@ -271,10 +300,9 @@ class FeedForward(nn.Module):
         from torchao._models.llama import kernels
 
         if norm is not None:
-            w13 = _int4_parts(self.w13)
-            if w13 is not None:  # RMSNorm -> w13 -> SwiGLU in one launch
-                g = kernels.int4_decode(x, *w13, norm_weight=norm.weight, eps=norm.eps,
-                                        epilogue="swiglu")
+            # RMSNorm -> w13 -> SwiGLU in one launch (int4 / int8 weight-only)
+            g = None if self.w13 is None else _fused_decode(x, self.w13, norm, "swiglu")
+            if g is not None:
                 return _linear_plus(g, self.w2, residual)
             x = kernels.rmsnorm(x, norm.weight, norm.eps)
         if self.w13 is not None:
@@ -373,9 +401,9 @@ class Transformer(nn.Module):
     def _head_fused(self, x: torch.Tensor) -> torch.Tensor:
         from torchao._models.llama import kernels
 
-        head = _int4_parts(self.output) if x.numel() == x.shape[-1] else None
-        if head is not None:  # final RMSNorm inside the head GEMV
-            return kernels.int4_decode(x, *head, norm_weight=self.norm.weight, eps=self.norm.eps)
+        y = _fused_decode(x, self.output, self.norm)  # final RMSNorm inside the head GEMV
+        if y is not None:
+            return y
         return self.output(kernels.rmsnorm(x, self.norm.weight, self.norm.eps))
 
     def _layers_prefill(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
