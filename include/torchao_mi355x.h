@@ -373,6 +373,18 @@ int tao_int8wo_decode_bf16(const uint16_t* x, const int8_t* w, const uint16_t* s
                            uint16_t* v_cache, int64_t n_head, int64_t n_kv_head, int64_t head_dim,
                            int64_t max_seq, void* stream);
 
+/* The same decode-step fusions on the int8 dynamic-activation linear (one token; the per-token
+ * int8 quantisation of the normalised token inside the kernel, as tao_int8_dyn_linear_bf16
+ * does for the plain token). Operands and epilogues as tao_int8wo_decode_bf16; equals
+ * rmsnorm -> tao_int8_dyn_linear_bf16 -> silu_mul / rope_kv up to the norm's fp32 sum order.
+ * K <= 32768 (<= 16384 with norm_weight). Replaces, at decode, the ops around the reference's
+ * Int8DynamicActivationInt8WeightConfig linears (model.py, quant_api.py:1258-1273). */
+int tao_int8dq_decode_bf16(const uint16_t* x, const int8_t* w, const uint16_t* scale, int64_t N,
+                           int64_t K, const uint16_t* norm_weight, float eps, int epilogue,
+                           uint16_t* y, const float* freqs, const int64_t* pos, uint16_t* k_cache,
+                           uint16_t* v_cache, int64_t n_head, int64_t n_kv_head, int64_t head_dim,
+                           int64_t max_seq, void* stream);
+
 /* Decode-step fused int4 linear, M = 1: y = epilogue(rmsnorm(x) W^T) in one launch, with the
  * operands of tao_int4wo_linear_bf16 (x [K] bf16, packed [N][K/8], scales_and_zeros [N][K/g]).
  *   norm_weight  NULL: x is used as is; else [K] bf16 and x -> bf16(bf16(x * rsqrt(mean(x^2) +

@@ -1,10 +1,11 @@
-"""The decode-fused int8 weight-only GEMV (tao_int8wo_decode_bf16) against the unfused chain it
-replaces: RMSNorm kernel -> int8 weight-only linear -> SiLU-mul / RoPE + KV write. Without the
-RMSNorm prologue the outputs are the linear's own bf16(bf16(sum) * scale) values, and every
-int8 partial sum of a 16-k chunk is exact, so the comparison is bit-exact up to the fp32 order of
-the chunk sums; with the prologue, the sum of squares inside rsqrt(mean(x^2) + eps) may round
-differently, so a normalised activation may differ by one bf16 ulp (tolerance per check). Also
-checked against the fp32 chain at the north-star bar (1e-2)."""
+"""The decode-fused int8 GEMVs (tao_int8wo_decode_bf16, and tao_int8dq_decode_bf16 for the
+dynamic-activation config) against the unfused chain they replace: RMSNorm kernel -> int8
+linear -> SiLU-mul / RoPE + KV write. Without the RMSNorm prologue the outputs are the linear's
+own bf16(bf16(sum) * scale) values: int8-dyn sums are exact integers (bit-exact), int8 weight-only
+sums may differ in fp32 order from the unfused launch shape. With the prologue, the sum of
+squares inside rsqrt(mean(x^2) + eps) may round differently, so a normalised activation may
+differ by one bf16 ulp (tolerance per check). Also checked against the fp32 chain at the
+north-star bar (1e-2)."""
 
 import math
 
@@ -13,7 +14,11 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from torchao.quantization import Int8WeightOnlyConfig, quantize_
+from torchao.quantization import (
+    Int8DynamicActivationInt8WeightConfig,
+    Int8WeightOnlyConfig,
+    quantize_,
+)
 
 pytestmark = pytest.mark.gpu
 
@@ -161,7 +166,7 @@ def test_graph_capture_errors_and_kv_guard():
         kernels.check_decode_status()
 
 
-@pytest.mark.parametrize("quant", ["int8wo"])
+@pytest.mark.parametrize("quant", ["int8wo", "int8dq"])
 def test_fused_int8_decode_in_the_harness(quant):
     """A tiny Llama on Int8WeightOnlyConfig: the fused one-token step (norms, RoPE + KV and
     SwiGLU inside the int8 GEMVs) tracks the torch-op step, and a HIP-graph replay equals it."""
@@ -199,3 +204,74 @@ def test_fused_int8_decode_in_the_harness(quant):
     dec.capture()
     graphed, _, _ = generate(model, prompt, T, dec)
     assert torch.equal(graphed, eager)
+
+
+# ---- int8 dynamic activation (tao_int8dq_decode_bf16) ---------------------------------------------
+def _int8dq_linear(N, K, seed=0):
+    torch.manual_seed(seed)
+    lin = nn.Linear(K, N, bias=False, device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        lin.weight.uniform_(-1 / math.sqrt(K), 1 / math.sqrt(K))
+    quantize_(lin, Int8DynamicActivationInt8WeightConfig())
+    from torchao._models.llama.model import _int8dq_parts
+
+    parts = _int8dq_parts(lin)
+    assert parts is not None
+    return lin, parts
+
+
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (128256, 4096), (1000, 512)])
+def test_dq_plain_is_the_fused_linear(N, K):
+    """No norm, no epilogue: the same kernel and launch shape as int8_dyn_linear (bit-exact)."""
+    from torchao._models.llama import kernels
+
+    lin, parts = _int8dq_linear(N, K)
+    x = torch.randn(1, 1, K, device=DEV, dtype=torch.bfloat16)
+    assert torch.equal(kernels.int8dq_decode(x, *parts), lin(x))
+
+
+@pytest.mark.parametrize("N,K", [(6144, 4096), (128256, 4096), (2048, 8192)])
+def test_dq_rmsnorm_prologue(N, K):
+    from torchao._models.llama import kernels
+
+    lin, parts = _int8dq_linear(N, K)
+    x = torch.randn(1, 1, K, device=DEV, dtype=torch.bfloat16) * 3
+    w = _norm_w(K)
+    got = kernels.int8dq_decode(x, *parts, norm_weight=w, eps=1e-5)
+    ref = lin(kernels.rmsnorm(x, w, 1e-5))
+    # a one-ulp change of a normalised element can move the token's int8 rounding: 1e-2
+    assert _rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("norm", [False, True])
+def test_dq_swiglu_and_rope_epilogues(norm):
+    from torchao._models.llama import kernels
+    from torchao._models.llama.model import ModelArgs, _rope_freqs
+
+    K = 4096
+    w = _norm_w(K) if norm else None
+    x = torch.randn(1, 1, K, device=DEV, dtype=torch.bfloat16)
+    xin = kernels.rmsnorm(x, w, 1e-5) if norm else x
+    lin, parts = _int8dq_linear(2 * 1024, K, seed=2)
+    got = kernels.int8dq_decode(x, *parts, norm_weight=w, eps=1e-5, epilogue="swiglu")
+    ref = kernels.silu_mul(lin(xin))
+    if norm:
+        assert _rel(got, ref) < 1e-2
+    else:
+        assert torch.equal(got, ref)
+    H, Hkv, D, T, pos = 32, 8, 128, 64, 17
+    lin, parts = _int8dq_linear((H + 2 * Hkv) * D, K, seed=3)
+    cfg = ModelArgs(n_layer=1, n_head=H, n_local_heads=Hkv, dim=H * D, rope_base=500000)
+    freqs = _rope_freqs(cfg, T).to(DEV)
+    p = torch.tensor([pos], device=DEV)
+    kc = torch.randn(1, Hkv, T, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    kc_ref, vc_ref = kc.clone(), vc.clone()
+    q = kernels.int8dq_decode(x, *parts, norm_weight=w, eps=1e-5, epilogue="rope_kv",
+                              rope=(freqs, p, kc, vc, H))
+    q_ref = kernels.rope_kv(lin(xin), freqs, p, kc_ref, vc_ref, H)
+    for a, b in ((q, q_ref), (kc, kc_ref), (vc, vc_ref)):
+        if norm:
+            assert _rel(a, b) < 1e-2
+        else:
+            assert torch.equal(a, b)

@@ -38,6 +38,7 @@ __device__ unsigned long long g_attn_stamps[1024 * 4];
 #endif
 int int4gemv_decode_status(unsigned* bits);
 int int8gemv_decode_status(unsigned* bits);
+int int8dyn_decode_status(unsigned* bits);
 
 namespace {
 
@@ -810,6 +811,7 @@ extern "C" int tao_decode_status(int* bits) {
   int rc = tao::decode_ops_status(&v);
   if (rc == TAO_OK) rc = tao::int4gemv_decode_status(&v);
   if (rc == TAO_OK) rc = tao::int8gemv_decode_status(&v);
+  if (rc == TAO_OK) rc = tao::int8dyn_decode_status(&v);
   *bits = (int)v;
   return rc;
 }

@@ -17,6 +17,8 @@
 
 namespace tao {
 
+TAO_DECODE_ERROR_WORD(int8dyn_decode_status)
+
 // Launch shape override of the int8 decode GEMVs (tao_tune_int8_gemv; 0 = heuristic), shared
 // with int8wo_gemv (int8_gemv.hip).
 
@@ -42,7 +44,23 @@ struct Int8DynGemvArgs {
   const uint16_t* bias;   // [N] or null
   uint16_t* y;            // [M][N]
   int M, N, K, Wk, G, S;
+  // decode-step fusions (tao_int8dq_decode_bf16, FQ only): RMSNorm of the token before its
+  // quantisation, SwiGLU / RoPE + KV-write epilogues (int8_gemv.hip's int8wo_decode_kernel)
+  const uint16_t* norm_w;
+  float eps;
+  const float* freqs;
+  const int64_t* pos;
+  uint16_t* k_cache;
+  uint16_t* v_cache;
+  int H, Hkv, D, T;
 };
+enum { kDqEpiNone = 0, kDqEpiSwiGLU = 1, kDqEpiRopeKV = 2 };
+
+__device__ __forceinline__ uint32_t dq_rmsnorm_pair(uint32_t xv, uint32_t wv, float r) {
+  const float lo = round_bf16(bf16lo_to_f32(xv) * r) * bf16lo_to_f32(wv);
+  const float hi = round_bf16(bf16hi_to_f32(xv) * r) * bf16hi_to_f32(wv);
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
 
 __device__ __forceinline__ int sdot4(uint32_t a, uint32_t b, int c) {
   return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
@@ -74,10 +92,11 @@ __device__ __forceinline__ float bf16_abs_max2(uint32_t d, float m) {
   return fmaxf(m, fabsf(bf16hi_to_f32(d)));
 }
 
-template <int MT, int RPW, int NPT>
+template <int MT, int RPW, int NPT, int EPI = kDqEpiNone>
 __global__ __launch_bounds__(512) void int8dyn_gemv_kernel(Int8DynGemvArgs a) {
   constexpr bool FQ = NPT > 0;  // NPT: 16-B pieces of the bf16 token per thread (K <= 8 NPT T)
   static_assert(!FQ || MT == 1, "the fused quantisation is per token, M == 1");
+  static_assert(EPI == kDqEpiNone || (FQ && RPW % 2 == 0), "epilogues: fused token, row pairs");
   constexpr int V = RPW * MT;
   // [G][Wk][V] int partials | (FQ) [8] wave maxima | (FQ) token q [K] int8
   extern __shared__ int lds_i[];
@@ -116,13 +135,38 @@ __global__ __launch_bounds__(512) void int8dyn_gemv_kernel(Int8DynGemvArgs a) {
     // barriers and the quantisation into LDS run under the weight loads' latency.
     const uint4* xr = reinterpret_cast<const uint4*>(a.x);
     const int nvec = K >> 3;
-    uint4 xv[NPT];
+    uint4 xv[NPT], gv[NPT];
 #pragma unroll
     for (int u = 0; u < NPT; ++u) {
       const int i = threadIdx.x + u * (int)blockDim.x;
       xv[u] = xr[i < nvec ? i : nvec - 1];  // clamped, masked below
+      if (a.norm_w != nullptr) gv[u] = reinterpret_cast<const uint4*>(a.norm_w)[i < nvec ? i : nvec - 1];
     }
     load_w(wk);  // every wave owns at least one slice (Wk <= S)
+    if (a.norm_w != nullptr) {  // RMSNorm of the token (the unfused rmsnorm_kernel's roundings)
+      float ss = 0.f;
+#pragma unroll
+      for (int u = 0; u < NPT; ++u) {
+        const bool ok = threadIdx.x + u * (int)blockDim.x < nvec;
+        const uint32_t d[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float p = ok ? bf16lo_to_f32(d[j]) : 0.f, q = ok ? bf16hi_to_f32(d[j]) : 0.f;
+          ss = fmaf(p, p, fmaf(q, q, ss));
+        }
+      }
+      ss = wave_sum(ss);
+      if (lane == 0) wmax[wave] = ss;
+      __syncthreads();
+      float t = 0.f;
+      for (int q = 0; q < nw; ++q) t += wmax[q];
+      const float rn = rsqrtf(t / (float)K + a.eps);
+#pragma unroll
+      for (int u = 0; u < NPT; ++u)
+        xv[u] = make_uint4(dq_rmsnorm_pair(xv[u].x, gv[u].x, rn), dq_rmsnorm_pair(xv[u].y, gv[u].y, rn),
+                           dq_rmsnorm_pair(xv[u].z, gv[u].z, rn), dq_rmsnorm_pair(xv[u].w, gv[u].w, rn));
+      __syncthreads();  // wmax is reused for the amax below
+    }
     // amax over K bf16, then quantise into LDS (int8_quant_per_token_kernel's arithmetic)
     float m = 0.f;
 #pragma unroll
@@ -206,28 +250,67 @@ __global__ __launch_bounds__(512) void int8dyn_gemv_kernel(Int8DynGemvArgs a) {
       for (int kk = 0; kk < Wk; ++kk) total += lds_i[(rg * Wk + kk) * V + widx];
     }
   }
-  if (writer) {
-    const int r = widx / MT, m = widx % MT;
-    const int n = row0 + r;
-    if (n < N && m < a.M) {
-      // bf16(c) * x_scale, * w_scale, each rounded (intmm.py:133-137, plain_layout.py:301-315);
-      // the MFMA path's Int8Dyn::epilogue
-      float o = round_bf16(round_bf16((float)total) * sx[m]);
-      o = round_bf16(o * bf16_to_f32(a.ws[n]));
-      if (a.bias != nullptr) o = round_bf16(o + bf16_to_f32(a.bias[n]));
-      a.y[(size_t)m * N + n] = f32_to_bf16(o);
+  if constexpr (EPI == kDqEpiNone) {
+    if (writer) {
+      const int r = widx / MT, m = widx % MT;
+      const int n = row0 + r;
+      if (n < N && m < a.M) {
+        // bf16(c) * x_scale, * w_scale, each rounded (intmm.py:133-137, plain_layout.py:301-315);
+        // the MFMA path's Int8Dyn::epilogue
+        float o = round_bf16(round_bf16((float)total) * sx[m]);
+        o = round_bf16(o * bf16_to_f32(a.ws[n]));
+        if (a.bias != nullptr) o = round_bf16(o + bf16_to_f32(a.bias[n]));
+        a.y[(size_t)m * N + n] = f32_to_bf16(o);
+      }
+    }
+  } else {
+    // the linear's output of this lane's row, then row pair (2p, 2p+1) meets in lane p
+    const int nr = row0 + (widx < V ? widx : 0);
+    float o = round_bf16(round_bf16((float)total) * sx[0]);
+    o = round_bf16(o * bf16_to_f32(a.ws[nr < N ? nr : N - 1]));
+    const int sh = Wk > 1 ? 0 : 6 - T;
+    const int pl = lane < RPW / 2 ? lane : 0;
+    const float ea = __shfl(o, (2 * pl) << sh);
+    const float eb = __shfl(o, (2 * pl + 1) << sh);
+    const int n = row0 + 2 * pl;
+    if ((Wk == 1 || wk == 0) && lane < RPW / 2 && n < N) {
+      if constexpr (EPI == kDqEpiSwiGLU) {
+        a.y[n >> 1] = f32_to_bf16(round_bf16(ea / (1.f + __expf(-ea))) * eb);
+      } else {
+        const int D = a.D, HD = a.H * a.D, KD = a.Hkv * a.D;
+        int64_t p = a.pos[0];
+        const bool pok = p >= 0 && p < a.T;
+        if (!pok) {
+          flag_decode_error(kDecodeErrKvPos);
+          p = p < 0 ? 0 : a.T - 1;
+        }
+        uint32_t ov = (uint32_t)f32_to_bf16(ea) | ((uint32_t)f32_to_bf16(eb) << 16);
+        if (n < HD + KD) {
+          const float2 cs = reinterpret_cast<const float2*>(a.freqs)[p * (D >> 1) + ((n % D) >> 1)];
+          const float o0 = ea * cs.x - eb * cs.y, o1 = eb * cs.x + ea * cs.y;
+          ov = (uint32_t)f32_to_bf16(o0) | ((uint32_t)f32_to_bf16(o1) << 16);
+        }
+        if (n < HD) {
+          reinterpret_cast<uint32_t*>(a.y)[n >> 1] = ov;
+        } else if (pok) {
+          const int nk = n < HD + KD ? n - HD : n - HD - KD;
+          uint16_t* cache = n < HD + KD ? a.k_cache : a.v_cache;
+          const size_t off = ((size_t)(nk / D) * a.T + p) * D + nk % D;
+          reinterpret_cast<uint32_t*>(cache)[off >> 1] = ov;
+        }
+      }
     }
   }
 }
 
 
-template <int MT, int RPW, int NPT>
+template <int MT, int RPW, int NPT, int EPI = kDqEpiNone>
 int launch_dyn_gemv_npt(Int8DynGemvArgs a, int grid, int threads, size_t lds, hipStream_t stream) {
-  launch((int8dyn_gemv_kernel<MT, RPW, NPT>), dim3(grid), dim3(threads), lds, stream, a);
+  launch((int8dyn_gemv_kernel<MT, RPW, NPT, EPI>), dim3(grid), dim3(threads), lds, stream, a);
   return check_launch("int8dyn_gemv_kernel");
 }
 
-template <int MT, int RPW, bool FQ>
+template <int MT, int RPW, bool FQ, int EPI = kDqEpiNone>
 int launch_dyn_gemv(Int8DynGemvArgs a, int wk, int g, hipStream_t stream) {
   const int nchunk = a.K / 16;
   a.S = (nchunk + 63) / 64;
@@ -246,11 +329,12 @@ int launch_dyn_gemv(Int8DynGemvArgs a, int wk, int g, hipStream_t stream) {
   if constexpr (FQ) {
     const size_t lds = (((size_t)nw * RPW * MT + 8 + 3) & ~(size_t)3) * sizeof(int) + (size_t)a.K;
     const int per = (a.K / 8 + threads - 1) / threads;  // pieces per thread
-    if (per <= 1) return launch_dyn_gemv_npt<MT, RPW, 1>(a, grid, threads, lds, stream);
-    if (per <= 2) return launch_dyn_gemv_npt<MT, RPW, 2>(a, grid, threads, lds, stream);
-    if (per <= 4) return launch_dyn_gemv_npt<MT, RPW, 4>(a, grid, threads, lds, stream);
-    if (per <= 8) return launch_dyn_gemv_npt<MT, RPW, 8>(a, grid, threads, lds, stream);
-    if (per <= 16) return launch_dyn_gemv_npt<MT, RPW, 16>(a, grid, threads, lds, stream);
+    if (per <= 1) return launch_dyn_gemv_npt<MT, RPW, 1, EPI>(a, grid, threads, lds, stream);
+    if (per <= 2) return launch_dyn_gemv_npt<MT, RPW, 2, EPI>(a, grid, threads, lds, stream);
+    if (per <= 4) return launch_dyn_gemv_npt<MT, RPW, 4, EPI>(a, grid, threads, lds, stream);
+    if (per <= 8) return launch_dyn_gemv_npt<MT, RPW, 8, EPI>(a, grid, threads, lds, stream);
+    if (a.norm_w == nullptr && per <= 16)  // (the norm's weight pieces double the registers)
+      return launch_dyn_gemv_npt<MT, RPW, 16, EPI>(a, grid, threads, lds, stream);
     TAO_CHECK_ARG(false, "int8 dyn linear: K (%d) too long for the token prologue", a.K);
   }
   return TAO_OK;
@@ -259,7 +343,7 @@ int launch_dyn_gemv(Int8DynGemvArgs a, int wk, int g, hipStream_t stream) {
 // M == 1 shape (experiments/sweep_int8.py, profiles/r1_sweep_int8.jsonl, fused path):
 // K <= 4096: 4 rows per wave, 2 waves along K, 2 row groups (one for the 128256-row head);
 // longer K: 8 rows per wave, 4 waves along K (4096x14336 11.5 us).
-template <bool FQ>
+template <bool FQ, int EPI = kDqEpiNone>
 int dyn_gemv_m1(Int8DynGemvArgs a, hipStream_t stream) {
   const int S = (a.K / 16 + 63) / 64;
   int rpw = 4, wk = S < 2 ? S : 2, g = a.N >= 65536 ? 1 : 2;
@@ -274,9 +358,9 @@ int dyn_gemv_m1(Int8DynGemvArgs a, hipStream_t stream) {
   if (trpw > 0) rpw = trpw;
   if (twk > 0) wk = twk;
   if (tg > 0) g = tg;
-  if (rpw == 2) return launch_dyn_gemv<1, 2, FQ>(a, wk, g, stream);
-  if (rpw == 8) return launch_dyn_gemv<1, 8, FQ>(a, wk, g, stream);
-  return launch_dyn_gemv<1, 4, FQ>(a, wk, g, stream);
+  if (rpw == 2) return launch_dyn_gemv<1, 2, FQ, EPI>(a, wk, g, stream);
+  if (rpw == 8) return launch_dyn_gemv<1, 8, FQ, EPI>(a, wk, g, stream);
+  return launch_dyn_gemv<1, 4, FQ, EPI>(a, wk, g, stream);
 }
 
 int int8dyn_gemv(Int8DynGemvArgs a, hipStream_t stream) {
@@ -457,6 +541,53 @@ int tao_int8_dyn_linear_bf16(const uint16_t* x, const int8_t* wq, const uint16_t
   Int8DynGemvArgs a{x, nullptr, reinterpret_cast<const uint4*>(wq), ws, bias, y,
                     1, (int)N, (int)K, 0, 0, 0};
   return dyn_gemv_m1<true>(a, as_stream(stream));
+}
+
+int tao_int8dq_decode_bf16(const uint16_t* x, const int8_t* wq, const uint16_t* ws, int64_t N,
+                           int64_t K, const uint16_t* norm_weight, float eps, int epilogue,
+                           uint16_t* y, const float* freqs, const int64_t* pos, uint16_t* k_cache,
+                           uint16_t* v_cache, int64_t n_head, int64_t n_kv_head, int64_t head_dim,
+                           int64_t max_seq, void* stream) {
+  TAO_CHECK_ARG(N >= 0 && K > 0 && K % 16 == 0 && K <= 32768 && N < (1LL << 31),
+                "int8dq decode: K (%lld) must be a positive multiple of 16, <= 32768",
+                (long long)K);
+  TAO_CHECK_ARG(epilogue >= kDqEpiNone && epilogue <= kDqEpiRopeKV,
+                "int8dq decode: epilogue must be 0 (none), 1 (swiglu) or 2 (rope_kv)");
+  TAO_CHECK_ARG(epilogue == kDqEpiNone || N % 2 == 0, "int8dq decode: N (%lld) must be even",
+                (long long)N);
+  TAO_CHECK_ALIGN(x, 16, "x");
+  TAO_CHECK_ALIGN(wq, 16, "wq");
+  Int8DynGemvArgs a{x, nullptr, reinterpret_cast<const uint4*>(wq), ws, nullptr, y,
+                    1, (int)N, (int)K, 0, 0, 0};
+  if (norm_weight != nullptr) TAO_CHECK_ALIGN(norm_weight, 16, "norm_weight");
+  a.norm_w = norm_weight;
+  a.eps = eps;
+  if (epilogue == kDqEpiRopeKV) {
+    TAO_CHECK_ARG(n_head > 0 && n_kv_head > 0 && head_dim > 0 && head_dim % 2 == 0 &&
+                      max_seq > 0 && N == (n_head + 2 * n_kv_head) * head_dim,
+                  "int8dq decode rope_kv: N (%lld) must be (n_head + 2 n_kv_head) * head_dim",
+                  (long long)N);
+    TAO_CHECK_ARG(freqs != nullptr && pos != nullptr && k_cache != nullptr && v_cache != nullptr,
+                  "int8dq decode rope_kv: freqs, pos and caches are required");
+    TAO_CHECK_ALIGN(k_cache, 4, "k_cache");
+    TAO_CHECK_ALIGN(v_cache, 4, "v_cache");
+    TAO_CHECK_ALIGN(y, 4, "y");
+    a.freqs = freqs;
+    a.pos = pos;
+    a.k_cache = k_cache;
+    a.v_cache = v_cache;
+    a.H = (int)n_head;
+    a.Hkv = (int)n_kv_head;
+    a.D = (int)head_dim;
+    a.T = (int)max_seq;
+  }
+  if (N == 0) return TAO_OK;
+  const hipStream_t st = as_stream(stream);
+  switch (epilogue) {
+    case kDqEpiSwiGLU: return dyn_gemv_m1<true, kDqEpiSwiGLU>(a, st);
+    case kDqEpiRopeKV: return dyn_gemv_m1<true, kDqEpiRopeKV>(a, st);
+    default: return dyn_gemv_m1<true>(a, st);
+  }
 }
 
 int tao_tune_int8_gemv(int rows_per_wave, int waves_k, int row_groups) {

@@ -85,6 +85,8 @@ _SIGNATURES = {
                                _p, _p, _p, _i64, _i64, _i64, _i64, _p],
     "tao_int8wo_decode_bf16": [_p, _p, _p, _i64, _i64, _p, ctypes.c_float, _int, _p, _p, _p, _p, _p,
                                _i64, _i64, _i64, _i64, _p],
+    "tao_int8dq_decode_bf16": [_p, _p, _p, _i64, _i64, _p, ctypes.c_float, _int, _p, _p, _p, _p, _p,
+                               _i64, _i64, _i64, _i64, _p],
 }
 _RESTYPES = {"tao_version": ctypes.c_char_p, "tao_last_error": ctypes.c_char_p}
 

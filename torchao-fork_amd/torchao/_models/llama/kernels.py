@@ -6,7 +6,7 @@ import torch
 
 from torchao import _lib
 
-__all__ = ["rmsnorm", "rope_kv", "attn_decode", "silu_mul", "int4_decode", "int8wo_decode", "argmax",
+__all__ = ["rmsnorm", "rope_kv", "attn_decode", "silu_mul", "int4_decode", "int8wo_decode", "int8dq_decode", "argmax",
            "argmax_advance", "check_decode_status"]
 
 
@@ -125,7 +125,8 @@ def int4_decode(x: torch.Tensor, packed: torch.Tensor, scale_and_zero: torch.Ten
 
 
 def int8wo_decode(x: torch.Tensor, w: torch.Tensor, scale: torch.Tensor, norm_weight=None,
-                  eps: float = 0.0, epilogue: str = "none", rope=None) -> torch.Tensor:
+                  eps: float = 0.0, epilogue: str = "none", rope=None,
+                  _entry: str = "tao_int8wo_decode_bf16") -> torch.Tensor:
     """One token through an int8 weight-only linear (w [N, K] int8, scale [N] bf16) with the
     int4_decode fusions (tao_int8wo_decode_bf16): optional RMSNorm of x; epilogue "none",
     "swiglu" or "rope_kv" as in int4_decode."""
@@ -149,10 +150,18 @@ def int8wo_decode(x: torch.Tensor, w: torch.Tensor, scale: torch.Tensor, norm_we
     else:
         y = torch.empty(*x.shape[:-1], N, dtype=x.dtype, device=x.device)
     ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
-    _lib.call("tao_int8wo_decode_bf16", x.data_ptr(), w.data_ptr(), scale.data_ptr(), N, K,
+    _lib.call(_entry, x.data_ptr(), w.data_ptr(), scale.data_ptr(), N, K,
               ptr(norm_weight), float(eps), epi, y.data_ptr(), ptr(freqs), ptr(pos), ptr(kc),
               ptr(vc), H, Hkv, D, T, _stream(x))
     return y
+
+
+def int8dq_decode(x: torch.Tensor, w: torch.Tensor, scale: torch.Tensor, norm_weight=None,
+                  eps: float = 0.0, epilogue: str = "none", rope=None) -> torch.Tensor:
+    """int8wo_decode for the int8 dynamic-activation linear (Int8DynamicActivationInt8Weight):
+    the (normalised) token is quantised per token inside the kernel (tao_int8dq_decode_bf16)."""
+    return int8wo_decode(x, w, scale, norm_weight, eps, epilogue, rope,
+                         _entry="tao_int8dq_decode_bf16")
 
 
 def argmax(logits: torch.Tensor) -> torch.Tensor:

@@ -194,6 +194,32 @@ def _int8wo_parts(lin: Optional[nn.Linear]):
     return impl.int_data, impl.scale.reshape(-1)
 
 
+def _int8dq_parts(lin: Optional[nn.Linear]):
+    """(int_data [N, K] int8, scale [N]) of an Int8DynamicActivationInt8WeightConfig linear with
+    the default per-token activation recipe on the GPU, else None."""
+    w = getattr(lin, "weight", None)
+    if w is None or lin.bias is not None or not w.is_cuda:
+        return None
+    from torchao.quantization.linear_activation_quantized_tensor import (
+        LinearActivationQuantizedTensor,
+    )
+    from torchao.quantization.quant_api import _int8_symm_per_token_reduced_range_quant
+
+    if not (isinstance(w, LinearActivationQuantizedTensor) and not w.quant_kwargs
+            and w.input_quant_func is _int8_symm_per_token_reduced_range_quant):
+        return None
+    # the weight criteria of the one-token int8-dyn dispatch (_fused_int8_dyn_decode)
+    from torchao.dtypes.affine_quantized_tensor import AffineQuantizedTensor
+    from torchao.dtypes.uintx.plain_layout import PlainLayout, _aqt_is_int8
+
+    inner = w.original_weight_tensor
+    if not (isinstance(inner, AffineQuantizedTensor) and _aqt_is_int8(inner)
+            and inner.dtype == torch.bfloat16 and isinstance(inner._layout, PlainLayout)
+            and len(inner.shape) == 2 and inner.tensor_impl.int_data.is_cuda):
+        return None
+    return inner.tensor_impl.int_data, inner.tensor_impl.scale.reshape(-1)
+
+
 def _fused_decode(x, lin, norm=None, epilogue="none", rope=None):
     """One token through ``lin`` with the decode fusions, on whichever fused kernel its weight
     format has (int4 weight-only, int8 weight-only); None if neither applies."""
@@ -209,6 +235,9 @@ def _fused_decode(x, lin, norm=None, epilogue="none", rope=None):
     p8 = _int8wo_parts(lin)
     if p8 is not None:
         return kernels.int8wo_decode(x, *p8, norm_weight=nw, eps=eps, epilogue=epilogue, rope=rope)
+    pq = _int8dq_parts(lin)
+    if pq is not None and (nw is None or x.shape[-1] <= 8192):
+        return kernels.int8dq_decode(x, *pq, norm_weight=nw, eps=eps, epilogue=epilogue, rope=rope)
     return None
 
 
