@@ -9,6 +9,6 @@ for i in $(seq "$N"); do
   for v in A B; do
     if [ "$v" = A ]; then export TORCHAO_MI355X_LIB="$LIBA"; else unset TORCHAO_MI355X_LIB; fi
     out=$(timeout -k 10 200 python3 -m torchao._models.llama.generate -q "$Q" --num_samples 3 2>/dev/null)
-    echo "$v $out" | cut -c1-260
+    echo "$v $(echo "$out" | tail -1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["quantization"], d["decode_tokens_per_s"], d["decode_ms_per_token"], d["prefill_ms"])')"
   done
 done
