@@ -136,6 +136,9 @@ def int8wo_decode(x: torch.Tensor, w: torch.Tensor, scale: torch.Tensor, norm_we
     if x.numel() != K:
         raise RuntimeError(f"int8wo_decode takes one token, got x of shape {tuple(x.shape)}")
     scale = scale.reshape(-1).contiguous()
+    _check(scale, torch.bfloat16, "int8 decode scale")
+    if scale.numel() != N:
+        raise RuntimeError(f"int8 decode: {scale.numel()} scales for {N} rows")
     if norm_weight is not None:
         _check(norm_weight, torch.bfloat16, "int8wo_decode norm_weight")
     epi = _EPILOGUES[epilogue]
