@@ -161,6 +161,33 @@ def calibrate_sharding(shapes, P, g, device, rehearsal, reps=20, pairs=None):
 
         for c in range(copies):
             go(c)
+        # the GEMVs replayed from one HIP graph, as the step runs them (eager launches are
+        # host-bound at these sizes: ~5-11 µs per launch against 3-5 µs replayed); no
+        # collective is captured here, so every rank issues the same calls either way
+        nonlocal sp
+        s = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        sp_eager = sp
+        try:
+            sp = s.cuda_stream
+            with torch.cuda.stream(s):
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph, stream=s):
+                    for i in range(reps):
+                        go(i % copies)
+                graph.replay()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                graph.replay()
+                e1.record(s)
+            e1.synchronize()
+            del graph
+            return e0.elapsed_time(e1) * 1e3 / reps
+        except Exception:  # graph capture unavailable: eager launches
+            torch.cuda.synchronize()
+        finally:
+            sp = sp_eager
+            torch.cuda.current_stream(device).wait_stream(s)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for i in range(reps):
