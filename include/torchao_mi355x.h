@@ -124,6 +124,15 @@ int tao_tune_gemm_table(int off);
 /* int4 MFMA GEMM kernel: 0 = built-in, 1 = the 32x32x16-MFMA kernel (gemm32_int4_kernel).
  * Calling thread only; for A/B measurement. */
 int tao_tune_int4_mfma32(int on);
+/* Weight-shared tile GEMM (csrc/gemm_tile.hip: 4 waves split the rows of a 64/128 x 64 tile, each
+ * weight dequantised once per workgroup into LDS, x fragments straight from global, split-K
+ * reduced by every slice): mode 0 = built-in routing, 1 = never (the MFMA kernels above),
+ * 2 = wherever it applies (K a multiple of its step, M above the GEMV crossover); splits 0 =
+ * built-in, else the largest power of two <= splits (<= 16). Calling thread only. */
+int tao_tune_gemm_tile(int mode, int splits);
+/* Number of split-K workspaces currently owned by captured graphs (each is released with its
+ * graph). Diagnostic for tests; never fails. */
+int tao_graph_workspace_count(void);
 
 /* M == 1 int4 linears without bias: 1 = stage x once per workgroup in LDS (the decode RMSNorm
  * prologue's copy, without the norm), 0 = built-in policy. Calling thread only; for sweeps. */

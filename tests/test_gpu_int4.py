@@ -243,50 +243,119 @@ def test_xlds_knob_m1(N, K, g):
 
 
 # ---- pinned to the reference's real producer: PyTorch-ROCm's aten int4 tile ops --------------
-# reference test/test_ops.py:260-272 SHAPES x inner_k_tiles {2,4,8} (N a multiple of 16 on ROCm)
-ATEN_SHAPES = [(16, 128), (32, 512), (64, 1024), (128, 4096), (256, 1024), (4096, 4096)]
+# reference test/test_ops.py:260-272: SHAPES x INNERKTILES (x QGROUP_SIZES for the dequant), the
+# full grid, plus small shapes (N a multiple of 16: PyTorch-ROCm's packer needs it).
+REF_SHAPES = [(4096, 4096), (4096, 11008), (11008, 4096), (4096, 14336), (14336, 4096)]
+ATEN_SHAPES = REF_SHAPES + [(16, 128), (32, 512), (64, 1024), (256, 1024)]
 
 
 @pytest.mark.parametrize("N,K", ATEN_SHAPES)
 @pytest.mark.parametrize("ikt", [2, 4, 8])
 def test_tile_pack_equals_aten_convert_weight_to_int4pack(N, K, ikt):
     """A11: pack == aten._convert_weight_to_int4pack(u8, ikt) bit for bit (the call at
-    tensor_core_tiled_layout.py:279, on this box's PyTorch-ROCm), and unpack inverts it
-    (test_ops.py:284-293)."""
+    tensor_core_tiled_layout.py:279, on this box's PyTorch-ROCm), and unpack inverts it on the
+    GPU and on the host (test_ops.py:284-293, the same grid)."""
     if K % (ikt * 16):
         pytest.skip("K not a multiple of ikt * 16")
-    g = torch.Generator().manual_seed(N + K + ikt)
-    q = torch.randint(0, 16, (N, K), generator=g, dtype=torch.int32).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(N + K + ikt)
+    q = torch.randint(0, 16, (N, K), generator=g, dtype=torch.int32, device=DEV)
     u8 = ((q[:, ::2] << 4) | q[:, 1::2]).to(torch.uint8).contiguous()
     ref = torch.ops.aten._convert_weight_to_int4pack(u8, ikt)
     ours = torchao.ops.pack_tensor_core_tiled_layout(q, ikt)  # default map on ROCm: "rocm"
     assert ours.shape == ref.shape and torch.equal(ours, ref.view(torch.int32))
-    assert torch.equal(torchao.ops.unpack_tensor_core_tiled_layout(ref.contiguous(), ikt), q)
+    unpacked = torchao.ops.unpack_tensor_core_tiled_layout(ref.contiguous(), ikt)
+    assert torch.equal(unpacked, q)
+    # the reference test's own check: re-packed bytes equal the input bytes
+    assert torch.equal(((unpacked[:, ::2] << 4) | unpacked[:, 1::2]).to(torch.uint8), u8)
     assert torch.equal(torchao.ops.unpack_tensor_core_tiled_layout(ref.cpu(), ikt), q.cpu())
 
 
-@pytest.mark.parametrize("N,K", [(16, 128), (64, 1024), (256, 1024), (128, 4096)])
-@pytest.mark.parametrize("ikt", [2, 4, 8])
-@pytest.mark.parametrize("g", [32, 64, 128, 256])
-def test_tile_dequant_vs_aten_weight_int4pack_mm_eye(N, K, ikt, g):
-    """A22, reference test_ops.py:339-402: dequantize_tensor_core_tiled_layout against
-    aten._weight_int4pack_mm(eye(K), packed, g, sz).t() of this box's PyTorch-ROCm. The
-    reference asserts diff 0 on CUDA; the measured ROCm bar is recorded in DESIGN §2 and
-    asserted here (1 bf16 ulp of |w|: the two sides round fma vs mul-then-add)."""
-    if K % (ikt * 16) or K % g:
-        pytest.skip("shape not valid for this ikt / group")
-    gen = torch.Generator().manual_seed(N * 7 + K + ikt + g)
-    q = torch.randint(0, 16, (N, K), generator=gen, dtype=torch.int32)
-    s = (torch.rand(K // g, N, generator=gen) * 0.05 + 0.001).to(torch.bfloat16)
-    z = ((torch.rand(K // g, N, generator=gen) - 0.5) * 0.2).to(torch.bfloat16)
-    sz = torch.stack([s, z], -1).contiguous().to(DEV)
-    u8 = ((q[:, ::2] << 4) | q[:, 1::2]).to(torch.uint8).contiguous().to(DEV)
-    packed = torch.ops.aten._convert_weight_to_int4pack(u8, ikt)
-    eye = torch.eye(K, device=DEV, dtype=torch.bfloat16)
-    ref = torch.ops.aten._weight_int4pack_mm(eye, packed, g, sz).t().contiguous()
-    ours = torchao.ops.dequantize_tensor_core_tiled_layout(packed.view(torch.int32), sz, g, ikt)
-    exact = oracle.dequant_tile_fma(q, sz.cpu(), g)
-    assert torch.equal(ours.cpu(), exact)
-    ulp = ref.float().abs().clamp_min(2 ** -126) * 2 ** -7
-    assert bool(((ours.float() - ref.float()).abs() <= ulp).all()), float(
-        (ours.float() - ref.float()).abs().max())
+# ---- checkpoints written by the reference's own classes (oracle/gen_golden_ckpt.py) -----------
+def _ref_ckpt_tags():
+    import os
+
+    from conftest import GOLDEN
+    return sorted(f[len("ref_ckpt_"):-3] for f in os.listdir(GOLDEN)
+                  if f.startswith("ref_ckpt_") and f.endswith(".pt"))
+
+
+@pytest.mark.parametrize("tag", _ref_ckpt_tags())
+def test_reference_written_checkpoint_runs_on_gpu(tag):
+    """a state dict pickled by the REFERENCE's TensorCoreTiledAQTTensorImpl /
+    AffineQuantizedTensor (tile-format storage, K padded to 1024) loads with
+    torch.load(weights_only=True, map_location=cuda) into this package. The tile storage is adopted
+    on the GPU (HIP unpack + row-stream pack), get_plain() returns the reference's (q, s, z) bit for
+    bit, and the linear matches the reference dequant -> F.linear output stored with it within the
+    north-star 1e-2 (and the fp32 accumulation of the same weights within 4e-3)."""
+    import os
+
+    import torchao.ops as tops
+    from conftest import GOLDEN
+
+    rec = load_golden(f"ref_ckpt_{tag}.npz")
+    qu8 = rec["q_u8"]
+    q = unpack_u8_nibbles(qu8.reshape(-1, qu8.shape[-1])).reshape(*qu8.shape[:-1], -1)
+    s, z, bias = bf16(rec["s"]), bf16(rec["z"]), bf16(rec["bias"])
+    N, K, g, E = int(rec["N"]), int(rec["K"]), int(rec["g"]), int(rec["E"])
+    path = os.path.join(GOLDEN, f"ref_ckpt_{tag}.pt")
+    with tops.checkpoint_tile_format(str(rec["fmt"])):
+        # the reference's own flow (test_quant_api.py:746-750, torchtune): load on the CPU (tile
+        # storage adopted by the host C++ unpack), then move every tensor to the GPU
+        sd = torch.load(path, weights_only=True, map_location="cpu")
+        sd = {k: v.to(DEV) for k, v in sd.items()}
+        # and straight onto the GPU (adopted by the HIP unpack kernel)
+        sd_dev = torch.load(path, weights_only=True, map_location=f"cuda:{torch.cuda.current_device()}")
+    aqt = sd["experts.weight" if E else "weight"]
+    aqt_dev = sd_dev["experts.weight" if E else "weight"]
+    assert aqt.device.type == "cuda" and aqt.tensor_impl.packed_weight.is_cuda
+    assert torch.equal(aqt_dev.tensor_impl.packed_weight, aqt.tensor_impl.packed_weight)
+    assert torch.equal(aqt_dev.tensor_impl.scale_and_zero, aqt.tensor_impl.scale_and_zero)
+    qq, ss, zz = aqt.tensor_impl.get_plain()
+    assert torch.equal(qq.cpu(), q) and torch.equal(ss.cpu(), s) and torch.equal(zz.cpu(), z)
+    x = bf16(rec["x"])
+    if E:  # MoE: expert 0's slice of the adopted [E, N, K/8] storage
+        impl = aqt.tensor_impl
+        y = torch.ops.torchao.int4_weight_only_linear(
+            x.to(DEV), impl.packed_weight[0].contiguous(), impl.scale_and_zero[0].contiguous(), g,
+            bias[0].to(DEV)).cpu()
+        q0, s0, z0, b0 = q[0], s[0], z[0], bias[0]
+    else:
+        from torchao.quantization import Int4WeightOnlyConfig, quantize_
+
+        lin = torch.nn.Linear(K, N, dtype=torch.bfloat16, device=DEV)
+        quantize_(lin, Int4WeightOnlyConfig(group_size=g))
+        lin.load_state_dict(sd, assign=True)  # reference test_quant_api.py:750
+        y = lin(x.to(DEV)).cpu()
+        q0, s0, z0, b0 = q, s, z, bias
+    assert oracle.rel_l2(y, bf16(rec["y_dequant"])) < TOL_REF
+    assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q0, s0, z0, g, b0)) < TOL_FP32
+
+
+def test_operands_on_another_device_raise():
+    """a weight, scale or bias that is not on x's device raises RuntimeError in
+    the C++ op kernels and the Python impls, instead of reaching a launch as a foreign pointer."""
+    N, K, g = 64, 256, 32
+    w, q, s, z = _qparams(N, K, g)
+    packed, sz = _gpu_weight(q, s, z)
+    x = oracle.make_activation(1, K, seed=1).to(DEV)
+    with pytest.raises(RuntimeError, match="same device"):
+        torch.ops.torchao.int4_weight_only_linear(x, packed.cpu(), sz, g, None)
+    with pytest.raises(RuntimeError, match="same device"):
+        torch.ops.torchao.int4_weight_only_linear(x, packed, sz.cpu(), g, None)
+    with pytest.raises(RuntimeError, match="same device"):
+        torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, torch.zeros(N, dtype=torch.bfloat16))
+    with pytest.raises(RuntimeError, match="same device"):
+        torch.ops.torchao.int4_dequantize(packed, sz.cpu(), g, 0)
+    s8 = oracle.int8_weight_qparams(w)
+    q8 = oracle.int8_weight_quantize(w, s8)
+    with pytest.raises(RuntimeError, match="same device"):
+        torch.ops.torchao.int8_weight_only_linear(x, q8, s8.to(DEV), None)
+    with pytest.raises(RuntimeError, match="same device"):
+        torch.ops.torchao.int8_weight_only_linear(x, q8.to(DEV), s8, None)
+    xq, xs = torch.ops.torchao.int8_quantize_per_token(x)
+    with pytest.raises(RuntimeError, match="same device"):
+        torch.ops.torchao.int8_scaled_mm(xq, xs, q8.to(DEV), s8, None)
+    with pytest.raises(RuntimeError, match="same device"):
+        torch.ops.torchao.int8_scaled_mm(xq, xs.cpu(), q8.to(DEV), s8.to(DEV), None)
+    with pytest.raises(RuntimeError, match="same device"):
+        torch.ops.torchao.int8_dyn_linear(x, q8, s8.to(DEV), None)

@@ -63,93 +63,186 @@ Tuning& tuning() {
 }
 
 // ---- split-K workspace --------------------------------------------------------------------------
+// Two counter arrays, both zeroed once:
+//  * cnt  (u32): gemm_mfma.hip's last-arriver tickets, each reset to 0 by its tile's last arriver;
+//  * sync (u64): gemm_tile.hip's epoch counters (arrivals advance by 64 per launch, claim words hold
+//    launch epochs; never reset). Separate arrays, so neither protocol sees the other's values.
 struct Workspace {
   void* slab = nullptr;
   size_t slab_cap = 0;
   unsigned* cnt = nullptr;
   size_t cnt_cap = 0;
+  unsigned long long* sync = nullptr;
+  size_t sync_cap = 0;
 };
-static std::mutex g_ws_mu;
-// eager: one per (device, stream); graphs: one per (device, capture sequence id), never freed
+static std::recursive_mutex g_ws_mu;
+// eager: one per (device, stream); graphs: one per (device, capture sequence id), owned by the graph
 static std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
 static std::map<std::pair<int, unsigned long long>, Workspace> g_ws_graph;
+// buffers of destroyed graphs, freed by the next eager call (a user-object destructor may not call
+// HIP; it runs once the graph, its executable copies and their pending launches are gone)
+static std::vector<void*> g_ws_retired;
 
 // Allocate zeroed counters without touching any stream that may be capturing: a private
 // non-blocking stream does the memset (it does not synchronise with the capturing stream).
-static int alloc_counters(unsigned** cnt, size_t n) {
-  if (hipMalloc(reinterpret_cast<void**>(cnt), n * sizeof(unsigned)) != hipSuccess)
+static int alloc_zeroed(void** p, size_t bytes) {
+  if (hipMalloc(p, bytes) != hipSuccess)
     return set_error(TAO_ERR_HIP, "split-K counter allocation failed");
   hipStream_t s = nullptr;
   if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
     return set_error(TAO_ERR_HIP, "split-K counter init: stream creation failed");
-  const bool ok = hipMemsetAsync(*cnt, 0, n * sizeof(unsigned), s) == hipSuccess &&
-                  hipStreamSynchronize(s) == hipSuccess;
+  const bool ok = hipMemsetAsync(*p, 0, bytes, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
   (void)hipStreamDestroy(s);
   return ok ? TAO_OK : set_error(TAO_ERR_HIP, "split-K counter init failed");
 }
 
-int split_workspace(hipStream_t stream, size_t slab_bytes, size_t counters, void** slab,
-                    unsigned** cnt) {
+static int alloc_set(Workspace& n, size_t slab_bytes, size_t counters, size_t sync_words) {
+  if (slab_bytes && hipMalloc(&n.slab, slab_bytes) != hipSuccess)
+    return set_error(TAO_ERR_HIP, "hipMalloc of %zu B split-K slabs failed", slab_bytes);
+  n.slab_cap = slab_bytes;
+  if (counters) {
+    const int rc = alloc_zeroed(reinterpret_cast<void**>(&n.cnt), counters * sizeof(unsigned));
+    if (rc != TAO_OK) return rc;
+  }
+  n.cnt_cap = counters;
+  if (sync_words) {
+    const int rc =
+        alloc_zeroed(reinterpret_cast<void**>(&n.sync), sync_words * sizeof(unsigned long long));
+    if (rc != TAO_OK) return rc;
+  }
+  n.sync_cap = sync_words;
+  return TAO_OK;
+}
+
+// One allocation set of a captured graph: released when the graph is destroyed (the
+// buffers used to live forever, so every re-capture leaked device memory).
+struct GraphBuffers {
+  std::pair<int, unsigned long long> key;
+  void* ptrs[3];
+};
+static void graph_buffers_release(void* arg) {
+  GraphBuffers* gb = static_cast<GraphBuffers*>(arg);
+  std::lock_guard<std::recursive_mutex> lock(g_ws_mu);
+  for (void* p : gb->ptrs)
+    if (p) g_ws_retired.push_back(p);
+  auto it = g_ws_graph.find(gb->key);
+  if (it != g_ws_graph.end() && it->second.slab == gb->ptrs[0] && it->second.cnt == gb->ptrs[1] &&
+      it->second.sync == gb->ptrs[2])
+    g_ws_graph.erase(it);
+  delete gb;
+}
+
+static void free_retired_locked() {
+  for (void* p : g_ws_retired) (void)hipFree(p);
+  g_ws_retired.clear();
+}
+
+static int get_workspace(hipStream_t stream, size_t slab_bytes, size_t counters, size_t sync_words,
+                         Workspace* out) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return set_error(TAO_ERR_HIP, "hipGetDevice failed");
-  std::lock_guard<std::mutex> lock(g_ws_mu);
+  std::lock_guard<std::recursive_mutex> lock(g_ws_mu);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   unsigned long long cap_id = 0;
-  if (hipStreamGetCaptureInfo(stream, &cs, &cap_id) != hipSuccess)
+  hipGraph_t graph = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t ndeps = 0;
+  if (hipStreamGetCaptureInfo_v2(stream, &cs, &cap_id, &graph, &deps, &ndeps) != hipSuccess)
     return set_error(TAO_ERR_HIP, "hipStreamGetCaptureInfo failed");
   if (cs == hipStreamCaptureStatusActive) {
-    // This capture's own workspace. Allocation is not a stream operation; relaxed mode lets
-    // this thread make it while a global-mode capture is open. A larger request later in the
-    // same capture retires the smaller buffers (kept: earlier nodes of this graph use them).
-    Workspace& w = g_ws_graph[{dev, cap_id}];
-    if (w.slab_cap < slab_bytes || w.cnt_cap < counters) {
+    // This capture's own workspace. Allocation is not a stream operation; relaxed mode lets this
+    // thread make it while a global-mode capture is open. A larger request later in the same
+    // capture allocates a new set; the graph owns every set (earlier nodes use the older ones).
+    const std::pair<int, unsigned long long> key{dev, cap_id};
+    Workspace& w = g_ws_graph[key];
+    if (w.slab_cap < slab_bytes || w.cnt_cap < counters || w.sync_cap < sync_words) {
       hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
       (void)hipThreadExchangeStreamCaptureMode(&mode);
-      int rc = TAO_OK;
       Workspace n;
-      n.slab_cap = std::max(slab_bytes, w.slab_cap);
-      n.cnt_cap = std::max(counters, w.cnt_cap);
-      if (hipMalloc(&n.slab, n.slab_cap) != hipSuccess)
-        rc = set_error(TAO_ERR_HIP, "hipMalloc of %zu B split-K slabs (capture) failed",
-                       n.slab_cap);
-      if (rc == TAO_OK) rc = alloc_counters(&n.cnt, n.cnt_cap);
+      int rc = alloc_set(n, std::max(slab_bytes, w.slab_cap), std::max(counters, w.cnt_cap),
+                         std::max(sync_words, w.sync_cap));
+      if (rc == TAO_OK) {
+        GraphBuffers* gb = new GraphBuffers{key, {n.slab, n.cnt, n.sync}};
+        hipUserObject_t obj = nullptr;
+        if (hipUserObjectCreate(&obj, gb, graph_buffers_release, 1,
+                                hipUserObjectNoDestructorSync) != hipSuccess ||
+            hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+          delete gb;
+          rc = set_error(TAO_ERR_HIP, "split-K workspace: graph user object failed");
+        }
+      }
       (void)hipThreadExchangeStreamCaptureMode(&mode);
       if (rc != TAO_OK) return rc;
-      w = n;  // the previous buffers are intentionally leaked: the graph references them
+      w = n;
     }
-    *slab = w.slab;
-    *cnt = w.cnt;
+    *out = w;
     return TAO_OK;
   }
   if (cs != hipStreamCaptureStatusNone)
     return set_error(TAO_ERR_HIP, "split-K launch on an invalidated capture");
+  free_retired_locked();
   Workspace& w = g_ws[{dev, stream}];
-  if (w.slab_cap < slab_bytes || w.cnt_cap < counters) {
+  if (w.slab_cap < slab_bytes || w.cnt_cap < counters || w.sync_cap < sync_words) {
     // only work queued on this stream can hold the old buffers (graphs never borrow them)
     if (hipStreamSynchronize(stream) != hipSuccess)
       return set_error(TAO_ERR_HIP, "hipStreamSynchronize failed");
-    const size_t sb = std::max(slab_bytes, w.slab_cap);
-    const size_t nc = std::max(counters, w.cnt_cap);
-    if (w.slab_cap < sb) {
+    if (w.slab_cap < slab_bytes) {
       (void)hipFree(w.slab);
       w.slab = nullptr;
       w.slab_cap = 0;
-      if (hipMalloc(&w.slab, sb) != hipSuccess)
-        return set_error(TAO_ERR_HIP, "hipMalloc of %zu B split-K slabs failed", sb);
-      w.slab_cap = sb;
+      if (hipMalloc(&w.slab, slab_bytes) != hipSuccess)
+        return set_error(TAO_ERR_HIP, "hipMalloc of %zu B split-K slabs failed", slab_bytes);
+      w.slab_cap = slab_bytes;
     }
-    if (w.cnt_cap < nc) {
+    if (w.cnt_cap < counters) {
       (void)hipFree(w.cnt);
       w.cnt = nullptr;
       w.cnt_cap = 0;
-      const int rc = alloc_counters(&w.cnt, nc);
+      const int rc = alloc_zeroed(reinterpret_cast<void**>(&w.cnt), counters * sizeof(unsigned));
       if (rc != TAO_OK) return rc;
-      w.cnt_cap = nc;
+      w.cnt_cap = counters;
+    }
+    if (w.sync_cap < sync_words) {
+      // epoch counters: a grown array restarts at zero, which the protocol allows (every tile
+      // counter is a multiple of 64 between launches and claim epochs only need to increase per
+      // counter; the old array is gone with its values)
+      (void)hipFree(w.sync);
+      w.sync = nullptr;
+      w.sync_cap = 0;
+      const int rc =
+          alloc_zeroed(reinterpret_cast<void**>(&w.sync), sync_words * sizeof(unsigned long long));
+      if (rc != TAO_OK) return rc;
+      w.sync_cap = sync_words;
     }
   }
+  *out = w;
+  return TAO_OK;
+}
+
+int split_workspace(hipStream_t stream, size_t slab_bytes, size_t counters, void** slab,
+                    unsigned** cnt) {
+  Workspace w;
+  const int rc = get_workspace(stream, slab_bytes, counters, 0, &w);
+  if (rc != TAO_OK) return rc;
   *slab = w.slab;
   *cnt = w.cnt;
   return TAO_OK;
+}
+
+int split_workspace_epoch(hipStream_t stream, size_t slab_bytes, size_t sync_words, void** slab,
+                          unsigned long long** sync) {
+  Workspace w;
+  const int rc = get_workspace(stream, slab_bytes, 0, sync_words, &w);
+  if (rc != TAO_OK) return rc;
+  *slab = w.slab;
+  *sync = w.sync;
+  return TAO_OK;
+}
+
+// Graph workspaces alive (for tests: re-capturing and destroying graphs must not grow this).
+int graph_workspace_count() {
+  std::lock_guard<std::recursive_mutex> lock(g_ws_mu);
+  return (int)g_ws_graph.size();
 }
 
 }  // namespace tao
@@ -173,6 +266,8 @@ int tao_tune_reset(void) {
   tao::tuning() = tao::Tuning{};
   return TAO_OK;
 }
+
+int tao_graph_workspace_count(void) { return tao::graph_workspace_count(); }
 
 int tao_tune_splitk_fenced(int fenced) {
   TAO_CHECK_ARG(fenced == 0 || fenced == 1, "tune: splitk_fenced must be 0 or 1");

@@ -45,6 +45,17 @@ int int4_check_linear_args(const uint16_t* x, const uint32_t* packed, const uint
                            uint16_t* y, int64_t M, int64_t N, int64_t K, int64_t group_size);
 int int8wo_gemv(const uint16_t* x, const int8_t* w, const uint16_t* scale, const uint16_t* bias,
                 uint16_t* y, int64_t M, int64_t N, int64_t K, hipStream_t stream);
+// gemm_tile.hip: the weight-shared tile GEMM (4 waves split the rows, weights dequantised once per
+// workgroup) and its routing rule
+int tile_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int gshift,
+              const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream,
+              int splits);
+int tile_int8wo(const uint16_t* x, const int8_t* w, const uint16_t* scale, const uint16_t* bias,
+                uint16_t* y, int M, int N, int K, hipStream_t stream, int splits);
+int tile_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uint16_t* ws,
+                 const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream,
+                 int splits);
+bool use_tile(int path, int64_t M, int64_t N, int64_t K);
 
 namespace {
 
@@ -1491,6 +1502,8 @@ int int8_scaled_mm_launch(const int8_t* xq, const uint16_t* xs, const int8_t* wq
   // The LDS-staged kernel where its unsplit 64-row tiles fill >= 192 workgroups (M >= 128):
   // M = 128 N = 6144 14.9 vs 20.0 µs, M = 256 4096^2 14.8 vs 16.5, M = 512 22.5 vs 30.8; ties at
   // N >= 14336; the per-wave-column kernel keeps M = 64..128 at N = 4096 (11.8 vs 12.6 µs).
+  if (use_tile(2, M, N, K))
+    return tile_int8dyn(xq, xs, wq, ws, bias, y, M, N, K, stream, tuning().tile_splits);
   const int algo = tao::tuning().gemm_algo;
   const long t64 = (long)((N + 63) / 64) * ((M + 63) / 64);
   const bool tuned = algo == 0 && tuned_shape(Int8Dyn::kPathId, M, N, K) != nullptr;
@@ -1515,6 +1528,9 @@ extern "C" int tao_int4wo_linear_bf16(const uint16_t* x, const uint32_t* packed,
   hipStream_t st = tao::as_stream(stream);
   if (tao::use_gemv(M, N, K))
     return tao::int4wo_gemv(x, packed, sz, bias, y, M, N, K, group_size, st);
+  if (tao::use_tile(0, M, N, K))
+    return tao::tile_int4(x, packed, sz, tao::gshift_of(group_size), bias, y, (int)M, (int)N,
+                          (int)K, st, tao::tuning().tile_splits);
   if (tao::tuning().int4_mfma32 == 1)  // 32x32x16 MFMA kernel (tao_tune_int4_mfma32)
     return tao::launch_gemm32_int4(x, packed, sz, tao::gshift_of(group_size), bias, y, (int)M,
                                    (int)N, (int)K, st);
@@ -1545,6 +1561,9 @@ extern "C" int tao_int8wo_linear_bf16(const uint16_t* x, const int8_t* w, const 
   TAO_CHECK_ALIGN(scale, 2, "scale");
   hipStream_t st = tao::as_stream(stream);
   if (tao::use_gemv(M, N, K)) return tao::int8wo_gemv(x, w, scale, bias, y, M, N, K, st);
+  if (tao::use_tile(1, M, N, K))
+    return tao::tile_int8wo(x, w, scale, bias, y, (int)M, (int)N, (int)K, st,
+                            tao::tuning().tile_splits);
   tao::Int8WO pol;
   pol.w = reinterpret_cast<const uint4*>(w);
   pol.scale = scale;

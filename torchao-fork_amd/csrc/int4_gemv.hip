@@ -1,8 +1,10 @@
 // int4 group-quantised weight-only linear, skinny-M (decode) path: y[M][N] = x[M][K] W^T.
 //
 // Replaces aten._weight_int4pack_mm at torchao/dtypes/uintx/tensor_core_tiled_layout.py:104
-// for M <= 8. HBM-bound: every packed weight byte and every (scale, zero) pair is read exactly
-// once, with 16-B non-temporal loads; x (<= 8 x K bf16) stays in L1/L2.
+// for skinny M: the built-in crossover (gemm_mfma.hip use_gemv) sends M <= 2, or M <= 4 for
+// weights of at most 32 Mi elements, here; the kernel itself is instantiated up to M = 8, the
+// cap of tao_tune_linear_crossover. HBM-bound: every packed weight byte and every (scale, zero)
+// pair is read exactly once, with 16-B non-temporal loads; x (<= 8 x K bf16) stays in L1/L2.
 //
 // Work decomposition:
 //   * a "slice" is 2048 consecutive k of one row = 64 lanes x 32 k = one 1-KiB wave load

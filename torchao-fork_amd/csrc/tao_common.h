@@ -29,14 +29,18 @@ int check_launch(const char* what);
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- split-K workspace (capi.cpp) ------------------------------------------------------------
-// Scratch for the partial-sum slabs of split-K launches plus a zeroed array of arrival counters
-// (each reset by its tile's last arriver). Eager calls use one workspace per (device, stream),
+// Scratch for the partial-sum slabs of split-K launches plus zeroed counter arrays: `cnt` (u32
+// tickets, each reset by its tile's last arriver: gemm_mfma.hip) or `sync` (u64 epoch counters and
+// claim words, never reset: gemm_tile.hip). Eager calls use one workspace per (device, stream),
 // grown after a synchronisation of that stream (nothing else ever holds its pointers). A graph
-// capture gets a workspace of its own, per capture sequence, allocated during the capture
-// (relaxed capture mode) and never freed: a replay can never share scratch with eager work or
-// with another graph, and no pointer a graph holds is ever released.
+// capture gets a workspace of its own, per capture sequence, allocated during the capture (relaxed
+// capture mode) and owned by the graph through a user object: a replay never shares scratch with
+// eager work or another graph, and the buffers are released when the graph is destroyed.
 int split_workspace(hipStream_t stream, size_t slab_bytes, size_t counters, void** slab,
                     unsigned** cnt);
+int split_workspace_epoch(hipStream_t stream, size_t slab_bytes, size_t sync_words, void** slab,
+                          unsigned long long** sync);
+int graph_workspace_count();
 
 // ---- launch-shape overrides (tao_tune_*, tao_tune_reset) --------------------------------------
 // Zero means "built-in choice". Thread-local: a tao_tune_* call re-routes only launches issued
@@ -56,6 +60,7 @@ struct Tuning {
   int gemm_table = 0;                            // MFMA GEMM measured-shape table: 0 on, 1 off
   int int4_mfma32 = 0;                           // int4 GEMM on 32x32x16 MFMAs: 0 off, 1 on
   int quant_block = 0;                           // per-token int8 quant: 0 wave kernel, 1 block
+  int gemm_tile = 0, tile_splits = 0;            // weight-shared tile GEMM: 0 auto, 1 off, 2 on
 };
 Tuning& tuning();
 

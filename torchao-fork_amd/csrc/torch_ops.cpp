@@ -52,6 +52,18 @@ T* mptr(const Tensor& t) {
   return reinterpret_cast<T*>(t.data_ptr());
 }
 
+// Every operand must live on x's device: the kernels take raw device pointers, so a weight left
+// on another GPU (e.g. after a partial .to()) or on the host would reach the launch as a foreign
+// pointer. The reference's aten ops raise on such inputs; so does this.
+void check_device(const Tensor& x, const Tensor& t, const char* name) {
+  TORCH_CHECK(x.is_cuda(), "expected x on a HIP device, got ", x.device());
+  TORCH_CHECK(t.device() == x.device(), name, " is on ", t.device(), " but x is on ", x.device(),
+              ": all operands must be on the same device");
+}
+void check_device(const Tensor& x, const std::optional<Tensor>& t, const char* name) {
+  if (t.has_value()) check_device(x, *t, name);
+}
+
 std::optional<Tensor> bf16_bias(const std::optional<Tensor>& bias) {
   if (!bias.has_value()) return std::nullopt;
   return bias->to(at::kBFloat16).contiguous();
@@ -74,6 +86,9 @@ Tensor int4_weight_only_linear(const Tensor& x, const Tensor& packed_w, const Te
   TORCH_CHECK(x.size(-1) == K, "x last dim ", x.size(-1), " != K ", K);
   TORCH_CHECK(packed_w.is_contiguous(), "packed_w must be contiguous");
   TORCH_CHECK(sz.is_contiguous(), "scales_and_zeros must be contiguous");
+  check_device(x, packed_w, "packed_w");
+  check_device(x, sz, "scales_and_zeros");
+  check_device(x, bias, "bias");
   const Tensor x2 = rows_of(x, K);
   const int64_t M = x2.size(0);
   const std::optional<Tensor> b = bf16_bias(bias);
@@ -98,6 +113,9 @@ Tensor int8_weight_only_linear(const Tensor& x, const Tensor& w_int8, const Tens
   const int64_t N = w_int8.size(0), K = w_int8.size(1);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16, "int8 weight-only linear (HIP) needs bf16 x");
   TORCH_CHECK(x.size(-1) == K, "x last dim ", x.size(-1), " != K ", K);
+  check_device(x, w_int8, "w_int8");
+  check_device(x, scale, "scale");
+  check_device(x, bias, "bias");
   const Tensor x2 = rows_of(x, K);
   const int64_t M = x2.size(0);
   const Tensor w = w_int8.contiguous();
@@ -134,6 +152,10 @@ Tensor int8_scaled_mm(const Tensor& x_int8, const Tensor& x_scale, const Tensor&
   const int64_t N = w_int8.size(0), K = w_int8.size(1);
   TORCH_CHECK(x_int8.scalar_type() == at::kChar, "x_int8 must be int8");
   TORCH_CHECK(x_int8.size(-1) == K, "x last dim ", x_int8.size(-1), " != K ", K);
+  check_device(x_int8, x_scale, "x_scale");
+  check_device(x_int8, w_int8, "w_int8");
+  check_device(x_int8, w_scale, "w_scale");
+  check_device(x_int8, bias, "bias");
   const Tensor x2 = x_int8.reshape({-1, K}).contiguous();
   const int64_t M = x2.size(0);
   const Tensor xs = x_scale.reshape({-1}).to(at::kBFloat16).contiguous();
@@ -157,6 +179,9 @@ Tensor int8_dyn_linear(const Tensor& x, const Tensor& w_int8, const Tensor& w_sc
   TORCH_CHECK(x.scalar_type() == at::kBFloat16, "int8_dyn_linear (HIP) needs bf16 x");
   TORCH_CHECK(x.size(-1) == K, "x last dim ", x.size(-1), " != K ", K);
   TORCH_CHECK(x.numel() == K, "int8_dyn_linear is one token (x.numel() == K)");
+  check_device(x, w_int8, "w_int8");
+  check_device(x, w_scale, "w_scale");
+  check_device(x, bias, "bias");
   const Tensor x2 = rows_of(x, K);
   const Tensor ws = w_scale.reshape({-1}).to(at::kBFloat16).contiguous();
   const Tensor w = w_int8.contiguous();

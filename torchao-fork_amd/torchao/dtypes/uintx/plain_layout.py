@@ -5,7 +5,8 @@ quantized tensors as they are. Two quantized-linear pairs are registered from he
 
 * int8 weight-only (:232-266): the reference runs ``torch.mm(x, w.t().to(x.dtype)) * scale``,
   materialising a bf16 copy of W; here ``torch.ops.torchao.int8_weight_only_linear`` reads the
-  int8 weight once (HIP GEMV for M <= 8, bf16-MFMA tiles above) with the same three bf16
+  int8 weight once (HIP GEMV for M <= 2, or M <= 4 for weights of at most 32 Mi elements;
+  bf16-MFMA tiles above) with the same three bf16
   roundings (mm output, * scale, + bias).
 * int8 dynamic activation x int8 weight (:269-315): ``int_scaled_matmul`` + weight scale become
   one int8-MFMA kernel with the two scales fused in its epilogue

@@ -11,7 +11,8 @@ its linear calls:
 * here: the gfx950 row-stream layout ``packed_weight`` int32 ``[N][K/8]`` (dword d of row n =
   k 8d..8d+7, bits 4i / 16+4i = q[8d+2i] / q[8d+2i+1]) + ``scale_and_zero`` bf16
   ``[N][K/g][2]``, no padding (K % group_size == 0 is already required by the config), linear
-  via ``torch.ops.torchao.int4_weight_only_linear`` (HIP GEMV for M <= 8, bf16 MFMA above).
+  via ``torch.ops.torchao.int4_weight_only_linear`` (HIP GEMV for M <= 2, or M <= 4 for weights
+  of at most 32 Mi elements; bf16 MFMA above — csrc/gemm_mfma.hip ``gemv_max_m``).
 
 ``get_plain`` unpacks exactly (HIP kernel / host C++) instead of the reference's K x K identity
 matmul through the int4 GEMM (:465-517). ``inner_k_tiles`` is kept as a field (it names the
@@ -182,11 +183,16 @@ class TensorCoreTiledAQTTensorImpl(AQTTensorImpl):
         """Called when an AQT is unpickled / unflattened with this impl (AffineQuantizedTensor
         .__setstate__): storage in the reference tile format (a torchao checkpoint) is converted
         to the gfx950 row-stream layout, un-padded to the AQT's logical ``shape``; storage of
-        this layout is returned as is."""
+        this layout is returned as is. The tile map (CUDA or ROCm build) must have been chosen
+        explicitly (``torchao.ops.checkpoint_tile_format`` / ``set_default_tile_format``);
+        otherwise this raises rather than guess."""
         if not _is_tile_storage(impl.packed_weight):
             return impl
+        from torchao.ops import chosen_checkpoint_tile_format
+
         packed, sz = convert_from_tensor_core_tiled(
-            impl.packed_weight, impl.scale_and_zero, impl._layout.inner_k_tiles, shape)
+            impl.packed_weight, impl.scale_and_zero, impl._layout.inner_k_tiles, shape,
+            chosen_checkpoint_tile_format())
         return cls(packed, sz, impl.transposed, impl._layout)
 
     @classmethod

@@ -90,6 +90,16 @@ def _require_contig(t: Tensor, name: str):
     torch._check(t.is_contiguous(), lambda: f"{name} must be contiguous")
 
 
+def _same_device(x: Tensor, **operands):
+    """Every operand on x's device (the kernels take raw device pointers; a tensor on another
+    GPU or the host would reach the launch as a foreign pointer). RuntimeError otherwise, like
+    the C++ op kernels (csrc/torch_ops.cpp check_device)."""
+    for name, t in operands.items():
+        if t is not None and t.device != x.device:
+            raise RuntimeError(f"{name} is on {t.device} but x is on {x.device}: all operands "
+                               "must be on the same device")
+
+
 # ---------------------------------------------------------------------------------------------
 # reference tile format (torchao/ops.py:255-377)
 # ---------------------------------------------------------------------------------------------
@@ -106,9 +116,50 @@ def default_tile_format() -> int:
 
 def set_default_tile_format(fmt) -> None:
     """Select the map that tile_format=-1 means: "cuda" / 0 to read a TensorCoreTiledLayout
-    checkpoint written by a CUDA build of torchao, "rocm" / 1 for one written on ROCm."""
-    global _default_tile_format
+    checkpoint written by a CUDA build of torchao, "rocm" / 1 for one written on ROCm. This is
+    also the explicit choice that lets reference checkpoints load (``checkpoint_tile_format``)."""
+    global _default_tile_format, _chosen_tile_format
     _default_tile_format = _tile_format(fmt)
+    _chosen_tile_format = _default_tile_format
+
+
+# The map a reference checkpoint's tile storage is read with. The two maps share the tile
+# tensor's shape and cannot be told apart from the bytes, and CUDA builds write most
+# checkpoints, so loading never guesses: None until set_default_tile_format() or the
+# checkpoint_tile_format() context chooses one (ADVICE r2).
+_chosen_tile_format = None
+
+
+class checkpoint_tile_format:
+    """``with torchao.ops.checkpoint_tile_format("cuda"): torch.load(...)`` — the nibble map of
+    the reference TensorCoreTiledLayout storage being loaded, for the duration of the block."""
+
+    def __init__(self, fmt):
+        self.fmt = _tile_format(fmt) if fmt != -1 else -1
+        torch._check(self.fmt != -1, lambda: "checkpoint_tile_format needs 'cuda' or 'rocm'")
+
+    def __enter__(self):
+        global _chosen_tile_format
+        self._prev = _chosen_tile_format
+        _chosen_tile_format = self.fmt
+        return self
+
+    def __exit__(self, *exc):
+        global _chosen_tile_format
+        _chosen_tile_format = self._prev
+        return False
+
+
+def chosen_checkpoint_tile_format() -> int:
+    """The explicitly chosen map for reference tile storage; raises if none was chosen."""
+    if _chosen_tile_format is None:
+        raise RuntimeError(
+            "this checkpoint holds int4 weights in the reference's TensorCoreTiledLayout tile "
+            "format, whose nibble map depends on the PyTorch build that wrote it (CUDA or ROCm) "
+            "and cannot be detected from the bytes. Choose it before loading: "
+            "torchao.ops.set_default_tile_format('cuda' | 'rocm'), or "
+            "`with torchao.ops.checkpoint_tile_format('cuda' | 'rocm'): torch.load(...)`")
+    return _chosen_tile_format
 
 
 def _tile_format(fmt) -> int:
@@ -198,6 +249,7 @@ def _dequant_tile_cuda(packed_w, scales_and_zeros, group_size, inner_k_tiles, ti
     fmt = _tile_format(tile_format)
     _check_tile_n(N, fmt)
     _check_tile_sz(scales_and_zeros, group_size, N, K)
+    _same_device(packed_w, scales_and_zeros=scales_and_zeros)
     _require_contig(packed_w, "packed_w")
     _require_contig(scales_and_zeros, "scales_and_zeros")
     out = torch.empty((N, K), dtype=torch.bfloat16, device=packed_w.device)
@@ -339,6 +391,7 @@ def _(packed_w: Tensor, scales_and_zeros: Tensor, group_size: int, mode: int = 0
 
 def _int4_dequant_cuda(packed_w, scales_and_zeros, group_size, mode=0):
     N, K = _check_int4_weight(packed_w, scales_and_zeros, group_size)
+    _same_device(packed_w, scales_and_zeros=scales_and_zeros)
     _require_contig(packed_w, "packed_w")
     _require_contig(scales_and_zeros, "scales_and_zeros")
     out = torch.empty((N, K), dtype=torch.bfloat16, device=packed_w.device)
@@ -364,6 +417,7 @@ def _int4_linear_cuda(x, packed_w, scales_and_zeros, group_size, bias=None):
     N, K = _check_int4_weight(packed_w, scales_and_zeros, group_size)
     torch._check(x.dtype is torch.bfloat16, lambda: "int4 weight-only linear needs bf16 input")
     torch._check(x.size(-1) == K, lambda: f"x last dim {x.size(-1)} != K {K}")
+    _same_device(x, packed_w=packed_w, scales_and_zeros=scales_and_zeros, bias=bias)
     x2 = x.reshape(-1, K)
     if not x2.is_contiguous() or x2.data_ptr() % 16:
         x2 = x2.contiguous()
@@ -399,6 +453,7 @@ def _int8wo_linear_cuda(x, w_int8, scale, bias=None):
     N, K = _check_int8_weight(w_int8, scale)
     torch._check(x.dtype is torch.bfloat16, lambda: "int8 weight-only linear (HIP) needs bf16 x")
     torch._check(x.size(-1) == K, lambda: f"x last dim {x.size(-1)} != K {K}")
+    _same_device(x, w_int8=w_int8, scale=scale, bias=bias)
     x2 = x.reshape(-1, K)
     if not x2.is_contiguous() or x2.data_ptr() % 16:
         x2 = x2.contiguous()
@@ -446,6 +501,7 @@ def _int8_scaled_mm_cuda(x_int8, x_scale, w_int8, w_scale, bias=None):
     N, K = _check_int8_weight(w_int8, w_scale)
     torch._check(x_int8.dtype is torch.int8, lambda: "x_int8 must be int8")
     torch._check(x_int8.size(-1) == K, lambda: f"x last dim {x_int8.size(-1)} != K {K}")
+    _same_device(x_int8, x_scale=x_scale, w_int8=w_int8, w_scale=w_scale, bias=bias)
     x2 = x_int8.reshape(-1, K).contiguous()
     M = x2.size(0)
     xs = x_scale.reshape(-1).to(torch.bfloat16).contiguous()
@@ -475,6 +531,7 @@ def _int8_dyn_linear_cuda(x, w_int8, w_scale, bias=None):
     torch._check(x.dtype is torch.bfloat16, lambda: "int8_dyn_linear (HIP) needs bf16 x")
     torch._check(x.size(-1) == K, lambda: f"x last dim {x.size(-1)} != K {K}")
     torch._check(x.numel() == K, lambda: "int8_dyn_linear is one token (x.numel() == K)")
+    _same_device(x, w_int8=w_int8, w_scale=w_scale, bias=bias)
     x2 = x.reshape(1, K)
     if not x2.is_contiguous() or x2.data_ptr() % 16:
         x2 = x2.contiguous()
