@@ -21,16 +21,22 @@ large linears can gain. --shard-policy size / all / none override the measuremen
 Total work is fixed as P grows ("strong" scaling); value counts the whole model's bytes once
 per step.
 
---model 70b runs BASELINE config 5's shapes instead (Llama-3-70B: 80 layers, 43.4 GB of int4
-weights per step; the 1/2/4/8-GPU column-sharded curve of the north star); the default and
-headline workload is the 8B.
+At P > 1 the line also carries config5_70b: BASELINE config 5's Llama-3-70B linear step (80
+layers, 43.4 GB of int4 weights per token) under the fixed Megatron plan (pairs + head gather,
+~1/P of the weights per rank), collectives inside the step's HIP graph, with the GEMV-only and
+collectives-only times beside the whole step (--no-config5 skips it). --model 70b makes the 70B
+the headline instead; the default headline stays the 8B, so the N = 1 point equals BENCH.
 
 Reported (one JSON line, rank 0):
   value        = algorithmic bytes per step x steps / wall time  (GB/s, whole job)
   linear_steps_per_s = steps / wall time (linears only; the model's decode rate is e2e_decode)
   north_star   = BASELINE's per-launch target shape (int4 g32 M=1 4096x4096, wo at 8B): us per
                  launch inside a replayed graph of that shape's launches, and its fraction of
-                 8 TB/s (target 0.70); roofline.per_shape_graph / per_shape_frac hold every shape
+                 8 TB/s (target 0.70, reported unmet while it is), split into the kernel's own
+                 span (dispatch-packet events) and the launch-to-launch gap;
+                 roofline.per_shape_graph / per_shape_frac hold every shape
+  unfused_w13_step = the same 8B step in the reference's module layout (w1, w3 apart: 161
+                 launches, the same bytes), one HIP graph
   roofline     = the GEMV kernel: algorithmic bytes per step / GPU time per step of the
                  GEMV-only graph replayed back to back (HIP events on the replay stream, i.e. the
                  sum of the step's kernel durations in the timed regime), against the MI355X
@@ -139,11 +145,14 @@ def make_int4_weight(N, K, g, seed, device):
 
 
 def calibrate_sharding(shapes, P, g, device, rehearsal, reps=20, pairs=None):
-    """Per (N, K): time the whole-N GEMV and the N/P GEMV + its all-gather (eager launches on
-    the current stream, each shape's weights rotated over copies past the 256 MiB Infinity
-    Cache; GPU events; max over ranks so every rank takes the same decision). An M = 1
-    all-gather is latency-bound (~10 µs class), so only linears whose GEMV saves more than
-    that are worth sharding."""
+    """Per (N, K): time the whole-N GEMV and the N/P GEMV + its all-gather, and per Megatron
+    pair the replicated pair against colwise + rowwise + all-reduce (GEMVs and RCCL collectives
+    each replayed from a HIP graph, as the step runs them; each shape's weights rotated over
+    copies past the 256 MiB Infinity Cache; GPU events; max over ranks so every rank takes the
+    same decision). An M = 1 collective is latency-bound (~10 µs class), so only linears whose
+    GEMV saves more than that are worth sharding. In a gloo rehearsal the collectives are the
+    host-staged ones that rehearsal steps take, timed as such: its decision table is real for
+    that transport (and says "replicate" for nearly everything)."""
     from torchao import _lib
 
     lib = _lib.lib()
@@ -196,34 +205,71 @@ def calibrate_sharding(shapes, P, g, device, rehearsal, reps=20, pairs=None):
         e1.synchronize()
         return e0.elapsed_time(e1) * 1e3 / reps
 
-    def gather_us(N):
-        y_loc = torch.zeros(N // P, device=device, dtype=torch.bfloat16)
-        y = torch.empty(N, device=device, dtype=torch.bfloat16)
-        if rehearsal:
-            return 1e9  # host-staged gloo gathers: never worth it
+    def collective_us(fn):
+        """µs per collective: RCCL ones captured `reps` times in one HIP graph and replayed (as
+        the step runs them; eager if capture fails); in a gloo rehearsal the host-staged path the
+        rehearsal step takes, timed on the host clock."""
         for _ in range(3):
-            dist.all_gather_into_tensor(y, y_loc)
+            fn()
+        torch.cuda.synchronize()
+        if rehearsal:
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) * 1e6 / reps
+        s = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(graph, stream=s):
+                    for _ in range(reps):
+                        fn()
+                graph.replay()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                graph.replay()
+                e1.record(s)
+            e1.synchronize()
+            del graph
+            return e0.elapsed_time(e1) * 1e3 / reps
+        except Exception:  # capture of collectives unavailable: eager
+            torch.cuda.synchronize()
+        finally:
+            torch.cuda.current_stream(device).wait_stream(s)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(reps):
-            dist.all_gather_into_tensor(y, y_loc)
+            fn()
         e1.record()
         e1.synchronize()
         return e0.elapsed_time(e1) * 1e3 / reps
 
+    def gather_us(N):
+        y_loc = torch.zeros(N // P, device=device, dtype=torch.bfloat16)
+        y = torch.empty(N, device=device, dtype=torch.bfloat16)
+
+        def fn():
+            if rehearsal:
+                parts = [torch.empty_like(y_loc, device="cpu") for _ in range(P)]
+                dist.all_gather(parts, y_loc.cpu())
+                y.copy_(torch.cat(parts))
+            else:
+                dist.all_gather_into_tensor(y, y_loc)
+        return collective_us(fn)
+
     def allreduce_us(N):
         y = torch.zeros(N, device=device, dtype=torch.bfloat16)
-        if rehearsal:
-            return 1e9
-        for _ in range(3):
-            dist.all_reduce(y)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            dist.all_reduce(y)
-        e1.record()
-        e1.synchronize()
-        return e0.elapsed_time(e1) * 1e3 / reps
+
+        def fn():
+            if rehearsal:
+                t = y.cpu()
+                dist.all_reduce(t)
+                y.copy_(t)
+            else:
+                dist.all_reduce(y)
+        return collective_us(fn)
 
     def agree(vals):  # max over ranks so every rank takes the same decision
         t = torch.tensor(vals, dtype=torch.float64, device="cpu" if rehearsal else device)
@@ -570,6 +616,243 @@ def cpu_baseline(cfg, g, budget_s=12.0):
     }
 
 
+def pair_map(lins):
+    """Megatron pairs of a Llama block (colwise -> rowwise): wqkv -> wo, w1||w3 (or w1, w3) -> w2.
+    {index: ("col", partner) | ("row", first colwise partner)}."""
+    pair_of = {}
+    for i, (name, N, K) in enumerate(lins):
+        if name.endswith("attention.wo"):
+            pair_of[i - 1], pair_of[i] = ("col", i), ("row", i - 1)
+        elif name.endswith("feed_forward.w2"):
+            j = i - 1
+            while j >= 0 and lins[j][0].rsplit(".", 1)[0] == name.rsplit(".", 1)[0]:
+                pair_of[j] = ("col", i)
+                j -= 1
+            pair_of[i] = ("row", j + 1)
+    return pair_of
+
+
+def shard_kinds(lins, P, g, policy, calib, shard_min_elems=64 << 20):
+    """Per linear: whole (replicated), gather (colwise + all-gather), local (colwise, output
+    consumed by its rowwise partner), reduce (rowwise on K/P + all-reduce)."""
+    pair_of = pair_map(lins)
+
+    def pair_sharded(i):
+        kind, j = pair_of[i]
+        a, b = (i, j) if kind == "col" else (j, i)
+        (_, Na, Ka), (_, Nb, Kb) = lins[a], lins[b]
+        if Na % P or Kb % (P * g):
+            return False
+        if policy == "tp":
+            return True
+        return bool(calib.get(("pair", Na, Ka, Nb, Kb), {}).get("shard"))
+
+    kinds = []
+    for i, (name, N, K) in enumerate(lins):
+        kind = "whole"
+        if P > 1 and policy != "none":
+            if i in pair_of and policy in ("tp", "auto") and pair_sharded(i):
+                kind = "local" if pair_of[i][0] == "col" else "reduce"
+            elif policy == "auto" and i not in pair_of and N % P == 0:
+                kind = "gather" if calib[(N, K)]["shard"] else "whole"
+            elif policy in ("all", "size") and N % P == 0:
+                kind = "gather" if policy == "all" or N * K >= shard_min_elems else "whole"
+            elif policy == "tp" and i not in pair_of and N % P == 0:
+                kind = "gather"
+        kinds.append(kind)
+    return kinds
+
+
+class LinearStep:
+    """Every int4 linear of one decoded token (M = 1), sharded per `kinds`, with its packed
+    weights, inputs and outputs resident in HBM; `step()` issues the GEMVs on the current stream
+    and the collectives their kinds need (RCCL; host-staged gloo in a rehearsal)."""
+
+    def __init__(self, lins, kinds, P, rank, g, device, rehearsal):
+        from torchao import _lib
+
+        self.lib = _lib.lib()
+        self.P, self.g, self.device, self.rehearsal = P, g, device, rehearsal
+        self.plan, self.xs, self.bytes_per_step = [], {}, 0
+        for i, ((name, N, K), kind) in enumerate(zip(lins, kinds)):
+            n_loc = N // P if kind in ("gather", "local") else N
+            k_loc = K // P if kind == "reduce" else K
+            packed, sz = make_int4_weight(n_loc, k_loc, g,
+                                          seed=1000 * i + (rank if kind != "whole" else 0),
+                                          device=device)
+            if k_loc not in self.xs:
+                self.xs[k_loc] = torch.randn(1, k_loc, device=device, dtype=torch.bfloat16)
+            y_loc = torch.empty(n_loc, device=device, dtype=torch.bfloat16)  # M = 1 row
+            y_full = (torch.empty(N, device=device, dtype=torch.bfloat16) if kind == "gather"
+                      else y_loc)
+            self.plan.append((name, n_loc, k_loc, packed, sz, y_loc, y_full, kind))
+            self.bytes_per_step += int4_alg_bytes(N, K, g)
+        self.weight_bytes_per_rank = sum(e[3].numel() * 4 + e[4].numel() * 2 for e in self.plan)
+        self.stream = torch.cuda.Stream(device)
+        torch.cuda.synchronize()
+
+    def counts(self):
+        return {k: sum(e[7] == k for e in self.plan) for k in ("local", "reduce", "gather", "whole")}
+
+    def step(self, do_gemv=True, do_comm=True, only=None):
+        sp = torch.cuda.current_stream(self.device).cuda_stream
+        g, xs = self.g, self.xs
+        for (_, n_loc, K, packed, sz, y_loc, y_full, kind) in self.plan:
+            if only is not None and (n_loc, K) != only:
+                continue
+            if do_gemv:
+                rc = self.lib.tao_int4wo_linear_bf16(xs[K].data_ptr(), packed.data_ptr(),
+                                                     sz.data_ptr(), None, y_loc.data_ptr(), 1,
+                                                     n_loc, K, g, sp)
+                if rc:
+                    raise RuntimeError(self.lib.tao_last_error().decode())
+            if not do_comm or kind in ("whole", "local"):
+                continue
+            if kind == "gather":
+                if self.rehearsal:
+                    parts = [torch.empty_like(y_loc, device="cpu") for _ in range(self.P)]
+                    dist.all_gather(parts, y_loc.cpu())
+                    y_full.copy_(torch.cat(parts))
+                else:
+                    dist.all_gather_into_tensor(y_full, y_loc)
+            elif self.rehearsal:  # reduce
+                t = y_loc.cpu()
+                dist.all_reduce(t)
+                y_loc.copy_(t)
+            else:
+                dist.all_reduce(y_loc)
+
+    def capture(self, **kw):
+        graph = torch.cuda.CUDAGraph()
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            self.step(**kw)  # warm-up outside capture (RCCL communicators, allocator)
+            with torch.cuda.graph(graph, stream=self.stream):
+                self.step(**kw)
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        torch.cuda.synchronize()
+        return graph
+
+    def try_capture(self, **kw):
+        if self.rehearsal:
+            return None
+        try:
+            return self.capture(**kw)
+        except Exception as e:  # graph capture of collectives is runtime dependent
+            print(f"[bench] graph capture failed ({e}); timing eager launches", file=sys.stderr)
+            torch.cuda.synchronize()
+            return None
+
+    def replay_ms(self, graph, reps):
+        """GPU time per replay of `graph` back to back (HIP events on the replay stream)."""
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(self.stream):
+            graph.replay()
+            ev0.record(self.stream)
+            for _ in range(reps):
+                graph.replay()
+            ev1.record(self.stream)
+        ev1.synchronize()
+        return ev0.elapsed_time(ev1) / reps
+
+    def wall_ms(self, run, steps, warmup):
+        """Driver contract: barrier + synchronize on both sides of exactly `steps` runs, max over
+        ranks. Returns ms per step."""
+        P = self.P
+
+        def barrier():
+            if P > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+
+        for _ in range(warmup):
+            run()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        if P > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64,
+                             device="cpu" if self.rehearsal else self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed / steps * 1e3
+
+    def release(self):
+        self.plan, self.xs = [], {}
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+
+def parallelism_desc(step, policy):
+    c = step.counts()
+    return (f"tp{step.P} (shard policy {policy}): "
+            + ", ".join(f"{c[k]} {k}" for k in ("local", "reduce", "gather", "whole"))
+            + f" of {len(step.plan)} linears (local = colwise feeding its rowwise partner, "
+            "reduce = rowwise + RCCL all-reduce, gather = colwise + RCCL all-gather, whole = "
+            "replicated)")
+
+
+def config5_record(P, rank, g, device, rehearsal, steps, warmup):
+    """BASELINE config 5 at P > 1: the 80-layer Llama-3-70B linear step (321 launches, 43.4 GB of
+    int4 weights per token) under the fixed Megatron plan of DESIGN §6 (wqkv colwise -> wo
+    rowwise + all-reduce, w1||w3 colwise -> w2 rowwise + all-reduce, output head colwise +
+    all-gather: ~1/P of the weights per rank), the collectives captured in the step's graph.
+    Times the whole step (driver contract: barrier, max over ranks), the GEMV-only graph and the
+    collectives-only graph separately."""
+    _, cfg = MODELS["70b"]
+    lins = llama_linears(cfg)
+    st = LinearStep(lins, shard_kinds(lins, P, g, "tp", {}), P, rank, g, device, rehearsal)
+    t_build = time.perf_counter()
+    graph = st.try_capture()
+    ms = st.wall_ms(graph.replay if graph is not None else st.step, steps, warmup)
+    ggemv = st.try_capture(do_comm=False)
+    gemv_ms = st.replay_ms(ggemv, max(steps, 5)) if ggemv is not None else None
+    gcomm = st.try_capture(do_gemv=False)
+    comm_ms = st.wall_ms(gcomm.replay if gcomm is not None else (lambda: st.step(do_gemv=False)),
+                         steps, 2)
+    rec = {
+        "workload": f"Llama-3-70B int4 g{g} weight-only linears, M=1 decode: "
+                    + workload_desc(cfg) + f" ({len(st.plan)} GEMV launches/step)",
+        "value": round(st.bytes_per_step / (ms * 1e-3) / 1e9, 2),
+        "unit": "GB/s",
+        "linear_steps_per_s": round(1e3 / ms, 2),
+        "ms_per_step": round(ms, 4),
+        "gemv_ms_per_step": round(gemv_ms, 4) if gemv_ms is not None else None,
+        "collectives_ms_per_step": round(comm_ms, 4),
+        "bytes_per_step": st.bytes_per_step,
+        "weight_bytes_per_rank": st.weight_bytes_per_rank,
+        "parallelism": parallelism_desc(st, "tp"),
+        "hip_graph": graph is not None,
+        "collectives": "RCCL in the step graph" if graph is not None else
+                       ("host-staged gloo (rehearsal)" if rehearsal else "RCCL, eager"),
+        "scaling": "strong",
+    }
+    del graph, ggemv, gcomm
+    st.release()
+    rec["setup_s"] = round(time.perf_counter() - t_build, 1)
+    return rec
+
+
+def unfused_record(cfg, g, device, steps):
+    """The reference's module layout at P = 1: w1 and w3 as two linears (161 launches, the same
+    bytes as the merged step), one HIP graph, replay GPU time and wall time per step."""
+    lins = llama_linears(cfg, fuse_w13=False)
+    st = LinearStep(lins, ["whole"] * len(lins), 1, 0, g, device, False)
+    graph = st.capture()
+    ms = st.wall_ms(graph.replay, steps, 3)
+    gpu_ms = st.replay_ms(graph, max(steps, 10))
+    rec = {"workload": workload_desc(cfg, False) + f" ({len(st.plan)} GEMV launches/step)",
+           "value": round(st.bytes_per_step / (ms * 1e-3) / 1e9, 2), "unit": "GB/s",
+           "ms_per_step": round(ms, 4), "kernel_ms_per_step": round(gpu_ms, 4),
+           "launches": len(st.plan)}
+    del graph
+    st.release()
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -602,6 +885,8 @@ def main():
     ap.add_argument("--model", default="8b", choices=sorted(MODELS),
                     help="8b = the headline workload (BASELINE config 2); 70b = config 5's "
                          "shapes (43 GB of int4 weights per step)")
+    ap.add_argument("--no-config5", action="store_true",
+                    help="P > 1: skip the Llama-3-70B (BASELINE config 5) sub-record")
     ap.add_argument("--no-fuse-w13", action="store_true",
                     help="w1 and w3 as two linears (the reference's module layout, 161 launches)")
     args = ap.parse_args()
@@ -625,7 +910,7 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=device)
 
-    import torchao
+    import torchao  # noqa: F401
     from torchao import _lib
 
     _lib.lib()  # fail loudly if the native library is missing
@@ -633,17 +918,7 @@ def main():
     g, P = args.group_size, world
     lins = llama_linears(cfg, fuse_w13=not args.no_fuse_w13)
     policy = "all" if args.shard_all else args.shard_policy
-    # Megatron pairs of a Llama block (colwise -> rowwise): wqkv -> wo, w1||w3 (or w1, w3) -> w2
-    pair_of = {}
-    for i, (name, N, K) in enumerate(lins):
-        if name.endswith("attention.wo"):
-            pair_of[i - 1], pair_of[i] = ("col", i), ("row", i - 1)
-        elif name.endswith("feed_forward.w2"):
-            j = i - 1
-            while j >= 0 and lins[j][0].rsplit(".", 1)[0] == name.rsplit(".", 1)[0]:
-                pair_of[j] = ("col", i)
-                j -= 1
-            pair_of[i] = ("row", j + 1)
+    pair_of = pair_map(lins)
     calib = {}
     if P > 1 and policy == "auto":
         pairs = sorted({((lins[i][1], lins[i][2]), (lins[j][1], lins[j][2]))
@@ -651,130 +926,22 @@ def main():
         calib = calibrate_sharding(sorted({(N, K) for _, N, K in lins}), P, g, device,
                                    rehearsal, pairs=pairs)
 
-    def pair_sharded(i):
-        kind, j = pair_of[i]
-        a, b = (i, j) if kind == "col" else (j, i)
-        (_, Na, Ka), (_, Nb, Kb) = lins[a], lins[b]
-        if Na % P or Kb % (P * g):
-            return False
-        if policy == "tp":
-            return True
-        return bool(calib.get(("pair", Na, Ka, Nb, Kb), {}).get("shard"))
-
     # ---- build the sharded weights, inputs and outputs (all resident in HBM) ----
-    # kinds: whole (replicated), gather (colwise + all-gather), local (colwise, output consumed
-    # by its rowwise partner), reduce (rowwise on K/P + all-reduce)
-    plan, bytes_per_step = [], 0
-    xs = {}
-    n_sharded = 0
-    for i, (name, N, K) in enumerate(lins):
-        kind = "whole"
-        if P > 1 and policy != "none":
-            if i in pair_of and policy in ("tp", "auto") and pair_sharded(i):
-                kind = "local" if pair_of[i][0] == "col" else "reduce"
-            elif policy == "auto" and i not in pair_of and N % P == 0:
-                kind = "gather" if calib[(N, K)]["shard"] else "whole"
-            elif policy in ("all", "size") and N % P == 0:
-                kind = "gather" if policy == "all" or N * K >= args.shard_min_elems else "whole"
-            elif policy == "tp" and i not in pair_of and N % P == 0:
-                kind = "gather"
-        n_sharded += kind != "whole"
-        n_loc = N // P if kind in ("gather", "local") else N
-        k_loc = K // P if kind == "reduce" else K
-        packed, sz = make_int4_weight(n_loc, k_loc, g,
-                                      seed=1000 * i + (rank if kind != "whole" else 0),
-                                      device=device)
-        if k_loc not in xs:
-            xs[k_loc] = torch.randn(1, k_loc, device=device, dtype=torch.bfloat16)
-        y_loc = torch.empty(n_loc, device=device, dtype=torch.bfloat16)  # M = 1 row
-        y_full = torch.empty(N, device=device, dtype=torch.bfloat16) if kind == "gather" else y_loc
-        plan.append((name, n_loc, k_loc, packed, sz, y_loc, y_full, kind))
-        bytes_per_step += int4_alg_bytes(N, K, g)
-    torch.cuda.synchronize()
+    st = LinearStep(lins, shard_kinds(lins, P, g, policy, calib, args.shard_min_elems), P, rank,
+                    g, device, rehearsal)
+    plan, xs, bytes_per_step, stream = st.plan, st.xs, st.bytes_per_step, st.stream
+    step, capture = st.step, st.capture
 
-    stream = torch.cuda.Stream(device)
-    lib = _lib.lib()
-
-    def step(do_gemv=True, do_comm=True, only=None):
-        sp = torch.cuda.current_stream(device).cuda_stream
-        for (_, n_loc, K, packed, sz, y_loc, y_full, kind) in plan:
-            if only is not None and (n_loc, K) != only:
-                continue
-            if do_gemv:
-                rc = lib.tao_int4wo_linear_bf16(xs[K].data_ptr(), packed.data_ptr(), sz.data_ptr(),
-                                                None, y_loc.data_ptr(), 1, n_loc, K, g, sp)
-                if rc:
-                    raise RuntimeError(lib.tao_last_error().decode())
-            if not do_comm or kind in ("whole", "local"):
-                continue
-            if kind == "gather":
-                if rehearsal:
-                    parts = [torch.empty_like(y_loc, device="cpu") for _ in range(P)]
-                    dist.all_gather(parts, y_loc.cpu())
-                    y_full.copy_(torch.cat(parts))
-                else:
-                    dist.all_gather_into_tensor(y_full, y_loc)
-            elif rehearsal:  # reduce
-                t = y_loc.cpu()
-                dist.all_reduce(t)
-                y_loc.copy_(t)
-            else:
-                dist.all_reduce(y_loc)
-
-    def capture(**kw):
-        graph = torch.cuda.CUDAGraph()
-        stream.wait_stream(torch.cuda.current_stream(device))
-        with torch.cuda.stream(stream):
-            step(**kw)  # warm-up outside capture (RCCL communicators, allocator)
-            with torch.cuda.graph(graph, stream=stream):
-                step(**kw)
-        torch.cuda.current_stream(device).wait_stream(stream)
-        torch.cuda.synchronize()
-        return graph
-
-    graph = None
-    if not args.no_graph and not rehearsal:
-        try:
-            graph = capture()
-        except Exception as e:  # graph capture of collectives is runtime dependent
-            print(f"[bench] graph capture failed ({e}); timing eager launches", file=sys.stderr)
-            graph = None
+    graph = None if args.no_graph else st.try_capture()
     run = graph.replay if graph is not None else step
-
-    def barrier():
-        if P > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        run()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if P > 1:
-        t = torch.tensor([elapsed], device="cpu" if rehearsal else device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    ms = st.wall_ms(run, args.steps, args.warmup)
+    elapsed = ms * args.steps * 1e-3
 
     # ---- roofline: GEMV-only graph replayed back to back, GPU events on the replay stream ----
     groof = graph if (graph is not None and P == 1) else None
     if groof is None and graph is not None:
         groof = capture(do_comm=False)
-    kernel_ms = None
-    if groof is not None:
-        reps = max(args.steps, 10)
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        with torch.cuda.stream(stream):
-            groof.replay()
-            ev0.record(stream)
-            for _ in range(reps):
-                groof.replay()
-            ev1.record(stream)
-        ev1.synchronize()
-        kernel_ms = ev0.elapsed_time(ev1) / reps
+    kernel_ms = st.replay_ms(groof, max(args.steps, 10)) if groof is not None else None
 
     # per-shape breakdown: one eager step, events written by each kernel's dispatch packet
     with _lib.KernelTimer(len(plan)) as timer:
@@ -804,16 +971,7 @@ def main():
         for (n_loc, K) in sorted({(e[1], e[2]) for e in plan}):
             gs_ = capture(do_comm=False, only=(n_loc, K))
             cnt = sum(1 for e in plan if (e[1], e[2]) == (n_loc, K))
-            reps = max(args.steps, 10)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            with torch.cuda.stream(stream):
-                gs_.replay()
-                e0.record(stream)
-                for _ in range(reps):
-                    gs_.replay()
-                e1.record(stream)
-            e1.synchronize()
-            us = e0.elapsed_time(e1) * 1e3 / reps / cnt
+            us = st.replay_ms(gs_, max(args.steps, 10)) * 1e3 / cnt
             b = int4_alg_bytes(n_loc, K, g)
             per_shape_graph[f"{n_loc}x{K}"] = {
                 "launches": cnt, "us": round(us, 3), "GBps": round(b / (us * 1e-6) / 1e9, 1),
@@ -830,16 +988,10 @@ def main():
 
     comm_ms = None
     if P > 1:
-        gcomm = capture(do_gemv=False) if graph is not None else None
-        fn = gcomm.replay if gcomm is not None else (lambda: step(do_gemv=False))
-        for _ in range(2):
-            fn()
-        barrier()
-        tc = time.perf_counter()
-        for _ in range(args.steps):
-            fn()
-        barrier()
-        comm_ms = (time.perf_counter() - tc) / args.steps * 1e3
+        gcomm = st.try_capture(do_gemv=False) if graph is not None else None
+        comm_ms = st.wall_ms(gcomm.replay if gcomm is not None else (lambda: step(do_gemv=False)),
+                             args.steps, 2)
+        del gcomm
 
     ref_gpu = None
     if P == 1 and not args.no_reference_gpu:
@@ -848,8 +1000,8 @@ def main():
             ref_ms, ref_diff = reference_gpu_step(plan, xs, g, device, args.steps)
             ref_gpu = {
                 "op": "aten._weight_int4pack_mm (PyTorch-ROCm; the reference's GPU int4 GEMM, "
-                      "tensor_core_tiled_layout.py:104), same weights, same 129-call step in one "
-                      "HIP graph",
+                      "tensor_core_tiled_layout.py:104), same weights, same "
+                      f"{len(plan)}-call step in one HIP graph",
                 "value": round(bytes_per_step / (ref_ms * 1e-3) / 1e9, 2),
                 "unit": "GB/s",
                 "ms_per_step": round(ref_ms, 4),
@@ -865,12 +1017,20 @@ def main():
     config2 = config2_shapes(device) if extras and args.model == "8b" else None
     copy_gbps = hbm_copy_gbps(device) if extras else None
 
+    unfused = None
+    if P == 1 and args.model == "8b" and not args.no_fuse_w13 and not args.no_extras \
+            and graph is not None:
+        unfused = unfused_record(cfg, g, device, args.steps)
+    config5 = None
+    if P > 1 and args.model == "8b" and not args.no_config5:
+        config5 = config5_record(P, rank, g, device, rehearsal, max(2, min(args.steps, 10)),
+                                 min(args.warmup, 2))
+
     cpu = None
     if rank == 0 and P == 1 and not args.no_cpu_baseline and args.model == "8b":
         cpu = cpu_baseline(cfg, g)
 
     if rank == 0:
-        ms = elapsed / args.steps * 1e3
         rec = {
             "metric": f"int4 WO linear GB/s + tokens/s vs CPU dequant path, {model_name} shapes M=1",
             "value": round(bytes_per_step * args.steps / elapsed / 1e9, 2),
@@ -896,13 +1056,7 @@ def main():
                 "seq_len": 1,
                 "group_size": g,
                 "bytes_per_step": bytes_per_step,
-                "parallelism": (f"tp{P} (shard policy {policy}): "
-                                + ", ".join(f"{sum(e[7] == k for e in plan)} {k}" for k in
-                                            ("local", "reduce", "gather", "whole"))
-                                + " of " + str(len(plan)) + " linears (local = colwise feeding "
-                                "its rowwise partner, reduce = rowwise + RCCL all-reduce, gather = "
-                                "colwise + RCCL all-gather, whole = replicated)"
-                                if P > 1 else "single-gpu"),
+                "parallelism": parallelism_desc(st, policy) if P > 1 else "single-gpu",
                 "hip_graph": graph is not None,
             },
             "roofline": {
@@ -930,10 +1084,22 @@ def main():
         ns = per_shape_graph.get("4096x4096") if per_shape_graph else None
         if ns is not None:
             # north_star (BASELINE.json): int4 g32 M=1 4096x4096 at >= 70% of HBM peak per
-            # launch; the graph-replayed in-step number (wo's shape at 8B)
+            # launch; the graph-replayed in-step number (wo's shape at 8B), split into the
+            # kernel's own span (dispatch-packet events of the eager step's launches of this
+            # shape) and the launch-to-launch gap the graph leaves between kernels
+            span = per_shape.get("4096x4096", {}).get("us")
             rec["north_star"] = {"shape": f"4096x4096 int4 g{g} M=1",
                                  "us_per_launch": ns["us"], "GBps": ns["GBps"],
-                                 "frac": ns["frac"], "target_frac": 0.70}
+                                 "frac": ns["frac"], "target_frac": 0.70, "met": ns["frac"] >= 0.70,
+                                 "kernel_span_us": span,
+                                 "launch_gap_us": round(ns["us"] - span, 3) if span else None,
+                                 "span_frac": (round(int4_alg_bytes(4096, 4096, g) / (span * 1e-6)
+                                                     / 1e9 / HBM_PEAK_GBPS, 4) if span else None)}
+        if unfused is not None:
+            # the reference's module layout (w1, w3 apart): the same bytes in 161 launches
+            rec["unfused_w13_step"] = unfused
+        if config5 is not None:
+            rec["config5_70b"] = config5
         if ref_gpu is not None:
             rec["reference_gpu"] = ref_gpu
             if "value" in ref_gpu:

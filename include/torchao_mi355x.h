@@ -72,8 +72,9 @@ int tao_int4wo_linear_bf16(const uint16_t* x, const uint32_t* packed, const uint
 int tao_tune_reset(void);
 
 /* Split-K / last-arriver hand-off form for the calling thread: 0 = fence-free sc1 protocol
- * (built-in; MI355X_MICROARCH.md "Hand-offs measured with sc1 loads in place of the acquire",
- * first row), 1 = the same plus agent release / acquire fences (the HIP memory-model form).
+ * (built-in under the HIP 7.2 runtime it was validated on; MI355X_MICROARCH.md "Hand-offs
+ * measured with sc1 loads in place of the acquire", first row), 1 = the same plus agent release /
+ * acquire fences (the HIP memory-model form; built-in under any other runtime version).
  * Both give bit-identical results (tests/test_gpu_gemm_tiles.py). */
 int tao_tune_splitk_fenced(int fenced);
 

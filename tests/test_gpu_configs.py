@@ -113,6 +113,79 @@ def test_config4_llama3_8b_full_width_int4_graph_decode_vs_oracle():
     kernels.check_decode_status()
 
 
+def test_config4_deeper_greedy_graph_decode_vs_oracle():
+    """full Llama-3-8B width, 4 layers, a 128-token prompt, then 32 tokens
+    decoded GREEDILY by one captured HIP graph that feeds itself (fused decode step, on-device
+    argmax -> next token, position += 1). The oracle (oracle/llama_ref.py, fp32 over the
+    reference's int4-dequantized weights) then runs over the prompt plus the decoded tokens:
+    every step's logits within 1e-2 relative, and where the oracle's top-2 margin decides the
+    argmax, the token the graph picked is the oracle's."""
+    from torchao._models.llama.generate import apply_quantization
+
+    torch.manual_seed(0)
+    n_layer, P, N, g = 4, 128, 32, 32
+    model, cfg = _llama3_8b_truncated(n_layer=n_layer, seed=11)
+    W = {}
+    for name, p in model.named_parameters():
+        t = p.detach().cpu()
+        if name.endswith(("wqkv.weight", "wo.weight", "w1.weight", "w2.weight", "w3.weight",
+                          "output.weight")):
+            W[name] = llama_ref.int4_dequant_weight(t, g)
+        else:
+            W[name] = t.float()
+    prompt = torch.randint(0, cfg.vocab_size, (P,), generator=torch.Generator().manual_seed(9))
+
+    model.fuse_w13()
+    apply_quantization(model, f"int4wo-{g}")
+    model.setup_caches(1, P + N)
+    assert model.enable_fused_kernels()
+    with torch.no_grad():
+        pre = model(prompt.view(1, P).to(DEV), torch.arange(P, device=DEV))[0].float().cpu()
+    cur = torch.zeros(1, 1, dtype=torch.int64, device=DEV)
+    pos = torch.zeros(1, dtype=torch.int64, device=DEV)
+    out = torch.empty(1, 1, cfg.vocab_size, dtype=torch.float32, device=DEV)
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.no_grad(), torch.cuda.stream(stream):
+        cur.fill_(int(pre[-1].argmax()))
+        pos.fill_(P)
+        out.copy_(model(cur, pos))  # eager warm-up; its cache row is rewritten by the replay
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            out.copy_(model(cur, pos))
+            cur.copy_(out.argmax(-1))
+            pos.add_(1)
+    torch.cuda.current_stream().wait_stream(stream)
+    tokens, logits = [int(pre[-1].argmax())], []
+    cur.fill_(tokens[0])
+    pos.fill_(P)
+    for _ in range(N):
+        graph.replay()
+        torch.cuda.synchronize()
+        logits.append(out[0, 0].cpu())
+        tokens.append(int(cur[0, 0]))
+    assert int(pos[0]) == P + N
+    seq = torch.cat([prompt, torch.tensor(tokens[:N])])
+    ref = llama_ref.llama_forward_fp32(W, cfg.n_layer, cfg.n_head, cfg.n_local_heads,
+                                       cfg.rope_base, cfg.norm_eps, seq)  # [P + N, V]
+    del W
+    assert _rel(pre, ref[:P]) < 1e-2
+    worst, agree, decided = 0.0, 0, 0
+    for i, got in enumerate([pre[-1]] + logits):
+        want = ref[P - 1 + i]
+        worst = max(worst, _rel(got, want))
+        top2 = want.topk(2).values
+        if float(top2[0] - top2[1]) > 3e-2 * float(want.abs().max()):  # argmax decided
+            decided += 1
+            agree += int(tokens[i] == int(want.argmax()))
+        assert tokens[i] == int(got.argmax())  # the graph's on-device pick = host argmax
+    assert worst < 1e-2, worst
+    assert decided > 0 and agree == decided, (agree, decided)
+    from torchao._models.llama import kernels
+
+    kernels.check_decode_status()
+
+
 # Llama-3-70B linears (SURVEY §8a C5): wqkv, wo, w1||w3 merged, w2, output head
 SHAPES_70B = [(10240, 8192), (8192, 8192), (57344, 8192), (8192, 28672), (128256, 8192)]
 

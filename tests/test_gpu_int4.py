@@ -270,6 +270,43 @@ def test_tile_pack_equals_aten_convert_weight_to_int4pack(N, K, ikt):
     assert torch.equal(torchao.ops.unpack_tensor_core_tiled_layout(ref.cpu(), ikt), q.cpu())
 
 
+@pytest.mark.parametrize("N,K", REF_SHAPES + [(256, 1024)])
+@pytest.mark.parametrize("ikt", [2, 4, 8])
+@pytest.mark.parametrize("g", [32, 64, 128, 256])
+def test_tile_dequant_equals_aten_identity_mm(N, K, ikt, g):
+    """The reference protocol of test_ops.py:339-402 on the full SHAPES x INNERKTILES x
+    QGROUP_SIZES grid: the weight dequantised by aten._weight_int4pack_mm(eye(K)) (this box's
+    PyTorch-ROCm, the reference's int4 linear at tensor_core_tiled_layout.py:104) equals the HIP
+    dequant op BIT FOR BIT (diff == 0), and both differ from the group-wise python dequant
+    (two bf16 roundings) by the same max |diff| < 0.1."""
+    from torchao.quantization.utils import (get_groupwise_affine_qparams,
+                                            groupwise_affine_dequantize_tensor_from_qparams,
+                                            groupwise_affine_quantize_tensor_from_qparams,
+                                            pack_tinygemm_scales_and_zeros)
+    if K % (ikt * 16):
+        pytest.skip("K not a multiple of ikt * 16")
+    gen = torch.Generator(device=DEV).manual_seed(N * 7 + K + ikt * 3 + g)
+    t = torch.randn(N, K, generator=gen, device=DEV).to(torch.bfloat16)
+    s, z = get_groupwise_affine_qparams(t, n_bit=4, groupsize=g, dtype=torch.bfloat16)
+    q = groupwise_affine_quantize_tensor_from_qparams(t, s, z, n_bit=4, groupsize=g)
+    assert q.dtype == torch.uint8 and q.shape == (N, K // 2)
+    packed = torch.ops.aten._convert_weight_to_int4pack(q, ikt)
+    sz = pack_tinygemm_scales_and_zeros(s, z)
+    assert sz.shape == (K // g, N, 2)
+    dq_ao = groupwise_affine_dequantize_tensor_from_qparams(q, s, z, n_bit=4, groupsize=g)
+    eye = torch.eye(K, device=DEV, dtype=torch.bfloat16)
+    dq_id = torch.ops.aten._weight_int4pack_mm(eye, packed, g, sz).t()
+    del eye
+    dq_op = torchao.ops.dequantize_tensor_core_tiled_layout(packed, sz, g, ikt)
+    diff_ao_id = (dq_id - dq_ao).abs().max()
+    diff_op_id = (dq_op - dq_id).abs().max()
+    diff_op_ao = (dq_op - dq_ao).abs().max()
+    assert diff_op_id == 0
+    assert torch.equal(dq_op.view(torch.int16), dq_id.contiguous().view(torch.int16))
+    assert diff_op_ao == diff_ao_id
+    assert diff_op_ao < 1e-1
+
+
 # ---- checkpoints written by the reference's own classes (oracle/gen_golden_ckpt.py) -----------
 def _ref_ckpt_tags():
     import os

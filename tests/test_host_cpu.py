@@ -489,3 +489,41 @@ def test_intmm_cpu_paths_exact():
     assert torch.equal(safe_int_mm(a[:, :60], b[:60, :20]), (a[:, :60].long() @ b[:60, :20].long()).int())
     s = (torch.rand(17, 1, generator=g) + 0.5).to(torch.bfloat16)
     assert torch.equal(int_scaled_matmul(a, b, s), exact.to(torch.bfloat16) * s)
+
+
+def test_groupwise_helpers_match_oracle_restatement():
+    """quantization/utils.py's group-wise helpers (reference utils.py:325-513) against the
+    oracle's independent restatement: same (s, z), same codes, same two-rounding dequant."""
+    from torchao.quantization.utils import (get_groupwise_affine_qparams,
+                                            groupwise_affine_dequantize_tensor_from_qparams,
+                                            groupwise_affine_quantize_tensor_from_qparams)
+    for N, K, g in [(16, 256, 32), (24, 512, 128), (8, 256, 256)]:
+        w = oracle.make_linear_weight(N, K, seed=N + K)
+        s, z = get_groupwise_affine_qparams(w, 4, g)
+        s0, z0 = oracle.int4_qparams(w, g)
+        assert torch.equal(s, s0) and torch.equal(z, z0)
+        q = groupwise_affine_quantize_tensor_from_qparams(w, s, z, 4, g)
+        assert q.dtype == torch.int32 and torch.equal(q, oracle.int4_quantize(w, s0, z0, g))
+        dq = groupwise_affine_dequantize_tensor_from_qparams(q, s, z, 4, g)
+        assert torch.equal(dq, oracle.int4_dequantize(q, s0, z0, g))
+    with pytest.raises(ValueError):
+        get_groupwise_affine_qparams(torch.zeros(4, 96), 4, 64)
+
+
+def test_bench_shard_plans():
+    """bench.py's plans: the config-5 Megatron plan (pairs + head gather) at P = 2, 4, 8 shards
+    every linear of the 70B step; unfused 8B has 161 linears, fused 129."""
+    import bench
+    _, c70 = bench.MODELS["70b"]
+    _, c8 = bench.MODELS["8b"]
+    assert len(bench.llama_linears(c8)) == 129
+    assert len(bench.llama_linears(c8, fuse_w13=False)) == 161
+    lins = bench.llama_linears(c70)
+    for P in (2, 4, 8):
+        kinds = bench.shard_kinds(lins, P, 32, "tp", {})
+        assert kinds.count("local") == 160 and kinds.count("reduce") == 160
+        assert kinds.count("gather") == 1 and kinds.count("whole") == 0
+    unf = bench.llama_linears(c8, fuse_w13=False)
+    kinds = bench.shard_kinds(unf, 4, 32, "tp", {})
+    assert kinds.count("local") == 96 and kinds.count("reduce") == 64
+    assert bench.shard_kinds(lins, 1, 32, "tp", {}) == ["whole"] * len(lins)

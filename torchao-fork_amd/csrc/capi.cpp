@@ -57,6 +57,15 @@ static void profile_release() {
   g_prof.active = false;
 }
 
+bool fence_free_validated() {
+  static const bool ok = [] {
+    int v = 0;
+    if (hipRuntimeGetVersion(&v) != hipSuccess) return false;
+    return v / 100000 == 7 * 100 + 2;  // ROCm / HIP 7.2 (HIP_VERSION major * 100 + minor)
+  }();
+  return ok;
+}
+
 Tuning& tuning() {
   static thread_local Tuning t;
   return t;

@@ -400,6 +400,150 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
   }
 }
 
+// ---- decode attention, one launch, packed-bf16 math (default for caches of <= 1024 rows) -----
+// Same geometry as attn_single_kernel (a workgroup of NW waves per (batch, query head), the
+// waves merged through LDS), rebuilt around what its timeline showed: the key loop was VALU
+// bound (every k and v element converted to f32 and multiplied on its own: ~170 wave
+// instructions per 16 keys, 4 waves a SIMD) and a 300-key cache took two dependent load rounds.
+//   * 32 keys per wave per round (512 per workgroup): at <= 512 keys every load of the launch —
+//     q, and each wave's K rows (4 lanes x 64 B per key, 2 keys a lane) and V rows (a dim pair a
+//     lane) — is issued at once: one round trip;
+//   * scores by v_dot2c_f32_bf16 on the packed bf16 q and k (2 exact products per op, f32 sum):
+//     16 ops per key-quarter instead of 32 multiply-adds and 32 conversions;
+//   * P.V by v_dot2c_f32_bf16 on key pairs: p rounded to bf16 (as flash attention feeds its PV
+//     product) and packed two keys a dword, broadcast by v_readlane (no LDS shuffles), v pairs
+//     formed by v_perm; the softmax denominator sums the same rounded p, so the output is an
+//     exactly normalised weighted mean of the V rows.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_dot2_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
+    int H, int Hkv, int T, float scale) {
+  constexpr int D = 128, KPW = 32, ROUND = NW * KPW;
+  __shared__ float wm[NW], wl[NW];
+  __shared__ float wo[NW][D];
+  const int bh = blockIdx.x;  // b * H + h
+  const int b = bh / H, h = bh % H, kvh = h / (H / Hkv);
+  const int L = attn_len(pos[0], T);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar key indices
+  const int kq = lane >> 2, p = lane & 3;
+  const size_t head = (size_t)(b * Hkv + kvh) * T;
+  const uint16_t* kb = kc + head * D + p * 8;
+  // V rows by buffer loads: the row offset (wave-uniform) in a scalar register, the lane's
+  // dim pair in the vector offset
+  const Rsrc vr = make_rsrc(vc + head * D, (uint32_t)((size_t)L * D * 2));
+
+  uint4 ka[4], kb2[4];  // keys t0 + kq and t0 + 16 + kq: dims v*32 + 8p + e, packed bf16
+  uint32_t vv[KPW];     // the wave's 32 keys' V dim pair `lane`
+  auto load_round = [&](int t0) __attribute__((always_inline)) {
+    const int ta = t0 + kq < L ? t0 + kq : L - 1, tb = t0 + 16 + kq < L ? t0 + 16 + kq : L - 1;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      ka[v] = *reinterpret_cast<const uint4*>(kb + (size_t)ta * D + v * 32);
+      kb2[v] = *reinterpret_cast<const uint4*>(kb + (size_t)tb * D + v * 32);
+    }
+#pragma unroll
+    for (int j = 0; j < KPW; ++j) {
+      const int tj = t0 + j < L ? t0 + j : L - 1;  // clamped, weighted 0 below
+      vv[j] = __builtin_amdgcn_raw_buffer_load_b32(vr, lane * 4, tj * (D * 2), 0);
+    }
+  };
+  uint4 qv[4];  // q dims v*32 + 8p + e, packed bf16 (no conversion)
+  {
+    const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bh * D + p * 8);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) qv[v] = qp[v * 4];
+  }
+
+  // q's loads and the first round's K / V loads are all in flight before the first wait;
+  // caches past 512 keys take one more round trip per round
+  float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
+#pragma unroll 1
+  for (int t0 = wave * KPW; t0 < L; t0 += ROUND) {
+    load_round(t0);
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const uint32_t qw[4] = {qv[v].x, qv[v].y, qv[v].z, qv[v].w};
+      const uint32_t aw[4] = {ka[v].x, ka[v].y, ka[v].z, ka[v].w};
+      const uint32_t bw[4] = {kb2[v].x, kb2[v].y, kb2[v].z, kb2[v].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sa = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, qw[e]),
+                                             __builtin_bit_cast(bf16x2_t, aw[e]), sa, false);
+        sb = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, qw[e]),
+                                             __builtin_bit_cast(bf16x2_t, bw[e]), sb, false);
+      }
+    }
+    sa += xor_partner<1>(sa, lane_id());
+    sb += xor_partner<1>(sb, lane_id());
+    sa += xor_partner<2>(sa, lane_id());
+    sb += xor_partner<2>(sb, lane_id());
+    const bool va = t0 + kq < L, vb_ok = t0 + 16 + kq < L;
+    sa = va ? sa * scale : -INFINITY;
+    sb = vb_ok ? sb * scale : -INFINITY;
+    float mx = fmaxf(sa, sb);
+    mx = wave_bfly<4, 64>(mx, lane_id(), [](float a, float c) { return fmaxf(a, c); });
+    const float mn = fmaxf(m, mx);  // finite: key t0 < L is valid
+    const float corr = __expf(m - mn);
+    // p rounded to bf16; the denominator sums the rounded values
+    const uint16_t pa = va ? f32_to_bf16(__expf(sa - mn)) : (uint16_t)0;
+    const uint16_t pb = vb_ok ? f32_to_bf16(__expf(sb - mn)) : (uint16_t)0;
+    float es = bf16_to_f32(pa) + bf16_to_f32(pb);  // 4 lanes per key: xor 4..32 counts each once
+    es = wave_bfly<4, 64>(es, lane_id(), [](float a, float c) { return a + c; });
+    l = fmaf(l, corr, es);
+    o0 *= corr;
+    o1 *= corr;
+    // pair (key 2i, key 2i + 1) of each half: lanes 8i and 8i + 4 hold them
+    const uint32_t na = (uint32_t)xor_partner<4>((int)pa, lane_id());
+    const uint32_t nb = (uint32_t)xor_partner<4>((int)pb, lane_id());
+    const uint32_t ppa = (uint32_t)pa | (na << 16), ppb = (uint32_t)pb | (nb << 16);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t sA = (uint32_t)__builtin_amdgcn_readlane((int)ppa, 8 * i);
+      const uint32_t sB = (uint32_t)__builtin_amdgcn_readlane((int)ppb, 8 * i);
+      const uint32_t a0 = vv[2 * i], a1 = vv[2 * i + 1];
+      const uint32_t b0 = vv[16 + 2 * i], b1 = vv[16 + 2 * i + 1];
+      o0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, sA),
+                                           __builtin_bit_cast(bf16x2_t, __builtin_amdgcn_perm(a1, a0, 0x05040100u)),
+                                           o0, false);
+      o1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, sA),
+                                           __builtin_bit_cast(bf16x2_t, __builtin_amdgcn_perm(a1, a0, 0x07060302u)),
+                                           o1, false);
+      o0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, sB),
+                                           __builtin_bit_cast(bf16x2_t, __builtin_amdgcn_perm(b1, b0, 0x05040100u)),
+                                           o0, false);
+      o1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, sB),
+                                           __builtin_bit_cast(bf16x2_t, __builtin_amdgcn_perm(b1, b0, 0x07060302u)),
+                                           o1, false);
+    }
+    m = mn;
+  }
+  if (lane == 0) {
+    wm[wave] = m;  // -inf: the wave had no keys
+    wl[wave] = l;
+  }
+  wo[wave][2 * lane] = o0;
+  wo[wave][2 * lane + 1] = o1;
+  __syncthreads();
+  if (wave == 0) {
+    const int nw = (L + KPW - 1) / KPW < NW ? (L + KPW - 1) / KPW : NW;  // waves with keys
+    float M = -INFINITY;
+    for (int w = 0; w < nw; ++w) M = fmaxf(M, wm[w]);
+    float a0 = 0.f, a1 = 0.f, ls = 0.f;
+    for (int w = 0; w < nw; ++w) {
+      const float f = __expf(wm[w] - M);
+      ls = fmaf(wl[w], f, ls);
+      a0 = fmaf(wo[w][2 * lane], f, a0);
+      a1 = fmaf(wo[w][2 * lane + 1], f, a1);
+    }
+    const float inv = 1.f / ls;
+    reinterpret_cast<uint32_t*>(out)[(size_t)bh * (D / 2) + lane] =
+        (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
+  }
+}
+
 // ---- decode attention in one launch, split over key chunks (opt-in, tao_tune_attn 2 / 3) -----
 // Flash-decoding with the merge in the same launch: a workgroup per (batch, kv head, CH-key
 // chunk) serves the G query heads of its kv head (GQA: each K/V byte is read once, not G
@@ -722,6 +866,11 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
     return check_launch("attn_chunk_fused_kernel");
   }
   if (T <= kSingleMaxT && mode == 0) {  // partial is not touched
+    launch(attn_dot2_kernel<16>, dim3((unsigned)(B * H)), dim3(64 * 16), 0, st, q, k_cache,
+           v_cache, pos, out, (int)H, (int)Hkv, (int)T, scale);
+    return check_launch("attn_dot2_kernel");
+  }
+  if (T <= kSingleMaxT && mode == 4) {  // the round-1 single-pass kernel (f32 math)
     launch((attn_single_kernel<128, kSingleWaves>), dim3((unsigned)(B * H)),
            dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
            (int)T, scale);
@@ -761,10 +910,10 @@ extern "C" int tao_debug_attn_stamps(unsigned long long* out, int n) {
 #endif
 
 int tao_tune_attn(int mode) {
-  TAO_CHECK_ARG(mode >= 0 && mode <= 3,
-                "tune: attention mode must be 0 (auto: single-pass up to 1024 keys, else split), "
-                "1 (two-launch split), 2 (one launch, 32-key chunks) or 3 (one launch, 64-key "
-                "chunks)");
+  TAO_CHECK_ARG(mode >= 0 && mode <= 4,
+                "tune: attention mode must be 0 (auto: packed-bf16 single pass up to 1024 keys, "
+                "else split), 1 (two-launch split), 2 (one launch, 32-key chunks), 3 (one launch, "
+                "64-key chunks) or 4 (the f32 single pass up to 1024 keys, else split)");
   tao::tuning().attn_mode = mode;
   return TAO_OK;
 }

@@ -368,7 +368,10 @@ int i8_decode(const uint16_t* x, const int8_t* w, const uint16_t* scale, uint16_
   int g = tg > 0 ? tg : 2;
   const int wke = wk < S ? wk : S;
   while (wke * g < 8 && 64 * wke * g * 8 * 4 < K) g *= 2;
+  while (g > 1 && wke * g > 8) g /= 2;  // __launch_bounds__(512) and the prologue's 16 slots
   const int threads = 64 * wke * g;
+  if (threads > 512)
+    return set_error(TAO_ERR_INVALID_ARGUMENT, "int8 decode: %d waves along K exceed 8", wke);
   const bool pro = fu.norm_w != nullptr;
   if (pro && threads * 8 * 4 < K)
     return set_error(TAO_ERR_INVALID_ARGUMENT, "int8 decode: K (%d) too long for the RMSNorm prologue", K);

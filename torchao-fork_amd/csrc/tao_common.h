@@ -46,6 +46,11 @@ int graph_workspace_count();
 // Zero means "built-in choice". Thread-local: a tao_tune_* call re-routes only launches issued
 // from the calling thread, and tao_tune_reset() (torchao.kernel.tuning() on exit) restores the
 // built-in shapes, so sweeps cannot re-route another thread's model.
+// The fence-free split-K hand-off (last_arriver, fenced == 0) rests on sc1 stores / loads as
+// measured on gfx950 under the HIP runtime this library was validated with (ROCm 7.2, DESIGN
+// §4.2a). Under any other runtime major.minor the fenced form is the default instead.
+bool fence_free_validated();
+
 struct Tuning {
   int rpw = 0, wk = 0, g = 0, occ = 0;           // int4 GEMV (tao_tune_int4_gemv)
   int xlds = 0, norm = 0;                        // int4 GEMV x staging / deferred norm
@@ -54,7 +59,7 @@ struct Tuning {
   int max_gemv_m = 0;                            // GEMV <-> MFMA crossover
   int i8_rpw = 0, i8_wk = 0, i8_g = 0;           // int8 GEMVs (tao_tune_int8_gemv)
   int attn_mode = 0;                             // decode attention (tao_tune_attn)
-  int splitk_fenced = 0;                         // split-K hand-off with agent fences
+  int splitk_fenced = fence_free_validated() ? 0 : 1;  // split-K hand-off with agent fences
   int gemm_order = 0;                            // MFMA GEMM tile order: 0 plain, 1 XCD-grouped
   int gemm_nw = 0;                               // MFMA GEMM 16-col blocks per wave: 0 auto, 1, 2
   int gemm_table = 0;                            // MFMA GEMM measured-shape table: 0 on, 1 off

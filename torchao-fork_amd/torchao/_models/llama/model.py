@@ -191,6 +191,10 @@ def _int8wo_parts(lin: Optional[nn.Linear]):
     if not _linear_fp_act_int8_weight_check(torch.empty(0, dtype=torch.bfloat16), w, None):
         return None
     impl = w.tensor_impl
+    # the fused kernels read bf16 per-row scales; anything else (fp32 scales of an fp32-quantized
+    # weight) takes the regular linear, which casts them
+    if impl.scale.dtype != torch.bfloat16 or impl.scale.numel() != impl.int_data.shape[0]:
+        return None
     return impl.int_data, impl.scale.reshape(-1)
 
 
