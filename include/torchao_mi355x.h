@@ -72,11 +72,15 @@ int tao_int4wo_linear_bf16(const uint16_t* x, const uint32_t* packed, const uint
 int tao_tune_reset(void);
 
 /* Split-K / last-arriver hand-off form for the calling thread: 0 = fence-free sc1 protocol
- * (built-in under the HIP 7.2 runtime it was validated on; MI355X_MICROARCH.md "Hand-offs
+ * (built-in under the HIP 7.0 / 7.2 runtimes it was validated on; MI355X_MICROARCH.md "Hand-offs
  * measured with sc1 loads in place of the acquire", first row), 1 = the same plus agent release /
  * acquire fences (the HIP memory-model form; built-in under any other runtime version).
  * Both give bit-identical results (tests/test_gpu_gemm_tiles.py). */
 int tao_tune_splitk_fenced(int fenced);
+
+/* The calling thread's current split-K hand-off form (0 fence-free, 1 fenced): the built-in
+ * choice unless tao_tune_splitk_fenced overrode it. No device work. */
+int tao_query_splitk_fenced(void);
 
 /* Tuning hook (benchmarks / autotuning sweeps): override the M == 1 int4 GEMV launch shape,
  * for the calling thread. rows_per_wave in {1,2,4,8}; waves_k = waves splitting K inside a workgroup

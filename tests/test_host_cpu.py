@@ -71,6 +71,22 @@ def test_library_metadata_and_error_reporting():
         _lib.call("tao_int4wo_linear_bf16", None, None, None, None, None, 1, 8, 96, 48, None)
 
 
+def test_fence_free_handoff_is_default_under_torchs_runtime():
+    """Inside a PyTorch process the HIP runtime is the one torch bundles (7.0 for 2.10+rocm7.0),
+    not /opt/rocm's 7.2. Round 3 once gated the fence-free split-K hand-off on 7.2 alone, which
+    silently switched every split-K GEMM and decode-attention merge to the fenced form (int4
+    M=128 4096^2 15.5 -> 22.4 us on the box). Both runtimes are validated; the default must be
+    fence-free here (no device work: the query reads the thread's tuning state)."""
+    import torch  # noqa: F401  (loads torch's bundled libamdhip64 first, as in production)
+
+    lib = _lib.lib()
+    assert lib.tao_query_splitk_fenced() == 0
+    _lib.call("tao_tune_splitk_fenced", 1)
+    assert lib.tao_query_splitk_fenced() == 1
+    _lib.call("tao_tune_reset")
+    assert lib.tao_query_splitk_fenced() == 0
+
+
 def test_gfx950_code_object_embedded():
     blob = open(_lib.library_path(), "rb").read()
     assert b"gfx950" in blob

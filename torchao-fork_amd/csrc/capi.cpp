@@ -61,7 +61,11 @@ bool fence_free_validated() {
   static const bool ok = [] {
     int v = 0;
     if (hipRuntimeGetVersion(&v) != hipSuccess) return false;
-    return v / 100000 == 7 * 100 + 2;  // ROCm / HIP 7.2 (HIP_VERSION major * 100 + minor)
+    // HIP_VERSION = major * 10^7 + minor * 10^5 + patch. Inside a PyTorch process the runtime is
+    // the one torch bundles (7.0 for torch 2.10+rocm7.0, the runtime every GPU test of rounds 1-3
+    // ran under); standalone C-ABI programs load /opt/rocm's 7.2. Both are validated.
+    const int mm = v / 100000;
+    return mm == 700 || mm == 702;
   }();
   return ok;
 }
@@ -283,6 +287,8 @@ int tao_tune_splitk_fenced(int fenced) {
   tao::tuning().splitk_fenced = fenced;
   return TAO_OK;
 }
+
+int tao_query_splitk_fenced(void) { return tao::tuning().splitk_fenced; }
 
 int tao_profile_begin(int capacity) {
   TAO_CHECK_ARG(capacity > 0 && capacity <= (1 << 20), "profile: capacity out of range");

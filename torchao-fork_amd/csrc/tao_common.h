@@ -47,8 +47,9 @@ int graph_workspace_count();
 // from the calling thread, and tao_tune_reset() (torchao.kernel.tuning() on exit) restores the
 // built-in shapes, so sweeps cannot re-route another thread's model.
 // The fence-free split-K hand-off (last_arriver, fenced == 0) rests on sc1 stores / loads as
-// measured on gfx950 under the HIP runtime this library was validated with (ROCm 7.2, DESIGN
-// §4.2a). Under any other runtime major.minor the fenced form is the default instead.
+// measured on gfx950 under the HIP runtimes this library was validated with (torch's bundled 7.0
+// and /opt/rocm's 7.2). Under any other runtime major.minor the fenced form is the
+// default instead.
 bool fence_free_validated();
 
 struct Tuning {
@@ -201,7 +202,7 @@ __device__ __forceinline__ int attn_len(int64_t p, int T) {
 // agent-scope atomic add to one unsharded counter, the workgroup whose add came last is told by
 // the value it returned, its other waves load after a workgroup barrier joined behind an LDS
 // word, sc1 stores and sc1 loads of 16 B (and 8 B in decode attention), hipMalloc'd memory. That
-// row is a measured gfx950 / ROCm 7.2 behaviour, not an HIP memory-model guarantee (the guide
+// row is a measured gfx950 / ROCm 7.0-7.2 behaviour, not an HIP memory-model guarantee (the guide
 // says so); the fences it removes cost 1.7-6.5 µs each.
 // fenced == 1 (tao_tune_splitk_fenced): the memory-model form on top of the same stores and
 // loads: release fence (buffer_wbl2 sc1 + asm vmcnt(0), the guide's compiler-hazard fix) before
