@@ -1,0 +1,174 @@
+// Streaming skeleton of an x-resident prefill tile, no math (companion of probe_stream.hip, whose
+// per-step LDS ring + barrier structure measured ~43 GB/s per CU): the workgroup LDS-DMAs its whole
+// x tile (BM rows x XB bytes, L2-resident) once, then every wave streams ITS OWN weight rows into
+// registers with no barrier, DEPTH chunks of (rows x 1 KiB) in flight, in one of two patterns:
+//   PAT 0: a wave instruction reads 16 rows x 64 B (lane l: row l % 16, bytes 16 (l / 16)) -- the
+//          MFMA 16x16x64-i8 / 16x16x32-bf16 B-fragment order, no regrouping needed;
+//   PAT 1: a wave instruction reads 1 row x 1 KiB (the GEMV pattern; needs an LDS regroup);
+//   PAT 2: PAT 1 by LDS-DMA into a per-wave LDS ring of DEPTH chunks (XB = 0: no x tile at all).
+// Weights rotate over 20 copies (past the 256 MiB Infinity Cache). µs per launch over 50 launches.
+//
+//   hipcc --offload-arch=gfx950 -O3 -o experiments/build/probe_stream5 experiments/probe_stream5.hip
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ Rsrc make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void glds16(Rsrc r, uint32_t voff, uint32_t soff, void* dst) {
+  const uint32_t lds_addr = (uint32_t)(uintptr_t)(lds_ptr_t)dst;
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "s"(lds_addr), "v"(voff), "s"(r), "s"(soff) : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// RW = weight rows per wave (16 or 32), chunk = RW rows x 1 KiB = RW wave instructions
+template <int BM, int BN, int XB, int WB, int PAT, int DEPTH, int NT, int RL = 1024>
+__global__ __launch_bounds__(256) void xres_kernel(const uint8_t* __restrict__ x,
+                                                   const uint8_t* __restrict__ w, uint32_t* sink) {
+  constexpr int RW = BN / 4;
+  constexpr int XP = BM * XB / 1024;  // x DMA pieces (8 rows x 128 B)
+  static_assert(XP % 4 == 0, "x tile");
+  constexpr int NCH = WB / RL;        // chunks per row
+  constexpr int IPC = RW * RL / 1024; // instructions per chunk (PAT 0: RW/16 groups x 16 64-B
+                                      // columns; PAT 1 / 2: one per row, RL = 1 KiB)
+  constexpr int WSTAGE = PAT == 2 ? RW * RL : 0;  // per-wave LDS chunk (PAT 2)
+  static_assert(BM * XB + 4 * DEPTH * WSTAGE <= 160 * 1024, "LDS");
+  __shared__ uint4 xs[(BM * XB + 4 * DEPTH * WSTAGE) / 16 > 0 ? (BM * XB + 4 * DEPTH * WSTAGE) / 16 : 1];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n0 = blockIdx.x * BN + wave * RW, m0 = blockIdx.y * BM;
+  const Rsrc xr = make_rsrc(x, 0x7fffffff), wr = make_rsrc(w, 0x7fffffff);
+  // x tile once
+#pragma unroll
+  for (int i = 0; i < XP / 4; ++i) {
+    const int p = wave * (XP / 4) + i;
+    const int h = p / (BM / 8), rg = p % (BM / 8);
+    const int row = 8 * rg + (lane >> 3);
+    glds16(xr, (uint32_t)(m0 + row) * XB + 128u * h + 16u * (lane & 7), 0,
+           reinterpret_cast<uint8_t*>(xs) + p * 1024);
+  }
+  // per-instruction lane offsets within a chunk
+  auto voff = [&](int i) __attribute__((always_inline)) -> uint32_t {
+    if (PAT == 0) {
+      const int grp = i / 16, col = i % 16;  // 16-row group, 64-B column of the 1 KiB chunk
+      return (uint32_t)(n0 + 16 * grp + (lane & 15)) * WB + 64u * col + 16u * (lane >> 4);
+    }
+    // PAT 1 / 2: instruction i covers rows (1024 / RL) i .. of the chunk, RL bytes each
+    return (uint32_t)(n0 + i * (1024 / RL) + lane / (RL / 16)) * WB + 16u * (lane % (RL / 16));
+  };
+  u32x4 buf[PAT == 2 ? 1 : DEPTH][PAT == 2 ? 1 : IPC];
+  auto issue = [&](int c, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < IPC; ++i) {
+      if constexpr (PAT == 2)
+        glds16(wr, voff(i), c * RL,
+               reinterpret_cast<uint8_t*>(xs) + BM * XB + ((wave * DEPTH + slot) * RW + i) * 1024);
+      else
+        buf[slot][i] = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, voff(i), c * RL, NT ? 2 : 0));
+    }
+  };
+  // chunks still in flight after chunk c's issue window: min(NCH - 1, c + DEPTH - 1) - c
+  auto wait_chunks = [&](int pending) __attribute__((always_inline)) {
+    switch (pending) {
+      case 0: wait_vm<0>(); break;
+      case 1: wait_vm<IPC>(); break;
+      case 2: wait_vm<2 * IPC>(); break;
+      case 3: wait_vm<3 * IPC>(); break;
+      case 4: wait_vm<4 * IPC>(); break;
+      case 5: wait_vm<5 * IPC>(); break;
+      case 6: wait_vm<6 * IPC>(); break;
+      default: wait_vm<7 * IPC>(); break;
+    }
+  };
+#pragma unroll
+  for (int c = 0; c < DEPTH - 1 && c < NCH; ++c) issue(c, c % DEPTH);
+  uint32_t acc = 0;
+  {
+    const int pend = (DEPTH - 1 < NCH ? DEPTH - 1 : NCH);  // W chunks issued after x
+    wait_chunks(pend);                                     // x landed (issued first)
+  }
+  __syncthreads();
+  acc ^= reinterpret_cast<const uint32_t*>(xs)[threadIdx.x];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    if (c + DEPTH - 1 < NCH) issue(c + DEPTH - 1, (c + DEPTH - 1) % DEPTH);
+    const int last = (c + DEPTH - 1 < NCH ? c + DEPTH - 1 : NCH - 1);
+    wait_chunks(last - c);
+#pragma unroll
+    for (int i = 0; i < IPC; ++i) {
+      if constexpr (PAT == 2)
+        acc ^= reinterpret_cast<const uint32_t*>(xs)[(BM * XB + ((wave * DEPTH + c % DEPTH) * RW + i) * 1024) / 4 + lane];
+      else
+        acc ^= buf[c % DEPTH][i][0] ^ buf[c % DEPTH][i][3];
+    }
+  }
+  wait_vm<0>();
+  if (acc == 0x12345678u) sink[blockIdx.x] = acc;
+}
+
+template <int BM, int BN, int XB, int WB, int PAT, int DEPTH, int NT, int RL = 1024>
+static void run(const char* tag, const uint8_t* x, const uint8_t* wbig, size_t wcopy, int copies,
+                int M, int N, uint32_t* sink) {
+  const dim3 grid(N / BN, M / BM);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  for (int i = 0; i < 10; ++i)
+    xres_kernel<BM, BN, XB, WB, PAT, DEPTH, NT, RL><<<grid, 256>>>(x, wbig + (i % copies) * wcopy, sink);
+  hipEventRecord(a);
+  const int iters = 50;
+  for (int i = 0; i < iters; ++i)
+    xres_kernel<BM, BN, XB, WB, PAT, DEPTH, NT, RL><<<grid, 256>>>(x, wbig + (i % copies) * wcopy, sink);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms = 0;
+  hipEventElapsedTime(&ms, a, b);
+  const double us = ms * 1000.0 / iters;
+  const double wg_bytes = (double)BM * XB + (double)BN * WB;
+  printf("{\"probe\": \"%s\", \"BM\": %d, \"BN\": %d, \"x_row_B\": %d, \"w_row_B\": %d, \"pat\": %d, "
+         "\"depth\": %d, \"nt\": %d, \"RL\": %d, \"workgroups\": %d, \"KB_per_wg\": %.0f, \"us\": %.2f, "
+         "\"GBps_per_wg\": %.1f, \"weight_TBps\": %.2f}\n",
+         tag, BM, BN, XB, WB, PAT, DEPTH, NT, RL, (int)(grid.x * grid.y), wg_bytes / 1024, us,
+         wg_bytes / us / 1e3, (double)N * WB / us / 1e6);
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+}
+
+int main() {
+  const int M = 128, N = 4096;
+  uint8_t *x = nullptr, *w = nullptr;
+  uint32_t* sink = nullptr;
+  const size_t wcopy = (size_t)N * 4096;
+  const int copies = 20;
+  if (hipMalloc(&x, (size_t)M * 8192) != hipSuccess || hipMalloc(&w, wcopy * copies) != hipSuccess ||
+      hipMalloc(&sink, 1 << 16) != hipSuccess)
+    return 1;
+  hipMemset(x, 1, (size_t)M * 8192);
+  hipMemset(w, 1, wcopy * copies);
+  // W stream alone by LDS-DMA into per-wave rings (no x, no barrier): run length per row
+  run<32, 64, 0, 4096, 2, 2, 0, 1024>("i8-nox-dma", x, w, wcopy, copies, M, N, sink);
+  run<32, 64, 0, 4096, 2, 4, 0, 512>("i8-nox-dma", x, w, wcopy, copies, M, N, sink);
+  run<32, 64, 0, 4096, 2, 8, 0, 256>("i8-nox-dma", x, w, wcopy, copies, M, N, sink);
+  run<32, 64, 0, 4096, 2, 4, 0, 256>("i8-nox-dma", x, w, wcopy, copies, M, N, sink);
+  run<32, 64, 0, 4096, 2, 8, 0, 128>("i8-nox-dma", x, w, wcopy, copies, M, N, sink);
+  // with the x tile resident (128 KiB): 32 KiB left for the rings
+  run<32, 64, 4096, 4096, 2, 4, 0, 128>("i8-dma", x, w, wcopy, copies, M, N, sink);
+  run<32, 64, 4096, 4096, 2, 2, 0, 256>("i8-dma", x, w, wcopy, copies, M, N, sink);
+  run<16, 128, 0, 2048, 2, 1, 0, 1024>("i4-nox-dma", x, w, wcopy, copies, M, N, sink);
+  run<16, 128, 0, 2048, 2, 4, 0, 256>("i4-nox-dma", x, w, wcopy, copies, M, N, sink);
+  run<16, 128, 8192, 2048, 2, 2, 0, 128>("i4-dma", x, w, wcopy, copies, M, N, sink);
+  return hipDeviceSynchronize() == hipSuccess ? 0 : 2;
+}

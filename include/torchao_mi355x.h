@@ -135,6 +135,12 @@ int tao_tune_int4_mfma32(int on);
  * 2 = wherever it applies (K a multiple of its step, M above the GEMV crossover); splits 0 =
  * built-in, else the largest power of two <= splits (<= 16). Calling thread only. */
 int tao_tune_gemm_tile(int mode, int splits);
+
+/* Tuning hook: the unsplit "stream" prefill GEMM (gemm_stream.hip: 32 x 64 tiles, wave-private
+ * LDS-DMA weight streams, x in double-buffered 1-KiB-per-row phases) for the int4 weight-only and
+ * int8 dynamic linears. mode 0 = built-in routing (M in [33, 256] with N % 64 == 0 and K a multiple
+ * of 512 (int4) / 1024 (int8)), 1 = never, 2 = wherever the shape is supported. Thread-local. */
+int tao_tune_gemm_stream(int mode);
 /* Number of split-K workspaces currently owned by captured graphs (each is released with its
  * graph). Diagnostic for tests; never fails. */
 int tao_graph_workspace_count(void);

@@ -67,6 +67,7 @@ struct Tuning {
   int int4_mfma32 = 0;                           // int4 GEMM on 32x32x16 MFMAs: 0 off, 1 on
   int quant_block = 0;                           // per-token int8 quant: 0 wave kernel, 1 block
   int gemm_tile = 0, tile_splits = 0;            // weight-shared tile GEMM: 0 auto, 1 off, 2 on
+  int gemm_stream = 0;                           // stream tile GEMM (gemm_stream.hip): 0 auto, 1 off, 2 on
 };
 Tuning& tuning();
 
