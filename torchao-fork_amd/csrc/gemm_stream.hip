@@ -28,6 +28,13 @@
 // (plain_layout.py:294-315) at prefill shapes.
 #include "tao_common.h"
 
+// Timing-only variant builds (experiments/stream_debug.sh; never the shipped library): 1 no
+// fragment reads / MFMAs, 2 no weight DMA, 3 no x (and scale/zero) DMA, 4 no DMA at all.
+// Results are wrong in every variant.
+#ifndef TAO_STREAM_DEBUG
+#define TAO_STREAM_DEBUG 0
+#endif
+
 namespace tao {
 namespace {
 
@@ -309,6 +316,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
   // x phase p: this wave's 8 rows (one DMA instruction of 1 KiB each), swizzled slots
   auto issue_x = [&](int p) __attribute__((always_inline)) {
     uint8_t* dst = xs0 + (p & 1) * kXBuf;
+    if (TAO_STREAM_DEBUG == 3 || TAO_STREAM_DEBUG == 4) return;
 #pragma unroll
     for (int i = 0; i < kXI; ++i) {
       const int row = wave * kXI + i;
@@ -321,6 +329,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       pol.issue_z(zr, n_w, p, lane, zs0 + ((p & 1) * kNW + wave) * P::kZBuf);
   };
   auto issue_chunk = [&](int c) __attribute__((always_inline)) {
+    if (TAO_STREAM_DEBUG == 2 || TAO_STREAM_DEBUG == 4) return;
     pol.issue_w(wr, n_w, c, lane, ws0 + (wave * P::kD + c % P::kD) * P::kChunk);
   };
 
@@ -364,7 +373,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       // p + 1 (issued after every chunk of phase p: D - 1 >= kCPP)
       const int last = c + P::kD - 1 < nchunk ? c + P::kD - 1 : nchunk - 1;
       vm_wait_dyn<0, 31>((last - c) * P::kWI + (more ? xzi : 0));
-      pol.compute(ws0 + (wave * P::kD + c % P::kD) * P::kChunk, zb, xb, cin, lane, acc);
+      if (TAO_STREAM_DEBUG != 1) pol.compute(ws0 + (wave * P::kD + c % P::kD) * P::kChunk, zb, xb, cin, lane, acc);
     }
   }
 
