@@ -141,6 +141,13 @@ int tao_tune_gemm_tile(int mode, int splits);
  * int8 dynamic linears. mode 0 = built-in routing (M in [33, 256] with N % 64 == 0 and K a multiple
  * of 512 (int4) / 1024 (int8)), 1 = never, 2 = wherever the shape is supported. Thread-local. */
 int tao_tune_gemm_stream(int mode);
+/* The k-split prefill GEMM (gemm_ksplit.hip: an unsplit 32 x 64 tile per workgroup whose waves
+ * split K, operands loaded straight into MFMA fragments, partials summed through LDS in wave
+ * order) for the int4 weight-only and int8 dynamic linears. mode 0 = built-in routing, 1 = never,
+ * 2 = wherever the shape is supported. shape: 0 built-in, 1 = 16 waves (int8) / 8 waves x 1 block
+ * in flight (int4), 2 = 8 waves x 2 (int8) / 1 (int4) blocks, 3 = 8 waves x 4 (int8) / 2 (int4)
+ * blocks. Thread-local. */
+int tao_tune_gemm_ksplit(int mode, int shape);
 /* Number of split-K workspaces currently owned by captured graphs (each is released with its
  * graph). Diagnostic for tests; never fails. */
 int tao_graph_workspace_count(void);
@@ -153,6 +160,11 @@ int tao_tune_int4_xlds(int mode);
  * bf16 roundings before the slices; built-in), 1 = deferred (stage bf16(x * norm_weight), scale
  * each output by rsqrt(mean(x^2) + eps) at the end). Calling thread only; for measurement. */
 int tao_tune_int4_norm(int mode);
+
+/* Row blocks per workgroup of tao_int4wo_decode_bf16 with the RMSNorm prologue: each workgroup
+ * walks bpw blocks of rows (grid-stride) and normalises x once for all of them. 0 = built-in,
+ * 1..64. Calling thread only; for sweeps. */
+int tao_tune_int4_decode_bpw(int bpw);
 
 /* packed[N][K/8] <- q[N][K] (int32 values 0..15).
  * Replaces aten._convert_weight_to_int4pack(u8, inner_k_tiles) at
@@ -331,8 +343,9 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
                          int64_t Hkv, int64_t D, int64_t T, float scale, void* stream);
 
 /* Calling thread's choice of the decode-attention kernel: 0 = single-pass workgroup per query head
- * for T <= 1024, else the two-launch split (default); 1 = two-launch split; 2 / 3 = one launch
- * over 32 / 64-key chunks merged by the kv head's last arriving chunk. */
+ * (f32 math) for T <= 1024, else the two-launch split (default); 1 = two-launch split; 2 / 3 = one
+ * launch over 32 / 64-key chunks merged by the kv head's last arriving chunk; 4 = as 0 with the
+ * packed-bf16 single-pass kernel (measured slower). */
 int tao_tune_attn(int mode);
 
 /* Device-side faults of the decode kernels since the last call, read and cleared (synchronous:

@@ -400,7 +400,7 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
   }
 }
 
-// ---- decode attention, one launch, packed-bf16 math (default for caches of <= 1024 rows) -----
+// ---- decode attention, one launch, packed-bf16 math (tao_tune_attn 4; measured slower) -------
 // Same geometry as attn_single_kernel (a workgroup of NW waves per (batch, query head), the
 // waves merged through LDS), rebuilt around what its timeline showed: the key loop was VALU
 // bound (every k and v element converted to f32 and multiplied on its own: ~170 wave
@@ -865,12 +865,16 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
     }
     return check_launch("attn_chunk_fused_kernel");
   }
-  if (T <= kSingleMaxT && mode == 0) {  // partial is not touched
+  // Single pass, a workgroup per query head. The f32 kernel is the default: the packed-bf16
+  // one (mode 4) loads every key of a <= 512-key cache in one round trip but measured slower
+  // at every length (experiments/attn_time.py, profiles/r3_attn_time_dot2_vs_f32.jsonl: 328
+  // keys 6.20 vs 5.76 µs per graph launch; e2e 662 vs 668 tokens/s).
+  if (T <= kSingleMaxT && mode == 4) {  // partial is not touched
     launch(attn_dot2_kernel<16>, dim3((unsigned)(B * H)), dim3(64 * 16), 0, st, q, k_cache,
            v_cache, pos, out, (int)H, (int)Hkv, (int)T, scale);
     return check_launch("attn_dot2_kernel");
   }
-  if (T <= kSingleMaxT && mode == 4) {  // the round-1 single-pass kernel (f32 math)
+  if (T <= kSingleMaxT && mode == 0) {  // the f32 single-pass kernel
     launch((attn_single_kernel<128, kSingleWaves>), dim3((unsigned)(B * H)),
            dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
            (int)T, scale);
@@ -911,9 +915,9 @@ extern "C" int tao_debug_attn_stamps(unsigned long long* out, int n) {
 
 int tao_tune_attn(int mode) {
   TAO_CHECK_ARG(mode >= 0 && mode <= 4,
-                "tune: attention mode must be 0 (auto: packed-bf16 single pass up to 1024 keys, "
+                "tune: attention mode must be 0 (auto: f32 single pass up to 1024 keys, "
                 "else split), 1 (two-launch split), 2 (one launch, 32-key chunks), 3 (one launch, "
-                "64-key chunks) or 4 (the f32 single pass up to 1024 keys, else split)");
+                "64-key chunks) or 4 (packed-bf16 single pass up to 1024 keys, else split)");
   tao::tuning().attn_mode = mode;
   return TAO_OK;
 }

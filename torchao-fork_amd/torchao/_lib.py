@@ -46,11 +46,13 @@ _SIGNATURES = {
     "tao_tune_int4_mfma32": [_int],
     "tao_tune_int4_xlds": [_int],
     "tao_tune_int4_norm": [_int],
+    "tao_tune_int4_decode_bpw": [_int],
     "tao_tune_reset": [],
     "tao_tune_splitk_fenced": [_int],
     "tao_query_splitk_fenced": [],
     "tao_tune_gemm_tile": [_int, _int],
     "tao_tune_gemm_stream": [_int],
+    "tao_tune_gemm_ksplit": [_int, _int],
     "tao_graph_workspace_count": [],
     "tao_int4_pack": [_p, _p, _i64, _i64, _p],
     "tao_int4_pack_u8": [_p, _p, _i64, _i64, _p],

@@ -82,12 +82,20 @@ def silu_mul(a: torch.Tensor, b=None) -> torch.Tensor:
 _EPILOGUES = {"none": 0, "swiglu": 1, "rope_kv": 2}
 
 
+# Output heads (N >= HEAD_ROWS) normalise in their own RMSNorm launch unless HEAD_PROLOGUE.
+HEAD_ROWS = 65536
+HEAD_PROLOGUE = False
+
+
 def prologue_pays(N: int, K: int) -> bool:
     """Whether the RMSNorm prologue inside the GEMV beats a separate RMSNorm launch: every
     workgroup of the GEMV re-normalises the row, so it pays while K or the grid is small.
-    Measured (experiments/bench_decode.py; profiles/r1_bench_decode*.jsonl): Llama-3-8B wqkv,
-    w1||w3 and head and 70B wqkv gain 2-7 µs; 70B w1||w3 (57344x8192) and head (128256x8192)
-    lose 3-9 µs."""
+    Measured (experiments/bench_decode.py; profiles/r1_bench_decode*.jsonl,
+    r3_bench_decode_bpw.jsonl): Llama-3-8B wqkv and w1||w3 and 70B wqkv gain 1-6 µs; 70B
+    w1||w3 (57344x8192) loses 3-9 µs; the vocabulary heads (128256 rows, 8016 workgroups) lose
+    7.5 µs at K 4096 (round 3: fused 61.3 vs RMSNorm launch + GEMV 53.9 µs)."""
+    if N >= HEAD_ROWS and not HEAD_PROLOGUE:
+        return False
     return K <= 4096 or N < 16384
 
 
