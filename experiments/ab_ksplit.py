@@ -32,7 +32,7 @@ def main():
         ref = run(0).float()
         row = {"path": path, "M": M, "N": N, "K": K, "old_us": round(old_us, 2)}
         best = None
-        for shape in (1, 2, 3):
+        for shape in (1, 2, 3, 4):
             _lib.call("tao_tune_gemm_ksplit", 2, shape)
             us = kernel_us(run, launches)
             out = run(0).float()

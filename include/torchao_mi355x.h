@@ -144,9 +144,9 @@ int tao_tune_gemm_stream(int mode);
 /* The k-split prefill GEMM (gemm_ksplit.hip: an unsplit 32 x 64 tile per workgroup whose waves
  * split K, operands loaded straight into MFMA fragments, partials summed through LDS in wave
  * order) for the int4 weight-only and int8 dynamic linears. mode 0 = built-in routing, 1 = never,
- * 2 = wherever the shape is supported. shape: 0 built-in, 1 = 16 waves (int8) / 8 waves x 1 block
- * in flight (int4), 2 = 8 waves x 2 (int8) / 1 (int4) blocks, 3 = 8 waves x 4 (int8) / 2 (int4)
- * blocks. Thread-local. */
+ * 2 = wherever the shape is supported. shape: 0 built-in, 1 = 32 x 64 output tile, 2 = 64 x 32,
+ * 3 = 128 x 16, 4 = 128 x 16 on 16 waves (int8) / 32 x 64 with one k-block in flight (int4).
+ * Thread-local. */
 int tao_tune_gemm_ksplit(int mode, int shape);
 /* Number of split-K workspaces currently owned by captured graphs (each is released with its
  * graph). Diagnostic for tests; never fails. */

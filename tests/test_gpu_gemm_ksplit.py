@@ -47,8 +47,10 @@ INT4_SHAPES = [(128, 4096, 4096), (5, 64, 1024), (17, 128, 1024), (33, 192, 2048
 
 @pytest.mark.parametrize("M,N,K", INT4_SHAPES)
 @pytest.mark.parametrize("g", [32, 128])
-def test_ksplit_int4(ksplit, M, N, K, g):
-    ksplit(2)
+@pytest.mark.parametrize("shape", [0, 1, 3, 4])
+def test_ksplit_int4(ksplit, M, N, K, g, shape):
+    """Every output tile (32 x 64, 64 x 32, 128 x 16) and ring depth."""
+    ksplit(2, shape)
     q, s, z, packed, sz = _int4(N, K, g, seed=M + N + g)
     x = oracle.make_activation(M, K, seed=M)
     bias = oracle.make_activation(1, N, seed=7).reshape(N)
@@ -62,7 +64,7 @@ def test_ksplit_int4(ksplit, M, N, K, g):
 @pytest.mark.parametrize("shape", [1, 3])
 def test_ksplit_int4_group_sizes_and_shapes(ksplit, g, shape):
     """g = 64 and 256: the (scale, zero) word index (4 kb + q) >> log2(g / 32) splits into a block
-    part and a lane part; both ring depths."""
+    part and a lane part; two output tiles."""
     ksplit(2, shape)
     M, N, K = 96, 320, 6144
     q, s, z, packed, sz = _int4(N, K, g, seed=g)
@@ -77,7 +79,7 @@ INT8_SHAPES = [(128, 4096, 4096), (5, 64, 512), (31, 128, 1024), (33, 192, 2048)
 
 
 @pytest.mark.parametrize("M,N,K", INT8_SHAPES)
-@pytest.mark.parametrize("shape", [0, 1, 2])
+@pytest.mark.parametrize("shape", [0, 1, 2, 3, 4])
 def test_ksplit_int8dyn_bit_exact(ksplit, M, N, K, shape):
     ksplit(2, shape)
     w = oracle.make_linear_weight(N, K, seed=M + N)

@@ -31,6 +31,11 @@
 // (plain_layout.py:294-315) at prefill shapes.
 #include "tao_common.h"
 
+// Cache policy of the weight loads (timing experiments only): kNT (non-temporal) or 0.
+#ifndef TAO_KSPLIT_WAUX
+#define TAO_KSPLIT_WAUX kNT
+#endif
+
 namespace tao {
 namespace {
 
@@ -39,7 +44,7 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
-constexpr int kBM = 32, kBN = 64;
+// Output tile: RB x 16 rows by CB x 16 columns, RB x CB = 8 MFMA tiles per wave.
 
 __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
   const f32x2_t v = {lo, hi};
@@ -47,18 +52,20 @@ __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
 }
 
 // ---- int8 dynamic activation ------------------------------------------------------------------
+template <int RB, int CB>
 struct KInt8Dyn {
   static constexpr int kKB = 64;  // k per block
+  static constexpr int kRB = RB, kCB = CB;
   typedef i32x4_t Acc;
   struct Frag {
-    uint4 a[2], b[4];
+    uint4 a[RB], b[CB];
   };
   struct Args {
     const uint8_t* x;  // [M][K] int8
     const uint8_t* w;  // [N][K] int8
   };
   Rsrc xr, wr;
-  uint32_t xoff[2], woff[4];  // per-lane byte offsets of the fragments' rows at k = 16 q
+  uint32_t xoff[RB], woff[CB];  // per-lane byte offsets of the fragments' rows at k = 16 q
   __device__ __forceinline__ void init(const Args& a, int m0, int n0, int M, int N, int K,
                                        int lane) {
     const uint8_t* x = a.x;
@@ -67,25 +74,25 @@ struct KInt8Dyn {
     xr = make_rsrc(x, (uint32_t)M * (uint32_t)K);
     wr = make_rsrc(w, (uint32_t)N * (uint32_t)K);
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
+    for (int rb = 0; rb < RB; ++rb) {
       const int m = m0 + 16 * rb + r < M ? m0 + 16 * rb + r : M - 1;  // clamped, masked at the end
       xoff[rb] = (uint32_t)m * (uint32_t)K + 16u * (uint32_t)q;
     }
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) woff[cb] = (uint32_t)(n0 + 16 * cb + r) * (uint32_t)K + 16u * q;
+    for (int cb = 0; cb < CB; ++cb) woff[cb] = (uint32_t)(n0 + 16 * cb + r) * (uint32_t)K + 16u * q;
   }
   __device__ __forceinline__ void load(Frag& f, int kb) const {
     const uint32_t so = (uint32_t)kb * 64u;
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) f.b[cb] = bload16<kNT>(wr, woff[cb], so);
+    for (int cb = 0; cb < CB; ++cb) f.b[cb] = bload16<TAO_KSPLIT_WAUX>(wr, woff[cb], so);
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb) f.a[rb] = bload16(xr, xoff[rb], so);
+    for (int rb = 0; rb < RB; ++rb) f.a[rb] = bload16(xr, xoff[rb], so);
   }
-  __device__ __forceinline__ void compute(const Frag& f, Acc (&acc)[2][4]) const {
+  __device__ __forceinline__ void compute(const Frag& f, Acc (&acc)[RB][CB]) const {
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+    for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
+      for (int cb = 0; cb < CB; ++cb)
         acc[rb][cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
             __builtin_bit_cast(i32x4_t, f.a[rb]), __builtin_bit_cast(i32x4_t, f.b[cb]),
             acc[rb][cb], 0, 0, 0);
@@ -97,13 +104,15 @@ struct KInt8Dyn {
 };
 
 // ---- int4 weight-only -------------------------------------------------------------------------
+template <int RB, int CB>
 struct KInt4 {
   static constexpr int kKB = 128;
+  static constexpr int kRB = RB, kCB = CB;
   typedef f32x4_t Acc;
   struct Frag {
-    uint4 a[2][4];  // x: row block rb, MFMA j
-    uint4 w[4];     // nibbles: column block cb
-    uint32_t sz[4]; // (scale, zero) of column block cb
+    uint4 a[RB][4];  // x: row block rb, MFMA j
+    uint4 w[CB];     // nibbles: column block cb
+    uint32_t sz[CB]; // (scale, zero) of column block cb
   };
   struct Args {
     const uint16_t* x;   // [M][K] bf16
@@ -112,7 +121,7 @@ struct KInt4 {
     int gshift;          // g = 32 << gshift
   };
   Rsrc xr, wr, zr;
-  uint32_t xoff[2], woff[4], zoff[4];
+  uint32_t xoff[RB], woff[CB], zoff[CB];
   int gshift;
   __device__ __forceinline__ void init(const Args& a, int m0, int n0, int M, int N, int K,
                                        int lane) {
@@ -127,12 +136,12 @@ struct KInt4 {
     const uint32_t zrow = (uint32_t)(K >> (5 + gs)) * 4u;  // bytes of (scale, zero) per row
     zr = make_rsrc(sz, (uint32_t)N * zrow);
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
+    for (int rb = 0; rb < RB; ++rb) {
       const int m = m0 + 16 * rb + r < M ? m0 + 16 * rb + r : M - 1;
       xoff[rb] = (uint32_t)m * (uint32_t)K * 2u + 64u * (uint32_t)q;
     }
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
+    for (int cb = 0; cb < CB; ++cb) {
       const uint32_t n = (uint32_t)(n0 + 16 * cb + r);
       woff[cb] = n * (uint32_t)(K >> 1) + 16u * (uint32_t)q;
       // group of k = 128 kb + 32 q is (4 kb + q) >> gs = ((4 kb) >> gs) + (q >> gs): groups are
@@ -144,11 +153,11 @@ struct KInt4 {
     const uint32_t sw = (uint32_t)kb * 64u, sx = (uint32_t)kb * 256u;
     const uint32_t sz = 4u * (uint32_t)((4 * kb) >> gshift);
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) f.w[cb] = bload16<kNT>(wr, woff[cb], sw);
+    for (int cb = 0; cb < CB; ++cb) f.w[cb] = bload16<TAO_KSPLIT_WAUX>(wr, woff[cb], sw);
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) f.sz[cb] = bload4<kNT>(zr, zoff[cb], sz);
+    for (int cb = 0; cb < CB; ++cb) f.sz[cb] = bload4<TAO_KSPLIT_WAUX>(zr, zoff[cb], sz);
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+    for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int j = 0; j < 4; ++j) f.a[rb][j] = bload16(xr, xoff[rb] + 16u * (uint32_t)j, sx);
   }
@@ -166,9 +175,9 @@ struct KInt4 {
     const float w3 = __builtin_fmaf(q37[0], s, zc), w7 = __builtin_fmaf(q37[1], s, zc);
     return make_uint4(pk_bf16(w0, w1), pk_bf16(w2, w3), pk_bf16(w4, w5), pk_bf16(w6, w7));
   }
-  __device__ __forceinline__ void compute(const Frag& f, Acc (&acc)[2][4]) const {
+  __device__ __forceinline__ void compute(const Frag& f, Acc (&acc)[RB][CB]) const {
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
+    for (int cb = 0; cb < CB; ++cb) {
       const float s = bf16lo_to_f32(f.sz[cb]);
       const float zc = bf16hi_to_f32(f.sz[cb]) - 8.f * s;  // q * s + zc == (q - 8) * s + z
       const uint32_t d4[4] = {f.w[cb].x, f.w[cb].y, f.w[cb].z, f.w[cb].w};
@@ -176,7 +185,7 @@ struct KInt4 {
       for (int j = 0; j < 4; ++j) {
         const uint4 b = dq8(d4[j], s, zc);
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
+        for (int rb = 0; rb < RB; ++rb)
           acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               __builtin_bit_cast(bf16x8_t, f.a[rb][j]), __builtin_bit_cast(bf16x8_t, b),
               acc[rb][cb], 0, 0, 0);
@@ -195,16 +204,18 @@ __global__ __launch_bounds__(NW * 64) void gemm_ksplit_kernel(
   __shared__ __attribute__((aligned(16))) uint4 red[NW][512];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int n0 = blockIdx.x * kBN, m0 = blockIdx.y * kBM;
+  constexpr int RB = P::kRB, CB = P::kCB;
+  static_assert(RB * CB == 8, "8 MFMA tiles per wave");
+  const int n0 = blockIdx.x * (16 * CB), m0 = blockIdx.y * (16 * RB);
   const int nb = K / (P::kKB * NW);  // k-blocks of this wave: wave + i NW, i < nb
   P pol;
   pol.init(args, m0, n0, M, N, K, lane);
 
-  Acc acc[2][4];
+  Acc acc[RB][CB];
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+  for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = Acc{0, 0, 0, 0};
+    for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = Acc{0, 0, 0, 0};
 
   typename P::Frag f[D];
 #pragma unroll
@@ -223,10 +234,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_ksplit_kernel(
 
   // the NW partial tiles -> LDS, summed in wave order
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+  for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
-      red[wave][(rb * 4 + cb) * 64 + lane] = __builtin_bit_cast(uint4, acc[rb][cb]);
+    for (int cb = 0; cb < CB; ++cb)
+      red[wave][(rb * CB + cb) * 64 + lane] = __builtin_bit_cast(uint4, acc[rb][cb]);
   __syncthreads();
 #pragma unroll
   for (int e = threadIdx.x; e < 512; e += NW * 64) {
@@ -234,12 +245,12 @@ __global__ __launch_bounds__(NW * 64) void gemm_ksplit_kernel(
 #pragma unroll
     for (int w = 1; w < NW; ++w) t += __builtin_bit_cast(Acc, red[w][e]);
     const int rc = e >> 6, l = e & 63;
-    const int col = n0 + 16 * (rc & 3) + (l & 15);
+    const int col = n0 + 16 * (rc % CB) + (l & 15);
     const float cf = kColF ? bf16_to_f32(colf[col]) : 1.f;
     const float bv = bias != nullptr ? bf16_to_f32(bias[col]) : 0.f;
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii) {
-      const int m = m0 + 16 * (rc >> 2) + 4 * (l >> 4) + ii;
+      const int m = m0 + 16 * (rc / CB) + 4 * (l >> 4) + ii;
       if (m < M) {
         float v = P::epi(t[ii], kRowF ? bf16_to_f32(rowf[m]) : 1.f, cf);
         if (bias != nullptr) v = round_bf16(v + bv);
@@ -249,56 +260,67 @@ __global__ __launch_bounds__(NW * 64) void gemm_ksplit_kernel(
   }
 }
 
-// Launch shapes: NW waves, D k-blocks in flight per wave. K must split into NW x D x kKB pieces.
-struct KShape {
-  int nw, d;
+// Launch shapes: an RB x CB tile of 16 x 16 MFMA blocks per workgroup, NW waves, D k-blocks in
+// flight per wave. K must split into NW x D x kKB pieces; the ring depth is halved until it
+// divides the wave's k-blocks.
+struct KCfg {
+  int rb, cb, nw, d;
 };
 
-template <class P>
-bool kshape_ok(int64_t K, KShape s) {
-  const int64_t per = (int64_t)P::kKB * s.nw;
-  return K % per == 0 && (K / per) % s.d == 0 && K / per >= s.d;
+template <int KB>
+bool kcfg_ok(int64_t K, KCfg c) {
+  const int64_t per = (int64_t)KB * c.nw;
+  return K % per == 0 && (K / per) % c.d == 0 && K / per >= c.d;
 }
 
-// The configured ring depth is halved until it divides the wave's k-blocks.
-template <class P>
-KShape fit_depth(int64_t K, KShape s) {
-  while (s.d > 1 && !kshape_ok<P>(K, s)) s.d /= 2;
-  return s;
+template <int KB>
+KCfg fit_depth(int64_t K, KCfg c) {
+  while (c.d > 1 && !kcfg_ok<KB>(K, c)) c.d /= 2;
+  return c;
 }
 
-KShape kshape_int8(int64_t K) {
-  const int t = tuning().gemm_ksplit_shape;
-  KShape s{8, 4};
-  if (t == 1) s = {16, 2};
-  if (t == 2) s = {8, 2};
-  return fit_depth<KInt8Dyn>(K, s);
+// tao_tune_gemm_ksplit shape: 0 built-in; 1 32 x 64 tile, 2 64 x 32, 3 128 x 16, 4 128 x 16 on
+// 16 waves (int8) / 32 x 64 with one block in flight (int4)
+KCfg kcfg_int8(int64_t K) {
+  KCfg c{8, 1, 8, 4};
+  switch (tuning().gemm_ksplit_shape) {
+    case 1: c = {2, 4, 8, 4}; break;
+    case 2: c = {4, 2, 8, 4}; break;
+    case 3: c = {8, 1, 8, 4}; break;
+    case 4: c = {8, 1, 16, 2}; break;
+    default: break;
+  }
+  return fit_depth<64>(K, c);
 }
 
-KShape kshape_int4(int64_t K) {
-  const int t = tuning().gemm_ksplit_shape;
-  KShape s{8, 2};
-  if (t == 1 || t == 2) s = {8, 1};  // (16 waves spill the int4 fragments at 128 VGPRs)
-  return fit_depth<KInt4>(K, s);
+KCfg kcfg_int4(int64_t K) {  // (64 x 32 with two blocks in flight spills: one)
+  KCfg c{4, 2, 8, 1};
+  switch (tuning().gemm_ksplit_shape) {
+    case 1: c = {2, 4, 8, 2}; break;
+    case 2: c = {4, 2, 8, 1}; break;
+    case 3: c = {8, 1, 8, 1}; break;
+    case 4: c = {2, 4, 8, 1}; break;
+    default: break;
+  }
+  return fit_depth<128>(K, c);
 }
 
 }  // namespace
 
 // ---- routing and launchers ------------------------------------------------------------------
-// path 0 int4, 2 int8 dynamic. Shapes the kernel covers: N % 64 == 0, K split evenly over the
-// waves and the ring (kshape_ok), operands below 4 GiB. Auto routing (tuning().gemm_ksplit == 0):
-// none until measured (profiles/r3_ab_ksplit*.jsonl).
+// path 0 int4, 2 int8 dynamic. Shapes the kernel covers: N a multiple of the tile's columns, K
+// split evenly over the waves (kcfg_ok), operands below 4 GiB. Auto routing
+// (tuning().gemm_ksplit == 0): none until measured (profiles/r3_ab_ksplit*.jsonl).
 bool use_ksplit(int path, int64_t M, int64_t N, int64_t K, int64_t group_size) {
   const int mode = tuning().gemm_ksplit;
   if (mode == 1) return false;
   if (path != 0 && path != 2) return false;
-  if (N % kBN != 0 || M < 1 || N * K >= (int64_t(1) << 32) || M * K * 2 >= (int64_t(1) << 32))
-    return false;
+  if (M < 1 || N * K >= (int64_t(1) << 32) || M * K * 2 >= (int64_t(1) << 32)) return false;
   if (path == 0 && (group_size < 32 || group_size > 256 || (group_size & (group_size - 1))))
     return false;
-  const bool ok = path == 2 ? kshape_ok<KInt8Dyn>(K, kshape_int8(K))
-                            : kshape_ok<KInt4>(K, kshape_int4(K));
-  if (!ok) return false;
+  const KCfg c = path == 2 ? kcfg_int8(K) : kcfg_int4(K);
+  const bool ok = path == 2 ? kcfg_ok<64>(K, c) : kcfg_ok<128>(K, c);
+  if (!ok || N % (16 * c.cb) != 0) return false;
   if (mode == 2) return true;
   const Tuning& t = tuning();
   if (t.bm || t.kg || t.splits || t.gemm_nw || t.int4_mfma32 || t.gemm_algo || t.gemm_tile ||
@@ -311,7 +333,7 @@ template <class P, int NW, int D, bool kRowF, bool kColF>
 int launch_ksplit(const typename P::Args& a, const uint16_t* rowf, const uint16_t* colf,
                   const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream,
                   const char* name) {
-  const dim3 grid((unsigned)(N / kBN), (unsigned)((M + kBM - 1) / kBM));
+  const dim3 grid((unsigned)(N / (16 * P::kCB)), (unsigned)((M + 16 * P::kRB - 1) / (16 * P::kRB)));
   launch(gemm_ksplit_kernel<P, NW, D, kRowF, kColF>, grid, dim3(NW * 64), 0, stream, a, rowf,
          colf, bias, y, M, N, K);
   return check_launch(name);
@@ -319,33 +341,44 @@ int launch_ksplit(const typename P::Args& a, const uint16_t* rowf, const uint16_
 
 int ksplit_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int gshift,
                 const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream) {
-  const KShape s = kshape_int4(K);
-  TAO_CHECK_ARG(N % kBN == 0 && kshape_ok<KInt4>(K, s) && gshift >= 0 && gshift <= 3,
-                "k-split GEMM: N %% 64, K a multiple of %d and g in {32..256} required",
-                KInt4::kKB * s.nw * s.d);
-  KInt4::Args a{x, packed, reinterpret_cast<const uint32_t*>(sz), gshift};
+  const KCfg c = kcfg_int4(K);
+  TAO_CHECK_ARG(N % (16 * c.cb) == 0 && kcfg_ok<128>(K, c) && gshift >= 0 && gshift <= 3,
+                "k-split GEMM: N %% %d, K a multiple of %d and g in {32..256} required",
+                16 * c.cb, 128 * c.nw * c.d);
   const char* nm = "gemm_ksplit_kernel<int4>";
-  if (s.d == 1)
-    return launch_ksplit<KInt4, 8, 1, false, false>(a, nullptr, nullptr, bias, y, M, N, K, stream, nm);
-  return launch_ksplit<KInt4, 8, 2, false, false>(a, nullptr, nullptr, bias, y, M, N, K, stream, nm);
+#define TAO_KS4(RB_, CB_, NW_, D_)                                                              \
+  if (c.rb == RB_ && c.cb == CB_ && c.nw == NW_ && c.d == D_) {                                \
+    typename KInt4<RB_, CB_>::Args a{x, packed, reinterpret_cast<const uint32_t*>(sz), gshift}; \
+    return launch_ksplit<KInt4<RB_, CB_>, NW_, D_, false, false>(a, nullptr, nullptr, bias, y, M, \
+                                                                 N, K, stream, nm);            \
+  }
+  TAO_KS4(2, 4, 8, 2) TAO_KS4(2, 4, 8, 1) TAO_KS4(4, 2, 8, 1) TAO_KS4(8, 1, 8, 1)
+#undef TAO_KS4
+  TAO_CHECK_ARG(false, "k-split GEMM: no int4 instance for this shape");
+  return TAO_ERR_UNSUPPORTED;
 }
 
 int ksplit_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uint16_t* ws,
                    const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream) {
-  const KShape s = kshape_int8(K);
-  TAO_CHECK_ARG(N % kBN == 0 && kshape_ok<KInt8Dyn>(K, s),
-                "k-split GEMM: N %% 64 and K a multiple of %d required", KInt8Dyn::kKB * s.nw * s.d);
-  KInt8Dyn::Args a{reinterpret_cast<const uint8_t*>(xq), reinterpret_cast<const uint8_t*>(wq)};
+  const KCfg c = kcfg_int8(K);
+  TAO_CHECK_ARG(N % (16 * c.cb) == 0 && kcfg_ok<64>(K, c),
+                "k-split GEMM: N %% %d and K a multiple of %d required", 16 * c.cb,
+                64 * c.nw * c.d);
   const char* nm = "gemm_ksplit_kernel<int8dyn>";
-  if (s.nw == 16 && s.d == 2)
-    return launch_ksplit<KInt8Dyn, 16, 2, true, true>(a, xs, ws, bias, y, M, N, K, stream, nm);
-  if (s.nw == 16)
-    return launch_ksplit<KInt8Dyn, 16, 1, true, true>(a, xs, ws, bias, y, M, N, K, stream, nm);
-  if (s.d == 1)
-    return launch_ksplit<KInt8Dyn, 8, 1, true, true>(a, xs, ws, bias, y, M, N, K, stream, nm);
-  if (s.d == 2)
-    return launch_ksplit<KInt8Dyn, 8, 2, true, true>(a, xs, ws, bias, y, M, N, K, stream, nm);
-  return launch_ksplit<KInt8Dyn, 8, 4, true, true>(a, xs, ws, bias, y, M, N, K, stream, nm);
+#define TAO_KS8(RB_, CB_, NW_, D_)                                                              \
+  if (c.rb == RB_ && c.cb == CB_ && c.nw == NW_ && c.d == D_) {                                \
+    typename KInt8Dyn<RB_, CB_>::Args a{reinterpret_cast<const uint8_t*>(xq),                  \
+                                        reinterpret_cast<const uint8_t*>(wq)};                 \
+    return launch_ksplit<KInt8Dyn<RB_, CB_>, NW_, D_, true, true>(a, xs, ws, bias, y, M, N, K,  \
+                                                                  stream, nm);                 \
+  }
+  TAO_KS8(2, 4, 8, 4) TAO_KS8(2, 4, 8, 2) TAO_KS8(2, 4, 8, 1)
+  TAO_KS8(4, 2, 8, 4) TAO_KS8(4, 2, 8, 2) TAO_KS8(4, 2, 8, 1)
+  TAO_KS8(8, 1, 8, 4) TAO_KS8(8, 1, 8, 2) TAO_KS8(8, 1, 8, 1)
+  TAO_KS8(8, 1, 16, 2) TAO_KS8(8, 1, 16, 1)
+#undef TAO_KS8
+  TAO_CHECK_ARG(false, "k-split GEMM: no int8 instance for this shape");
+  return TAO_ERR_UNSUPPORTED;
 }
 
 }  // namespace tao
@@ -353,7 +386,7 @@ int ksplit_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const
 extern "C" int tao_tune_gemm_ksplit(int mode, int shape) {
   TAO_CHECK_ARG(mode >= 0 && mode <= 2,
                 "tune: gemm k-split mode must be 0 (auto), 1 (off) or 2 (on)");
-  TAO_CHECK_ARG(shape >= 0 && shape <= 3, "tune: gemm k-split shape must be 0..3");
+  TAO_CHECK_ARG(shape >= 0 && shape <= 4, "tune: gemm k-split shape must be 0..4");
   tao::tuning().gemm_ksplit = mode;
   tao::tuning().gemm_ksplit_shape = shape;
   return TAO_OK;
