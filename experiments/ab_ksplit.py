@@ -22,7 +22,13 @@ FULL = QUICK + [(p, M, N, K) for p in ("int4", "int8dyn") for M in (32, 64, 96, 
                 for (N, K) in LLAMA8B if (p, M, N, K) not in QUICK]
 
 
+SHAPES = (1, 2, 3, 4)
+
+
 def main():
+    global SHAPES
+    if "--rot" in sys.argv:
+        SHAPES = (1, 17, 2, 18, 3, 19)
     configs = QUICK if "--quick" in sys.argv else FULL
     mk = {"int4": make_int4, "int8dyn": make_int8dyn}
     for path, M, N, K in configs:
@@ -32,7 +38,7 @@ def main():
         ref = run(0).float()
         row = {"path": path, "M": M, "N": N, "K": K, "old_us": round(old_us, 2)}
         best = None
-        for shape in (1, 2, 3, 4):
+        for shape in SHAPES:
             _lib.call("tao_tune_gemm_ksplit", 2, shape)
             us = kernel_us(run, launches)
             out = run(0).float()

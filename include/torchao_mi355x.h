@@ -145,8 +145,8 @@ int tao_tune_gemm_stream(int mode);
  * split K, operands loaded straight into MFMA fragments, partials summed through LDS in wave
  * order) for the int4 weight-only and int8 dynamic linears. mode 0 = built-in routing, 1 = never,
  * 2 = wherever the shape is supported. shape: 0 built-in, 1 = 32 x 64 output tile, 2 = 64 x 32,
- * 3 = 128 x 16, 4 = 128 x 16 on 16 waves (int8) / 32 x 64 with one k-block in flight (int4).
- * Thread-local. */
+ * 3 = 128 x 16, 4 = 128 x 16 on 16 waves (int8) / 32 x 64 with one k-block in flight (int4);
+ * + 16: each workgroup walks its k-blocks from a rotated start. Thread-local. */
 int tao_tune_gemm_ksplit(int mode, int shape);
 /* Number of split-K workspaces currently owned by captured graphs (each is released with its
  * graph). Diagnostic for tests; never fails. */

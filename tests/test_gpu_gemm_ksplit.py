@@ -47,9 +47,9 @@ INT4_SHAPES = [(128, 4096, 4096), (5, 64, 1024), (17, 128, 1024), (33, 192, 2048
 
 @pytest.mark.parametrize("M,N,K", INT4_SHAPES)
 @pytest.mark.parametrize("g", [32, 128])
-@pytest.mark.parametrize("shape", [0, 1, 3, 4])
+@pytest.mark.parametrize("shape", [0, 1, 3, 4, 17])
 def test_ksplit_int4(ksplit, M, N, K, g, shape):
-    """Every output tile (32 x 64, 64 x 32, 128 x 16) and ring depth."""
+    """Every output tile (32 x 64, 64 x 32, 128 x 16), ring depth and the rotated block order."""
     ksplit(2, shape)
     q, s, z, packed, sz = _int4(N, K, g, seed=M + N + g)
     x = oracle.make_activation(M, K, seed=M)
@@ -79,7 +79,7 @@ INT8_SHAPES = [(128, 4096, 4096), (5, 64, 512), (31, 128, 1024), (33, 192, 2048)
 
 
 @pytest.mark.parametrize("M,N,K", INT8_SHAPES)
-@pytest.mark.parametrize("shape", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("shape", [0, 1, 2, 3, 4, 17, 19])
 def test_ksplit_int8dyn_bit_exact(ksplit, M, N, K, shape):
     ksplit(2, shape)
     w = oracle.make_linear_weight(N, K, seed=M + N)

@@ -199,7 +199,8 @@ struct KInt4 {
 template <class P, int NW, int D, bool kRowF, bool kColF>
 __global__ __launch_bounds__(NW * 64) void gemm_ksplit_kernel(
     typename P::Args args, const uint16_t* __restrict__ rowf, const uint16_t* __restrict__ colf,
-    const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K) {
+    const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K,
+    int rotate) {
   typedef typename P::Acc Acc;
   __shared__ __attribute__((aligned(16))) uint4 red[NW][512];
   const int lane = threadIdx.x & 63;
@@ -218,15 +219,25 @@ __global__ __launch_bounds__(NW * 64) void gemm_ksplit_kernel(
     for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = Acc{0, 0, 0, 0};
 
   typename P::Frag f[D];
+  // rotate: the workgroup walks its wave's blocks from a rotated start, so that the workgroups
+  // sharing an operand tile (the M tiles of one weight tile, the N tiles of one x tile) do not
+  // all miss on the same lines at once; wave w still takes exactly the blocks = w mod NW
+  const int rot =
+      rotate ? (int)((blockIdx.y * (unsigned)((nb + 3) / 4) + blockIdx.x) % (unsigned)nb) : 0;
+  auto blk = [&](int i) __attribute__((always_inline)) {
+    int j = i + rot;
+    j = j >= nb ? j - nb : j;
+    return wave + j * NW;
+  };
 #pragma unroll
-  for (int d = 0; d < D; ++d) pol.load(f[d], wave + d * NW);
+  for (int d = 0; d < D; ++d) pol.load(f[d], blk(d));
   int i = 0;
 #pragma unroll 1
   for (; i + D < nb; i += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       pol.compute(f[d], acc);
-      pol.load(f[d], wave + (i + D + d) * NW);
+      pol.load(f[d], blk(i + D + d));
     }
   }
 #pragma unroll
@@ -335,7 +346,7 @@ int launch_ksplit(const typename P::Args& a, const uint16_t* rowf, const uint16_
                   const char* name) {
   const dim3 grid((unsigned)(N / (16 * P::kCB)), (unsigned)((M + 16 * P::kRB - 1) / (16 * P::kRB)));
   launch(gemm_ksplit_kernel<P, NW, D, kRowF, kColF>, grid, dim3(NW * 64), 0, stream, a, rowf,
-         colf, bias, y, M, N, K);
+         colf, bias, y, M, N, K, tuning().gemm_ksplit_rot);
   return check_launch(name);
 }
 
@@ -386,8 +397,10 @@ int ksplit_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const
 extern "C" int tao_tune_gemm_ksplit(int mode, int shape) {
   TAO_CHECK_ARG(mode >= 0 && mode <= 2,
                 "tune: gemm k-split mode must be 0 (auto), 1 (off) or 2 (on)");
-  TAO_CHECK_ARG(shape >= 0 && shape <= 4, "tune: gemm k-split shape must be 0..4");
+  TAO_CHECK_ARG((shape & 15) <= 4 && shape >= 0 && shape < 32,
+                "tune: gemm k-split shape must be 0..4 (+16: rotated block order)");
   tao::tuning().gemm_ksplit = mode;
-  tao::tuning().gemm_ksplit_shape = shape;
+  tao::tuning().gemm_ksplit_shape = shape & 15;
+  tao::tuning().gemm_ksplit_rot = shape >> 4;
   return TAO_OK;
 }
