@@ -52,7 +52,6 @@ def main():
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--model", default="8b", choices=["8b", "70b"])
-    ap.add_argument("--bpw", default="", help="row blocks per workgroup to time, e.g. 1,2,4,8")
     args = ap.parse_args()
     L = args.layers
     K, H, Hkv, D, T, I = 4096, 32, 8, 128, 512, 14336
@@ -108,10 +107,6 @@ def main():
             _lib.call("tao_tune_int4_norm", 1)  # deferred RMSNorm scale
             res["fused_deferred_norm_us"] = round(time_graph(fused, n), 3)
             _lib.call("tao_tune_int4_norm", 0)
-            for b in [int(v) for v in args.bpw.split(",") if v]:
-                _lib.call("tao_tune_int4_decode_bpw", b)
-                res[f"fused_bpw{b}_us"] = round(time_graph(fused, n), 3)
-                _lib.call("tao_tune_int4_decode_bpw", 0)
             if t == (0, 0, 0, 0):
                 res["unfused_us"] = round(time_graph(unfused, n), 3)
                 res["gemv_only_us"] = round(time_graph(plain, n), 3)

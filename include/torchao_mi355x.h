@@ -161,11 +161,6 @@ int tao_tune_int4_xlds(int mode);
  * each output by rsqrt(mean(x^2) + eps) at the end). Calling thread only; for measurement. */
 int tao_tune_int4_norm(int mode);
 
-/* Row blocks per workgroup of tao_int4wo_decode_bf16 with the RMSNorm prologue: each workgroup
- * walks bpw blocks of rows (grid-stride) and normalises x once for all of them. 0 = built-in,
- * 1..64. Calling thread only; for sweeps. */
-int tao_tune_int4_decode_bpw(int bpw);
-
 /* packed[N][K/8] <- q[N][K] (int32 values 0..15).
  * Replaces aten._convert_weight_to_int4pack(u8, inner_k_tiles) at
  * torchao/dtypes/uintx/tensor_core_tiled_layout.py:279 (device kernel). K % 8 == 0. */

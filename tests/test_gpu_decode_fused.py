@@ -208,51 +208,3 @@ def test_deferred_norm_mode(N, K, epi):
         ref32 = F.silu(a) * b
     rel = (got.float() - ref32).norm() / ref32.norm()
     assert rel < 1e-2, float(rel)
-
-
-@pytest.mark.parametrize("bpw", [2, 3, 7, 64])
-@pytest.mark.parametrize("op", ["none", "swiglu", "rope_kv", "head", "k8192"])
-def test_row_blocks_per_workgroup_bit_identical(op, bpw):
-    """tao_tune_int4_decode_bpw: with the RMSNorm prologue a workgroup may walk several row blocks
-    (grid-stride) and normalise x once. Every row is still computed by one wave with the same
-    arithmetic, so outputs and cache rows are BIT-identical to one block per workgroup, for every
-    epilogue, uneven block counts (bpw 3, 7) and more blocks per workgroup than there are.
-    k8192: a kernel that keeps one block per workgroup (x in 4 pieces per thread) ignores it."""
-    from torchao import _lib
-    from torchao._models.llama import kernels
-    from torchao._models.llama.model import ModelArgs, _rope_freqs
-
-    H, Hkv, D, T = 32, 8, 128, 64
-    K = 8192 if op == "k8192" else 4096
-    N = {"none": 4096, "swiglu": 2 * 14336, "rope_kv": (H + 2 * Hkv) * D, "head": 128256,
-         "k8192": 10240}[op]
-    lin, parts = _int4_linear(N, K, seed=5)
-    x = torch.randn(1, 1, K, device=DEV, dtype=torch.bfloat16) * 2
-    w = _norm_w(K, seed=6)
-    cfg = ModelArgs(n_layer=1, n_head=H, n_local_heads=Hkv, dim=H * D, rope_base=500000)
-    freqs = _rope_freqs(cfg, T).to(DEV)
-    p = torch.tensor([9], device=DEV)
-    epi = op if op in ("swiglu", "rope_kv") else "none"
-
-    def run():
-        kc = torch.zeros(1, Hkv, T, D, device=DEV, dtype=torch.bfloat16)
-        vc = torch.zeros_like(kc)
-        y = kernels.int4_decode(x, *parts, norm_weight=w, eps=1e-5, epilogue=epi,
-                                rope=(freqs, p, kc, vc, H))
-        return y, kc, vc
-
-    try:
-        ref = run()
-        _lib.call("tao_tune_int4_decode_bpw", bpw)
-        got = run()
-        for a, b in zip(got, ref):
-            assert torch.equal(a, b)
-        # and the deferred-norm mode walks blocks the same way
-        _lib.call("tao_tune_int4_norm", 1)
-        got_d = run()
-        _lib.call("tao_tune_int4_decode_bpw", 1)
-        ref_d = run()
-        for a, b in zip(got_d, ref_d):
-            assert torch.equal(a, b)
-    finally:
-        _lib.call("tao_tune_reset")

@@ -90,7 +90,7 @@ template <int MT, int RPW, int WPE, bool PAIR, int NPT = 0, int EPI = kEpiNone>
 __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     const uint16_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
     const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K, int gshift,
-    int Wk, int G, int S, int nblk, GemvFuse fu) {
+    int Wk, int G, int S, GemvFuse fu) {
   constexpr bool PRO = NPT > 0;
   static_assert(!(PRO || EPI) || (MT == 1 && RPW % 2 == 0), "fusions are M == 1, row pairs");
   constexpr int V = RPW * MT;
@@ -102,10 +102,7 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int wk = wave % Wk;
   const int rg = wave / Wk;
-  // Row blocks (G * RPW rows each): one per workgroup, except with the RMSNorm prologue, where
-  // a workgroup may walk several (grid-stride, nblk in all) and normalises x only once.
-  int blk = blockIdx.x;
-  int row0 = (blk * G + rg) * RPW;
+  const int row0 = (blockIdx.x * G + rg) * RPW;
   const int nchunk = K >> 5;               // 32-k chunks per row
   const int ngroups = K >> (5 + gshift);   // quantisation groups per row
 
@@ -315,18 +312,8 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     if constexpr (PRO && decltype(first)::value) norm_finish();
     do_slice(wv0, szv0, cc0, cv0);
   };
-  // Row blocks: one per workgroup, except that the RMSNorm prologue's kernels with x in <= 2
-  // pieces per thread (K <= 4096 at 256 threads) may walk several (WALK), normalising x once.
-  // (At NPT 4 the second path's registers spill: those keep one block per workgroup.)
-  constexpr bool WALK = PRO && NPT <= 2;
-  bool first = true;
-  for (;;) {
   if constexpr (PAIR && PRO) {
-    if (!WALK || first) {
-      pair_step(wk, std::true_type{});
-    } else {
-      pair_step(wk, std::false_type{});
-    }
+    pair_step(wk, std::true_type{});
     for (int s = wk + 2 * Wk; s < S; s += 2 * Wk) pair_step(s, std::false_type{});
   } else if constexpr (PAIR) {
     for (int s = wk; s < S; s += 2 * Wk) {
@@ -340,11 +327,7 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
       if (s + Wk < S) do_slice(wv1, szv1, cc1, cv1);  // wave-uniform
     }
   } else if constexpr (PRO) {
-    if (!WALK || first) {
-      single_step(wk, std::true_type{});
-    } else {
-      single_step(wk, std::false_type{});
-    }
+    single_step(wk, std::true_type{});
     for (int s = wk + Wk; s < S; s += Wk) single_step(s, std::false_type{});
   } else {
     for (int s = wk; s < S; s += Wk) {
@@ -459,21 +442,6 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
       }
     }
   }
-  if constexpr (!WALK) {
-    break;
-  } else {
-    // the workgroup's next row block (grid-stride; the bound is workgroup-uniform)
-    blk += gridDim.x;
-    if (blk >= nblk) break;
-    first = false;
-    row0 = (blk * G + rg) * RPW;
-#pragma unroll
-    for (int r = 0; r < RPW; ++r)
-#pragma unroll
-      for (int m = 0; m < MT; ++m) acc[r][m] = 0.f;
-    if (Wk > 1) __syncthreads();  // the previous block's cross-wave partials are read out
-  }
-  }  // row blocks
 }
 
 int gshift_of(int64_t g) {
@@ -501,15 +469,12 @@ GemvShape default_shape(int S) {
 template <int MT, int RPW, int WPE, int NPT = 0, int EPI = kEpiNone>
 int launch_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
                 const uint16_t* bias, uint16_t* y, int M, int N, int K, int gshift,
-                GemvShape sh, hipStream_t stream, const GemvFuse& fu = GemvFuse{}, int bpw = 1) {
+                GemvShape sh, hipStream_t stream, const GemvFuse& fu = GemvFuse{}) {
   const int nchunk = K / 32;
   const int S = (nchunk + 63) / 64;
   const int wk = sh.wk < S ? sh.wk : S;
   const int rows_per_wg = sh.g * RPW;
-  const int nblk = (N + rows_per_wg - 1) / rows_per_wg;
-  // row blocks per workgroup: only the RMSNorm prologue's kernels with NPT <= 2 walk several
-  // (the kernel's WALK); every other grid has one workgroup per block
-  const int grid = NPT > 0 && NPT <= 2 && bpw > 1 ? (nblk + bpw - 1) / bpw : nblk;
+  const int grid = (N + rows_per_wg - 1) / rows_per_wg;
   const int threads = 64 * wk * sh.g;
   constexpr bool PRO = NPT > 0;
   const size_t lds = PRO ? (((size_t)sh.g * wk * RPW * MT + 8 + 3) & ~(size_t)3) * sizeof(float) +
@@ -518,11 +483,11 @@ int launch_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
   if (S > wk)
     launch((int4wo_gemv_kernel<MT, RPW, WPE, true, NPT, EPI>), dim3(grid), dim3(threads), lds,
            stream, x, reinterpret_cast<const uint4*>(packed),
-           reinterpret_cast<const uint32_t*>(sz), bias, y, M, N, K, gshift, wk, sh.g, S, nblk, fu);
+           reinterpret_cast<const uint32_t*>(sz), bias, y, M, N, K, gshift, wk, sh.g, S, fu);
   else
     launch((int4wo_gemv_kernel<MT, RPW, WPE, false, NPT, EPI>), dim3(grid), dim3(threads), lds,
            stream, x, reinterpret_cast<const uint4*>(packed),
-           reinterpret_cast<const uint32_t*>(sz), bias, y, M, N, K, gshift, wk, sh.g, S, nblk, fu);
+           reinterpret_cast<const uint32_t*>(sz), bias, y, M, N, K, gshift, wk, sh.g, S, fu);
   return check_launch("int4wo_gemv_kernel");
 }
 
@@ -583,7 +548,7 @@ M1Shape m1_shape(int N, int S) {
 template <int NPT, int EPI>
 int launch_decode_rows(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
                        uint16_t* y, int N, int K, int gs, hipStream_t stream, const GemvFuse& fu,
-                       const M1Shape& c, int bpw = 1) {
+                       const M1Shape& c) {
   if constexpr (NPT == 0 && EPI == kEpiNone) {  // the plain linear: the product path's shapes
     if (c.rpw == 8)
       return launch_gemv<1, 8, 4>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream);
@@ -593,14 +558,13 @@ int launch_decode_rows(const uint16_t* x, const uint32_t* packed, const uint16_t
   if (c.rpw <= 2) {
     if constexpr (NPT > 0)
       return launch_gemv<1, 2, 4, NPT, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream,
-                                            fu, bpw);
+                                            fu);
     else
       return launch_gemv<1, 2, 8, NPT, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream,
                                             fu);
   }
   if (c.occ == 4 || NPT > 0)
-    return launch_gemv<1, 4, 4, NPT, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream, fu,
-                                          bpw);
+    return launch_gemv<1, 4, 4, NPT, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream, fu);
   return launch_gemv<1, 4, 8, 0, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream, fu);
 }
 
@@ -621,14 +585,9 @@ int launch_decode(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
     const int wk = c.sh.wk < S ? c.sh.wk : S;
     while (64 * wk * c.sh.g * 8 * kMaxNormPT < K && wk * c.sh.g * 2 <= 8) c.sh.g *= 2;
     const int threads = 64 * wk * c.sh.g;
-    // Row blocks per workgroup: every workgroup pays the normalisation's VALU work (~150
-    // instructions per wave for K = 4096), so a workgroup walks several row blocks and
-    // normalises x once (tao_tune_int4_decode_bpw; 0 = built-in).
-    int bpw = tao::tuning().decode_bpw;
-    if (bpw <= 0) bpw = 1;
     if (threads * 8 * 2 >= K)
-      return launch_decode_rows<2, EPI>(x, packed, sz, y, N, K, gs, stream, fu, c, bpw);
-    return launch_decode_rows<4, EPI>(x, packed, sz, y, N, K, gs, stream, fu, c, bpw);
+      return launch_decode_rows<2, EPI>(x, packed, sz, y, N, K, gs, stream, fu, c);
+    return launch_decode_rows<4, EPI>(x, packed, sz, y, N, K, gs, stream, fu, c);
   } else {
     return launch_decode_rows<0, EPI>(x, packed, sz, y, N, K, gs, stream, fu, c);
   }
@@ -703,12 +662,6 @@ extern "C" int tao_debug_gemv_stamps(unsigned long long* out, int n) {
 extern "C" int tao_tune_int4_norm(int mode) {
   TAO_CHECK_ARG(mode == 0 || mode == 1, "tune: norm mode must be 0 (exact) or 1 (deferred)");
   tao::tuning().norm = mode;
-  return TAO_OK;
-}
-
-extern "C" int tao_tune_int4_decode_bpw(int bpw) {
-  TAO_CHECK_ARG(bpw >= 0 && bpw <= 64, "tune: decode row blocks per workgroup must be 0..64");
-  tao::tuning().decode_bpw = bpw;
   return TAO_OK;
 }
 

@@ -46,7 +46,6 @@ _SIGNATURES = {
     "tao_tune_int4_mfma32": [_int],
     "tao_tune_int4_xlds": [_int],
     "tao_tune_int4_norm": [_int],
-    "tao_tune_int4_decode_bpw": [_int],
     "tao_tune_reset": [],
     "tao_tune_splitk_fenced": [_int],
     "tao_query_splitk_fenced": [],

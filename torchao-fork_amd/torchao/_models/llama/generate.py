@@ -236,9 +236,6 @@ def main(argv=None):
     ap.add_argument("--deferred_norm", action="store_true",
                     help="fused RMSNorm scales the GEMV outputs by rsqrt(mean(x^2)+eps) instead "
                          "of normalising x first (one bf16 rounding fewer; tao_tune_int4_norm 1)")
-    ap.add_argument("--decode_bpw", type=int, default=0,
-                    help="row blocks per workgroup of the fused RMSNorm GEMVs (0 = built-in; "
-                         "tao_tune_int4_decode_bpw)")
     ap.add_argument("--head_prologue", action="store_true",
                     help="fuse the final RMSNorm into the output head GEMV (kernels.HEAD_PROLOGUE)")
     ap.add_argument("--attn_mode", type=int, default=-1,
@@ -252,13 +249,11 @@ def main(argv=None):
         from torchao._models.llama import kernels
 
         kernels.HEAD_PROLOGUE = True
-    if args.deferred_norm or args.decode_bpw or args.attn_mode >= 0:
+    if args.deferred_norm or args.attn_mode >= 0:
         from torchao import _lib
 
         if args.deferred_norm:
             _lib.call("tao_tune_int4_norm", 1)
-        if args.decode_bpw:
-            _lib.call("tao_tune_int4_decode_bpw", args.decode_bpw)
         if args.attn_mode >= 0:
             _lib.call("tao_tune_attn", args.attn_mode)
     device = torch.device(args.device)
