@@ -338,9 +338,10 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
                          int64_t Hkv, int64_t D, int64_t T, float scale, void* stream);
 
 /* Calling thread's choice of the decode-attention kernel: 0 = single-pass workgroup per query head
- * (f32 math) for T <= 1024, else the two-launch split (default); 1 = two-launch split; 2 / 3 = one
- * launch over 32 / 64-key chunks merged by the kv head's last arriving chunk; 4 = as 0 with the
- * packed-bf16 single-pass kernel (measured slower). */
+ * (f32 math, whole-line K loads) for T <= 1024, else the two-launch split (default); 1 = two-launch
+ * split; 2 / 3 = one launch over 32 / 64-key chunks merged by the kv head's last arriving chunk;
+ * 4 = as 0 with the packed-bf16 single-pass kernel (measured slower); 5 = as 0 with half-line K
+ * loads (the round-1 kernel). */
 int tao_tune_attn(int mode);
 
 /* Device-side faults of the decode kernels since the last call, read and cleared (synchronous:

@@ -170,12 +170,13 @@ def test_fused_kernels_match_torch_ops_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("G", [1, 2, 4, 8])
 def test_attn_decode_modes_gpu(mode, G):
-    """Every decode-attention kernel (tao_tune_attn: 0 f32 single pass up to 1024 keys, 1
-    two-launch split, 2 / 3 one launch over 32 / 64-key chunks merged by the last arriver, 4
-    packed-bf16 single pass) against fp32 SDPA, GQA groups 1..8, lengths across chunk edges; the one-launch kernels are also
+    """Every decode-attention kernel (tao_tune_attn: 0 f32 single pass (whole-line K loads) up to
+    1024 keys, 1 two-launch split, 2 / 3 one launch over 32 / 64-key chunks merged by the last
+    arriver, 4 packed-bf16 single pass, 5 f32 single pass with half-line K loads) against fp32
+    SDPA, GQA groups 1..8, lengths across chunk edges; the one-launch kernels are also
     run-to-run identical (chunks merged in chunk order whatever the arrival order) and leave
     their counters reset (the same workspace serves every call)."""
     import torch.nn.functional as F

@@ -265,7 +265,10 @@ constexpr int kSingleMaxT = 1024;
 // two-launch split, 2 / 3 = attn_chunk_fused_kernel with 32 / 64-key chunks
 constexpr int kSingleWaves = TAO_ATTN_WAVES;
 
-template <int D, int NW>
+// FULLK: each K load instruction covers 8 keys x 128 B (whole cache lines; lane l: key
+// t0 + 8 i + l / 8, dims 64 h + 8 (l % 8) ..) instead of 16 keys x 64 B (half lines: the L2 moves
+// half the bytes per instruction, profiles/r3_probe_l2_pattern.jsonl); 8 lanes per key.
+template <int D, int NW, bool FULLK = false>
 __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
@@ -282,8 +285,116 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int kq = lane >> 2, p = lane & 3;
   const size_t head = (size_t)(b * Hkv + kvh) * T;
-  const uint16_t* kb = kc + head * D + p * 8;
   const uint32_t* vb = reinterpret_cast<const uint32_t*>(vc + head * D) + lane;
+  if constexpr (FULLK) {
+    // lane (g = l / 8, p8 = l % 8): keys t0 + g and t0 + 8 + g, dims 64 h + 8 p8 + e (h < 2, e < 8)
+    const int g = lane >> 3, p8 = lane & 7;
+    const uint16_t* kbase = kc + head * D + p8 * 8;
+    uint4 ka[2], kb2[2];
+    uint32_t vv[16];
+    auto load_step = [&](int t0) __attribute__((always_inline)) {
+      const int ta = t0 + g < L ? t0 + g : L - 1, tb = t0 + 8 + g < L ? t0 + 8 + g : L - 1;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        ka[h] = *reinterpret_cast<const uint4*>(kbase + (size_t)ta * D + 64 * h);
+        kb2[h] = *reinterpret_cast<const uint4*>(kbase + (size_t)tb * D + 64 * h);
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int tj = t0 + j < L ? t0 + j : L - 1;
+        vv[j] = vb[(size_t)tj * (D / 2)];
+      }
+    };
+    load_step(wave * 16);
+    float qr[16];
+    {
+      const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bh * D + p8 * 8);
+      uint4 qv[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) qv[h] = qp[h * 8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t w[4] = {qv[h].x, qv[h].y, qv[h].z, qv[h].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          qr[h * 8 + 2 * e] = bf16lo_to_f32(w[e]);
+          qr[h * 8 + 2 * e + 1] = bf16hi_to_f32(w[e]);
+        }
+      }
+    }
+    float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
+    for (int t0 = wave * 16; t0 < L; t0 += NW * 16) {
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t wa[4] = {ka[h].x, ka[h].y, ka[h].z, ka[h].w};
+        const uint32_t wb[4] = {kb2[h].x, kb2[h].y, kb2[h].z, kb2[h].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sa = fmaf(qr[h * 8 + 2 * e], bf16lo_to_f32(wa[e]),
+                    fmaf(qr[h * 8 + 2 * e + 1], bf16hi_to_f32(wa[e]), sa));
+          sb = fmaf(qr[h * 8 + 2 * e], bf16lo_to_f32(wb[e]),
+                    fmaf(qr[h * 8 + 2 * e + 1], bf16hi_to_f32(wb[e]), sb));
+        }
+      }
+      float vf[32];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        vf[2 * j] = bf16lo_to_f32(vv[j]);
+        vf[2 * j + 1] = bf16hi_to_f32(vv[j]);
+      }
+      if (t0 + NW * 16 < L) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
+      sa = wave_bfly<1, 8>(sa, lane_id(), [](float a, float c) { return a + c; });
+      sb = wave_bfly<1, 8>(sb, lane_id(), [](float a, float c) { return a + c; });
+      const bool va = t0 + g < L, vbk = t0 + 8 + g < L;
+      sa = va ? sa * scale : -INFINITY;
+      sb = vbk ? sb * scale : -INFINITY;
+      float mx = fmaxf(sa, sb);
+      mx = wave_bfly<8, 64>(mx, lane_id(), [](float a, float c) { return fmaxf(a, c); });
+      const float mn = fmaxf(m, mx);  // finite: key t0 < L is valid
+      const float corr = __expf(m - mn);
+      const float ea = va ? __expf(sa - mn) : 0.f, eb = vbk ? __expf(sb - mn) : 0.f;
+      float es = ea + eb;  // each key sits in 8 lanes of one group: xor 8..32 counts it once
+      es = wave_bfly<8, 64>(es, lane_id(), [](float a, float c) { return a + c; });
+      l = fmaf(l, corr, es);
+      o0 *= corr;
+      o1 *= corr;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float pa = __shfl(ea, 8 * j, 64), pb = __shfl(eb, 8 * j, 64);
+        o0 = fmaf(pa, vf[2 * j], o0);
+        o1 = fmaf(pa, vf[2 * j + 1], o1);
+        o0 = fmaf(pb, vf[2 * (j + 8)], o0);
+        o1 = fmaf(pb, vf[2 * (j + 8) + 1], o1);
+      }
+      m = mn;
+    }
+    if (lane == 0) {
+      wm[wave] = m;
+      wl[wave] = l;
+    }
+    wo[wave][2 * lane] = o0;
+    wo[wave][2 * lane + 1] = o1;
+    __syncthreads();
+    if (wave == 0) {
+      float M = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w]);
+      float a0 = 0.f, a1 = 0.f, ls = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const float f = wm[w] == -INFINITY ? 0.f : __expf(wm[w] - M);  // waves with no keys
+        ls = fmaf(wl[w], f, ls);
+        a0 = fmaf(wo[w][2 * lane], f, a0);
+        a1 = fmaf(wo[w][2 * lane + 1], f, a1);
+      }
+      const float inv = 1.f / ls;
+      reinterpret_cast<uint32_t*>(out)[(size_t)bh * (D / 2) + lane] =
+          (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
+    }
+    return;
+  }
+  const uint16_t* kb = kc + head * D + p * 8;
 
   // One step = 16 keys of this wave: lane (kq, p) loads 4 x 16 B of key t0 + kq, and the 16
   // keys' V dim pair `lane`. The first step's K/V loads are issued before q's, so q (fresh from
@@ -874,7 +985,16 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
            v_cache, pos, out, (int)H, (int)Hkv, (int)T, scale);
     return check_launch("attn_dot2_kernel");
   }
-  if (T <= kSingleMaxT && mode == 0) {  // the f32 single-pass kernel
+  // The f32 kernel with whole-line K loads is the default (per graph launch 3.92 / 5.63 / 7.06 /
+  // 10.21 µs at 128 / 328 / 512 / 900 keys vs 4.07 / 5.72 / 7.13 / 10.32 with the half-line
+  // loads of mode 5; e2e within noise: profiles/r3_attn_time_fullk.jsonl, r3_ab_e2e_attn5.jsonl).
+  if (T <= kSingleMaxT && mode == 0) {  // the f32 single-pass kernel, whole-line K loads
+    launch((attn_single_kernel<128, kSingleWaves, true>), dim3((unsigned)(B * H)),
+           dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
+           (int)T, scale);
+    return check_launch("attn_single_kernel<fullk>");
+  }
+  if (T <= kSingleMaxT && mode == 5) {  // the f32 single-pass kernel, 16 keys x 64 B K loads
     launch((attn_single_kernel<128, kSingleWaves>), dim3((unsigned)(B * H)),
            dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
            (int)T, scale);
@@ -914,10 +1034,11 @@ extern "C" int tao_debug_attn_stamps(unsigned long long* out, int n) {
 #endif
 
 int tao_tune_attn(int mode) {
-  TAO_CHECK_ARG(mode >= 0 && mode <= 4,
+  TAO_CHECK_ARG(mode >= 0 && mode <= 5,
                 "tune: attention mode must be 0 (auto: f32 single pass up to 1024 keys, "
                 "else split), 1 (two-launch split), 2 (one launch, 32-key chunks), 3 (one launch, "
-                "64-key chunks) or 4 (packed-bf16 single pass up to 1024 keys, else split)");
+                "64-key chunks), 4 (packed-bf16 single pass up to 1024 keys, else split) or 5 "
+                "(f32 single pass with half-line K loads)");
   tao::tuning().attn_mode = mode;
   return TAO_OK;
 }
