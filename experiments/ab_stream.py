@@ -28,14 +28,17 @@ def main():
         _lib.call("tao_tune_gemm_stream", 1)
         old_us = kernel_us(run, launches)
         ref = run(0).float()
-        _lib.call("tao_tune_gemm_stream", 2)
-        new_us = kernel_us(run, launches)
-        out = run(0).float()
-        rel = float((out - ref).norm() / ref.norm().clamp_min(1e-30))
+        row = {"path": path, "M": M, "N": N, "K": K, "old_us": round(old_us, 2)}
+        for mode, key in ((2, "stream"), (4, "stream_rot_m"), (5, "stream_rot_mn")):
+            _lib.call("tao_tune_gemm_stream", mode)
+            us = kernel_us(run, launches)
+            out = run(0).float()
+            row[f"{key}_us"] = round(us, 2)
+            row[f"{key}_rel_vs_old"] = float((out - ref).norm() / ref.norm().clamp_min(1e-30))
         _lib.call("tao_tune_gemm_stream", 0)
-        print(json.dumps({"path": path, "M": M, "N": N, "K": K, "old_us": round(old_us, 2),
-                          "stream_us": round(new_us, 2), "speedup": round(old_us / new_us, 2),
-                          "rel_vs_old": rel}), flush=True)
+        row["speedup"] = round(old_us / min(row["stream_us"], row["stream_rot_m_us"],
+                                            row["stream_rot_mn_us"]), 2)
+        print(json.dumps(row), flush=True)
 
 
 if __name__ == "__main__":

@@ -139,7 +139,9 @@ int tao_tune_gemm_tile(int mode, int splits);
 /* Tuning hook: the unsplit "stream" prefill GEMM (gemm_stream.hip: 32 x 64 tiles, wave-private
  * LDS-DMA weight streams, x in double-buffered 1-KiB-per-row phases) for the int4 weight-only and
  * int8 dynamic linears. mode 0 = built-in routing (M in [33, 256] with N % 64 == 0 and K a multiple
- * of 512 (int4) / 1024 (int8)), 1 = never, 2 = wherever the shape is supported. Thread-local. */
+ * of 512 (int4) / 1024 (int8)), 1 = never, 2 = wherever the shape is supported, 4 / 5 = as 2 with
+ * each workgroup walking the K phases from a start rotated by its M tile (4) or its M and N
+ * tiles (5). Thread-local. */
 int tao_tune_gemm_stream(int mode);
 /* The k-split prefill GEMM (gemm_ksplit.hip: an unsplit 32 x 64 tile per workgroup whose waves
  * split K, operands loaded straight into MFMA fragments, partials summed through LDS in wave

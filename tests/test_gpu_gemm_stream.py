@@ -161,3 +161,23 @@ def test_stream_unsupported_shapes_fall_back(stream):
     xq, xs = oracle.int8_act_quant(x)
     y = torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), None).cpu()
     assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="cpu"))
+
+
+@pytest.mark.parametrize("mode", [4, 5])
+def test_stream_rotated_phases(stream, mode):
+    """Phases walked from a rotated start per workgroup (tao_tune_gemm_stream 4 / 5): int8 dynamic
+    stays bit-exact (int32 sums), int4 within the oracle bars and run-to-run identical."""
+    stream(mode)
+    M, N, K = 128, 512, 4096
+    w = oracle.make_linear_weight(N, K, seed=21)
+    wq, ws = oracle.int8_dyn_weight(w)
+    x = oracle.make_activation(M, K, seed=22)
+    xq, xs = oracle.int8_act_quant(x)
+    y = torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), None).cpu()
+    assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="cpu"))
+    for g in (32, 128):
+        q, s, z, packed, sz = _int4(N, K, g, seed=g + 5)
+        xd = x.to(DEV)
+        a = torch.ops.torchao.int4_weight_only_linear(xd, packed, sz, g, None)
+        assert torch.equal(torch.ops.torchao.int4_weight_only_linear(xd, packed, sz, g, None), a)
+        assert oracle.rel_l2(a.cpu(), oracle.int4_linear_fp32(x, q, s, z, g)) < TOL_FP32

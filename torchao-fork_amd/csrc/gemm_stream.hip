@@ -270,7 +270,7 @@ template <class P, bool kRowF, bool kColF>
 __global__ __launch_bounds__(256) void gemm_stream_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ rowf,
     const uint16_t* __restrict__ colf, const uint16_t* __restrict__ bias,
-    uint16_t* __restrict__ y, int M, int N, int K) {
+    uint16_t* __restrict__ y, int M, int N, int K, int rotate) {
   typedef typename P::Acc Acc;
   typedef StreamLds<P> L;
   __shared__ __attribute__((aligned(16))) uint8_t lds[L::kTotal];
@@ -284,6 +284,16 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
   const int n_w = n0 + 16 * wave;
   const int nphase = K / P::kPK;
   const int nchunk = nphase * P::kCPP;
+  // rotate 1: the workgroup walks the phases from a start set by its M tile (rotate 2: and its
+  // N tile), so that the workgroups sharing a weight (x) tile do not all miss on the same lines
+  // at once. Only the memory offsets rotate; LDS slots and the k order per phase are unchanged.
+  const int rot = rotate == 0 ? 0
+                  : (int)((blockIdx.y * (unsigned)((nphase + 3) / 4) +
+                           (rotate == 2 ? blockIdx.x : 0u)) % (unsigned)nphase);
+  auto phys_p = [&](int p) __attribute__((always_inline)) {
+    const int q = p + rot;
+    return q >= nphase ? q - nphase : q;
+  };
   constexpr int XB = P::kPK == 1024 ? 1 : 2;  // x bytes per element
   const uint32_t xrow = (uint32_t)K * XB;
 
@@ -322,15 +332,16 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       const int row = wave * kXI + i;
       const int m = m0 + row < M ? m0 + row : M - 1;
       const uint32_t ch = ((uint32_t)lane & ~15u) | (((uint32_t)lane & 15u) ^ pol.x_swz(row & 15));
-      dma<16, false>(xr, (uint32_t)m * xrow + 16u * ch, (uint32_t)p * kPhaseRow,
+      dma<16, false>(xr, (uint32_t)m * xrow + 16u * ch, (uint32_t)phys_p(p) * kPhaseRow,
                      dst + row * kPhaseRow);
     }
     if constexpr (P::kPK != 1024)
-      pol.issue_z(zr, n_w, p, lane, zs0 + ((p & 1) * kNW + wave) * P::kZBuf);
+      pol.issue_z(zr, n_w, phys_p(p), lane, zs0 + ((p & 1) * kNW + wave) * P::kZBuf);
   };
   auto issue_chunk = [&](int c) __attribute__((always_inline)) {
     if (TAO_STREAM_DEBUG == 2 || TAO_STREAM_DEBUG == 4) return;
-    pol.issue_w(wr, n_w, c, lane, ws0 + (wave * P::kD + c % P::kD) * P::kChunk);
+    const int pc = phys_p(c / P::kCPP) * P::kCPP + c % P::kCPP;  // the chunk's memory offset
+    pol.issue_w(wr, n_w, pc, lane, ws0 + (wave * P::kD + c % P::kD) * P::kChunk);
   };
 
   Acc acc[2];
@@ -426,7 +437,7 @@ int stream_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, i
   const dim3 grid((unsigned)(N / kBN), (unsigned)((M + kBM - 1) / kBM));
   launch(gemm_stream_kernel<SInt4, false, false>, grid, dim3(256), 0, stream,
          reinterpret_cast<const uint8_t*>(x), pol, (const uint16_t*)nullptr,
-         (const uint16_t*)nullptr, bias, y, M, N, K);
+         (const uint16_t*)nullptr, bias, y, M, N, K, tuning().gemm_stream_rot);
   return check_launch("gemm_stream_kernel<int4>");
 }
 
@@ -441,14 +452,18 @@ int stream_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const
   pol.K = K;
   const dim3 grid((unsigned)(N / kBN), (unsigned)((M + kBM - 1) / kBM));
   launch(gemm_stream_kernel<SInt8Dyn, true, true>, grid, dim3(256), 0, stream,
-         reinterpret_cast<const uint8_t*>(xq), pol, xs, ws, bias, y, M, N, K);
+         reinterpret_cast<const uint8_t*>(xq), pol, xs, ws, bias, y, M, N, K,
+         tuning().gemm_stream_rot);
   return check_launch("gemm_stream_kernel<int8dyn>");
 }
 
 }  // namespace tao
 
 extern "C" int tao_tune_gemm_stream(int mode) {
-  TAO_CHECK_ARG(mode >= 0 && mode <= 2, "tune: gemm stream mode must be 0 (auto), 1 (off) or 2 (on)");
-  tao::tuning().gemm_stream = mode;
+  TAO_CHECK_ARG(mode >= 0 && mode <= 5 && mode != 3,
+                "tune: gemm stream mode must be 0 (auto), 1 (off), 2 (on), 4 (on, phases rotated by "
+                "M tile) or 5 (on, rotated by M and N tile)");
+  tao::tuning().gemm_stream = mode <= 2 ? mode : 2;
+  tao::tuning().gemm_stream_rot = mode <= 2 ? 0 : mode - 3;
   return TAO_OK;
 }

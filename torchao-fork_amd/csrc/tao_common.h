@@ -68,6 +68,7 @@ struct Tuning {
   int quant_block = 0;                           // per-token int8 quant: 0 wave kernel, 1 block
   int gemm_tile = 0, tile_splits = 0;            // weight-shared tile GEMM: 0 auto, 1 off, 2 on
   int gemm_stream = 0;                           // stream tile GEMM (gemm_stream.hip): 0 auto, 1 off, 2 on
+  int gemm_stream_rot = 0;                       // stream tile GEMM phase rotation: 0, 1 (M tile), 2 (+N)
   int gemm_ksplit = 0, gemm_ksplit_shape = 0;    // k-split tile GEMM: 0 auto, 1 off, 2 on; shape
   int gemm_ksplit_rot = 0;                       // k-split: rotated block order per workgroup
 };
