@@ -339,6 +339,17 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
                          const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
                          int64_t Hkv, int64_t D, int64_t T, float scale, void* stream);
 
+/* tao_attn_decode_bf16 whose launch also streams up to 4 device regions (pf_ptrs[r], pf_bytes[r]
+ * bytes, 16-B aligned) into the MALL with pf_wgs extra workgroups, dropping the data: the
+ * harness passes the next linear's weights (wo), so they come from the Infinity Cache instead
+ * of HBM. The attention result is identical to tao_attn_decode_bf16's. The prefetch rides only
+ * on the single-pass kernel (tao_tune_attn 0, T <= 1024); other modes ignore it. */
+int tao_attn_decode_pf_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                            const int64_t* pos, float* partial, uint16_t* out, int64_t B,
+                            int64_t H, int64_t Hkv, int64_t D, int64_t T, float scale,
+                            const void* const* pf_ptrs, const int64_t* pf_bytes, int n_pf,
+                            int pf_wgs, void* stream);
+
 /* Calling thread's choice of the decode-attention kernel: 0 = single-pass workgroup per query head
  * (f32 math, whole-line K loads) for T <= 1024, else the two-launch split (default); 1 = two-launch
  * split; 2 / 3 = one launch over 32 / 64-key chunks merged by the kv head's last arriving chunk;

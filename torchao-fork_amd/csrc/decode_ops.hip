@@ -265,6 +265,18 @@ constexpr int kSingleMaxT = 1024;
 // two-launch split, 2 / 3 = attn_chunk_fused_kernel with 32 / 64-key chunks
 constexpr int kSingleWaves = TAO_ATTN_WAVES;
 
+// Weight prefetch riding on the attention launch (tao_attn_decode_pf_bf16): workgroups past the
+// B x H attention workgroups stream up to 4 regions (the next linear's weights) with
+// default-policy 16-B loads and drop the data, so the bytes sit in the MALL when that linear
+// runs. One attention workgroup per head leaves most CUs idle for the launch's ~5 µs.
+struct AttnPf {
+  const uint4* p[4];
+  uint32_t n16[4];  // 16-B units per region
+  int n;            // regions
+  int nbh;          // B x H: the attention workgroups; blockIdx.x >= nbh prefetch
+};
+__device__ unsigned g_attn_pf_sink;
+
 // FULLK: each K load instruction covers 8 keys x 128 B (whole cache lines; lane l: key
 // t0 + 8 i + l / 8, dims 64 h + 8 (l % 8) ..) instead of 16 keys x 64 B (half lines: the L2 moves
 // half the bytes per instruction, profiles/r3_probe_l2_pattern.jsonl); 8 lanes per key.
@@ -272,13 +284,34 @@ template <int D, int NW, bool FULLK = false>
 __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
-    int H, int Hkv, int T, float scale) {
+    int H, int Hkv, int T, float scale, AttnPf pf) {
 #if TAO_ATTN_STAMPS
   const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
 #endif
   static_assert(D == 128, "head_dim 128");
   __shared__ float wm[NW], wl[NW];
   __shared__ float wo[NW][D];
+  if (pf.n > 0 && (int)blockIdx.x >= pf.nbh) {  // prefetch role (workgroup-uniform)
+    const uint32_t w = blockIdx.x - pf.nbh, nw = gridDim.x - pf.nbh;
+    constexpr uint32_t kT = NW * 64, kU = 8;  // threads, loads in flight per thread
+    uint32_t acc = 0;
+    for (int r = 0; r < pf.n; ++r) {
+      const uint4* base = pf.p[r];
+      const uint32_t n16 = pf.n16[r];
+      for (uint32_t u0 = w * kT * kU + threadIdx.x; u0 < n16; u0 += nw * kT * kU) {
+        uint4 v[kU];
+#pragma unroll
+        for (uint32_t j = 0; j < kU; ++j) {
+          const uint32_t u = u0 + j * kT;
+          v[j] = base[u < n16 ? u : n16 - 1];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kU; ++j) acc ^= v[j].x ^ v[j].w;
+      }
+    }
+    if (acc == 0x9E3779B9u) g_attn_pf_sink = acc;  // keeps the loads; the value is irrelevant
+    return;
+  }
   const int bh = blockIdx.x;  // b * H + h
   const int b = bh / H, h = bh % H, kvh = h / (H / Hkv);
   const int L = attn_len(pos[0], T);
@@ -943,9 +976,10 @@ int tao_rope_kv_bf16(const uint16_t* qkv, const float* freqs, const int64_t* pos
   return check_launch("rope_kv_kernel");
 }
 
-int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
-                         const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
-                         int64_t Hkv, int64_t D, int64_t T, float scale, void* stream) {
+static int attn_decode(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                       const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
+                       int64_t Hkv, int64_t D, int64_t T, float scale, tao::AttnPf pf,
+                       int pf_wgs, void* stream) {
   TAO_CHECK_ARG(D == 128, "attn_decode: head_dim must be 128 (got %lld)", (long long)D);
   TAO_CHECK_ARG(B > 0 && Hkv > 0 && H % Hkv == 0 && T > 0, "attn_decode: bad sizes");
   const int G = (int)(H / Hkv);
@@ -989,15 +1023,15 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
   // 10.21 µs at 128 / 328 / 512 / 900 keys vs 4.07 / 5.72 / 7.13 / 10.32 with the half-line
   // loads of mode 5; e2e within noise: profiles/r3_attn_time_fullk.jsonl, r3_ab_e2e_attn5.jsonl).
   if (T <= kSingleMaxT && mode == 0) {  // the f32 single-pass kernel, whole-line K loads
-    launch((attn_single_kernel<128, kSingleWaves, true>), dim3((unsigned)(B * H)),
+    launch((attn_single_kernel<128, kSingleWaves, true>), dim3((unsigned)(B * H + pf_wgs)),
            dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
-           (int)T, scale);
+           (int)T, scale, pf);
     return check_launch("attn_single_kernel<fullk>");
   }
   if (T <= kSingleMaxT && mode == 5) {  // the f32 single-pass kernel, 16 keys x 64 B K loads
     launch((attn_single_kernel<128, kSingleWaves>), dim3((unsigned)(B * H)),
            dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
-           (int)T, scale);
+           (int)T, scale, tao::AttnPf{});
     return check_launch("attn_single_kernel");
   }
   const int NC = (int)((T + kChunk - 1) / kChunk);
@@ -1024,6 +1058,37 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
 #undef TAO_ATTN
   }
   return check_launch("attn_decode");
+}
+
+int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                         const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
+                         int64_t Hkv, int64_t D, int64_t T, float scale, void* stream) {
+  return attn_decode(q, k_cache, v_cache, pos, partial, out, B, H, Hkv, D, T, scale,
+                     tao::AttnPf{}, 0, stream);
+}
+
+int tao_attn_decode_pf_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                            const int64_t* pos, float* partial, uint16_t* out, int64_t B,
+                            int64_t H, int64_t Hkv, int64_t D, int64_t T, float scale,
+                            const void* const* pf_ptrs, const int64_t* pf_bytes, int n_pf,
+                            int pf_wgs, void* stream) {
+  TAO_CHECK_ARG(n_pf >= 0 && n_pf <= 4, "attn_decode_pf: 0..4 prefetch regions (got %d)", n_pf);
+  TAO_CHECK_ARG(pf_wgs >= 0 && pf_wgs <= 4096, "attn_decode_pf: 0..4096 prefetch workgroups");
+  tao::AttnPf pf{};
+  int n = 0;
+  for (int r = 0; r < n_pf; ++r) {
+    TAO_CHECK_ARG(pf_bytes[r] >= 0 && pf_bytes[r] < (int64_t(1) << 36),
+                  "attn_decode_pf: region %d size out of range", r);
+    TAO_CHECK_ALIGN(pf_ptrs[r], 16, "prefetch region");
+    if (pf_bytes[r] < 16) continue;
+    pf.p[n] = reinterpret_cast<const uint4*>(pf_ptrs[r]);
+    pf.n16[n] = (uint32_t)(pf_bytes[r] / 16);  // a trailing partial 16 B is left out
+    ++n;
+  }
+  pf.n = pf_wgs > 0 ? n : 0;
+  pf.nbh = (int)(B * H);
+  return attn_decode(q, k_cache, v_cache, pos, partial, out, B, H, Hkv, D, T, scale, pf,
+                     pf.n > 0 ? pf_wgs : 0, stream);
 }
 #if TAO_ATTN_STAMPS
 extern "C" int tao_debug_attn_stamps(unsigned long long* out, int n) {

@@ -238,6 +238,9 @@ def main(argv=None):
                          "of normalising x first (one bf16 rounding fewer; tao_tune_int4_norm 1)")
     ap.add_argument("--head_prologue", action="store_true",
                     help="fuse the final RMSNorm into the output head GEMV (kernels.HEAD_PROLOGUE)")
+    ap.add_argument("--attn_prefetch_wgs", type=int, default=-1,
+                    help="workgroups that stream wo's weights into the MALL beside the decode "
+                         "attention (kernels.ATTN_PREFETCH_WGS; -1 = built-in, 0 = off)")
     ap.add_argument("--attn_mode", type=int, default=-1,
                     help="decode attention kernel (tao_tune_attn; -1 = built-in)")
     ap.add_argument("--device", default="cuda")
@@ -245,10 +248,13 @@ def main(argv=None):
     ap.add_argument("--write_result", type=Path, default=None)
     args = ap.parse_args(argv)
 
-    if args.head_prologue:
+    if args.head_prologue or args.attn_prefetch_wgs >= 0:
         from torchao._models.llama import kernels
 
-        kernels.HEAD_PROLOGUE = True
+        if args.head_prologue:
+            kernels.HEAD_PROLOGUE = True
+        if args.attn_prefetch_wgs >= 0:
+            kernels.ATTN_PREFETCH_WGS = args.attn_prefetch_wgs
     if args.deferred_norm or args.attn_mode >= 0:
         from torchao import _lib
 
