@@ -354,7 +354,8 @@ int tao_attn_decode_pf_bf16(const uint16_t* q, const uint16_t* k_cache, const ui
  * (f32 math, whole-line K loads) for T <= 1024, else the two-launch split (default); 1 = two-launch
  * split; 2 / 3 = one launch over 32 / 64-key chunks merged by the kv head's last arriving chunk;
  * 4 = as 0 with the packed-bf16 single-pass kernel (measured slower); 5 = as 0 with half-line K
- * loads (the round-1 kernel). */
+ * loads (the round-1 kernel); 6 = as 0 with 32 keys per wave step (one load round trip up to 512
+ * keys). */
 int tao_tune_attn(int mode);
 
 /* Device-side faults of the decode kernels since the last call, read and cleared (synchronous:

@@ -81,6 +81,12 @@ def test_graph_decode_matches_eager_gpu(quant):
     # a second run replays the same graph from a fresh prefill
     again, _, _ = generate(model, prompt, T, dec)
     assert torch.equal(again, eager)
+    # several steps per graph launch (4 here: T - 1 = 9 steps = 2 four-step replays + 1 single)
+    dec4 = GraphDecoder(model, 1, P + T, dev, steps_per_graph=4)
+    dec4.reset(prompt, prefill(model, prompt, torch.arange(P, device=dev)))
+    dec4.capture()
+    graphed4, _, _ = generate(model, prompt, T, dec4)
+    assert torch.equal(graphed4, eager)
     # the graph-captured prefill gives the same first token and caches; a second prompt
     # through the same prefill graph matches its eager run too
     pre = GraphPrefill(model, (1, P), dev)
@@ -170,12 +176,13 @@ def test_fused_kernels_match_torch_ops_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("G", [1, 2, 4, 8])
 def test_attn_decode_modes_gpu(mode, G):
     """Every decode-attention kernel (tao_tune_attn: 0 f32 single pass (whole-line K loads) up to
     1024 keys, 1 two-launch split, 2 / 3 one launch over 32 / 64-key chunks merged by the last
-    arriver, 4 packed-bf16 single pass, 5 f32 single pass with half-line K loads) against fp32
+    arriver, 4 packed-bf16 single pass, 5 f32 single pass with half-line K loads, 6 32 keys per
+    wave step) against fp32
     SDPA, GQA groups 1..8, lengths across chunk edges; the one-launch kernels are also
     run-to-run identical (chunks merged in chunk order whatever the arrival order) and leave
     their counters reset (the same workspace serves every call)."""

@@ -280,7 +280,10 @@ __device__ unsigned g_attn_pf_sink;
 // FULLK: each K load instruction covers 8 keys x 128 B (whole cache lines; lane l: key
 // t0 + 8 i + l / 8, dims 64 h + 8 (l % 8) ..) instead of 16 keys x 64 B (half lines: the L2 moves
 // half the bytes per instruction, profiles/r3_probe_l2_pattern.jsonl); 8 lanes per key.
-template <int D, int NW, bool FULLK = false>
+// KEYS32 (with FULLK): each wave takes 32 keys per step, both 16-key sets' loads issued at once,
+// so a cache of <= 512 keys is one load round trip per wave instead of two above 256 keys (no
+// cross-step prefetch: the registers hold one step).
+template <int D, int NW, bool FULLK = false, bool KEYS32 = false>
 __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
@@ -319,6 +322,119 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
   const int kq = lane >> 2, p = lane & 3;
   const size_t head = (size_t)(b * Hkv + kvh) * T;
   const uint32_t* vb = reinterpret_cast<const uint32_t*>(vc + head * D) + lane;
+  if constexpr (FULLK && KEYS32) {
+    const int g = lane >> 3, p8 = lane & 7;
+    const uint16_t* kbase = kc + head * D + p8 * 8;
+    uint4 ka[2][2], kb2[2][2];
+    uint32_t vv[2][16];
+    auto load_step = [&](int t0) __attribute__((always_inline)) {
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const int t1 = t0 + 16 * st;
+        const int ta = t1 + g < L ? t1 + g : L - 1, tb = t1 + 8 + g < L ? t1 + 8 + g : L - 1;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          ka[st][h] = *reinterpret_cast<const uint4*>(kbase + (size_t)ta * D + 64 * h);
+          kb2[st][h] = *reinterpret_cast<const uint4*>(kbase + (size_t)tb * D + 64 * h);
+        }
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int tj = t0 + 16 * st + j < L ? t0 + 16 * st + j : L - 1;
+          vv[st][j] = vb[(size_t)tj * (D / 2)];
+        }
+    };
+    const int first = wave * 32;
+    if (first < L) load_step(first);
+    float qr[16];
+    {
+      const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bh * D + p8 * 8);
+      uint4 qv[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) qv[h] = qp[h * 8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t w[4] = {qv[h].x, qv[h].y, qv[h].z, qv[h].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          qr[h * 8 + 2 * e] = bf16lo_to_f32(w[e]);
+          qr[h * 8 + 2 * e + 1] = bf16hi_to_f32(w[e]);
+        }
+      }
+    }
+    float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
+    for (int t0 = first; t0 < L; t0 += NW * 32) {
+      if (t0 != first) load_step(t0);
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const int t1 = t0 + 16 * st;
+        if (t1 >= L) break;  // wave-uniform
+        float sa = 0.f, sb = 0.f;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t wa[4] = {ka[st][h].x, ka[st][h].y, ka[st][h].z, ka[st][h].w};
+          const uint32_t wb[4] = {kb2[st][h].x, kb2[st][h].y, kb2[st][h].z, kb2[st][h].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            sa = fmaf(qr[h * 8 + 2 * e], bf16lo_to_f32(wa[e]),
+                      fmaf(qr[h * 8 + 2 * e + 1], bf16hi_to_f32(wa[e]), sa));
+            sb = fmaf(qr[h * 8 + 2 * e], bf16lo_to_f32(wb[e]),
+                      fmaf(qr[h * 8 + 2 * e + 1], bf16hi_to_f32(wb[e]), sb));
+          }
+        }
+        sa = wave_bfly<1, 8>(sa, lane_id(), [](float a, float c) { return a + c; });
+        sb = wave_bfly<1, 8>(sb, lane_id(), [](float a, float c) { return a + c; });
+        const bool va = t1 + g < L, vbk = t1 + 8 + g < L;
+        sa = va ? sa * scale : -INFINITY;
+        sb = vbk ? sb * scale : -INFINITY;
+        float mx = fmaxf(sa, sb);
+        mx = wave_bfly<8, 64>(mx, lane_id(), [](float a, float c) { return fmaxf(a, c); });
+        const float mn = fmaxf(m, mx);  // finite: key t1 < L is valid
+        const float corr = __expf(m - mn);
+        const float ea = va ? __expf(sa - mn) : 0.f, eb = vbk ? __expf(sb - mn) : 0.f;
+        float es = ea + eb;
+        es = wave_bfly<8, 64>(es, lane_id(), [](float a, float c) { return a + c; });
+        l = fmaf(l, corr, es);
+        o0 *= corr;
+        o1 *= corr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float pa = __shfl(ea, 8 * j, 64), pb = __shfl(eb, 8 * j, 64);
+          o0 = fmaf(pa, bf16lo_to_f32(vv[st][j]), o0);
+          o1 = fmaf(pa, bf16hi_to_f32(vv[st][j]), o1);
+          o0 = fmaf(pb, bf16lo_to_f32(vv[st][j + 8]), o0);
+          o1 = fmaf(pb, bf16hi_to_f32(vv[st][j + 8]), o1);
+        }
+        m = mn;
+      }
+    }
+    if (lane == 0) {
+      wm[wave] = m;
+      wl[wave] = l;
+    }
+    wo[wave][2 * lane] = o0;
+    wo[wave][2 * lane + 1] = o1;
+    __syncthreads();
+    if (wave == 0) {
+      float M = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w]);
+      float a0 = 0.f, a1 = 0.f, ls = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const float f = wm[w] == -INFINITY ? 0.f : __expf(wm[w] - M);  // waves with no keys
+        ls = fmaf(wl[w], f, ls);
+        a0 = fmaf(wo[w][2 * lane], f, a0);
+        a1 = fmaf(wo[w][2 * lane + 1], f, a1);
+      }
+      const float inv = 1.f / ls;
+      reinterpret_cast<uint32_t*>(out)[(size_t)bh * (D / 2) + lane] =
+          (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
+    }
+    return;
+  }
   if constexpr (FULLK) {
     // lane (g = l / 8, p8 = l % 8): keys t0 + g and t0 + 8 + g, dims 64 h + 8 p8 + e (h < 2, e < 8)
     const int g = lane >> 3, p8 = lane & 7;
@@ -1028,6 +1144,12 @@ static int attn_decode(const uint16_t* q, const uint16_t* k_cache, const uint16_
            (int)T, scale, pf);
     return check_launch("attn_single_kernel<fullk>");
   }
+  if (T <= kSingleMaxT && mode == 6) {  // whole-line K loads, 32 keys per wave step
+    launch((attn_single_kernel<128, kSingleWaves, true, true>), dim3((unsigned)(B * H + pf_wgs)),
+           dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
+           (int)T, scale, pf);
+    return check_launch("attn_single_kernel<fullk, keys32>");
+  }
   if (T <= kSingleMaxT && mode == 5) {  // the f32 single-pass kernel, 16 keys x 64 B K loads
     launch((attn_single_kernel<128, kSingleWaves>), dim3((unsigned)(B * H)),
            dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
@@ -1099,11 +1221,11 @@ extern "C" int tao_debug_attn_stamps(unsigned long long* out, int n) {
 #endif
 
 int tao_tune_attn(int mode) {
-  TAO_CHECK_ARG(mode >= 0 && mode <= 5,
+  TAO_CHECK_ARG(mode >= 0 && mode <= 6,
                 "tune: attention mode must be 0 (auto: f32 single pass up to 1024 keys, "
                 "else split), 1 (two-launch split), 2 (one launch, 32-key chunks), 3 (one launch, "
-                "64-key chunks), 4 (packed-bf16 single pass up to 1024 keys, else split) or 5 "
-                "(f32 single pass with half-line K loads)");
+                "64-key chunks), 4 (packed-bf16 single pass up to 1024 keys, else split), 5 "
+                "(f32 single pass with half-line K loads) or 6 (32 keys per wave step)");
   tao::tuning().attn_mode = mode;
   return TAO_OK;
 }

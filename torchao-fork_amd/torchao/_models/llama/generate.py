@@ -100,13 +100,18 @@ class GraphDecoder:
     place) and ``tokens`` [B, max_len] (each produced token stored at its position), so a
     replay is the whole per-token work with no host involvement."""
 
-    def __init__(self, model: Transformer, batch: int, max_len: int, device):
+    def __init__(self, model: Transformer, batch: int, max_len: int, device,
+                 steps_per_graph: int = 1):
         self.model = model
         self.cur = torch.zeros(batch, 1, dtype=torch.int64, device=device)
         self.pos = torch.zeros(1, dtype=torch.int64, device=device)
         self.tokens = torch.zeros(batch, max_len, dtype=torch.int64, device=device)
         self.stream = torch.cuda.Stream(device)
         self.graph = None
+        # steps_per_graph > 1: a second graph holds that many steps back to back (the step is
+        # device-driven, so k steps replay as one graph launch: one launch overhead per k tokens)
+        self.steps_per_graph = max(1, int(steps_per_graph))
+        self.graph_k = None
 
     @torch.no_grad()
     def _step(self):
@@ -129,6 +134,11 @@ class GraphDecoder:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph, stream=self.stream):
                 self._step()
+            if self.steps_per_graph > 1:
+                self.graph_k = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph_k, stream=self.stream):
+                    for _ in range(self.steps_per_graph):
+                        self._step()
         torch.cuda.current_stream().wait_stream(self.stream)
         self.cur.copy_(saved[0])
         self.pos.copy_(saved[1])
@@ -143,6 +153,14 @@ class GraphDecoder:
 
     def step(self):
         self.graph.replay()
+
+    def run(self, n: int):
+        """n decode steps: the k-step graph n // k times, then single steps."""
+        k = self.steps_per_graph if self.graph_k is not None else 1
+        for _ in range(n // k if k > 1 else 0):
+            self.graph_k.replay()
+        for _ in range(n % k if k > 1 else n):
+            self.graph.replay()
 
 
 class GraphPrefill:
@@ -192,8 +210,7 @@ def generate(model: Transformer, prompt: torch.Tensor, max_new_tokens: int,
     t1 = time.perf_counter()
     if decoder is not None:
         decoder.reset(prompt, tok)
-        for _ in range(1, max_new_tokens):
-            decoder.step()
+        decoder.run(max_new_tokens - 1)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         _check_status(model)
@@ -241,6 +258,8 @@ def main(argv=None):
     ap.add_argument("--attn_prefetch_wgs", type=int, default=-1,
                     help="workgroups that stream wo's weights into the MALL beside the decode "
                          "attention (kernels.ATTN_PREFETCH_WGS; -1 = built-in, 0 = off)")
+    ap.add_argument("--steps_per_graph", type=int, default=1,
+                    help="decode steps captured back to back in one HIP graph (1 = one per token)")
     ap.add_argument("--attn_mode", type=int, default=-1,
                     help="decode attention kernel (tao_tune_attn; -1 = built-in)")
     ap.add_argument("--device", default="cuda")
@@ -285,7 +304,7 @@ def main(argv=None):
 
     decoder = prefiller = None
     if not args.no_graph:
-        decoder = GraphDecoder(model, B, P + T, device)
+        decoder = GraphDecoder(model, B, P + T, device, steps_per_graph=args.steps_per_graph)
         # capture after an eager prefill so every kernel and workspace has been set up
         decoder.reset(prompt, prefill(model, prompt, torch.arange(P, device=device)))
         decoder.capture()
