@@ -258,8 +258,10 @@ def main(argv=None):
     ap.add_argument("--attn_prefetch_wgs", type=int, default=-1,
                     help="workgroups that stream wo's weights into the MALL beside the decode "
                          "attention (kernels.ATTN_PREFETCH_WGS; -1 = built-in, 0 = off)")
-    ap.add_argument("--steps_per_graph", type=int, default=1,
-                    help="decode steps captured back to back in one HIP graph (1 = one per token)")
+    ap.add_argument("--steps_per_graph", type=int, default=32,
+                    help="decode steps captured back to back in one HIP graph launch (1 = one "
+                         "per token; 32: 717.6 vs 710.1 tokens/s, "
+                         "profiles/r3_ab_e2e_steps_per_graph.jsonl)")
     ap.add_argument("--attn_mode", type=int, default=-1,
                     help="decode attention kernel (tao_tune_attn; -1 = built-in)")
     ap.add_argument("--device", default="cuda")
