@@ -339,6 +339,15 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
                          const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
                          int64_t Hkv, int64_t D, int64_t T, float scale, void* stream);
 
+/* Prefill attention: S queries per (batch, head), q [B][H][S][D] bf16 (RoPE applied), query s at
+ * position pos[s] attending cache keys 0..pos[s] (the causal mask of a prompt written into the
+ * caches at pos), GQA (H % Hkv == 0), D == 128: out [B][S][H*D] bf16, fp32 softmax. Replaces the
+ * masked F.scaled_dot_product_attention over the caches of the reference's Attention.forward
+ * (gpt-fast model.py) at prefill. */
+int tao_attn_prefill_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                          const int64_t* pos, uint16_t* out, int64_t B, int64_t H, int64_t Hkv,
+                          int64_t D, int64_t S, int64_t T, float scale, void* stream);
+
 /* tao_attn_decode_bf16 whose launch also streams up to 4 device regions (pf_ptrs[r], pf_bytes[r]
  * bytes, 16-B aligned) into the MALL with pf_wgs extra workgroups, dropping the data: the
  * harness passes the next linear's weights (wo), so they come from the Infinity Cache instead

@@ -381,3 +381,32 @@ def test_attn_decode_weight_prefetch_gpu():
             kernels.attn_decode(q, kc, vc, pos, 1.0, prefetch=regions + regions[:2])
     finally:
         kernels.ATTN_PREFETCH_WGS = old
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [1, 4, 8])
+@pytest.mark.parametrize("S,p0,T", [(1, 0, 64), (7, 0, 64), (128, 0, 328), (33, 37, 128),
+                                    (200, 50, 1024)])
+def test_attn_prefill_gpu(G, S, p0, T):
+    """tao_attn_prefill_bf16: S queries at positions p0 .. p0 + S - 1 against the cache keys
+    0..pos (the causal mask of gpt-fast's prefill over the caches), GQA, vs fp32 SDPA with that
+    mask; output [B, S, H * D]."""
+    import torch.nn.functional as F
+
+    from torchao._models.llama import kernels
+
+    dev = torch.device("cuda")
+    B, Hkv, D = 2, 2 if G == 8 else 8 // G, 128
+    H = Hkv * G
+    g = torch.Generator(device=dev).manual_seed(S + p0 + G)
+    kc = torch.randn(B, Hkv, T, D, device=dev, dtype=torch.bfloat16, generator=g)
+    vc = torch.randn(B, Hkv, T, D, device=dev, dtype=torch.bfloat16, generator=g)
+    q = torch.randn(B, H, S, D, device=dev, dtype=torch.bfloat16, generator=g)
+    pos = torch.arange(p0, p0 + S, device=dev)
+    got = kernels.attn_prefill(q, kc, vc, pos, 1 / math.sqrt(D))
+    mask = torch.arange(T, device=dev)[None, :] <= pos[:, None]  # [S, T]
+    ref = F.scaled_dot_product_attention(q.float(), kc.float(), vc.float(), attn_mask=mask,
+                                         enable_gqa=True)
+    ref = ref.transpose(1, 2).reshape(B, S, H * D)
+    torch.testing.assert_close(got.float(), ref, rtol=2e-2, atol=2e-2)
+    assert torch.equal(kernels.attn_prefill(q, kc, vc, pos, 1 / math.sqrt(D)), got)

@@ -287,7 +287,7 @@ template <int D, int NW, bool FULLK = false, bool KEYS32 = false>
 __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
-    int H, int Hkv, int T, float scale, AttnPf pf) {
+    int H, int Hkv, int T, float scale, int S, AttnPf pf) {
 #if TAO_ATTN_STAMPS
   const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -315,9 +315,13 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     if (acc == 0x9E3779B9u) g_attn_pf_sink = acc;  // keeps the loads; the value is irrelevant
     return;
   }
-  const int bh = blockIdx.x;  // b * H + h
+  // S queries per (batch, head) (prefill; decode S = 1): q [B][H][S][D], query s at position
+  // pos[s] attends keys 0..pos[s]; out [B][S][H * D]
+  const int bhs = blockIdx.x;  // (b * H + h) * S + s
+  const int bh = bhs / S, s_q = bhs % S;
   const int b = bh / H, h = bh % H, kvh = h / (H / Hkv);
-  const int L = attn_len(pos[0], T);
+  const int L = attn_len(pos[s_q], T);
+  const size_t ooff = ((size_t)(b * S + s_q) * H + h) * (D / 2);  // output dword offset
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int kq = lane >> 2, p = lane & 3;
   const size_t head = (size_t)(b * Hkv + kvh) * T;
@@ -350,7 +354,7 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     if (first < L) load_step(first);
     float qr[16];
     {
-      const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bh * D + p8 * 8);
+      const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bhs * D + p8 * 8);
       uint4 qv[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) qv[h] = qp[h * 8];
@@ -430,7 +434,7 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
         a1 = fmaf(wo[w][2 * lane + 1], f, a1);
       }
       const float inv = 1.f / ls;
-      reinterpret_cast<uint32_t*>(out)[(size_t)bh * (D / 2) + lane] =
+      reinterpret_cast<uint32_t*>(out)[ooff + lane] =
           (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
     }
     return;
@@ -457,7 +461,7 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     load_step(wave * 16);
     float qr[16];
     {
-      const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bh * D + p8 * 8);
+      const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bhs * D + p8 * 8);
       uint4 qv[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) qv[h] = qp[h * 8];
@@ -538,7 +542,7 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
         a1 = fmaf(wo[w][2 * lane + 1], f, a1);
       }
       const float inv = 1.f / ls;
-      reinterpret_cast<uint32_t*>(out)[(size_t)bh * (D / 2) + lane] =
+      reinterpret_cast<uint32_t*>(out)[ooff + lane] =
           (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
     }
     return;
@@ -566,7 +570,7 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
   // lane p holds q dims v*32 + 8p + e (e < 8) in registers: 4 x 16 B straight from global
   float qr[32];
   {
-    const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bh * D + p * 8);
+    const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bhs * D + p * 8);
     uint4 qv[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) qv[v] = qp[v * 4];
@@ -650,7 +654,7 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
       a1 = fmaf(wo[w][2 * lane + 1], f, a1);
     }
     const float inv = 1.f / ls;
-    reinterpret_cast<uint32_t*>(out)[(size_t)bh * (D / 2) + lane] =
+    reinterpret_cast<uint32_t*>(out)[ooff + lane] =
         (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
 #if TAO_ATTN_STAMPS
     const unsigned long long st3 = __builtin_amdgcn_s_memrealtime();
@@ -1141,19 +1145,19 @@ static int attn_decode(const uint16_t* q, const uint16_t* k_cache, const uint16_
   if (T <= kSingleMaxT && mode == 0) {  // the f32 single-pass kernel, whole-line K loads
     launch((attn_single_kernel<128, kSingleWaves, true>), dim3((unsigned)(B * H + pf_wgs)),
            dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
-           (int)T, scale, pf);
+           (int)T, scale, 1, pf);
     return check_launch("attn_single_kernel<fullk>");
   }
   if (T <= kSingleMaxT && mode == 6) {  // whole-line K loads, 32 keys per wave step
     launch((attn_single_kernel<128, kSingleWaves, true, true>), dim3((unsigned)(B * H + pf_wgs)),
            dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
-           (int)T, scale, pf);
+           (int)T, scale, 1, pf);
     return check_launch("attn_single_kernel<fullk, keys32>");
   }
   if (T <= kSingleMaxT && mode == 5) {  // the f32 single-pass kernel, 16 keys x 64 B K loads
     launch((attn_single_kernel<128, kSingleWaves>), dim3((unsigned)(B * H)),
            dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
-           (int)T, scale, tao::AttnPf{});
+           (int)T, scale, 1, tao::AttnPf{});
     return check_launch("attn_single_kernel");
   }
   const int NC = (int)((T + kChunk - 1) / kChunk);
@@ -1180,6 +1184,23 @@ static int attn_decode(const uint16_t* q, const uint16_t* k_cache, const uint16_
 #undef TAO_ATTN
   }
   return check_launch("attn_decode");
+}
+
+int tao_attn_prefill_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                          const int64_t* pos, uint16_t* out, int64_t B, int64_t H, int64_t Hkv,
+                          int64_t D, int64_t S, int64_t T, float scale, void* stream) {
+  TAO_CHECK_ARG(D == 128, "attn_prefill: head_dim must be 128 (got %lld)", (long long)D);
+  TAO_CHECK_ARG(B > 0 && Hkv > 0 && H % Hkv == 0 && T > 0 && S > 0 && B * H * S < (1LL << 31),
+                "attn_prefill: bad sizes");
+  TAO_CHECK_ALIGN(q, 16, "q");
+  TAO_CHECK_ALIGN(k_cache, 16, "k_cache");
+  TAO_CHECK_ALIGN(out, 4, "out");
+  // one workgroup of 8 waves per (batch, head, query): 128 keys per round, the causal prefix of
+  // a 128-token prompt in one load round trip
+  launch((tao::attn_single_kernel<128, 8, true>), dim3((unsigned)(B * H * S)), dim3(64 * 8), 0,
+         as_stream(stream), q, k_cache, v_cache, pos, out, (int)H, (int)Hkv, (int)T, scale, (int)S,
+         tao::AttnPf{});
+  return check_launch("attn_single_kernel<prefill>");
 }
 
 int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,

@@ -253,6 +253,9 @@ def main(argv=None):
     ap.add_argument("--deferred_norm", action="store_true",
                     help="fused RMSNorm scales the GEMV outputs by rsqrt(mean(x^2)+eps) instead "
                          "of normalising x first (one bf16 rounding fewer; tao_tune_int4_norm 1)")
+    ap.add_argument("--sdpa_prefill", action="store_true",
+                    help="prefill attention through torch's masked SDPA instead of "
+                         "tao_attn_prefill_bf16 (kernels.PREFILL_ATTN)")
     ap.add_argument("--head_prologue", action="store_true",
                     help="fuse the final RMSNorm into the output head GEMV (kernels.HEAD_PROLOGUE)")
     ap.add_argument("--attn_prefetch_wgs", type=int, default=-1,
@@ -269,9 +272,11 @@ def main(argv=None):
     ap.add_argument("--write_result", type=Path, default=None)
     args = ap.parse_args(argv)
 
-    if args.head_prologue or args.attn_prefetch_wgs >= 0:
+    if args.head_prologue or args.attn_prefetch_wgs >= 0 or args.sdpa_prefill:
         from torchao._models.llama import kernels
 
+        if args.sdpa_prefill:
+            kernels.PREFILL_ATTN = False
         if args.head_prologue:
             kernels.HEAD_PROLOGUE = True
         if args.attn_prefetch_wgs >= 0:

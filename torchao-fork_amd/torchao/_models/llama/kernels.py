@@ -85,6 +85,22 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     return out
 
 
+def attn_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                 pos: torch.Tensor, scale: float) -> torch.Tensor:
+    """q [B, H, S, D] (query s at position pos[s]) against cache keys 0..pos[s] -> [B, S, H * D]
+    bf16 (tao_attn_prefill_bf16): the causal-masked SDPA of a prompt over the caches."""
+    _check(q, torch.bfloat16, "attn_prefill q")
+    _check(pos, torch.int64, "attn_prefill pos")
+    B, H, S, D = q.shape
+    _, Hkv, T, _ = k_cache.shape
+    if pos.numel() != S:
+        raise RuntimeError(f"attn_prefill: {pos.numel()} positions for {S} queries")
+    out = torch.empty(B, S, H * D, dtype=q.dtype, device=q.device)
+    _lib.call("tao_attn_prefill_bf16", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+              pos.data_ptr(), out.data_ptr(), B, H, Hkv, D, S, T, float(scale), _stream(q))
+    return out
+
+
 def silu_mul(a: torch.Tensor, b=None) -> torch.Tensor:
     """bf16(bf16(silu(a)) * b); with b None, ``a`` [..., 2n] holds interleaved (gate, up) pairs
     (an interleaved w13 output) and the result is [..., n]."""
@@ -102,6 +118,9 @@ def silu_mul(a: torch.Tensor, b=None) -> torch.Tensor:
 
 _EPILOGUES = {"none": 0, "swiglu": 1, "rope_kv": 2}
 
+
+# Prefill attention on tao_attn_prefill_bf16 (False: torch's masked SDPA over the caches).
+PREFILL_ATTN = True
 
 # Output heads (N >= HEAD_ROWS) normalise in their own RMSNorm launch unless HEAD_PROLOGUE.
 HEAD_ROWS = 65536

@@ -291,6 +291,11 @@ class Attention(nn.Module):
         kv = self.kv_cache
         q = kernels.rope_kv(self.wqkv(x), freqs_table, input_pos, kv.k_cache, kv.v_cache,
                             self.n_head)
+        if kernels.PREFILL_ATTN and self.head_dim == 128 and q.dtype == torch.bfloat16:
+            # the causal mask over the caches is keys 0..input_pos[s] for query s
+            y = kernels.attn_prefill(q, kv.k_cache, kv.v_cache, input_pos,
+                                     1.0 / math.sqrt(self.head_dim))
+            return self.wo(y)
         y = F.scaled_dot_product_attention(q, kv.k_cache, kv.v_cache, attn_mask=mask,
                                            enable_gqa=True)
         return self.wo(y.transpose(1, 2).reshape(B, S, self.n_head * self.head_dim))
