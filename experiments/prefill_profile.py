@@ -11,6 +11,12 @@ from torchao._models.llama.generate import apply_quantization, build_model, pref
 
 
 def main():
+    import sys
+
+    from torchao._models.llama import kernels
+
+    if "--native" in sys.argv:
+        kernels.PREFILL_ATTN = True
     dev = torch.device("cuda")
     model = build_model("Llama-3-8B", dev, seed=0)
     apply_quantization(model, "int4wo-32")

@@ -255,7 +255,9 @@ def main(argv=None):
                          "of normalising x first (one bf16 rounding fewer; tao_tune_int4_norm 1)")
     ap.add_argument("--sdpa_prefill", action="store_true",
                     help="prefill attention through torch's masked SDPA instead of "
-                         "tao_attn_prefill_bf16 (kernels.PREFILL_ATTN)")
+                         "tao_attn_prefill_bf16 (kernels.PREFILL_ATTN = False)")
+    ap.add_argument("--native_prefill_attn", action="store_true",
+                    help="prefill attention on tao_attn_prefill_bf16 (kernels.PREFILL_ATTN = True)")
     ap.add_argument("--head_prologue", action="store_true",
                     help="fuse the final RMSNorm into the output head GEMV (kernels.HEAD_PROLOGUE)")
     ap.add_argument("--attn_prefetch_wgs", type=int, default=-1,
@@ -272,11 +274,14 @@ def main(argv=None):
     ap.add_argument("--write_result", type=Path, default=None)
     args = ap.parse_args(argv)
 
-    if args.head_prologue or args.attn_prefetch_wgs >= 0 or args.sdpa_prefill:
+    if (args.head_prologue or args.attn_prefetch_wgs >= 0 or args.sdpa_prefill
+            or args.native_prefill_attn):
         from torchao._models.llama import kernels
 
         if args.sdpa_prefill:
             kernels.PREFILL_ATTN = False
+        if args.native_prefill_attn:
+            kernels.PREFILL_ATTN = True
         if args.head_prologue:
             kernels.HEAD_PROLOGUE = True
         if args.attn_prefetch_wgs >= 0:
