@@ -120,7 +120,7 @@ _EPILOGUES = {"none": 0, "swiglu": 1, "rope_kv": 2}
 
 
 # Prefill attention on tao_attn_prefill_bf16 (False: torch's masked SDPA over the caches).
-PREFILL_ATTN = False  # routed once GPU-validated
+PREFILL_ATTN = True
 
 # Output heads (N >= HEAD_ROWS) normalise in their own RMSNorm launch unless HEAD_PROLOGUE.
 HEAD_ROWS = 65536
