@@ -321,6 +321,12 @@ int tao_tune_int8_quant(int block);
 int tao_rmsnorm_bf16(const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t rows,
                      int64_t dim, float eps, void* stream);
 
+/* h = x + res (bf16, rounded as torch's bf16 add), stored, then y = RMSNorm(h) as
+ * tao_rmsnorm_bf16: the residual add and the next norm of a prefill block in one launch,
+ * bit-identical to the two. rows x dim, dim % 8 == 0. */
+int tao_add_rmsnorm_bf16(const uint16_t* x, const uint16_t* res, const uint16_t* w, uint16_t* h,
+                         uint16_t* y, int64_t rows, int64_t dim, float eps, void* stream);
+
 /* qkv [B*S][(H + 2 Hkv) * D] bf16 -> q_out [B][H][S][D] rotated; k (rotated) and v written to
  * k_cache / v_cache [B][Hkv][T][D] at positions pos[S] (int64). freqs: rotary table
  * [rows][D/2][2] fp32 (cos, sin), row pos[s]. Replaces apply_rotary_emb + KVCache.update

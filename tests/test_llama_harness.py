@@ -410,3 +410,36 @@ def test_attn_prefill_gpu(G, S, p0, T):
     ref = ref.transpose(1, 2).reshape(B, S, H * D)
     torch.testing.assert_close(got.float(), ref, rtol=2e-2, atol=2e-2)
     assert torch.equal(kernels.attn_prefill(q, kc, vc, pos, 1 / math.sqrt(D)), got)
+
+
+@pytest.mark.gpu
+def test_add_rmsnorm_and_fused_prefill_gpu():
+    """tao_add_rmsnorm_bf16 is bit-identical to (x + r, rmsnorm(x + r)); the prefill with the
+    residual adds fused into the norms gives logits bit-identical to the unfused prefill."""
+    from torchao._models.llama import kernels
+    from torchao._models.llama.generate import apply_quantization
+
+    dev = torch.device("cuda")
+    for rows, D in ((1, 4096), (128, 4096), (7, 1024)):
+        g = torch.Generator(device=dev).manual_seed(rows)
+        x = torch.randn(rows, D, device=dev, generator=g).to(torch.bfloat16)
+        r = torch.randn(rows, D, device=dev, generator=g).to(torch.bfloat16)
+        w = (torch.rand(D, device=dev, generator=g) + 0.5).to(torch.bfloat16)
+        h, y = kernels.add_rmsnorm(x, r, w, 1e-5)
+        assert torch.equal(h, x + r)
+        assert torch.equal(y, kernels.rmsnorm(x + r, w, 1e-5))
+    model = _tiny(dev)
+    apply_quantization(model, "int4wo-32")
+    model.setup_caches(1, 48)
+    model.enable_fused_kernels()
+    prompt = torch.randint(0, model.config.vocab_size, (1, 24), device=dev)
+    old = kernels.PREFILL_ADD_NORM
+    try:
+        outs = []
+        for flag in (False, True):
+            kernels.PREFILL_ADD_NORM = flag
+            with torch.no_grad():
+                outs.append(model._layers_prefill(prompt, torch.arange(24, device=dev)))
+        assert torch.equal(outs[0], outs[1])
+    finally:
+        kernels.PREFILL_ADD_NORM = old

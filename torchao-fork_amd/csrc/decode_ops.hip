@@ -87,6 +87,57 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const uint16_t* __restrict
   }
 }
 
+// ---- residual add + RMSNorm (prefill): h = bf16(x + r) stored, then y = RMSNorm(h) -----------
+// The add rounds as torch's bf16 `x + r` does (fp32 sum, RNE), the norm as rmsnorm_kernel, so the
+// pair is bit-identical to the two launches it replaces. One workgroup per row.
+__device__ __forceinline__ uint32_t add_pair_bf16(uint32_t a, uint32_t b) {
+  const float lo = bf16lo_to_f32(a) + bf16lo_to_f32(b);
+  const float hi = bf16hi_to_f32(a) + bf16hi_to_f32(b);
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+
+__global__ __launch_bounds__(256) void add_rmsnorm_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+    const uint16_t* __restrict__ w, uint16_t* __restrict__ h, uint16_t* __restrict__ y, int D,
+    float eps) {
+  __shared__ float red[4];
+  const size_t row = (size_t)blockIdx.x * D;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + row);
+  const uint4* rr = reinterpret_cast<const uint4*>(res + row);
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
+  uint4* hr = reinterpret_cast<uint4*>(h + row);
+  uint4* yr = reinterpret_cast<uint4*>(y + row);
+  const int nv = D / 8;
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < nv; i += 256) {
+    const uint4 a = xr[i], b = rr[i];
+    const uint4 v = make_uint4(add_pair_bf16(a.x, b.x), add_pair_bf16(a.y, b.y),
+                               add_pair_bf16(a.z, b.z), add_pair_bf16(a.w, b.w));
+    hr[i] = v;
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float lo = bf16lo_to_f32(d[j]), hi = bf16hi_to_f32(d[j]);
+      ss = fmaf(lo, lo, fmaf(hi, hi, ss));
+    }
+  }
+  const float r = rsqrtf(block_sum(ss, red) / (float)D + eps);
+  for (int i = threadIdx.x; i < nv; i += 256) {
+    const uint4 a = xr[i], b = rr[i], g = wr[i];
+    const uint32_t d[4] = {add_pair_bf16(a.x, b.x), add_pair_bf16(a.y, b.y),
+                           add_pair_bf16(a.z, b.z), add_pair_bf16(a.w, b.w)};
+    const uint32_t e[4] = {g.x, g.y, g.z, g.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float lo = round_bf16(bf16lo_to_f32(d[j]) * r) * bf16lo_to_f32(e[j]);
+      const float hi = round_bf16(bf16hi_to_f32(d[j]) * r) * bf16hi_to_f32(e[j]);
+      o[j] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+    }
+    yr[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // ---- RoPE on q, k + KV-cache write: one workgroup per token, one thread per pair -------------
 __global__ __launch_bounds__(256) void rope_kv_kernel(
     const uint16_t* __restrict__ qkv, const float* __restrict__ freqs,
@@ -1083,6 +1134,21 @@ int tao_rmsnorm_bf16(const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t 
   launch(rmsnorm_kernel, dim3((unsigned)rows), dim3(256), 0, as_stream(stream), x, w, y,
          (int)dim, eps);
   return check_launch("rmsnorm_kernel");
+}
+
+int tao_add_rmsnorm_bf16(const uint16_t* x, const uint16_t* res, const uint16_t* w, uint16_t* h,
+                         uint16_t* y, int64_t rows, int64_t dim, float eps, void* stream) {
+  TAO_CHECK_ARG(rows >= 0 && dim > 0 && dim % 8 == 0 && dim < (1 << 24),
+                "add_rmsnorm: dim (%lld) must be a positive multiple of 8", (long long)dim);
+  if (rows == 0) return TAO_OK;
+  TAO_CHECK_ALIGN(x, 16, "x");
+  TAO_CHECK_ALIGN(res, 16, "res");
+  TAO_CHECK_ALIGN(w, 16, "w");
+  TAO_CHECK_ALIGN(h, 16, "h");
+  TAO_CHECK_ALIGN(y, 16, "y");
+  launch(add_rmsnorm_kernel, dim3((unsigned)rows), dim3(256), 0, as_stream(stream), x, res, w, h,
+         y, (int)dim, eps);
+  return check_launch("add_rmsnorm_kernel");
 }
 
 int tao_rope_kv_bf16(const uint16_t* qkv, const float* freqs, const int64_t* pos,

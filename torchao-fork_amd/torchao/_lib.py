@@ -70,6 +70,7 @@ _SIGNATURES = {
     "tao_tune_int8_gemv": [_int, _int, _int],
     "tao_tune_int8_quant": [_int],
     "tao_rmsnorm_bf16": [_p, _p, _p, _i64, _i64, ctypes.c_float, _p],
+    "tao_add_rmsnorm_bf16": [_p, _p, _p, _p, _p, _i64, _i64, ctypes.c_float, _p],
     "tao_rope_kv_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p],
     "tao_attn_decode_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
                              ctypes.c_float, _p],

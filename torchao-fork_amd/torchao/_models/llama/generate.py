@@ -256,6 +256,9 @@ def main(argv=None):
     ap.add_argument("--sdpa_prefill", action="store_true",
                     help="prefill attention through torch's masked SDPA instead of "
                          "tao_attn_prefill_bf16 (kernels.PREFILL_ATTN = False)")
+    ap.add_argument("--prefill_add_norm", type=int, default=-1,
+                    help="1 / 0: fuse the prefill residual adds with the next RMSNorm or not "
+                         "(kernels.PREFILL_ADD_NORM; -1 = built-in)")
     ap.add_argument("--native_prefill_attn", action="store_true",
                     help="prefill attention on tao_attn_prefill_bf16 (kernels.PREFILL_ATTN = True)")
     ap.add_argument("--head_prologue", action="store_true",
@@ -275,9 +278,11 @@ def main(argv=None):
     args = ap.parse_args(argv)
 
     if (args.head_prologue or args.attn_prefetch_wgs >= 0 or args.sdpa_prefill
-            or args.native_prefill_attn):
+            or args.native_prefill_attn or args.prefill_add_norm >= 0):
         from torchao._models.llama import kernels
 
+        if args.prefill_add_norm >= 0:
+            kernels.PREFILL_ADD_NORM = bool(args.prefill_add_norm)
         if args.sdpa_prefill:
             kernels.PREFILL_ATTN = False
         if args.native_prefill_attn:

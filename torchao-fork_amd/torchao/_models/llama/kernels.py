@@ -30,6 +30,20 @@ def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
     return y
 
 
+def add_rmsnorm(x: torch.Tensor, res: torch.Tensor, weight: torch.Tensor, eps: float):
+    """(h, rmsnorm(h)) with h = x + res, in one launch (bit-identical to the two ops)."""
+    _check(x, torch.bfloat16, "add_rmsnorm x")
+    _check(res, torch.bfloat16, "add_rmsnorm res")
+    _check(weight, torch.bfloat16, "add_rmsnorm weight")
+    if res.shape != x.shape:
+        raise RuntimeError(f"add_rmsnorm: shapes {tuple(x.shape)} and {tuple(res.shape)} differ")
+    h, y = torch.empty_like(x), torch.empty_like(x)
+    D = x.shape[-1]
+    _lib.call("tao_add_rmsnorm_bf16", x.data_ptr(), res.data_ptr(), weight.data_ptr(),
+              h.data_ptr(), y.data_ptr(), x.numel() // D, D, float(eps), _stream(x))
+    return h, y
+
+
 def rope_kv(qkv: torch.Tensor, freqs: torch.Tensor, pos: torch.Tensor, k_cache: torch.Tensor,
             v_cache: torch.Tensor, n_head: int) -> torch.Tensor:
     """qkv [B, S, (H + 2 Hkv) D] -> rotated q [B, H, S, D]; k, v written to the caches at pos."""
@@ -121,6 +135,8 @@ _EPILOGUES = {"none": 0, "swiglu": 1, "rope_kv": 2}
 
 # Prefill attention on tao_attn_prefill_bf16 (False: torch's masked SDPA over the caches).
 PREFILL_ATTN = True
+# Prefill residual adds fused with the following RMSNorm (tao_add_rmsnorm_bf16).
+PREFILL_ADD_NORM = False
 
 # Output heads (N >= HEAD_ROWS) normalise in their own RMSNorm launch unless HEAD_PROLOGUE.
 HEAD_ROWS = 65536

@@ -460,11 +460,29 @@ class Transformer(nn.Module):
         return self.output(kernels.rmsnorm(x, self.norm.weight, self.norm.eps))
 
     def _layers_prefill(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
+        from torchao._models.llama import kernels
+
         mask = self.causal_mask[None, None, input_pos]  # [1, 1, S, T]
         x = self.tok_embeddings(idx)
+        if not kernels.PREFILL_ADD_NORM:
+            for blk in self.layers:
+                x = blk.forward_prefill(x, self.freqs, mask, input_pos)
+            return x
+        # each residual add fused with the RMSNorm that follows it (tao_add_rmsnorm_bf16): the
+        # w2 output of block i is added at block i + 1's attention norm, the last one at the end
+        pending = None
         for blk in self.layers:
-            x = blk.forward_prefill(x, self.freqs, mask, input_pos)
-        return x
+            an, fn, ff = blk.attention_norm, blk.ffn_norm, blk.feed_forward
+            if pending is None:
+                xn = kernels.rmsnorm(x, an.weight, an.eps)
+            else:
+                x, xn = kernels.add_rmsnorm(x, pending, an.weight, an.eps)
+            a = blk.attention.forward_prefill(xn, self.freqs, mask, input_pos)
+            x, hn = kernels.add_rmsnorm(x, a, fn.weight, fn.eps)
+            g = (kernels.silu_mul(ff.w13(hn)) if ff.w13 is not None
+                 else kernels.silu_mul(ff.w1(hn), ff.w3(hn)))
+            pending = ff.w2(g)
+        return x if pending is None else x + pending
 
     def prefill_next(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
         """Greedy next token [B, 1] after the prompt ``idx`` [B, S] (the reference's prefill:
