@@ -136,7 +136,7 @@ _EPILOGUES = {"none": 0, "swiglu": 1, "rope_kv": 2}
 # Prefill attention on tao_attn_prefill_bf16 (False: torch's masked SDPA over the caches).
 PREFILL_ATTN = True
 # Prefill residual adds fused with the following RMSNorm (tao_add_rmsnorm_bf16).
-PREFILL_ADD_NORM = False
+PREFILL_ADD_NORM = True
 
 # Output heads (N >= HEAD_ROWS) normalise in their own RMSNorm launch unless HEAD_PROLOGUE.
 HEAD_ROWS = 65536
