@@ -2,7 +2,7 @@
 
 python experiments/pmc_prefill_summary.py gpurun_out/r2_pmc_prefill > profiles/r2_pmc_prefill.jsonl
 
-Per configuration, medians over the GEMM dispatches (kernel names containing "gemm_") of every
+Per configuration, medians over the GEMM dispatches (kernel names containing "gemm": gemm_mfma_kernel, gemm32_int4_kernel, ...) of every
 counter, plus derived ratios:
   wait_frac        = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (both quad-cycles: the share of wave
                      time spent waiting on an instruction dependency, mostly vmcnt / lgkmcnt)
@@ -41,7 +41,7 @@ def main():
         vals = collections.defaultdict(list)
         for f in glob.glob(os.path.join(d, "p*", "*_counter_collection.csv")):
             for r in csv.DictReader(open(f)):
-                if "gemm_" not in r["Kernel_Name"]:
+                if "gemm" not in r["Kernel_Name"]:
                     continue
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
         med = {k: statistics.median(v) for k, v in vals.items()}
