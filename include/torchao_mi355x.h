@@ -150,6 +150,17 @@ int tao_tune_gemm_stream(int mode);
  * 3 = 128 x 16, 4 = 128 x 16 on 16 waves (int8) / 32 x 64 with one k-block in flight (int4);
  * + 16: each workgroup walks its k-blocks from a rotated start. Thread-local. */
 int tao_tune_gemm_ksplit(int mode, int shape);
+/* The single-fetch prefill GEMM (csrc/gemm_sf.hip: 128-row tiles so each weight tile is fetched by
+ * one workgroup, 8 waves, both operands by LDS-DMA in full lines, K split over workgroups with a
+ * fixed reducer) for the int4 weight-only and int8 dynamic linears. mode 0 = built-in routing,
+ * 1 = never, 2 = wherever the shape is supported (K % 128 (int4) / 256 (int8) == 0; M <= 128 per
+ * 128-row launch tile). bn (32 / 64 / 128), wm (waves along M: 2 / 4 / 8), splits, stages (2-4),
+ * a_steps (K steps of each publishing slice) and ks (int8 k step 128 / 256): 0 = built-in.
+ * Thread-local; for measurement. */
+int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages, int a_steps, int ks);
+/* Reducer poll timeouts of the single-fetch GEMM since the last call (*bits != 0: some split
+ * launch's outputs are invalid; never expected, see gemm_sf.hip). Synchronous. */
+int tao_gemm_sf_status(unsigned* bits);
 /* Number of split-K workspaces currently owned by captured graphs (each is released with its
  * graph). Diagnostic for tests; never fails. */
 int tao_graph_workspace_count(void);

@@ -1,0 +1,209 @@
+"""GPU parity of the single-fetch prefill GEMM (csrc/gemm_sf.hip) against the CPU oracle.
+
+128-row tiles (every weight tile fetched by one workgroup), 8 waves, both operands by LDS-DMA into
+XOR-swizzled images, K split over workgroups with a fixed reducer (slices 0..S-2 publish sc1
+partial tiles and add a ticket; slice S-1 polls it and sums in slice order). Checked here through
+the C-ABI (torch.ops.torchao.*): int8 dynamic BIT-EXACT against the reference CPU epilogue
+(kernel/intmm.py:133-137, plain_layout.py:301-315) at every tile / wave layout / split / ring
+depth / k step; int4 within the reference dequant -> F.linear bar (north star 1e-2) and 4e-3 of
+the fp32 accumulation of the same weights at every group size; partial M and N tiles, M > 128
+(several M tiles), asymmetric publisher slices, bias, run-to-run bit identity, the fenced
+hand-off, agreement with gemm_mfma.hip, graph capture and replay, and no reducer timeouts.
+"""
+
+import pytest
+import torch
+
+from oracle import oracle
+
+from torchao import _lib
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL_REF = 1e-2
+TOL_FP32 = 4e-3
+
+
+@pytest.fixture
+def sf():
+    def set_(mode, bn=0, wm=0, splits=0, stages=0, a_steps=0, ks=0):
+        _lib.call("tao_tune_gemm_sf", mode, bn, wm, splits, stages, a_steps, ks)
+    yield set_
+    _lib.call("tao_tune_reset")
+    st = torch.zeros(1, dtype=torch.int32)
+    _lib.call("tao_gemm_sf_status", st.data_ptr())
+    assert int(st.item()) == 0, "gemm_sf reducer poll timed out"
+
+
+def _int4(N, K, g, seed):
+    w = oracle.make_linear_weight(N, K, seed=seed)
+    s, z = oracle.int4_qparams(w, g)
+    q = oracle.int4_quantize(w, s, z, g)
+    packed = torch.ops.torchao.int4_pack(q.to(DEV))
+    sz = torch.stack([s, z], dim=-1).contiguous().to(DEV)
+    return q, s, z, packed, sz
+
+
+def _int8(M, N, K, seed):
+    w = oracle.make_linear_weight(N, K, seed=seed)
+    wq, ws = oracle.int8_dyn_weight(w)
+    x = oracle.make_activation(M, K, seed=seed + 1)
+    xq, xs = oracle.int8_act_quant(x)
+    return xq, xs, wq, ws
+
+
+# (bn, wm, splits, stages, a_steps, ks): every instantiated layout, split 1 / 2 / 4 / 8, ring
+# depths 2-4, both int8 k steps
+I8_CFGS = [(32, 8, 2, 3, 0, 256), (32, 4, 2, 3, 0, 256), (32, 8, 4, 4, 0, 256),
+           (64, 4, 4, 3, 0, 128), (64, 2, 4, 2, 0, 256), (64, 8, 1, 3, 0, 128),
+           (128, 2, 8, 2, 0, 128), (128, 4, 2, 4, 0, 128), (64, 4, 2, 3, 0, 256)]
+I8_SHAPES = [(128, 4096, 4096), (5, 64, 512), (64, 96, 1024), (100, 4096, 3072),
+             (128, 512, 14336), (200, 256, 2048), (1, 128, 256)]
+
+
+@pytest.mark.parametrize("M,N,K", I8_SHAPES)
+@pytest.mark.parametrize("cfg", I8_CFGS)
+def test_sf_int8dyn_bit_exact(sf, M, N, K, cfg):
+    sf(2, *cfg)
+    xq, xs, wq, ws = _int8(M, N, K, seed=M + N + K)
+    bias = oracle.make_activation(1, N, seed=3).reshape(N)
+    args = (xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV))
+    y = torch.ops.torchao.int8_scaled_mm(*args, bias.to(DEV)).cpu()
+    assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, bias, epilogue="cpu"))
+    y = torch.ops.torchao.int8_scaled_mm(*args, None).cpu()
+    assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="cpu"))
+
+
+def test_sf_int8dyn_extreme_values(sf):
+    """Saturated int8 operands (+-127, K = 8192): int32 partials of 127^2 K summed across 4 slices
+    stay exact."""
+    sf(2, 64, 4, 4, 3, 0, 256)
+    M, N, K = 128, 256, 8192
+    g = torch.Generator().manual_seed(0)
+    wq = (torch.randint(0, 2, (N, K), generator=g, dtype=torch.int8) * 254 - 127).to(torch.int8)
+    xq = (torch.randint(0, 2, (M, K), generator=g, dtype=torch.int8) * 254 - 127).to(torch.int8)
+    ws = torch.full((N,), 1e-4).to(torch.bfloat16)
+    xs = torch.full((M,), 1e-3).to(torch.bfloat16)
+    y = torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), None).cpu()
+    assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="cpu"))
+
+
+# (bn, wm, splits, stages, a_steps)
+I4_CFGS = [(64, 2, 4, 3, 0), (64, 4, 4, 3, 0), (64, 8, 2, 2, 0), (128, 2, 8, 2, 0),
+           (128, 4, 8, 3, 0), (128, 2, 1, 3, 0), (64, 2, 4, 4, 0)]
+I4_SHAPES = [(128, 4096, 4096), (17, 128, 1024), (100, 640, 4096), (128, 512, 14336),
+             (200, 192, 2048), (64, 96, 768)]
+
+
+@pytest.mark.parametrize("M,N,K", I4_SHAPES)
+@pytest.mark.parametrize("cfg", I4_CFGS)
+def test_sf_int4(sf, M, N, K, cfg):
+    sf(2, *cfg)
+    g = 32
+    q, s, z, packed, sz = _int4(N, K, g, seed=M + N)
+    x = oracle.make_activation(M, K, seed=M)
+    bias = oracle.make_activation(1, N, seed=7).reshape(N)
+    y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, bias.to(DEV)).cpu()
+    assert y.shape == (M, N)
+    assert oracle.rel_l2(y, oracle.int4_linear(x, q, s, z, g, bias)) < TOL_REF
+    assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, g, bias)) < TOL_FP32
+
+
+@pytest.mark.parametrize("g", [64, 128, 256])
+@pytest.mark.parametrize("cfg", [(64, 2, 4, 3, 0), (128, 4, 8, 2, 0)])
+def test_sf_int4_group_sizes(sf, g, cfg):
+    """g = 64 / 128 / 256: the (scale, zero) image holds, per 32-k lane group, the word
+    ((128 st) >> lg) + ((32 q) >> lg)."""
+    sf(2, *cfg)
+    M, N, K = 96, 320, 3072
+    q, s, z, packed, sz = _int4(N, K, g, seed=g)
+    x = oracle.make_activation(M, K, seed=g)
+    y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, None).cpu()
+    assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, g)) < TOL_FP32
+    assert oracle.rel_l2(y, oracle.int4_linear(x, q, s, z, g)) < TOL_REF
+
+
+@pytest.mark.parametrize("a_steps", [1, 3, 6])
+def test_sf_asymmetric_slices(sf, a_steps):
+    """Publishers taking fewer (or more) K steps than the reducer: same sums (int8 exact, int4
+    within the bars)."""
+    M, N, K = 128, 1024, 4096
+    sf(2, 32, 8, 2, 3, a_steps, 256)
+    xq, xs, wq, ws = _int8(M, N, K, seed=11)
+    y = torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), None).cpu()
+    assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="cpu"))
+    sf(2, 64, 2, 4, 3, a_steps)
+    q, s, z, packed, sz = _int4(N, K, 32, seed=12)
+    x = oracle.make_activation(M, K, seed=13)
+    y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, 32, None).cpu()
+    assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, 32)) < TOL_FP32
+
+
+def test_sf_deterministic_fenced_and_matches_old_kernel(sf):
+    """Run-to-run bit identity (slices summed in slice order whatever the arrival order), the
+    fenced hand-off gives the same bits, and agreement with gemm_mfma.hip (bit-identical for int8
+    dyn; fp32 summation orders apart for int4)."""
+    M, N, K, g = 128, 4096, 4096, 32
+    q, s, z, packed, sz = _int4(N, K, g, seed=1)
+    x = oracle.make_activation(M, K, seed=2).to(DEV)
+    sf(2, 64, 2, 4, 3)
+    a = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)
+    for _ in range(5):
+        assert torch.equal(torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None), a)
+    _lib.call("tao_tune_splitk_fenced", 1)
+    assert torch.equal(torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None), a)
+    _lib.call("tao_tune_splitk_fenced", 0)
+    sf(1)
+    old = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)
+    assert oracle.rel_l2(a.cpu(), old.cpu()) < 2e-3
+    xq, xs, wq, ws = _int8(M, N, K, seed=3)
+    args = (xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), None)
+    old8 = torch.ops.torchao.int8_scaled_mm(*args)
+    sf(2, 32, 8, 2, 3, 0, 256)
+    assert torch.equal(torch.ops.torchao.int8_scaled_mm(*args), old8)
+    _lib.call("tao_tune_splitk_fenced", 1)
+    assert torch.equal(torch.ops.torchao.int8_scaled_mm(*args), old8)
+
+
+def test_sf_graph_capture(sf):
+    """Captured split launches replay correctly (the reducer resets its ticket every launch) and
+    recompute on new input."""
+    sf(2, 64, 2, 4, 3)
+    M, N, K, g = 128, 1024, 2048, 32
+    q, s, z, packed, sz = _int4(N, K, g, seed=4)
+    x = oracle.make_activation(M, K, seed=5).to(DEV)
+    eager = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)
+    side = torch.cuda.Stream()
+    graph = torch.cuda.CUDAGraph()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph, stream=side):
+            out = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)
+    torch.cuda.current_stream().wait_stream(side)
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, eager)
+    x.copy_(oracle.make_activation(M, K, seed=6).to(DEV))
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None))
+
+
+def test_sf_unsupported_shapes_fall_back(sf):
+    """K not a multiple of the k step (int4 128, int8 256) or an invalid tile choice: the forced
+    mode routes to the other kernels, or reports the error."""
+    sf(2)
+    M, N, K = 64, 256, 1056
+    q, s, z, packed, sz = _int4(N, K, 32, seed=N)
+    x = oracle.make_activation(M, K, seed=K)
+    y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, 32, None).cpu()
+    assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, 32)) < TOL_FP32
+    xq, xs, wq, ws = _int8(64, 256, 1152, seed=9)
+    y = torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), None).cpu()
+    assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="cpu"))
+    sf(2, 32, 2)  # bn 32 with 2 waves along M: no kernel (wave tile narrower than 16 columns)
+    q, s, z, packed, sz = _int4(256, 1024, 32, seed=1)
+    with pytest.raises(RuntimeError, match="gemm_sf"):
+        torch.ops.torchao.int4_weight_only_linear(
+            oracle.make_activation(64, 1024, seed=1).to(DEV), packed, sz, 32, None)

@@ -543,3 +543,30 @@ def test_bench_shard_plans():
     kinds = bench.shard_kinds(unf, 4, 32, "tp", {})
     assert kinds.count("local") == 96 and kinds.count("reduce") == 64
     assert bench.shard_kinds(lins, 1, 32, "tp", {}) == ["whole"] * len(lins)
+
+
+@pytest.mark.parametrize("name", ["float_nopz", "int_nopz", "int_pz", "float_pz"])
+@pytest.mark.parametrize("gs", [32, 64])
+def test_groupwise_affine_qparams_every_branch_matches_reference(name, gs):
+    """get_groupwise_affine_qparams (quantization/utils.py:326-391) bit-exact to the reference's
+    own outputs (tests/golden/groupwise_qparams.npz, oracle/gen_golden_qparams.py) in all three
+    branches: float domain without zero preservation (tinygemm), integer domain without it
+    (_choose_qparams_affine_dont_preserve_zero: all-positive / all-negative groups differ from the
+    zero-preserving scheme), and zero-preserving choose_qparams_affine (either domain)."""
+    from torchao.quantization.quant_primitives import ZeroPointDomain
+    from torchao.quantization.utils import get_groupwise_affine_qparams
+
+    d = np.load(os.path.join(ROOT, "tests", "golden", "groupwise_qparams.npz"))
+    w = bf16(d["w"])
+    zpd = ZeroPointDomain.INT if name.startswith("int") else ZeroPointDomain.FLOAT
+    s, z = get_groupwise_affine_qparams(w, 4, gs, torch.bfloat16, zpd, name.endswith("_pz"))
+    assert torch.equal(s, bf16(d[f"{name}_g{gs}_s"]))
+    assert str(z.dtype) == str(d[f"{name}_g{gs}_zdtype"])
+    ref_z = d[f"{name}_g{gs}_z"]
+    if z.dtype == torch.int32:
+        assert torch.equal(z, torch.from_numpy(ref_z.astype(np.int32)))
+    else:
+        assert torch.equal(z, bf16(ref_z))
+    if name == "int_nopz":  # the branch the advisor found missing: differs from zero-preserving
+        s2, z2 = get_groupwise_affine_qparams(w, 4, gs, torch.bfloat16, zpd, True)
+        assert not (torch.equal(s, s2) and torch.equal(z, z2))

@@ -71,6 +71,9 @@ struct Tuning {
   int gemm_stream_rot = 0;                       // stream tile GEMM phase rotation: 0, 1 (M tile), 2 (+N)
   int gemm_ksplit = 0, gemm_ksplit_shape = 0;    // k-split tile GEMM: 0 auto, 1 off, 2 on; shape
   int gemm_ksplit_rot = 0;                       // k-split: rotated block order per workgroup
+  int gemm_sf = 0;                               // single-fetch GEMM: 0 auto, 1 off, 2 on
+  int sf_bn = 0, sf_wm = 0, sf_splits = 0;       // single-fetch GEMM shape overrides
+  int sf_stages = 0, sf_a_steps = 0, sf_ks = 0;
 };
 Tuning& tuning();
 
@@ -166,6 +169,49 @@ __device__ __forceinline__ uint32_t bload4(Rsrc r, uint32_t voff, uint32_t soff)
 }
 
 constexpr int kWave = 64;
+
+// ---- LDS-DMA (buffer_load ... lds) ------------------------------------------------------------
+// 64 lanes x SIZE bytes from per-lane buffer offsets into LDS at the wave-uniform `dst` + lane x
+// SIZE (lane-linear; swizzled images are made by choosing each lane's SOURCE). Issued by inline
+// asm: with the intrinsic, hipcc treats every pending DMA as a writer of any LDS a later ds_read
+// touches and waits vmcnt(0) before the first read of every step, which drains a ring. The caller
+// waits for its DMAs by hand (counted vmcnt before a barrier). M0 is saved and restored.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+template <int SIZE, int AUX = 0>
+__device__ __forceinline__ void dma_lds(Rsrc r, uint32_t voff, uint32_t soff, void* dst) {
+  static_assert((SIZE == 16 || SIZE == 4) && (AUX == 0 || AUX == kNT), "dma_lds: 16 / 4 B, nt or not");
+  const uint32_t lds_addr = (uint32_t)(uintptr_t)(lds_ptr_t)dst;
+  uint32_t keep;
+  if constexpr (SIZE == 16 && AUX == 0)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "s"(lds_addr), "v"(voff), "s"(r), "s"(soff) : "memory");
+  else if constexpr (SIZE == 16)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %2, %3, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "s"(lds_addr), "v"(voff), "s"(r), "s"(soff) : "memory");
+  else if constexpr (AUX == 0)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "buffer_load_dword %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "s"(lds_addr), "v"(voff), "s"(r), "s"(soff) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "buffer_load_dword %2, %3, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "s"(lds_addr), "v"(voff), "s"(r), "s"(soff) : "memory");
+}
+
+// Workgroup barrier that leaves vector-memory ops (LDS-DMA included) in flight: only this wave's
+// LDS ops are drained (a __syncthreads() would also wait vmcnt(0) while a DMA is pending).
+__device__ __forceinline__ void barrier_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 // ---- decode-step error word ------------------------------------------------------------------
 // Device-side argument faults of the decode kernels (a KV position outside [0, T)) are not

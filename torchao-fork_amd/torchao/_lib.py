@@ -52,6 +52,8 @@ _SIGNATURES = {
     "tao_tune_gemm_tile": [_int, _int],
     "tao_tune_gemm_stream": [_int],
     "tao_tune_gemm_ksplit": [_int, _int],
+    "tao_tune_gemm_sf": [_int, _int, _int, _int, _int, _int, _int],
+    "tao_gemm_sf_status": [_p],
     "tao_graph_workspace_count": [],
     "tao_int4_pack": [_p, _p, _i64, _i64, _p],
     "tao_int4_pack_u8": [_p, _p, _i64, _i64, _p],

@@ -229,6 +229,31 @@ def generate(model: Transformer, prompt: torch.Tensor, max_new_tokens: int,
     return out, t1 - t0, t2 - t1
 
 
+@torch.no_grad()
+def eager_token_check(model: Transformer, prompt: torch.Tensor, graph_tokens: torch.Tensor,
+                      n: int):
+    """Output check of a graph-decoded run: the first ``n`` greedy tokens decoded again EAGERLY
+    (prefill, then one ``model(tok, pos)`` forward per token, fp32 logits, torch argmax) against
+    ``graph_tokens`` [B, >= P + n]; also whether every eager step's logits were finite. Returns
+    (matching positions, n, first mismatching offset or None, all logits finite)."""
+    B, P = prompt.shape
+    device = prompt.device
+    tok = prefill(model, prompt, torch.arange(P, device=device))
+    toks, finite = [tok], True
+    pos = torch.tensor([P], device=device)
+    for _ in range(1, n):
+        logits = model(tok, pos)
+        finite = finite and bool(torch.isfinite(logits).all())
+        tok = logits[:, -1].argmax(dim=-1, keepdim=True).to(prompt.dtype)
+        toks.append(tok)
+        pos += 1
+    torch.cuda.synchronize()
+    _check_status(model)
+    eq = (torch.cat(toks, dim=1) == graph_tokens[:, P:P + n]).all(dim=0).cpu()
+    bad = (~eq).nonzero()
+    return int(eq.sum()), n, (int(bad[0]) if len(bad) else None), finite
+
+
 def _check_status(model: Transformer) -> None:
     if model.fused:
         from torchao._models.llama import kernels
@@ -272,6 +297,9 @@ def main(argv=None):
                          "profiles/r3_ab_e2e_steps_per_graph.jsonl)")
     ap.add_argument("--attn_mode", type=int, default=-1,
                     help="decode attention kernel (tao_tune_attn; -1 = built-in)")
+    ap.add_argument("--check_tokens", type=int, default=32,
+                    help="after timing, decode this many tokens again eagerly and report their "
+                         "agreement with the graph-decoded tokens (0 = skip)")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--write_result", type=Path, default=None)
@@ -357,6 +385,12 @@ def main(argv=None):
         "quantize_s": round(t_quant, 2),
         "sample_tokens": tokens[0, P:P + 16].tolist(),
     }
+    if decoder is not None and args.check_tokens > 0:
+        n = min(args.check_tokens, T)
+        match, n, first_bad, finite = eager_token_check(model, prompt, tokens, n)
+        res["graph_eager_token_match"] = f"{match}/{n}"
+        res["graph_eager_first_mismatch"] = first_bad
+        res["eager_logits_finite"] = finite
     print(json.dumps(res), flush=True)
     if args.write_result:
         with open(args.write_result, "a") as f:

@@ -34,6 +34,7 @@ _KNOBS = {
     "gemm_tile": ("tao_tune_gemm_tile", 2),
     "gemm_stream": ("tao_tune_gemm_stream", 1),
     "gemm_ksplit": ("tao_tune_gemm_ksplit", 2),
+    "gemm_sf": ("tao_tune_gemm_sf", 7),
 }
 
 

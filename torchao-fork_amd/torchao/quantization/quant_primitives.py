@@ -28,6 +28,7 @@ __all__ = [
     "quantize_affine",
     "dequantize_affine",
     "_choose_qparams_affine_tinygemm",
+    "_choose_qparams_affine_dont_preserve_zero",
     "_quantize_affine_tinygemm",
     "_dequantize_affine_tinygemm",
     "_quantize_affine_no_zero_point",
@@ -196,6 +197,33 @@ def _choose_qparams_affine_tinygemm(
     zero_point = mn + scale * mid
     zero_point_dtype = input.dtype if zero_point_dtype is None else zero_point_dtype
     return scale.to(dtype=scale_dtype, device=input.device), zero_point.to(zero_point_dtype)
+
+
+@torch.no_grad()
+def _choose_qparams_affine_dont_preserve_zero(
+    input: torch.Tensor,
+    mapping_type: MappingType,
+    block_size: Tuple[int, ...],
+    target_dtype: torch.dtype,
+    quant_min: Optional[Union[int, float]] = None,
+    quant_max: Optional[Union[int, float]] = None,
+    eps: Optional[float] = None,
+    scale_dtype: Optional[torch.dtype] = None,
+    zero_point_dtype: Optional[torch.dtype] = None,
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Integer zero-point domain WITHOUT zero preservation (quant_primitives.py:1310-1373): the
+    block's own [min, max] (not widened to include 0) maps to [qmin, qmax]; s = clamp((max - min)
+    / (qmax - qmin), eps), z = clamp(qmin - round(min / s), qmin, qmax) as an integer."""
+    quant_min, quant_max = _get_and_check_qmin_qmax(target_dtype, quant_min, quant_max)
+    assert mapping_type is MappingType.ASYMMETRIC, f"Unsupported mapping type: {mapping_type}"
+    scale_dtype = input.dtype if scale_dtype is None else scale_dtype
+    eps = torch.finfo(input.dtype).eps if eps is None else eps
+    assert len(block_size) == input.dim(), f"Got input dim:{input.dim()}, block_size: {block_size}"
+    mn, mx = _block_min_max(input, block_size)
+    scale = torch.clamp((mx - mn) / float(quant_max - quant_min), min=eps)
+    zero_point = torch.clamp(quant_min - _Round.apply(mn / scale), quant_min, quant_max)
+    zero_point_dtype = torch.int32 if zero_point_dtype is None else zero_point_dtype
+    return scale.to(dtype=scale_dtype, device=input.device), zero_point.to(dtype=zero_point_dtype)
 
 
 # ---------------------------------------------------------------------------------------------

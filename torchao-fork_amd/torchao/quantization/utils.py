@@ -75,9 +75,11 @@ def _int_mode(zero_point_domain):
 
 def get_groupwise_affine_qparams(w, n_bit=4, groupsize=128, dtype=torch.bfloat16,
                                  zero_point_domain=None, preserve_zero=False, eps=None):
-    """Asymmetric per-(row, group) (scale, zero) of a 2-D weight, each [N, K/groupsize].
-    Float zero-point domain without zero preservation is the tinygemm scheme the int4 kernels
-    consume; the integer domain preserves zero (choose_qparams_affine)."""
+    """Asymmetric per-(row, group) (scale, zero) of a 2-D weight, each [N, K/groupsize]
+    (quantization/utils.py:326-391). The reference's three-way choice: float zero-point domain
+    without zero preservation = the tinygemm scheme the int4 kernels consume; integer domain
+    without it = _choose_qparams_affine_dont_preserve_zero; otherwise choose_qparams_affine
+    (zero preserved)."""
     from torchao.quantization import quant_primitives as qp
     zero_point_domain = qp.ZeroPointDomain.FLOAT if zero_point_domain is None else zero_point_domain
     groupsize = min(groupsize, w.shape[-1])
@@ -85,10 +87,13 @@ def get_groupwise_affine_qparams(w, n_bit=4, groupsize=128, dtype=torch.bfloat16
         raise ValueError(f"bad group-wise qparams request: {tuple(w.shape)}, g={groupsize}, "
                          f"n_bit={n_bit}")
     int_zero = _int_mode(zero_point_domain)
-    if not int_zero and preserve_zero:
-        raise ValueError("float zero-point domain does not preserve zero")
     zdt = torch.int32 if int_zero else dtype
-    choose = qp.choose_qparams_affine if int_zero else qp._choose_qparams_affine_tinygemm
+    if not int_zero and not preserve_zero:
+        choose = qp._choose_qparams_affine_tinygemm
+    elif int_zero and not preserve_zero:
+        choose = qp._choose_qparams_affine_dont_preserve_zero
+    else:
+        choose = qp.choose_qparams_affine
     scale, zero = choose(w, qp.MappingType.ASYMMETRIC, (1, groupsize), torch.int32, 0,
                          2 ** n_bit - 1, 1e-6 if eps is None else eps, scale_dtype=dtype,
                          zero_point_dtype=zdt)
