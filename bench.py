@@ -21,9 +21,11 @@ large linears can gain. --shard-policy size / all / none override the measuremen
 Total work is fixed as P grows ("strong" scaling); value counts the whole model's bytes once
 per step.
 
-At P > 1 the line also carries config5_70b: BASELINE config 5's Llama-3-70B linear step (80
-layers, 43.4 GB of int4 weights per token) under the fixed Megatron plan (pairs + head gather,
-~1/P of the weights per rank), collectives inside the step's HIP graph, with the GEMV-only and
+The line also carries config5_70b: BASELINE config 5's Llama-3-70B linear step (80 layers,
+43.4 GB of int4 weights per token). At P = 1 every linear runs whole on the one GPU (the 1-GPU
+anchor of the 1/2/4/8 curve); at P > 1 under the Megatron plan (pairs + head gather) and, beside
+it as north_star_plan, the north star's plan (every linear column-sharded + RCCL all-gather),
+~1/P of the weights per rank, collectives inside the step's HIP graph, with the GEMV-only and
 collectives-only times beside the whole step (--no-config5 skips it). --model 70b makes the 70B
 the headline instead; the default headline stays the 8B, so the N = 1 point equals BENCH.
 
@@ -406,12 +408,43 @@ def config2_shapes(device, g=32, copies=32, reps=20):
     return out
 
 
+def graph_us_per_call(fn, copies, device, reps=3):
+    """us per call of fn(c), c over `copies` weight copies, captured once in a HIP graph and
+    replayed: events on the replay stream (launch gaps inside the graph included)."""
+    s = torch.cuda.Stream(device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+        for c in range(copies):
+            fn(c)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            for c in range(copies):
+                fn(c)
+        graph.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            graph.replay()
+        e1.record(s)
+    e1.synchronize()
+    torch.cuda.current_stream(device).wait_stream(s)
+    del graph
+    return e0.elapsed_time(e1) * 1e3 / reps / copies
+
+
 def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
     """BASELINE config 3 (int8 dynamic-activation int8-weight linear, M = 128, the MFMA int8
     path) and the int4 g32 linear at the same M on its bf16-MFMA path, timed per kernel by the
     dispatch packets' own events (tao_profile_*, as rocprofv3 reports them), weights rotated
     over copies past the 256 MiB Infinity Cache. Roofline: max(ops / MFMA peak, bytes / HBM
-    peak) is the attainable time; `frac` = attainable / measured."""
+    peak) is the attainable time; `frac` = attainable / measured.
+
+    Beside each, the REFERENCE's own GPU path on the same inputs, both sides captured in one HIP
+    graph over the same weight copies (graph_us, launch gaps included for both): config 3 as
+    safe_int_mm -> torch._int_mm (hipBLASLt int8) plus the int_scaled_matmul epilogue and the
+    weight scale (kernel/intmm.py:82,136-142; plain_layout.py:301-315; the per-token quant is
+    ours on both sides), int4 as aten._weight_int4pack_mm on the same nibbles repacked by
+    aten._convert_weight_to_int4pack (tensor_core_tiled_layout.py:104)."""
     from torchao import _lib
 
     def timed(fn, copies, launches):
@@ -427,6 +460,10 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
             raise RuntimeError(f"prefill_mfma: expected {reps * launches} kernels, got {len(d)}")
         return [sorted(d[j::launches])[len(d[j::launches]) // 2] * 1e3 for j in range(launches)]
 
+    def rel(a, b):
+        a, b = a.float(), b.float()
+        return round(float((a - b).norm() / b.norm().clamp_min(1e-30)), 5)
+
     out = {}
     # int8 dyn: per-token quant kernel + int8 MFMA GEMM with the fused scale epilogue
     copies = max(2, int(320e6 // (N * K)))
@@ -441,43 +478,84 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
         torch.ops.torchao.int8_scaled_mm(q, s, ws[c], wsc, None)
 
     quant_us, gemm_us = timed(int8dyn, copies, 2)
+    xq, xs = torch.ops.torchao.int8_quantize_per_token(x)
+    xs2 = xs.reshape(-1, 1)
+
+    def ours8(c):
+        return torch.ops.torchao.int8_scaled_mm(xq, xs, ws[c], wsc, None)
+
+    def ref8(c):  # the reference's GPU ops after the per-token quant
+        return ((torch._int_mm(xq, ws[c].t()) * xs2).to(torch.bfloat16)) * wsc
+
+    ref8_us = ours8_graph_us = ref8_diff = None
+    try:
+        ours8_graph_us = graph_us_per_call(ours8, copies, device)
+        ref8_us = graph_us_per_call(ref8, copies, device)
+        ref8_diff = rel(ref8(0), ours8(0))
+    except Exception as e:  # the hipBLASLt int8 path is build dependent: report, never fail
+        ref8_us = f"unavailable: {type(e).__name__}: {str(e)[:120]}"
     ops = 2 * M * N * K
     nbytes = N * K + N * 2 + M * K + M * 4 + M * N * 2  # int8 W + scales, int8 x + scales, bf16 y
     att = max(ops / (INT8_PEAK_TOPS * 1e12), nbytes / (HBM_PEAK_GBPS * 1e9)) * 1e6
     out["int8_dyn"] = {
         "config": f"BASELINE config 3: int8 dyn-act int8-weight linear M={M} N={N} K={K}",
-        "kernel": "gemm_mfma_kernel<Int8Dyn> (v_mfma_i32_16x16x64_i8)",
+        "kernel": "routed int8 dyn MFMA GEMM (v_mfma_i32_16x16x64_i8)",
         "gemm_us": round(gemm_us, 2), "quant_us": round(quant_us, 2),
         "TOPS": round(ops / (gemm_us * 1e-6) / 1e12, 1),
         "mfma_frac": round(ops / (gemm_us * 1e-6) / 1e12 / INT8_PEAK_TOPS, 4),
         "GBps": round(nbytes / (gemm_us * 1e-6) / 1e9, 1),
         "attainable_us": round(att, 2), "roofline_frac": round(att / gemm_us, 4),
+        "graph_us": round(ours8_graph_us, 2) if ours8_graph_us else None,
+        "reference_gpu_us": round(ref8_us, 2) if isinstance(ref8_us, float) else ref8_us,
+        "reference_gpu_op": "torch._int_mm (hipBLASLt int8, safe_int_mm) * x_scale -> bf16 * w_scale",
+        "reference_gpu_rel_l2": ref8_diff,
     }
     del ws
     # int4 g32 weight-only at the same M: bf16 MFMA with in-register nibble dequant
     copies = max(2, int(320e6 // (N * K // 2)))
-    w4 = []
+    w4, wref = [], []
     for c in range(copies):
         q = torch.randint(0, 16, (N, K), dtype=torch.int32, device=device, generator=gen)
         sz = (torch.rand(N, K // g, 2, device=device, generator=gen) * 0.02).to(torch.bfloat16)
         w4.append((torch.ops.torchao.int4_pack(q), sz))
+        try:
+            u8 = ((q[:, ::2] << 4) | q[:, 1::2]).to(torch.uint8)
+            wref.append((torch.ops.aten._convert_weight_to_int4pack(u8, 8),
+                         sz.transpose(0, 1).contiguous()))
+            del u8
+        except Exception:
+            wref = None
         del q
 
     def int4(c):
-        torch.ops.torchao.int4_weight_only_linear(x, w4[c][0], w4[c][1], g, None)
+        return torch.ops.torchao.int4_weight_only_linear(x, w4[c][0], w4[c][1], g, None)
 
     (us4,) = timed(int4, copies, 1)
+    ref4_us = ours4_graph_us = ref4_diff = None
+    try:
+        ours4_graph_us = graph_us_per_call(int4, copies, device)
+        if wref:
+            def ref4(c):
+                return torch.ops.aten._weight_int4pack_mm(x, wref[c][0], g, wref[c][1])
+            ref4_us = graph_us_per_call(ref4, copies, device)
+            ref4_diff = rel(ref4(0), int4(0))
+    except Exception as e:  # the aten op is build dependent: report, never fail
+        ref4_us = f"unavailable: {type(e).__name__}: {str(e)[:120]}"
     nbytes4 = int4_alg_bytes(N, K, g, M)
     att4 = max(ops / (BF16_PEAK_TFLOPS * 1e12), nbytes4 / (HBM_PEAK_GBPS * 1e9)) * 1e6
     out["int4_wo"] = {
         "config": f"int4 g{g} weight-only linear M={M} N={N} K={K} (prefill)",
-        "kernel": "gemm_mfma_kernel<Int4WO> (v_mfma_f32_16x16x32_bf16)",
+        "kernel": "routed int4 MFMA GEMM (v_mfma_f32_16x16x32_bf16)",
         "gemm_us": round(us4, 2),
         "TFLOPS": round(ops / (us4 * 1e-6) / 1e12, 1),
         "mfma_frac": round(ops / (us4 * 1e-6) / 1e12 / BF16_PEAK_TFLOPS, 4),
         "attainable_us": round(att4, 2), "roofline_frac": round(att4 / us4, 4),
+        "graph_us": round(ours4_graph_us, 2) if ours4_graph_us else None,
+        "reference_gpu_us": round(ref4_us, 2) if isinstance(ref4_us, float) else ref4_us,
+        "reference_gpu_op": "aten._weight_int4pack_mm (PyTorch-ROCm)",
+        "reference_gpu_rel_l2": ref4_diff,
     }
-    del w4
+    del w4, wref
     torch.cuda.empty_cache()
     return out
 
@@ -498,7 +576,8 @@ def e2e_decode(timeout_s=240):
     except Exception as e:  # reported, never fatal to the bench line
         return {"error": f"{type(e).__name__}: {str(e)[:200]}"}
     keep = ("model", "quantization", "weights", "batch_size", "prompt_length", "max_new_tokens",
-            "decode_tokens_per_s", "decode_ms_per_token", "prefill_ms", "tokens_per_s_incl_prefill")
+            "decode_tokens_per_s", "decode_ms_per_token", "prefill_ms", "tokens_per_s_incl_prefill",
+            "graph_eager_token_match", "graph_eager_first_mismatch", "eager_logits_finite")
     rec = {k: d[k] for k in keep if k in d}
     rec["config"] = "BASELINE config 4: Llama-3-8B quantize_(Int4WeightOnlyConfig(32)), greedy bs=1"
     return rec
@@ -780,8 +859,40 @@ class LinearStep:
             elapsed = float(t.item())
         return elapsed / steps * 1e3
 
+    def read_probe_graph(self, only=None):
+        """The step's launches replayed as PURE 16-B streaming reads of the same algorithmic byte
+        counts (tao_hbm_read_probe: one load per thread, 512-thread workgroups, each launch its own
+        buffer past the MALL): the floor any one-kernel-per-linear step reaches on this chip,
+        measured in the same run as the GEMV step. `only` = (n_loc, K) as step()."""
+        if not hasattr(self, "_rbufs"):
+            self._rbufs = [torch.empty((int4_alg_bytes(e[1], e[2], self.g) + 8191) // 8192 * 8192,
+                                       dtype=torch.uint8, device=self.device) for e in self.plan]
+            for b in self._rbufs:
+                b.fill_(7)
+            self._rsink = torch.zeros(1024, dtype=torch.int32, device=self.device)
+
+        def run():
+            sp = torch.cuda.current_stream(self.device).cuda_stream
+            for e, b in zip(self.plan, self._rbufs):
+                if only is not None and (e[1], e[2]) != only:
+                    continue
+                rc = self.lib.tao_hbm_read_probe(b.data_ptr(), b.numel(), self._rsink.data_ptr(), sp)
+                if rc:
+                    raise RuntimeError(self.lib.tao_last_error().decode())
+        graph = torch.cuda.CUDAGraph()
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            run()
+            with torch.cuda.graph(graph, stream=self.stream):
+                run()
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        torch.cuda.synchronize()
+        return graph
+
     def release(self):
         self.plan, self.xs = [], {}
+        if hasattr(self, "_rbufs"):
+            del self._rbufs, self._rsink
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
 
@@ -795,42 +906,58 @@ def parallelism_desc(step, policy):
             "replicated)")
 
 
-def config5_record(P, rank, g, device, rehearsal, steps, warmup):
-    """BASELINE config 5 at P > 1: the 80-layer Llama-3-70B linear step (321 launches, 43.4 GB of
-    int4 weights per token) under the fixed Megatron plan of DESIGN §6 (wqkv colwise -> wo
-    rowwise + all-reduce, w1||w3 colwise -> w2 rowwise + all-reduce, output head colwise +
-    all-gather: ~1/P of the weights per rank), the collectives captured in the step's graph.
-    Times the whole step (driver contract: barrier, max over ranks), the GEMV-only graph and the
+def config5_record(P, rank, g, device, rehearsal, steps, warmup, policy="tp"):
+    """BASELINE config 5: the 80-layer Llama-3-70B linear step (321 launches, 43.4 GB of int4
+    weights per token). At P = 1 every linear runs whole on the one GPU (43 GB fit in 288 GB of
+    HBM): the curve's 1-GPU anchor. At P > 1 one of two plans:
+      * policy "tp" (Megatron pairs; test_affine_quantized_tensor_parallel.py:49-80):
+        wqkv colwise -> wo rowwise + all-reduce, w1||w3 colwise -> w2 rowwise + all-reduce,
+        output head colwise + all-gather;
+      * policy "all" (the north star's plan): every linear column-sharded, its output
+        all-gathered over RCCL.
+    ~1/P of the weights per rank either way, the collectives captured in the step's graph. Times
+    the whole step (driver contract: barrier, max over ranks), the GEMV-only graph and the
     collectives-only graph separately."""
     _, cfg = MODELS["70b"]
     lins = llama_linears(cfg)
-    st = LinearStep(lins, shard_kinds(lins, P, g, "tp", {}), P, rank, g, device, rehearsal)
+    kinds = shard_kinds(lins, P, g, policy, {}) if P > 1 else ["whole"] * len(lins)
+    st = LinearStep(lins, kinds, P, rank, g, device, rehearsal)
     t_build = time.perf_counter()
     graph = st.try_capture()
     ms = st.wall_ms(graph.replay if graph is not None else st.step, steps, warmup)
-    ggemv = st.try_capture(do_comm=False)
-    gemv_ms = st.replay_ms(ggemv, max(steps, 5)) if ggemv is not None else None
-    gcomm = st.try_capture(do_gemv=False)
-    comm_ms = st.wall_ms(gcomm.replay if gcomm is not None else (lambda: st.step(do_gemv=False)),
-                         steps, 2)
+    gemv_ms = comm_ms = None
+    if P > 1:
+        ggemv = st.try_capture(do_comm=False)
+        gemv_ms = st.replay_ms(ggemv, max(steps, 5)) if ggemv is not None else None
+        gcomm = st.try_capture(do_gemv=False)
+        comm_ms = st.wall_ms(gcomm.replay if gcomm is not None
+                             else (lambda: st.step(do_gemv=False)), steps, 2)
+        del ggemv, gcomm
+    elif graph is not None:
+        gemv_ms = st.replay_ms(graph, max(steps, 5))
+    plan = ("single GPU: every linear whole" if P == 1 else
+            "Megatron pairs + head all-gather" if policy == "tp" else
+            "north star: every linear column-sharded + RCCL all-gather of its output")
     rec = {
         "workload": f"Llama-3-70B int4 g{g} weight-only linears, M=1 decode: "
                     + workload_desc(cfg) + f" ({len(st.plan)} GEMV launches/step)",
+        "plan": plan,
         "value": round(st.bytes_per_step / (ms * 1e-3) / 1e9, 2),
         "unit": "GB/s",
         "linear_steps_per_s": round(1e3 / ms, 2),
         "ms_per_step": round(ms, 4),
         "gemv_ms_per_step": round(gemv_ms, 4) if gemv_ms is not None else None,
-        "collectives_ms_per_step": round(comm_ms, 4),
+        "collectives_ms_per_step": round(comm_ms, 4) if comm_ms is not None else 0.0,
         "bytes_per_step": st.bytes_per_step,
         "weight_bytes_per_rank": st.weight_bytes_per_rank,
-        "parallelism": parallelism_desc(st, "tp"),
+        "parallelism": parallelism_desc(st, policy) if P > 1 else "single-gpu",
+        "n_gpus": P,
         "hip_graph": graph is not None,
-        "collectives": "RCCL in the step graph" if graph is not None else
-                       ("host-staged gloo (rehearsal)" if rehearsal else "RCCL, eager"),
+        "collectives": ("none" if P == 1 else "RCCL in the step graph" if graph is not None else
+                        ("host-staged gloo (rehearsal)" if rehearsal else "RCCL, eager")),
         "scaling": "strong",
     }
-    del graph, ggemv, gcomm
+    del graph
     st.release()
     rec["setup_s"] = round(time.perf_counter() - t_build, 1)
     return rec
@@ -973,10 +1100,19 @@ def main():
             cnt = sum(1 for e in plan if (e[1], e[2]) == (n_loc, K))
             us = st.replay_ms(gs_, max(args.steps, 10)) * 1e3 / cnt
             b = int4_alg_bytes(n_loc, K, g)
+            gr_ = st.read_probe_graph(only=(n_loc, K))
+            rus = st.replay_ms(gr_, max(args.steps, 10)) * 1e3 / cnt
             per_shape_graph[f"{n_loc}x{K}"] = {
                 "launches": cnt, "us": round(us, 3), "GBps": round(b / (us * 1e-6) / 1e9, 1),
-                "frac": round(b / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)}
-            del gs_
+                "frac": round(b / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+                "pure_read_us": round(rus, 3), "gemv_over_pure_read": round(us / rus, 3)}
+            del gs_, gr_
+    pure_read_ms = None
+    if graph is not None and P == 1:
+        # the one-launch-per-linear floor of THIS step, measured now
+        gr = st.read_probe_graph()
+        pure_read_ms = st.replay_ms(gr, max(args.steps, 10))
+        del gr
 
     # HBM traffic from the committed counter pass (rocprofv3 --pmc FETCH_SIZE of this bench,
     # P = 1 shapes): bytes per step, to set against the algorithmic bytes
@@ -1022,9 +1158,14 @@ def main():
             and graph is not None:
         unfused = unfused_record(cfg, g, device, args.steps)
     config5 = None
-    if P > 1 and args.model == "8b" and not args.no_config5:
-        config5 = config5_record(P, rank, g, device, rehearsal, max(2, min(args.steps, 10)),
-                                 min(args.warmup, 2))
+    if args.model == "8b" and not args.no_config5:
+        # release the 8B step's weights first (the 70B step needs 43 GB / P per rank)
+        st.release()
+        c5 = dict(steps=max(2, min(args.steps, 10)), warmup=min(args.warmup, 2))
+        config5 = config5_record(P, rank, g, device, rehearsal, policy="tp", **c5)
+        if P > 1:
+            config5["north_star_plan"] = config5_record(P, rank, g, device, rehearsal,
+                                                        policy="all", **c5)
 
     cpu = None
     if rank == 0 and P == 1 and not args.no_cpu_baseline and args.model == "8b":
@@ -1073,6 +1214,11 @@ def main():
                 "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic else None,
                 "launches": len(durs),
                 "kernel_ms_per_step": round(kernel_ms, 4),
+                # the same launches as pure 16-B streaming reads of the same bytes, one graph
+                # (tao_hbm_read_probe): the floor of a one-kernel-per-linear step, this run
+                "pure_read_ms_per_step": round(pure_read_ms, 4) if pure_read_ms else None,
+                "gemv_over_pure_read": (round(kernel_ms / pure_read_ms, 3)
+                                        if pure_read_ms else None),
                 "eager_kernel_ms_per_step": round(sum(durs), 4),
                 "per_shape_eager": per_shape,
                 "per_shape_graph": per_shape_graph or None,
@@ -1084,17 +1230,19 @@ def main():
         ns = per_shape_graph.get("4096x4096") if per_shape_graph else None
         if ns is not None:
             # north_star (BASELINE.json): int4 g32 M=1 4096x4096 at >= 70% of HBM peak per
-            # launch; the graph-replayed in-step number (wo's shape at 8B), split into the
-            # kernel's own span (dispatch-packet events of the eager step's launches of this
-            # shape) and the launch-to-launch gap the graph leaves between kernels
-            span = per_shape.get("4096x4096", {}).get("us")
+            # launch; the graph-replayed in-step number (wo's shape at 8B) beside a pure 16-B
+            # read of the same 10.5 MB replayed the same way (the floor of one dependent launch
+            # on this chip, DESIGN §5.1: launch gap ~1.35 us + one loaded HBM round trip)
             rec["north_star"] = {"shape": f"4096x4096 int4 g{g} M=1",
                                  "us_per_launch": ns["us"], "GBps": ns["GBps"],
                                  "frac": ns["frac"], "target_frac": 0.70, "met": ns["frac"] >= 0.70,
-                                 "kernel_span_us": span,
-                                 "launch_gap_us": round(ns["us"] - span, 3) if span else None,
-                                 "span_frac": (round(int4_alg_bytes(4096, 4096, g) / (span * 1e-6)
-                                                     / 1e9 / HBM_PEAK_GBPS, 4) if span else None)}
+                                 "pure_read_us": ns.get("pure_read_us"),
+                                 "pure_read_frac": (round(int4_alg_bytes(4096, 4096, g)
+                                                          / (ns["pure_read_us"] * 1e-6) / 1e9
+                                                          / HBM_PEAK_GBPS, 4)
+                                                    if ns.get("pure_read_us") else None),
+                                 "gemv_over_pure_read": ns.get("gemv_over_pure_read"),
+                                 "eager_kernel_us": per_shape.get("4096x4096", {}).get("us")}
         if unfused is not None:
             # the reference's module layout (w1, w3 apart): the same bytes in 161 launches
             rec["unfused_w13_step"] = unfused

@@ -136,20 +136,6 @@ int tao_tune_int4_mfma32(int on);
  * built-in, else the largest power of two <= splits (<= 16). Calling thread only. */
 int tao_tune_gemm_tile(int mode, int splits);
 
-/* Tuning hook: the unsplit "stream" prefill GEMM (gemm_stream.hip: 32 x 64 tiles, wave-private
- * LDS-DMA weight streams, x in double-buffered 1-KiB-per-row phases) for the int4 weight-only and
- * int8 dynamic linears. mode 0 = built-in routing (M in [33, 256] with N % 64 == 0 and K a multiple
- * of 512 (int4) / 1024 (int8)), 1 = never, 2 = wherever the shape is supported, 4 / 5 = as 2 with
- * each workgroup walking the K phases from a start rotated by its M tile (4) or its M and N
- * tiles (5). Thread-local. */
-int tao_tune_gemm_stream(int mode);
-/* The k-split prefill GEMM (gemm_ksplit.hip: an unsplit 32 x 64 tile per workgroup whose waves
- * split K, operands loaded straight into MFMA fragments, partials summed through LDS in wave
- * order) for the int4 weight-only and int8 dynamic linears. mode 0 = built-in routing, 1 = never,
- * 2 = wherever the shape is supported. shape: 0 built-in, 1 = 32 x 64 output tile, 2 = 64 x 32,
- * 3 = 128 x 16, 4 = 128 x 16 on 16 waves (int8) / 32 x 64 with one k-block in flight (int4);
- * + 16: each workgroup walks its k-blocks from a rotated start. Thread-local. */
-int tao_tune_gemm_ksplit(int mode, int shape);
 /* The single-fetch prefill GEMM (csrc/gemm_sf.hip: 128-row tiles so each weight tile is fetched by
  * one workgroup, 8 waves, both operands by LDS-DMA in full lines, K split over workgroups with a
  * fixed reducer) for the int4 weight-only and int8 dynamic linears. mode 0 = built-in routing,
@@ -161,6 +147,11 @@ int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages, int a_ste
 /* Reducer poll timeouts of the single-fetch GEMM since the last call (*bits != 0: some split
  * launch's outputs are invalid; never expected, see gemm_sf.hip). Synchronous. */
 int tao_gemm_sf_status(unsigned* bits);
+
+/* Measurement kernel (bench.py, not the product path): a pure streaming read of `bytes` (a
+ * positive multiple of 8192) from `buf` (16-B aligned) with 16-B non-temporal loads; `sink` is
+ * >= 4 KiB of device memory the kernel may write (it never does in practice). Graph-capturable. */
+int tao_hbm_read_probe(const void* buf, int64_t bytes, void* sink, void* stream);
 /* Number of split-K workspaces currently owned by captured graphs (each is released with its
  * graph). Diagnostic for tests; never fails. */
 int tao_graph_workspace_count(void);
@@ -237,50 +228,6 @@ int tao_dequantize_tensor_core_tiled_layout(const int32_t* packed_w,
  * torchao/dtypes/uintx/tensor_core_tiled_layout.py:279). K % (ikt*16) == 0. */
 int tao_pack_tensor_core_tiled_layout(const int32_t* q, int32_t* packed_w, int64_t N, int64_t K,
                                       int64_t inner_k_tiles, int tile_format, void* stream);
-
-/* ---- persistent decode chain (csrc/decode_chain.hip) ----------------------------------------
- * A sequence of dependent M = 1 int4 weight-only linears run by ONE launch (one workgroup per
- * CU, flag-chained phases; each workgroup issues its share of phase p+1's weight loads before
- * it waits for phase p's output). Phase p computes
- *     y = epilogue( [RMSNorm(x) if norm_w] @ dequant(packed, sz)^T ) [+ residual]
- * with the bf16 roundings of the unfused ops (tao_rmsnorm_bf16 -> tao_int4wo_linear_bf16 with
- * the residual as bias; epilogue 1 = SwiGLU over row pairs (2i, 2i+1) as tao_silu_mul_bf16).
- * x_phase names the earlier phase that writes x (its y buffer), or -1 for a vector written
- * before the launch. Replaces, for a Llama decode step, the per-linear
- * aten._weight_int4pack_mm calls (torchao/dtypes/uintx/tensor_core_tiled_layout.py:104) the
- * reference's model issues layer by layer (torchao/_models/llama/model.py:397-486). */
-typedef struct TaoChainPhase {
-  const uint32_t* packed;   /* [N][K/8] gfx950 row-stream int4 */
-  const uint16_t* sz;       /* [N][K/g][2] bf16 (scale, zero) */
-  const uint16_t* x;        /* [K] bf16 input (16-B aligned) */
-  const uint16_t* norm_w;   /* [K] RMSNorm weight, or NULL */
-  const uint16_t* residual; /* [N] (epilogue 1: [N/2]) bf16 added to the output, or NULL */
-  uint16_t* y;              /* [N] (epilogue 1: [N/2]) bf16 output (8-B aligned) */
-  int64_t N;                /* multiple of 4 */
-  int64_t K;                /* multiple of group_size, <= 32768 */
-  int64_t group_size;       /* 32, 64, 128, 256 */
-  int32_t x_phase;          /* earlier phase producing x, or -1 */
-  int32_t epilogue;         /* 0 = none, 1 = SwiGLU */
-  float eps;                /* RMSNorm epsilon */
-  int32_t reserved;
-} TaoChainPhase;
-
-/* Validate the phases, copy them to the device and allocate the chain's counters. The buffers
- * the phases name must outlive the handle; the handle is bound to the current device. */
-int tao_chain_create(const TaoChainPhase* phases, int n_phases, void** handle);
-/* Enqueue one run of the whole chain on `stream` (graph-capturable; no host sync). */
-int tao_chain_run(void* handle, void* stream);
-/* Synchronous status: aborted_phase = 0 if no wait timed out, else the phase index + 1 whose
- * input never arrived (the run's outputs are then invalid; call tao_chain_reset). launches =
- * runs completed. */
-int tao_chain_status(void* handle, int* aborted_phase, unsigned* launches);
-/* Device synchronise and zero the counters (after an abort). */
-int tao_chain_reset(void* handle);
-int tao_chain_destroy(void* handle);
-/* Measurement: later runs write per (phase, workgroup) wall-clock stamps (100 MHz) into the
- * device buffer `stamps` [n_phases][grid][4] = {phase start, input ready, tasks done,
- * signalled}; NULL turns it off. *grid receives the workgroup count. */
-int tao_chain_profile(void* handle, uint64_t* stamps, int* grid);
 
 /* ---- int8 weight-only ---------------------------------------------------------------------- */
 

@@ -56,19 +56,6 @@ int tile_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const u
                  const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream,
                  int splits);
 bool use_tile(int path, int64_t M, int64_t N, int64_t K);
-// gemm_stream.hip: the unsplit 32 x 64 tile with wave-private weight streams and its routing rule
-int stream_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int gshift,
-                const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream);
-int stream_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uint16_t* ws,
-                   const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream);
-bool use_stream(int path, int64_t M, int64_t N, int64_t K, int64_t group_size);
-// gemm_ksplit.hip: the unsplit 32 x 64 tile whose waves split K (register fragments, no LDS
-// staging in the k loop) and its routing rule
-int ksplit_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int gshift,
-                const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream);
-int ksplit_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uint16_t* ws,
-                   const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream);
-bool use_ksplit(int path, int64_t M, int64_t N, int64_t K, int64_t group_size);
 // gemm_sf.hip: the single-fetch prefill GEMM (128-row tiles, LDS-DMA, fixed-reducer split-K)
 bool use_sf(int path, int64_t M, int64_t N, int64_t K, int64_t group_size);
 int sf_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uint16_t* ws,
@@ -1522,8 +1509,6 @@ int int8_scaled_mm_launch(const int8_t* xq, const uint16_t* xs, const int8_t* wq
   // M = 128 N = 6144 14.9 vs 20.0 µs, M = 256 4096^2 14.8 vs 16.5, M = 512 22.5 vs 30.8; ties at
   // N >= 14336; the per-wave-column kernel keeps M = 64..128 at N = 4096 (11.8 vs 12.6 µs).
   if (use_sf(2, M, N, K, 0)) return sf_int8dyn(xq, xs, wq, ws, bias, y, M, N, K, stream);
-  if (use_ksplit(2, M, N, K, 0)) return ksplit_int8dyn(xq, xs, wq, ws, bias, y, M, N, K, stream);
-  if (use_stream(2, M, N, K, 0)) return stream_int8dyn(xq, xs, wq, ws, bias, y, M, N, K, stream);
   if (use_tile(2, M, N, K))
     return tile_int8dyn(xq, xs, wq, ws, bias, y, M, N, K, stream, tuning().tile_splits);
   const int algo = tao::tuning().gemm_algo;
@@ -1553,12 +1538,6 @@ extern "C" int tao_int4wo_linear_bf16(const uint16_t* x, const uint32_t* packed,
   if (tao::use_sf(0, M, N, K, group_size))
     return tao::sf_int4(x, packed, sz, tao::gshift_of(group_size) + 5, bias, y, (int)M, (int)N,
                         (int)K, st);
-  if (tao::use_ksplit(0, M, N, K, group_size))
-    return tao::ksplit_int4(x, packed, sz, tao::gshift_of(group_size), bias, y, (int)M, (int)N,
-                            (int)K, st);
-  if (tao::use_stream(0, M, N, K, group_size))
-    return tao::stream_int4(x, packed, sz, tao::gshift_of(group_size), bias, y, (int)M, (int)N,
-                            (int)K, st);
   if (tao::use_tile(0, M, N, K))
     return tao::tile_int4(x, packed, sz, tao::gshift_of(group_size), bias, y, (int)M, (int)N,
                           (int)K, st, tao::tuning().tile_splits);

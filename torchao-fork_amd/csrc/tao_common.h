@@ -67,10 +67,6 @@ struct Tuning {
   int int4_mfma32 = 0;                           // int4 GEMM on 32x32x16 MFMAs: 0 off, 1 on
   int quant_block = 0;                           // per-token int8 quant: 0 wave kernel, 1 block
   int gemm_tile = 0, tile_splits = 0;            // weight-shared tile GEMM: 0 auto, 1 off, 2 on
-  int gemm_stream = 0;                           // stream tile GEMM (gemm_stream.hip): 0 auto, 1 off, 2 on
-  int gemm_stream_rot = 0;                       // stream tile GEMM phase rotation: 0, 1 (M tile), 2 (+N)
-  int gemm_ksplit = 0, gemm_ksplit_shape = 0;    // k-split tile GEMM: 0 auto, 1 off, 2 on; shape
-  int gemm_ksplit_rot = 0;                       // k-split: rotated block order per workgroup
   int gemm_sf = 0;                               // single-fetch GEMM: 0 auto, 1 off, 2 on
   int sf_bn = 0, sf_wm = 0, sf_splits = 0;       // single-fetch GEMM shape overrides
   int sf_stages = 0, sf_a_steps = 0, sf_ks = 0;

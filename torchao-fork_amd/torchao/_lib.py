@@ -50,10 +50,9 @@ _SIGNATURES = {
     "tao_tune_splitk_fenced": [_int],
     "tao_query_splitk_fenced": [],
     "tao_tune_gemm_tile": [_int, _int],
-    "tao_tune_gemm_stream": [_int],
-    "tao_tune_gemm_ksplit": [_int, _int],
     "tao_tune_gemm_sf": [_int, _int, _int, _int, _int, _int, _int],
     "tao_gemm_sf_status": [_p],
+    "tao_hbm_read_probe": [_p, _i64, _p, _p],
     "tao_graph_workspace_count": [],
     "tao_int4_pack": [_p, _p, _i64, _i64, _p],
     "tao_int4_pack_u8": [_p, _p, _i64, _i64, _p],
@@ -82,12 +81,6 @@ _SIGNATURES = {
                                 ctypes.c_float, _p, _p, _int, _int, _p],
     "tao_tune_attn": [_int],
     "tao_decode_status": [_p],
-    "tao_chain_create": [_p, _int, _p],
-    "tao_chain_run": [_p, _p],
-    "tao_chain_status": [_p, _p, _p],
-    "tao_chain_reset": [_p],
-    "tao_chain_destroy": [_p],
-    "tao_chain_profile": [_p, _p, _p],
     "tao_silu_mul_bf16": [_p, _p, _p, _i64, _p],
     "tao_argmax_bf16": [_p, _p, _i64, _i64, _p],
     "tao_argmax_advance_bf16": [_p, _i64, _p, _p, _p, _i64, _p],

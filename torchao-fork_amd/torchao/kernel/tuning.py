@@ -32,8 +32,6 @@ _KNOBS = {
     "attn": ("tao_tune_attn", 1),
     "splitk_fenced": ("tao_tune_splitk_fenced", 1),
     "gemm_tile": ("tao_tune_gemm_tile", 2),
-    "gemm_stream": ("tao_tune_gemm_stream", 1),
-    "gemm_ksplit": ("tao_tune_gemm_ksplit", 2),
     "gemm_sf": ("tao_tune_gemm_sf", 7),
 }
 
