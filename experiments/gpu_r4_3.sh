@@ -1,0 +1,21 @@
+#!/bin/bash
+cd "$(dirname "$0")/.." || exit 1
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_gemm_sf.py > gpurun_out/r4_sf_tests2.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/r4_sf_tests2.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_llama_harness.py -k "attn_prefill or add_rmsnorm or config" > gpurun_out/r4_attn_tests.log 2>&1
+rc=$?; echo "attn tests rc=$rc"; tail -2 gpurun_out/r4_attn_tests.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 5 ]; then exit $rc; fi
+timeout -k 10 300 python -u experiments/sweep_sf.py --out gpurun_out/r4_sf_sweep2.jsonl > gpurun_out/r4_sf_sweep2.log 2>&1
+rc=$?; echo "sweep rc=$rc"
+[ $rc -eq 0 ] || exit $rc
+TORCHAO_MI355X_LIB=experiments/build/libsfst.so timeout -k 10 240 python -u experiments/sf_stamps.py > gpurun_out/r4_sf_stamps.log 2>&1
+rc=$?; echo "stamps rc=$rc"; tail -3 gpurun_out/r4_sf_stamps.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 240 python -u experiments/ref_prefill.py > gpurun_out/r4_ref_prefill.log 2>&1
+rc=$?; echo "ref rc=$rc"; tail -2 gpurun_out/r4_ref_prefill.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u experiments/ab_fenced.py > gpurun_out/r4_ab_fenced.log 2>&1
+rc=$?; echo "fenced rc=$rc"; tail -2 gpurun_out/r4_ab_fenced.log
+exit $rc

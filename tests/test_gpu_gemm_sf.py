@@ -89,8 +89,10 @@ def test_sf_int8dyn_extreme_values(sf):
 
 
 # (bn, wm, splits, stages, a_steps)
+# wm 1: the 32x32x16 kernel (gemm_sf32.hip), 2 or 4 waves of 128 x 32
 I4_CFGS = [(64, 2, 4, 3, 0), (64, 4, 4, 3, 0), (64, 8, 2, 2, 0), (128, 2, 8, 2, 0),
-           (128, 4, 8, 3, 0), (128, 2, 1, 3, 0), (64, 2, 4, 4, 0)]
+           (128, 4, 8, 3, 0), (128, 2, 1, 3, 0), (64, 2, 4, 4, 0), (128, 1, 8, 2, 0),
+           (128, 1, 4, 3, 0), (128, 1, 1, 3, 0), (64, 1, 4, 2, 0), (64, 1, 2, 3, 0)]
 I4_SHAPES = [(128, 4096, 4096), (17, 128, 1024), (100, 640, 4096), (128, 512, 14336),
              (200, 192, 2048), (64, 96, 768)]
 
@@ -110,7 +112,8 @@ def test_sf_int4(sf, M, N, K, cfg):
 
 
 @pytest.mark.parametrize("g", [64, 128, 256])
-@pytest.mark.parametrize("cfg", [(64, 2, 4, 3, 0), (128, 4, 8, 2, 0)])
+@pytest.mark.parametrize("cfg", [(64, 2, 4, 3, 0), (128, 4, 8, 2, 0), (128, 1, 4, 2, 0),
+                                 (64, 1, 2, 3, 0)])
 def test_sf_int4_group_sizes(sf, g, cfg):
     """g = 64 / 128 / 256: the (scale, zero) image holds, per 32-k lane group, the word
     ((128 st) >> lg) + ((32 q) >> lg)."""
@@ -132,11 +135,12 @@ def test_sf_asymmetric_slices(sf, a_steps):
     xq, xs, wq, ws = _int8(M, N, K, seed=11)
     y = torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), None).cpu()
     assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="cpu"))
-    sf(2, 64, 2, 4, 3, a_steps)
     q, s, z, packed, sz = _int4(N, K, 32, seed=12)
     x = oracle.make_activation(M, K, seed=13)
-    y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, 32, None).cpu()
-    assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, 32)) < TOL_FP32
+    for wm in (2, 1):
+        sf(2, 64, wm, 4, 3, a_steps)
+        y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, 32, None).cpu()
+        assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, 32)) < TOL_FP32
 
 
 def test_sf_deterministic_fenced_and_matches_old_kernel(sf):

@@ -386,7 +386,7 @@ def test_attn_decode_weight_prefetch_gpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("G", [1, 4, 8])
 @pytest.mark.parametrize("S,p0,T", [(1, 0, 64), (7, 0, 64), (128, 0, 328), (33, 37, 128),
-                                    (200, 50, 1024)])
+                                    (200, 50, 1024), (1536, 0, 2048), (17, 1000, 1100)])
 def test_attn_prefill_gpu(G, S, p0, T):
     """tao_attn_prefill_bf16: S queries at positions p0 .. p0 + S - 1 against the cache keys
     0..pos (the causal mask of gpt-fast's prefill over the caches), GQA, vs fp32 SDPA with that

@@ -18,6 +18,13 @@
 #include <atomic>
 
 #include "tao_common.h"
+
+namespace tao {
+// attn_mfma.hip: the MFMA prefill attention (tao_attn_prefill_bf16)
+int attn_prefill_mfma(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                      const int64_t* pos, uint16_t* out, int64_t B, int64_t H, int64_t Hkv,
+                      int64_t S, int64_t T, float scale, hipStream_t stream);
+}  // namespace tao
 #include "tao_reduce.h"
 
 #ifndef TAO_ATTN_WAVES
@@ -1260,13 +1267,12 @@ int tao_attn_prefill_bf16(const uint16_t* q, const uint16_t* k_cache, const uint
                 "attn_prefill: bad sizes");
   TAO_CHECK_ALIGN(q, 16, "q");
   TAO_CHECK_ALIGN(k_cache, 16, "k_cache");
-  TAO_CHECK_ALIGN(out, 4, "out");
-  // one workgroup of 8 waves per (batch, head, query): 128 keys per round, the causal prefix of
-  // a 128-token prompt in one load round trip
-  launch((tao::attn_single_kernel<128, 8, true>), dim3((unsigned)(B * H * S)), dim3(64 * 8), 0,
-         as_stream(stream), q, k_cache, v_cache, pos, out, (int)H, (int)Hkv, (int)T, scale, (int)S,
-         tao::AttnPf{});
-  return check_launch("attn_single_kernel<prefill>");
+  TAO_CHECK_ALIGN(out, 16, "out");
+  // MFMA flash-style kernel (attn_mfma.hip): a wave per 16 queries, K / V read once per block of
+  // 16 queries instead of once per query (the single-pass decode kernel generalised, which this
+  // replaces, re-read the prefix per query: 24 us per layer at S = 128)
+  return tao::attn_prefill_mfma(q, k_cache, v_cache, pos, out, B, H, Hkv, S, T, scale,
+                                as_stream(stream));
 }
 
 int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,

@@ -308,38 +308,62 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
     for (int b = 0; b < NT; ++b) acc[a][b] = Acc{0, 0, 0, 0};
 
   // ---- one step: fragments from stage `buf`, MFMAs -------------------------------------------------
+  // Every fragment read of the step is issued before the first MFMA (a sched_barrier keeps
+  // hipcc from interleaving them one read per MFMA, which exposed each ds_read's latency: one
+  // read in flight per wave, lgkmcnt(1) before every MFMA in the first build's ISA).
   auto compute = [&](int buf) __attribute__((always_inline)) {
     const uint4* img = lds + buf * (STAGE / 16);
     if constexpr (kI8) {
       constexpr int G = P::kXRow / 16;  // granules per image row
+      i32x4_t bf[P::kKB][NT], af[P::kKB][MT];
 #pragma unroll
       for (int kb = 0; kb < P::kKB; ++kb) {
         const int g = P::agran(kb, kq);
-        i32x4_t bf[NT];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
           const int n = wn * CN + 16 * nt + fr;
-          bf[nt] = __builtin_bit_cast(i32x4_t, img[XB / 16 + n * G + P::xpos(n, g)]);
+          bf[kb][nt] = __builtin_bit_cast(i32x4_t, img[XB / 16 + n * G + P::xpos(n, g)]);
         }
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int m = wm * RM + 16 * mt + fr;
-          const i32x4_t af = __builtin_bit_cast(i32x4_t, img[m * G + P::xpos(m, g)]);
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[nt], acc[mt][nt], 0, 0, 0);
+          af[kb][mt] = __builtin_bit_cast(i32x4_t, img[m * G + P::xpos(m, g)]);
         }
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kb = 0; kb < P::kKB; ++kb)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[mt][nt] =
+                __builtin_amdgcn_mfma_i32_16x16x64_i8(af[kb][mt], bf[kb][nt], acc[mt][nt], 0, 0, 0);
     } else {
       uint4 wv[NT];
-      float sc[NT], zc[NT];
+      uint32_t szw[NT];
+      bf16x8_t af[4][MT];
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int n = wn * CN + 16 * nt + fr;
         wv[nt] = img[XB / 16 + n * 4 + pos64(n, kq)];
-        const uint32_t szw = reinterpret_cast<const uint32_t*>(img)[(XB + WB) / 4 + n * 4 + posz(n, kq)];
-        sc[nt] = bf16lo_to_f32(szw);
-        zc[nt] = bf16hi_to_f32(szw) - 8.f * sc[nt];  // q*s + zc == (q - 8)*s + z
+        szw[nt] = reinterpret_cast<const uint32_t*>(img)[(XB + WB) / 4 + n * 4 + posz(n, kq)];
+      }
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const int g = P::agran(kb, kq);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const int m = wm * RM + 16 * mt + fr;
+          af[kb][mt] = __builtin_bit_cast(bf16x8_t, img[m * 16 + P::xpos(m, g)]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      float sc[NT], zc[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        sc[nt] = bf16lo_to_f32(szw[nt]);
+        zc[nt] = bf16hi_to_f32(szw[nt]) - 8.f * sc[nt];  // q*s + zc == (q - 8)*s + z
       }
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
@@ -349,15 +373,12 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
           const uint32_t wd = kb == 0 ? wv[nt].x : kb == 1 ? wv[nt].y : kb == 2 ? wv[nt].z : wv[nt].w;
           bf[nt] = deq8(wd, sc[nt], zc[nt]);
         }
-        const int g = P::agran(kb, kq);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const int m = wm * RM + 16 * mt + fr;
-          const bf16x8_t af = __builtin_bit_cast(bf16x8_t, img[m * 16 + P::xpos(m, g)]);
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[nt], acc[mt][nt], 0, 0, 0);
-        }
+            acc[mt][nt] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kb][mt], bf[nt], acc[mt][nt], 0, 0, 0);
       }
     }
   };
@@ -657,9 +678,16 @@ int sf_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uin
   return run(pol, sh.a_steps);
 }
 
+int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
+              const uint16_t* bias, uint16_t* y, int M, int N, int K, int bn, int splits,
+              int stages, int a_steps, hipStream_t stream);
+
 int sf_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
             const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream) {
   const SfShape sh = sf_shape(0, M, N, K);
+  if (sh.wm == 1)  // one wave along M: the 32x32x16 kernel (gemm_sf32.hip)
+    return sf32_int4(x, packed, sz, lg, bias, y, M, N, K, sh.bn, sh.splits, sh.stages,
+                     tuning().sf_a_steps, stream);
   const dim3 grid((N + sh.bn - 1) / sh.bn, sh.splits, (M + kBM - 1) / kBM);
   f32x4_t* slab = nullptr;
   unsigned* cnt = nullptr;
@@ -691,7 +719,8 @@ extern "C" int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages
                                 int ks) {
   TAO_CHECK_ARG(mode >= 0 && mode <= 2, "tune: gemm_sf mode must be 0, 1 or 2");
   TAO_CHECK_ARG(bn == 0 || bn == 32 || bn == 64 || bn == 128, "tune: gemm_sf bn must be 0, 32, 64, 128");
-  TAO_CHECK_ARG(wm == 0 || wm == 2 || wm == 4 || wm == 8, "tune: gemm_sf wm must be 0, 2, 4 or 8");
+  TAO_CHECK_ARG(wm == 0 || wm == 1 || wm == 2 || wm == 4 || wm == 8,
+                "tune: gemm_sf wm must be 0, 1 (int4: the 32x32x16 kernel), 2, 4 or 8");
   TAO_CHECK_ARG(splits >= 0 && splits <= 16, "tune: gemm_sf splits must be in [0, 16]");
   TAO_CHECK_ARG(stages == 0 || (stages >= 2 && stages <= 4), "tune: gemm_sf stages must be 0, 2, 3, 4");
   TAO_CHECK_ARG(a_steps >= 0, "tune: gemm_sf a_steps must be >= 0");
@@ -709,13 +738,17 @@ extern "C" int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages
 
 // Reducer poll timeouts since the last call (0 = none; a nonzero value means some outputs of a
 // split launch were invalid). Synchronous; not capturable.
+namespace tao {
+int sf32_status(unsigned* bits);
+}
+
 extern "C" int tao_gemm_sf_status(unsigned* bits) {
   unsigned v = 0, zero = 0;
   if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(tao::g_sf_err), sizeof(v)) != hipSuccess ||
       hipMemcpyToSymbol(HIP_SYMBOL(tao::g_sf_err), &zero, sizeof(zero)) != hipSuccess)
     return tao::set_error(TAO_ERR_HIP, "gemm_sf status: symbol copy failed");
   *bits = v;
-  return TAO_OK;
+  return tao::sf32_status(bits);
 }
 
 #if TAO_SF_STAMPS

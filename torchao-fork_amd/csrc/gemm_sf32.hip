@@ -1,0 +1,357 @@
+// Single-fetch int4 prefill GEMM on 32x32x16 MFMAs (the int4 member of the gemm_sf family):
+//   y[M][N] = bf16( x[M][K] . dequant(W)[N][K]^T ) (+ bias),  bf16 x, int4 row-stream W,
+//   B = bf16(fma(q, s, z - 8 s)) as the reference's dequantised weight.
+// Replaces aten._weight_int4pack_mm (tensor_core_tiled_layout.py:104) at prefill sizes.
+//
+// gemm_sf.hip's 16x16x32 int4 tile was bound by its per-wave work, not memory: with 8 waves in a
+// 2 (M) x 4 (N) layout every B fragment was dequantised twice (~14 VALU per 8 weights, partly
+// v_pk_fma_f32, which stalls beside MFMAs) and every A fragment read from LDS fed 1-2 MFMAs. Here
+// each wave owns a 128-row x 32-column output tile (4 accumulators of v_mfma_f32_32x32x16_bf16):
+//   * a B fragment (8 weights per lane) is dequantised once per workgroup and feeds 4 MFMAs;
+//   * an A fragment read (16 B per lane, 1 KiB per wave) feeds one 32x32x16 MFMA (2x the MACs of
+//     a 16x16x32), so LDS bytes per MAC halve;
+//   * the k order inside a 128-k step is permuted identically for A and B: lane half h owns k
+//     64 h .. 64 h + 63 and MFMA ks takes k 64 h + 8 ks + j, so a lane's B operand for the whole
+//     step is 32 contiguous nibble bytes of its column (two ds_read_b128) and its (scale, zero)
+//     words are those of groups 2 h and 2 h + 1 of the step (one ds_read_b64);
+//   * WV waves (2 or 4) = BN / 32 columns, one wave per SIMD: latency is covered by the LDS-DMA
+//     ring (NS stages, counted vmcnt, barriers that do not drain it), not by occupancy.
+// Images (16-B granule swizzles; each an involution, so a DMA lane filling position p fetches
+// granule pos(row, p)): x [128][256 B] at g ^ (r & 15); W [BN][64 B] at g ^ ((n >> 2) & 3);
+// (scale, zero) [BN][4 dwords] at q ^ (2 ((n >> 4) & 1)). All fragment reads conflict-free
+// (tests/test_host_cpu.py checks the bank map).
+// K split S ways with gemm_sf.hip's fixed-reducer hand-off (sc1 slabs + ticket, slice S - 1 sums
+// in slice order).
+#include <type_traits>
+
+#include "tao_common.h"
+
+namespace tao {
+namespace {
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kBM = 128;
+constexpr int kXRow = 256, kWRow = 64, kZRow = 16;  // bytes per row per 128-k step
+
+__device__ unsigned g_sf32_err = 0;
+
+template <int I, int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    sfor<I + 1, N>(f);
+  }
+}
+
+__device__ __forceinline__ uint32_t pkb(float lo, float hi) {
+  const f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+__device__ __forceinline__ int xpos(int row, int g) { return g ^ (row & 15); }
+__device__ __forceinline__ int wpos(int row, int g) { return g ^ ((row >> 2) & 3); }
+__device__ __forceinline__ int zpos(int row, int q) { return q ^ (((row >> 4) & 1) << 1); }
+
+// 8 nibbles of a row-stream dword -> bf16(fma(q, s, zc)) in k order; scalar fmas (v_pk_fma_f32
+// beside MFMAs costs ~22 extra cycles each: MI355X_MICROARCH.md cycle table)
+__device__ __forceinline__ bf16x8_t deq8s(uint32_t w, float sc, float zc) {
+  const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
+  const f32x2_t q04 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(lo, 512.f, false);
+  const f32x2_t q15 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(lo, 512.f, true);
+  const f32x2_t q26 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, false);
+  const f32x2_t q37 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, true);
+  const float w0 = __builtin_fmaf(q04[0], sc, zc), w4 = __builtin_fmaf(q04[1], sc, zc);
+  const float w1 = __builtin_fmaf(q15[0], sc, zc), w5 = __builtin_fmaf(q15[1], sc, zc);
+  const float w2 = __builtin_fmaf(q26[0], sc, zc), w6 = __builtin_fmaf(q26[1], sc, zc);
+  const float w3 = __builtin_fmaf(q37[0], sc, zc), w7 = __builtin_fmaf(q37[1], sc, zc);
+  const u32x4_t v = {pkb(w0, w1), pkb(w2, w3), pkb(w4, w5), pkb(w6, w7)};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_ahead(int ahead) {
+  switch (ahead) {
+    case 0: wait_vmcnt<0>(); break;
+    case 1: wait_vmcnt<N>(); break;
+    default: wait_vmcnt<2 * N>(); break;
+  }
+}
+
+template <int WV, int NS>
+__global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
+    const uint16_t* __restrict__ x, const uint32_t* __restrict__ wq, const uint32_t* __restrict__ sz,
+    int lg, const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K,
+    int a_steps, f32x16_t* __restrict__ slab, unsigned* __restrict__ cnt, int fenced) {
+  constexpr int BN = 32 * WV;
+  constexpr int XB = kBM * kXRow, WB = BN * kWRow, ZB = BN * kZRow;
+  constexpr int STAGE = XB + WB + ZB;
+  constexpr int PX = XB / 1024, PW = WB / 1024, PZ = ZB / 256;
+  constexpr int T = PX + PW + PZ;
+  static_assert(T % WV == 0 && PX % WV == 0 && (PW + PZ) % WV == 0, "DMA pieces per wave");
+  constexpr int R = T / WV;
+  static_assert(NS * STAGE <= 160 * 1024 && kBM * BN * 2 <= NS * STAGE, "LDS");
+  __shared__ uint4 lds[NS * STAGE / 16];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, h = lane >> 5;
+  const int n_blk = blockIdx.x * BN, m_blk = blockIdx.z * kBM;
+  const int S = gridDim.y, z = blockIdx.y;
+  const bool reducer = z == S - 1;
+  const int nsteps = K / 128;
+  const int s0 = z * a_steps;
+  const int J = reducer ? nsteps - s0 : a_steps;
+  const uint32_t row_bytes = (uint32_t)K * 2;
+
+  const Rsrc xrs = make_rsrc(x, (uint32_t)M * row_bytes);
+  const Rsrc wrs = make_rsrc(wq, (uint32_t)N * (uint32_t)(K >> 1));
+  const Rsrc zrs = make_rsrc(sz, (uint32_t)N * (uint32_t)(K >> lg) * 4u);
+  uint32_t dv[R];
+  int dd[R], dk[R];
+  sfor<0, R>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    if constexpr (r < PX / WV) {  // x: 4 rows x 256 B
+      const int i = r * WV + wave;
+      const int row = 4 * i + (lane >> 4), p = lane & 15;
+      const int gm = m_blk + row < M ? m_blk + row : M - 1;
+      dv[r] = (uint32_t)gm * row_bytes + 16u * (uint32_t)xpos(row, p);
+      dd[r] = i * 1024;
+      dk[r] = 0;
+    } else {
+      const int i = (r - PX / WV) * WV + wave;
+      const int row = 16 * (i < PW ? i : i - PW) + (lane >> 2), p = lane & 3;
+      const int gn = n_blk + row < N ? n_blk + row : N - 1;
+      if (i < PW) {  // W: 16 rows x 64 B
+        dv[r] = (uint32_t)gn * (uint32_t)(K >> 1) + 16u * (uint32_t)wpos(row, p);
+        dd[r] = XB + i * 1024;
+        dk[r] = 1;
+      } else {  // (scale, zero): 16 rows x 4 dwords, 4-B DMA; dword q = group of k 32 q
+        const int q = zpos(row, p);
+        dv[r] = ((uint32_t)gn * (uint32_t)(K >> lg) + (uint32_t)((32 * q) >> lg)) * 4u;
+        dd[r] = XB + WB + (i - PW) * 256;
+        dk[r] = 2;
+      }
+    }
+  });
+  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+    uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * STAGE;
+    sfor<0, R>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      if constexpr (r < PX / WV) {
+        dma_lds<16>(xrs, dv[r], (uint32_t)st * kXRow, base + dd[r]);
+      } else {
+        if (dk[r] == 1) dma_lds<16, kNT>(wrs, dv[r], (uint32_t)st * 64u, base + dd[r]);
+        else dma_lds<4, kNT>(zrs, dv[r], (uint32_t)(((128 * st) >> lg) * 4), base + dd[r]);
+      }
+    });
+  };
+
+  // bias of this lane's column (unconditional load: see gemm_sf.hip)
+  const int ncol = n_blk + 32 * wave + r32;
+  const uint16_t* bsrc = bias != nullptr ? bias : reinterpret_cast<const uint16_t*>(sz);
+  const float bsf = bf16_to_f32(bsrc[ncol < N ? ncol : N - 1]);
+
+  f32x16_t acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+
+  const int wrow = 32 * wave + r32;  // this lane's W row in the images
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const uint4* img = lds + buf * (STAGE / 16);
+    const uint4 b0 = img[XB / 16 + wrow * 4 + wpos(wrow, 2 * h)];
+    const uint4 b1 = img[XB / 16 + wrow * 4 + wpos(wrow, 2 * h + 1)];
+    const uint32_t* zi = reinterpret_cast<const uint32_t*>(img) + (XB + WB) / 4 + wrow * 4;
+    const uint32_t z0 = zi[zpos(wrow, 2 * h)], z1 = zi[zpos(wrow, 2 * h + 1)];
+    const float s0f = bf16lo_to_f32(z0), s1f = bf16lo_to_f32(z1);
+    const float c0 = bf16hi_to_f32(z0) - 8.f * s0f, c1 = bf16hi_to_f32(z1) - 8.f * s1f;
+    const uint32_t wd[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    // A fragments of ks and ks + 1 in flight while ks's MFMAs run
+    bf16x8_t af[2][4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int m = 32 * mt + r32;
+      af[0][mt] = __builtin_bit_cast(bf16x8_t, img[m * 16 + xpos(m, 8 * h)]);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      if (ks + 1 < 8) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const int m = 32 * mt + r32;
+          af[(ks + 1) & 1][mt] = __builtin_bit_cast(bf16x8_t, img[m * 16 + xpos(m, 8 * h + ks + 1)]);
+        }
+      }
+      const bf16x8_t bf = ks < 4 ? deq8s(wd[ks], s0f, c0) : deq8s(wd[ks], s1f, c1);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][mt], bf, acc[mt], 0, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < J) issue(s0 + p, p);
+  for (int j = 0; j < J; ++j) {
+    const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
+    wait_ahead<R>(ahead);
+    barrier_lgkm();
+    if (j + NS - 1 < J) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
+    compute(j % NS);
+  }
+  barrier_lgkm();
+
+  if (S > 1) {
+    constexpr uint32_t kSlice = kBM * BN * 4;
+    const unsigned tile = blockIdx.z * gridDim.x + blockIdx.x;
+    const Rsrc srs = make_rsrc(reinterpret_cast<const uint8_t*>(slab) + (size_t)tile * (S - 1) * kSlice,
+                               (uint32_t)(S - 1) * kSlice);
+    const uint32_t lo = (uint32_t)((wave * 4 * 64 + lane) * 64);  // 4 x 64 B per lane
+    unsigned* word = reinterpret_cast<unsigned*>(lds);
+    if (!reducer) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          bstore16<kSC1>(srs, lo + t * 64 * 64 + 16 * q, (uint32_t)z * kSlice,
+                         make_uint4(__float_as_uint(acc[t][4 * q]), __float_as_uint(acc[t][4 * q + 1]),
+                                    __float_as_uint(acc[t][4 * q + 2]),
+                                    __float_as_uint(acc[t][4 * q + 3])));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        if (fenced) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        (void)__hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (tid == 0) {
+      unsigned it = 0, ok = 1;
+      while (__hip_atomic_load(&cnt[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+             (unsigned)(S - 1)) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++it > (1u << 22)) {
+          ok = 0;
+          (void)__hip_atomic_fetch_or(&g_sf32_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      if (ok) __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (fenced) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *word = ok;
+    }
+    __syncthreads();
+    f32x16_t sum[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sum[t][i] = 0.f;
+    for (int zz = 0; zz < S - 1; ++zz) {
+      uint4 part[4][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          part[t][q] = bload16<kSC1>(srs, lo + t * 64 * 64 + 16 * q, (uint32_t)zz * kSlice);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sum[t][4 * q] += __uint_as_float(part[t][q].x);
+          sum[t][4 * q + 1] += __uint_as_float(part[t][q].y);
+          sum[t][4 * q + 2] += __uint_as_float(part[t][q].z);
+          sum[t][4 * q + 3] += __uint_as_float(part[t][q].w);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = sum[t] + acc[t];
+    __syncthreads();  // `word` lives where the output image goes
+  }
+
+  // epilogue: bf16 tile [128][BN] through LDS, rows out in 16-B pieces. C map (32x32x16): column
+  // lane & 31, row (i & 3) + 8 (i >> 2) + 4 h of accumulator tile t (rows 32 t ..)
+  uint16_t* out = reinterpret_cast<uint16_t*>(lds);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+      float v = round_bf16(acc[t][i]);
+      if (bias != nullptr) v = round_bf16(v + bsf);
+      out[r * BN + 32 * wave + r32] = f32_to_bf16(v);
+    }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  const bool full = n_blk + BN <= N && (N & 7) == 0 && ((uintptr_t)y & 15) == 0;
+  for (int c = tid; c < kBM * CPR; c += WV * 64) {
+    const int r = c / CPR, cc = c % CPR;
+    const int m = m_blk + r;
+    if (m >= M) continue;
+    const uint4 v = reinterpret_cast<const uint4*>(out)[c];
+    if (full) {
+      *reinterpret_cast<uint4*>(y + (size_t)m * N + n_blk + 8 * cc) = v;
+    } else {
+      const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+      for (int k = 0; k < 8; ++k)
+        if (n_blk + 8 * cc + k < N) y[(size_t)m * N + n_blk + 8 * cc + k] = e[k];
+    }
+  }
+}
+
+}  // namespace
+
+// bn 64 (2 waves) or 128 (4 waves); splits S; stages 2-3; a_steps = 128-k steps per publisher
+int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
+              const uint16_t* bias, uint16_t* y, int M, int N, int K, int bn, int splits,
+              int stages, int a_steps, hipStream_t stream) {
+  const int nsteps = K / 128;
+  if (splits > nsteps) splits = nsteps;
+  if (splits < 1) splits = 1;
+  if (a_steps <= 0 || a_steps * (splits - 1) >= nsteps) a_steps = nsteps / splits;
+  const dim3 grid((unsigned)((N + bn - 1) / bn), (unsigned)splits, (unsigned)((M + kBM - 1) / kBM));
+  f32x16_t* slab = nullptr;
+  unsigned* cnt = nullptr;
+  if (splits > 1) {
+    void* w = nullptr;
+    const size_t tiles = (size_t)grid.x * grid.z;
+    const int rc = split_workspace(stream, tiles * (splits - 1) * kBM * bn * 4, tiles, &w, &cnt);
+    if (rc != TAO_OK) return rc;
+    slab = reinterpret_cast<f32x16_t*>(w);
+  }
+  const int fenced = tuning().splitk_fenced;
+  auto go = [&](auto kern, int threads) {
+    launch(kern, grid, dim3(threads), 0, stream, x, packed, reinterpret_cast<const uint32_t*>(sz),
+           lg, bias, y, M, N, K, a_steps, slab, cnt, fenced);
+  };
+  if (bn == 128) {
+    if (stages == 2) go(gemm_sf32_int4_kernel<4, 2>, 256);
+    else go(gemm_sf32_int4_kernel<4, 3>, 256);
+  } else if (bn == 64) {
+    if (stages == 2) go(gemm_sf32_int4_kernel<2, 2>, 128);
+    else go(gemm_sf32_int4_kernel<2, 3>, 128);
+  } else {
+    return set_error(TAO_ERR_INVALID_ARGUMENT, "gemm_sf32: bn must be 64 or 128 (got %d)", bn);
+  }
+  return check_launch("gemm_sf32_int4_kernel");
+}
+
+int sf32_status(unsigned* bits) {
+  unsigned v = 0, zero = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_sf32_err), sizeof(v)) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(g_sf32_err), &zero, sizeof(zero)) != hipSuccess)
+    return set_error(TAO_ERR_HIP, "gemm_sf32 status: symbol copy failed");
+  *bits |= v;
+  return TAO_OK;
+}
+
+}  // namespace tao
