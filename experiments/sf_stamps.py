@@ -64,12 +64,15 @@ def run_case(path, M, N, K, cfg, gen, out):
     rec = {"path": path, "M": M, "N": N, "K": K, "cfg": list(cfg), "wgs": nwg}
     for k, name in enumerate(NAMES):
         vals = [(r[k] - t0) / 100.0 for r in st if r[k]]
-        rec[name] = [round(pct(vals, 0.0), 2), round(pct(vals, 0.5), 2), round(pct(vals, 1.0), 2)]
+        rec[name] = ([round(pct(vals, 0.0), 2), round(pct(vals, 0.5), 2), round(pct(vals, 1.0), 2)]
+                     if vals else None)
     red = [r for r in st if r[7] == 1]
     pub = [r for r in st if r[7] == 0]
     rec["reducer_loop_us"] = round(pct([(r[3] - r[2]) / 100 for r in red], 0.5), 2)
-    rec["reducer_wait_us"] = round(pct([(r[4] - r[3]) / 100 for r in red], 0.5), 2) if splits > 1 else 0
-    rec["reducer_epi_us"] = round(pct([(r[5] - r[4]) / 100 for r in red], 0.5), 2) if splits > 1 else 0
+    rec["reducer_wait_us"] = (round(pct([(r[4] - r[3]) / 100 for r in red], 0.5), 2)
+                              if splits > 1 and red else 0)
+    rec["reducer_epi_us"] = (round(pct([(r[5] - r[4]) / 100 for r in red], 0.5), 2)
+                             if splits > 1 and red else 0)
     if pub:
         rec["pub_loop_us"] = round(pct([(r[3] - r[2]) / 100 for r in pub], 0.5), 2)
         rec["pub_end_med"] = round(pct([(r[5] - t0) / 100 for r in pub], 0.5), 2)

@@ -144,6 +144,9 @@ int tao_tune_gemm_tile(int mode, int splits);
  * a_steps (K steps of each publishing slice) and ks (int8 k step 128 / 256): 0 = built-in.
  * Thread-local; for measurement. */
 int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages, int a_steps, int ks);
+/* Single-fetch GEMM operand staging: 0 = LDS-DMA ring (built-in), 1 = 16-B loads into a register
+ * ring (stages = its depth) written to two LDS buffers. Thread-local; for measurement. */
+int tao_tune_gemm_sf_reg(int reg);
 /* Reducer poll timeouts of the single-fetch GEMM since the last call (*bits != 0: some split
  * launch's outputs are invalid; never expected, see gemm_sf.hip). Synchronous. */
 int tao_gemm_sf_status(unsigned* bits);

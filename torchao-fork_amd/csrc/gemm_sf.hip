@@ -116,6 +116,7 @@ struct SfI8 {
   __device__ __forceinline__ uint32_t zsrc(int, int, int, int, int) const { return 0; }
   __device__ __forceinline__ uint32_t zsoff(int) const { return 0; }
   __device__ __forceinline__ const uint16_t* n_elems() const { return wscale; }  // >= N elements
+  __device__ __forceinline__ uint32_t zword(int, int, int) const { return 0; }
 };
 
 struct SfI4 {
@@ -154,6 +155,10 @@ struct SfI4 {
   __device__ __forceinline__ uint32_t zsoff(int st) const {
     return (uint32_t)(((128 * st) >> lg) * 4);
   }
+  // REG staging: byte offset of the (scale, zero) word of row gn for 32-k quarter q of step 0
+  __device__ __forceinline__ uint32_t zword(int gn, int q, int K) const {
+    return ((uint32_t)gn * (uint32_t)(K >> lg) + (uint32_t)((32 * q) >> lg)) * 4u;
+  }
   // >= N bf16 elements: the (scale, zero) array ([N][K/g][2], K >= g)
   __device__ __forceinline__ const uint16_t* n_elems() const {
     return reinterpret_cast<const uint16_t*>(sz);
@@ -189,7 +194,11 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
   }
 }
 
-template <class P, int BN, int WM, int NS>
+// REG: register staging instead of LDS-DMA (NS = register ring depth, two LDS buffers). The DMA
+// path's per-step time measured 0.59 us for 40 KiB per CU at config 3 (experiments/sf_stamps.py):
+// ~68 GB/s per CU, the LDS-DMA intake MI355X_MICROARCH.md's ring-gemm row reports; 16-B loads into
+// registers took in 96-112 GB/s per CU at 8-16 waves (DESIGN §4.2b intake table).
+template <class P, int BN, int WM, int NS, bool REG = false>
 __global__ __launch_bounds__(512) void gemm_sf_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int a_steps, typename P::Acc* __restrict__ slab,
@@ -216,9 +225,10 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   static_assert(XB % 1024 == 0 && WB % 1024 == 0 && ZB % 256 == 0, "DMA pieces");
   static_assert(T % kWaves == 0 && PX % kWaves == 0, "DMA pieces per wave");
   constexpr int R = T / kWaves;  // DMA instructions per wave per stage
-  static_assert(NS * STAGE <= 160 * 1024, "LDS");
-  static_assert(kBM * BN * 2 <= NS * STAGE, "epilogue image");
-  __shared__ uint4 lds[NS * STAGE / 16];
+  constexpr int NB = REG ? 2 : NS;  // LDS stage buffers
+  static_assert(NB * STAGE <= 160 * 1024, "LDS");
+  static_assert(kBM * BN * 2 <= NB * STAGE, "epilogue image");
+  __shared__ uint4 lds[NB * STAGE / 16];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -383,20 +393,117 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
     }
   };
 
-  // ---- the k loop: NS-1 stages in flight, one barrier per step ------------------------------------
+  // ---- the k loop ---------------------------------------------------------------------------------
+  if constexpr (!REG) {
+    // LDS-DMA: NS-1 stages in flight, one barrier per step
 #pragma unroll
-  for (int p = 0; p < NS - 1; ++p)
-    if (p < J) issue(s0 + p, p);
-  SF_MARK(1);
-  for (int j = 0; j < J; ++j) {
-    const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
-    wait_ahead<R>(ahead);  // this wave's DMAs of step j landed
-    barrier_lgkm();        // ... and every wave's; step j - 1's fragment reads are done
+    for (int p = 0; p < NS - 1; ++p)
+      if (p < J) issue(s0 + p, p);
+    SF_MARK(1);
+    for (int j = 0; j < J; ++j) {
+      const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
+      wait_ahead<R>(ahead);  // this wave's DMAs of step j landed
+      barrier_lgkm();        // ... and every wave's; step j - 1's fragment reads are done
 #if TAO_SF_STAMPS
-    if (j == 0) SF_MARK(2);
+      if (j == 0) SF_MARK(2);
 #endif
-    if (j + NS - 1 < J) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
-    compute(j % NS);
+      if (j + NS - 1 < J) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
+      compute(j % NS);
+    }
+  } else {
+    // Register staging: thread t loads granules t + 512 i of each image in source order (whole
+    // lines across consecutive threads) D = NS steps ahead, then writes them at their swizzled
+    // image positions (the layout the DMA path builds). Loads past the slice re-read its last
+    // step (never predicated: a branch around a load makes hipcc drain vmcnt at the join).
+    constexpr int D = NS;
+    constexpr int GX = P::kXRow / 16, GW = P::kWRow / 16;
+    constexpr int XG = kBM * GX / 512;                    // x granules per thread
+    constexpr int WGN = BN * GW, WG = (WGN + 511) / 512;  // W granules (all threads / per thread)
+    constexpr int ZGN = BN * P::kZRow / 4, ZG = (ZGN + 511) / 512;  // (scale, zero) dwords
+    static_assert(kBM * GX % 512 == 0, "x granules per thread");
+    uint32_t xv[XG], wv[WG], zv[ZG > 0 ? ZG : 1];
+    int xw[XG], ww[WG], zw[ZG > 0 ? ZG : 1];
+#pragma unroll
+    for (int i = 0; i < XG; ++i) {
+      const int e = tid + 512 * i, row = e / GX, g = e % GX;
+      const int gm = m_blk + row < M ? m_blk + row : M - 1;
+      xv[i] = (uint32_t)gm * row_bytes + 16u * (uint32_t)g;
+      xw[i] = row * P::kXRow + 16 * P::xpos(row, g);
+    }
+#pragma unroll
+    for (int i = 0; i < WG; ++i) {
+      const int e0 = tid + 512 * i, e = e0 < WGN ? e0 : WGN - 1;
+      const int row = e / GW, g = e % GW;
+      const int gn = n_blk + row < N ? n_blk + row : N - 1;
+      if constexpr (P::kZRow > 0) {  // int4 nibbles: K / 2 bytes per row
+        wv[i] = (uint32_t)gn * (uint32_t)(K >> 1) + 16u * (uint32_t)g;
+        ww[i] = e0 < WGN ? XB + row * P::kWRow + 16 * pos64(row, g) : -1;
+      } else {
+        wv[i] = (uint32_t)gn * (uint32_t)K + 16u * (uint32_t)g;
+        ww[i] = e0 < WGN ? XB + row * P::kWRow + 16 * P::xpos(row, g) : -1;
+      }
+    }
+    if constexpr (ZG > 0) {
+#pragma unroll
+      for (int i = 0; i < ZG; ++i) {
+        const int e0 = tid + 512 * i, e = e0 < ZGN ? e0 : ZGN - 1;
+        const int row = e >> 2, q = e & 3;
+        const int gn = n_blk + row < N ? n_blk + row : N - 1;
+        zv[i] = pol.zword(gn, q, K);
+        zw[i] = e0 < ZGN ? XB + WB + row * 16 + 4 * posz(row, q) : -1;
+      }
+    }
+    uint4 xr[D][XG], wr[D][WG];
+    uint32_t zr[D][ZG > 0 ? ZG : 1];
+    auto load = [&](int j, uint4 (&xd)[XG], uint4 (&wd)[WG], uint32_t (&zd)[ZG > 0 ? ZG : 1])
+        __attribute__((always_inline)) {
+      const int st = s0 + (j < J ? j : J - 1);
+#pragma unroll
+      for (int i = 0; i < XG; ++i) xd[i] = bload16(xrs, xv[i], (uint32_t)st * P::kXRow);
+#pragma unroll
+      for (int i = 0; i < WG; ++i) wd[i] = bload16<kNT>(wrs, wv[i], pol.wsoff(st));
+      if constexpr (ZG > 0) {
+#pragma unroll
+        for (int i = 0; i < ZG; ++i) zd[i] = bload4<kNT>(zrs, zv[i], pol.zsoff(st));
+      }
+    };
+    auto store = [&](const uint4 (&xd)[XG], const uint4 (&wd)[WG],
+                     const uint32_t (&zd)[ZG > 0 ? ZG : 1], int buf) __attribute__((always_inline)) {
+      uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * STAGE;
+#pragma unroll
+      for (int i = 0; i < XG; ++i) *reinterpret_cast<uint4*>(base + xw[i]) = xd[i];
+#pragma unroll
+      for (int i = 0; i < WG; ++i)
+        if (WGN % 512 == 0 || ww[i] >= 0) *reinterpret_cast<uint4*>(base + ww[i]) = wd[i];
+      if constexpr (ZG > 0) {
+#pragma unroll
+        for (int i = 0; i < ZG; ++i)
+          if (ZGN % 512 == 0 || zw[i] >= 0) *reinterpret_cast<uint32_t*>(base + zw[i]) = zd[i];
+      }
+    };
+    sfor<0, D>([&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      load(p, xr[p], wr[p], zr[p]);
+    });
+    SF_MARK(1);
+    store(xr[0], wr[0], zr[0], 0);
+    __syncthreads();
+#if TAO_SF_STAMPS
+    SF_MARK(2);
+#endif
+    auto body = [&](auto uc, int j) __attribute__((always_inline)) {
+      constexpr int u = decltype(uc)::value;
+      load(j + D, xr[u], wr[u], zr[u]);  // ring slot u held step j, already in LDS
+      compute(j & 1);
+      if (j + 1 < J) store(xr[(u + 1) % D], wr[(u + 1) % D], zr[(u + 1) % D], (j + 1) & 1);
+      __syncthreads();
+    };
+    int j = 0;
+    for (; j + D <= J; j += D)
+      sfor<0, D>([&](auto uc) { body(uc, j + decltype(uc)::value); });
+    sfor<0, D - 1>([&](auto uc) {
+      if (j + decltype(uc)::value < J) body(uc, j + decltype(uc)::value);
+    });
   }
   barrier_lgkm();  // all fragment reads done: the LDS is free for the epilogue image
   SF_MARK(3);
@@ -564,17 +671,18 @@ struct SfShape {
   int bn, wm, splits, stages, a_steps;
 };
 
-template <class P, int BN, int WM, int NS>
+template <class P, int BN, int WM, int NS, bool REG>
 bool sf_go(dim3 grid, hipStream_t stream, const uint8_t* x, const P& pol, const uint16_t* bias,
            uint16_t* y, int M, int N, int K, int a, typename P::Acc* slab, unsigned* cnt) {
   constexpr int STAGE = kBM * P::kXRow + BN * P::kWRow + BN * P::kZRow;
-  if constexpr (NS * STAGE <= 160 * 1024 && (kBM * P::kXRow + BN * P::kWRow + BN * P::kZRow) > 0) {
+  constexpr int NB = REG ? 2 : NS;
+  if constexpr (NB * STAGE <= 160 * 1024 && (kBM * P::kXRow + BN * P::kWRow + BN * P::kZRow) > 0) {
     constexpr int T = (kBM * P::kXRow) / 1024 + (BN * P::kWRow) / 1024 + (BN * P::kZRow) / 256;
     if constexpr (T % kWaves == 0 && (BN * P::kWRow) % 1024 == 0 && (BN * P::kZRow) % 256 == 0 &&
                   BN / (kWaves / WM) >= 16)
     {
-      launch(gemm_sf_kernel<P, BN, WM, NS>, grid, dim3(512), 0, stream, x, pol, bias, y, M, N, K,
-             a, slab, cnt, tuning().splitk_fenced);
+      launch(gemm_sf_kernel<P, BN, WM, NS, REG>, grid, dim3(512), 0, stream, x, pol, bias, y, M,
+             N, K, a, slab, cnt, tuning().splitk_fenced);
       return true;
     }
   }
@@ -586,9 +694,11 @@ int sf_dispatch_wm(const SfShape& sh, dim3 grid, hipStream_t st, const uint8_t* 
                    const uint16_t* bias, uint16_t* y, int M, int N, int K, int a,
                    typename P::Acc* slab, unsigned* cnt) {
   bool ok = false;
+  const bool reg = tuning().sf_reg != 0;
   auto go = [&](auto wmc, auto nsc) {
-    ok = sf_go<P, BN, decltype(wmc)::value, decltype(nsc)::value>(grid, st, x, pol, bias, y, M, N,
-                                                                  K, a, slab, cnt);
+    constexpr int W = decltype(wmc)::value, S_ = decltype(nsc)::value;
+    ok = reg ? sf_go<P, BN, W, S_, true>(grid, st, x, pol, bias, y, M, N, K, a, slab, cnt)
+             : sf_go<P, BN, W, S_, false>(grid, st, x, pol, bias, y, M, N, K, a, slab, cnt);
   };
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
@@ -733,6 +843,13 @@ extern "C" int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages
   t.sf_stages = stages;
   t.sf_a_steps = a_steps;
   t.sf_ks = ks;
+  return TAO_OK;
+}
+
+// Register staging instead of LDS-DMA for the single-fetch GEMM (1), or the DMA ring (0, built-in).
+extern "C" int tao_tune_gemm_sf_reg(int reg) {
+  TAO_CHECK_ARG(reg == 0 || reg == 1, "tune: gemm_sf_reg must be 0 or 1");
+  tao::tuning().sf_reg = reg;
   return TAO_OK;
 }
 
