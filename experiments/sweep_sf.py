@@ -79,7 +79,7 @@ def main():
     ap.add_argument("--paths", default="int8,int4")
     ap.add_argument("--shapes", default="")
     ap.add_argument("--reps", type=int, default=30)
-    ap.add_argument("--reg", type=int, default=-1, help="1: only register staging, 0: only DMA")
+    ap.add_argument("--seams", default="1,0", help="split-K seams to time (1 spread, 0 fixed reducer)")
     args = ap.parse_args()
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     out = open(args.out, "a")
@@ -103,15 +103,6 @@ def main():
                  (128, 1, 2, 3, 0), (128, 1, 1, 3, 0), (64, 1, 4, 2, 0), (64, 1, 2, 3, 0),
                  (64, 1, 8, 2, 0), (128, 1, 8, 3, 0)],
     }
-    reg_cfgs = {
-        "int8": [(32, 8, 2, 2, 0, 256), (32, 8, 2, 3, 0, 256), (32, 8, 2, 4, 0, 256),
-                 (32, 4, 2, 3, 0, 256), (32, 8, 1, 3, 0, 256), (32, 8, 2, 3, 6, 256),
-                 (64, 4, 4, 3, 0, 128), (64, 4, 4, 4, 0, 128), (64, 4, 2, 3, 0, 256),
-                 (64, 4, 1, 3, 0, 128), (64, 2, 4, 2, 0, 256), (128, 4, 8, 3, 0, 128)],
-        "int4": [(64, 2, 4, 2, 0), (64, 2, 4, 3, 0), (64, 2, 4, 4, 0), (64, 4, 4, 3, 0),
-                 (64, 8, 4, 3, 0), (64, 2, 2, 3, 0), (64, 2, 1, 3, 0), (128, 2, 4, 2, 0),
-                 (128, 2, 8, 2, 0), (128, 2, 2, 2, 0), (128, 2, 1, 2, 0), (64, 4, 2, 3, 0)],
-    }
     for path in args.paths.split(","):
         for (M, N, K) in shapes:
             run, copies = (int8_case if path == "int8" else int4_case)(M, N, K, gen)
@@ -122,14 +113,13 @@ def main():
             rec = {"path": path, "M": M, "N": N, "K": K, "cfg": "incumbent", "us": round(base * 1e3, 2)}
             print(json.dumps(rec), flush=True)
             out.write(json.dumps(rec) + "\n")
-            todo = [(c, 0) for c in cfgs[path]] + [(c, 1) for c in reg_cfgs[path]]
-            for cfg, reg in todo:
-                if args.reg >= 0 and reg != args.reg:
-                    continue
+            seams = [int(v) for v in args.seams.split(",")]
+            todo = [(c, sm) for c in cfgs[path] for sm in seams if sm == 0 or c[2] in (2, 4, 8)]
+            for cfg, seam in todo:
                 _lib.call("tao_tune_reset")
                 try:
                     sf(2, *cfg)
-                    _lib.call("tao_tune_gemm_sf_reg", reg)
+                    _lib.call("tao_tune_gemm_sf_seam", seam)
                     y = run(0)
                     torch.cuda.synchronize()
                     if path == "int8":
@@ -137,7 +127,7 @@ def main():
                     else:
                         ok = float((y.float() - ref.float()).norm() / ref.float().norm()) < 2e-3
                     us = median(timed(run, copies, args.reps)) * 1e3
-                    rec = {"path": path, "M": M, "N": N, "K": K, "cfg": list(cfg), "reg": reg,
+                    rec = {"path": path, "M": M, "N": N, "K": K, "cfg": list(cfg), "seam": seam,
                            "us": round(us, 2), "speedup": round(base * 1e3 / us, 3), "ok": ok}
                 except RuntimeError as e:
                     rec = {"path": path, "M": M, "N": N, "K": K, "cfg": list(cfg), "error": str(e)[:120]}

@@ -137,16 +137,16 @@ int tao_tune_int4_mfma32(int on);
 int tao_tune_gemm_tile(int mode, int splits);
 
 /* The single-fetch prefill GEMM (csrc/gemm_sf.hip: 128-row tiles so each weight tile is fetched by
- * one workgroup, 8 waves, both operands by LDS-DMA in full lines, K split over workgroups with a
- * fixed reducer) for the int4 weight-only and int8 dynamic linears. mode 0 = built-in routing,
+ * one workgroup, 8 waves, both operands by LDS-DMA in full lines, K split over workgroups) for the int4 weight-only and int8 dynamic linears. mode 0 = built-in routing,
  * 1 = never, 2 = wherever the shape is supported (K % 128 (int4) / 256 (int8) == 0; M <= 128 per
  * 128-row launch tile). bn (32 / 64 / 128), wm (waves along M: 2 / 4 / 8), splits, stages (2-4),
  * a_steps (K steps of each publishing slice) and ks (int8 k step 128 / 256): 0 = built-in.
  * Thread-local; for measurement. */
 int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages, int a_steps, int ks);
-/* Single-fetch GEMM operand staging: 0 = LDS-DMA ring (built-in), 1 = 16-B loads into a register
- * ring (stages = its depth) written to two LDS buffers. Thread-local; for measurement. */
-int tao_tune_gemm_sf_reg(int reg);
+/* Single-fetch GEMM split-K seam: 1 = spread (built-in: each of a tile's S workgroups sums and
+ * stores 1/S of the tile; splits 2 / 4 / 8 only, others take 0), 0 = fixed reducer (slice S-1
+ * sums the whole tile). Thread-local; for measurement. */
+int tao_tune_gemm_sf_seam(int seam);
 /* Reducer poll timeouts of the single-fetch GEMM since the last call (*bits != 0: some split
  * launch's outputs are invalid; never expected, see gemm_sf.hip). Synchronous. */
 int tao_gemm_sf_status(unsigned* bits);

@@ -145,25 +145,32 @@ def test_sf_asymmetric_slices(sf, a_steps):
 
 @pytest.mark.parametrize("cfg8,cfg4", [((32, 8, 2, 3, 0, 256), (64, 2, 4, 3, 0)),
                                        ((64, 4, 4, 2, 0, 128), (64, 4, 2, 2, 0)),
-                                       ((32, 4, 1, 4, 0, 256), (128, 2, 8, 2, 0)),
-                                       ((64, 8, 2, 3, 5, 256), (64, 8, 1, 4, 0))])
+                                       ((32, 4, 8, 4, 0, 256), (128, 2, 8, 2, 0)),
+                                       ((64, 8, 2, 3, 5, 256), (64, 8, 8, 4, 0))])
 @pytest.mark.parametrize("M,N,K", [(128, 4096, 4096), (100, 640, 3072), (200, 192, 2048)])
-def test_sf_register_staging(sf, cfg8, cfg4, M, N, K):
-    """tao_tune_gemm_sf_reg 1: 16-B loads into a register ring written to two LDS buffers (the
-    images the DMA path builds): int8 dyn bit-exact, int4 within the bars, g = 32 and 128."""
-    sf(2, *cfg8)
-    _lib.call("tao_tune_gemm_sf_reg", 1)
-    xq, xs, wq, ws = _int8(M, N, K, seed=M + K)
-    y = torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), None).cpu()
-    assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="cpu"))
-    sf(2, *cfg4)
-    _lib.call("tao_tune_gemm_sf_reg", 1)
-    for g in (32, 128):
-        q, s, z, packed, sz = _int4(N, K, g, seed=N + g)
-        x = oracle.make_activation(M, K, seed=g)
-        y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, None).cpu()
-        assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, g)) < TOL_FP32
-        assert oracle.rel_l2(y, oracle.int4_linear(x, q, s, z, g)) < TOL_REF
+def test_sf_spread_seam_matches_fixed_reducer(sf, cfg8, cfg4, M, N, K):
+    """tao_tune_gemm_sf_seam: the spread seam (each of a tile's S workgroups sums 1/S of it) and
+    the fixed reducer add the same partials in the same slice order: int8 bit-exact to the
+    oracle, int4 bit-identical between the seams (g = 32 and 128) and within the bars; M tiles
+    past 128 and ragged N tiles exercise the 1-D grid order."""
+    outs = {}
+    for seam in (0, 1):
+        sf(2, *cfg8)
+        _lib.call("tao_tune_gemm_sf_seam", seam)
+        xq, xs, wq, ws = _int8(M, N, K, seed=M + K)
+        y = torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), None).cpu()
+        assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="cpu"))
+        sf(2, *cfg4)
+        _lib.call("tao_tune_gemm_sf_seam", seam)
+        for g in (32, 128):
+            q, s, z, packed, sz = _int4(N, K, g, seed=N + g)
+            x = oracle.make_activation(M, K, seed=g)
+            y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, None).cpu()
+            outs.setdefault(g, []).append(y)
+            assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, g)) < TOL_FP32
+            assert oracle.rel_l2(y, oracle.int4_linear(x, q, s, z, g)) < TOL_REF
+    for g, (a, b) in outs.items():
+        assert torch.equal(a, b), g
 
 
 def test_sf_deterministic_fenced_and_matches_old_kernel(sf):

@@ -151,6 +151,14 @@ def test_tile_graph_capture_and_workspace_released(tile):
                 out = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)
         torch.cuda.current_stream().wait_stream(stream)
         assert _lib.lib().tao_graph_workspace_count() == base + 1
+        # an eager split-K launch needing a larger workspace between capture and
+        # replay (the step that frees retired buffers) must not free the graph's one
+        xb = oracle.make_activation(256, K, seed=6).to(DEV)
+        big = torch.ops.torchao.int4_weight_only_linear(xb, packed, sz, g, None)
+        torch.cuda.synchronize()
+        assert _lib.lib().tao_graph_workspace_count() == base + 1
+        assert big.shape == (256, N)
+        del xb, big
         for _ in range(2):
             graph.replay()
         torch.cuda.synchronize()

@@ -447,6 +447,25 @@ def test_reference_tile_checkpoint_without_chosen_map_raises():
     assert tops._chosen_tile_format is None  # the context restores "not chosen"
 
 
+def test_generate_tile_format_flag_reaches_checkpoint_load(tmp_path):
+    """generate.py --tile_format wraps the checkpoint torch.load in
+    checkpoint_tile_format, so a reference tile checkpoint loads from the CLI path; without the
+    flag the load raises naming the context."""
+    from torchao._models.llama.generate import build_model, main
+
+    sd, *_ = _reference_tile_state(48, 1024, 32, 8, "cuda", seed=6)
+    path = tmp_path / "tile.pt"
+    torch.save(sd, path)
+    with pytest.raises(RuntimeError, match="checkpoint_tile_format"):
+        build_model("stories15M", torch.device("cpu"), checkpoint_path=path)
+    # the tile tensor now deserialises; the state dict is not a stories15M one, which
+    # load_state_dict reports only after torch.load succeeded
+    with pytest.raises(RuntimeError, match="Unexpected key|Missing key"):
+        build_model("stories15M", torch.device("cpu"), checkpoint_path=path, tile_format="cuda")
+    with pytest.raises(SystemExit):
+        main(["--tile_format", "cuda11"])
+
+
 def _ref_ckpt_cases():
     return sorted(f[len("ref_ckpt_"):-3] for f in os.listdir(os.path.join(ROOT, "tests", "golden"))
                   if f.startswith("ref_ckpt_") and f.endswith(".pt"))

@@ -15,11 +15,13 @@
 //     by choosing each lane's source so that every ds_read_b128 fragment read is conflict-free;
 //   * 8 waves and NS-1 stages (32-48 KiB each) in flight per CU: a counted vmcnt + a barrier
 //     that does not drain vector memory keep them in flight across every step;
-//   * K split S ways over workgroups (the grid fills the 256 CUs) with a fixed reducer: slices
-//     0..S-2 publish their fp32 / int32 partial tile (sc1 stores, one ticket add), slice S-1
-//     (dispatched last, so a publisher never waits behind it) polls the ticket, sums the slabs
-//     in slice order (run-to-run deterministic; int32 exact) and runs the epilogue. Publishers
-//     may take fewer K steps than the reducer (`a_steps`) so their publish overlaps its work.
+//   * K split S ways over workgroups (the grid fills the 256 CUs). Spread seam (built-in): each
+//     of a tile's S workgroups publishes the fp32 / int32 partials of the waves it does not own
+//     (sc1 stores, one ticket add), waits for all S, and its owned 8/S waves sum their fragments
+//     over the slices in slice order (run-to-run deterministic; int32 exact) and run the
+//     epilogue of their wave tiles. Fixed-reducer seam (tao_tune_gemm_sf_seam 0): slices
+//     0..S-2 publish whole tiles, slice S-1 (dispatched last) sums them; publishers may take
+//     fewer K steps than the reducer (`a_steps`).
 // Wave layout: WM x WN waves over the 128 x BN tile (wave tile 128/WM x BN/WN).
 #include <type_traits>
 
@@ -116,7 +118,6 @@ struct SfI8 {
   __device__ __forceinline__ uint32_t zsrc(int, int, int, int, int) const { return 0; }
   __device__ __forceinline__ uint32_t zsoff(int) const { return 0; }
   __device__ __forceinline__ const uint16_t* n_elems() const { return wscale; }  // >= N elements
-  __device__ __forceinline__ uint32_t zword(int, int, int) const { return 0; }
 };
 
 struct SfI4 {
@@ -155,10 +156,6 @@ struct SfI4 {
   __device__ __forceinline__ uint32_t zsoff(int st) const {
     return (uint32_t)(((128 * st) >> lg) * 4);
   }
-  // REG staging: byte offset of the (scale, zero) word of row gn for 32-k quarter q of step 0
-  __device__ __forceinline__ uint32_t zword(int gn, int q, int K) const {
-    return ((uint32_t)gn * (uint32_t)(K >> lg) + (uint32_t)((32 * q) >> lg)) * 4u;
-  }
   // >= N bf16 elements: the (scale, zero) array ([N][K/g][2], K >= g)
   __device__ __forceinline__ const uint16_t* n_elems() const {
     return reinterpret_cast<const uint16_t*>(sz);
@@ -194,15 +191,15 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
   }
 }
 
-// REG: register staging instead of LDS-DMA (NS = register ring depth, two LDS buffers). The DMA
-// path's per-step time measured 0.59 us for 40 KiB per CU at config 3 (experiments/sf_stamps.py):
-// ~68 GB/s per CU, the LDS-DMA intake MI355X_MICROARCH.md's ring-gemm row reports; 16-B loads into
-// registers took in 96-112 GB/s per CU at 8-16 waves (DESIGN §4.2b intake table).
-template <class P, int BN, int WM, int NS, bool REG = false>
+// Grid: one dimension, ntn N tiles x S slices x M tiles. seam 0 (fixed reducer): N tile fastest,
+// so every tile's reducer (slice S-1) is dispatched after all publishers. seam 1 (spread): slice
+// fastest, so a tile's S workgroups are dispatched together (they wait for one another: the
+// launcher takes this seam only when S divides the 8 waves and the grid's resident set holds S).
+template <class P, int BN, int WM, int NS>
 __global__ __launch_bounds__(512) void gemm_sf_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int a_steps, typename P::Acc* __restrict__ slab,
-    unsigned* __restrict__ cnt, int fenced) {
+    unsigned* __restrict__ cnt, int fenced, int S, int ntn, int seam) {
 #if TAO_SF_STAMPS
   const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
   unsigned long long stamp[6] = {t_entry, 0, 0, 0, 0, 0};
@@ -225,7 +222,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   static_assert(XB % 1024 == 0 && WB % 1024 == 0 && ZB % 256 == 0, "DMA pieces");
   static_assert(T % kWaves == 0 && PX % kWaves == 0, "DMA pieces per wave");
   constexpr int R = T / kWaves;  // DMA instructions per wave per stage
-  constexpr int NB = REG ? 2 : NS;  // LDS stage buffers
+  constexpr int NB = NS;  // LDS stage buffers
   static_assert(NB * STAGE <= 160 * 1024, "LDS");
   static_assert(kBM * BN * 2 <= NB * STAGE, "epilogue image");
   __shared__ uint4 lds[NB * STAGE / 16];
@@ -234,12 +231,24 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int fr = lane & 15, kq = lane >> 4;
-  const int n_blk = blockIdx.x * BN, m_blk = blockIdx.z * kBM;
-  const int S = gridDim.y, z = blockIdx.y;
-  const bool reducer = z == S - 1;
+  const int bid = blockIdx.x;
+  int z, nb, mb;
+  if (seam) {
+    z = bid % S;
+    nb = (bid / S) % ntn;
+    mb = bid / (S * ntn);
+  } else {
+    nb = bid % ntn;
+    z = (bid / ntn) % S;
+    mb = bid / (S * ntn);
+  }
+  const int n_blk = nb * BN, m_blk = mb * kBM;
+  const unsigned tile = (unsigned)(mb * ntn + nb);
+  const bool last = z == S - 1;
+  const bool reducer = last && !seam;  // fixed-reducer seam: the one workgroup that sums
   const int nsteps = K / P::kKStep;
   const int s0 = z * a_steps;
-  const int J = reducer ? nsteps - s0 : a_steps;  // launcher: every slice >= 1 step
+  const int J = last ? nsteps - s0 : a_steps;  // launcher: every slice >= 1 step
   const uint32_t row_bytes = (uint32_t)K * P::kABytes;
 
   // ---- DMA slots: this wave's R pieces per stage (piece i = 8 r + wave) --------------------------
@@ -393,130 +402,42 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
     }
   };
 
-  // ---- the k loop ---------------------------------------------------------------------------------
-  if constexpr (!REG) {
-    // LDS-DMA: NS-1 stages in flight, one barrier per step
+  // ---- the k loop: LDS-DMA, NS-1 stages in flight, one barrier per step ----------------------------
+  // (a register-staged variant -- 16-B loads into a register ring, two LDS buffers -- measured
+  // 5-15% slower at every swept shape: profiles/r4_sf_sweep_reg.jsonl)
 #pragma unroll
-    for (int p = 0; p < NS - 1; ++p)
-      if (p < J) issue(s0 + p, p);
-    SF_MARK(1);
-    for (int j = 0; j < J; ++j) {
-      const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
-      wait_ahead<R>(ahead);  // this wave's DMAs of step j landed
-      barrier_lgkm();        // ... and every wave's; step j - 1's fragment reads are done
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < J) issue(s0 + p, p);
+  SF_MARK(1);
+  for (int j = 0; j < J; ++j) {
+    const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
+    wait_ahead<R>(ahead);  // this wave's DMAs of step j landed
+    barrier_lgkm();        // ... and every wave's; step j - 1's fragment reads are done
 #if TAO_SF_STAMPS
-      if (j == 0) SF_MARK(2);
+    if (j == 0) SF_MARK(2);
 #endif
-      if (j + NS - 1 < J) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
-      compute(j % NS);
-    }
-  } else {
-    // Register staging: thread t loads granules t + 512 i of each image in source order (whole
-    // lines across consecutive threads) D = NS steps ahead, then writes them at their swizzled
-    // image positions (the layout the DMA path builds). Loads past the slice re-read its last
-    // step (never predicated: a branch around a load makes hipcc drain vmcnt at the join).
-    constexpr int D = NS;
-    constexpr int GX = P::kXRow / 16, GW = P::kWRow / 16;
-    constexpr int XG = kBM * GX / 512;                    // x granules per thread
-    constexpr int WGN = BN * GW, WG = (WGN + 511) / 512;  // W granules (all threads / per thread)
-    constexpr int ZGN = BN * P::kZRow / 4, ZG = (ZGN + 511) / 512;  // (scale, zero) dwords
-    static_assert(kBM * GX % 512 == 0, "x granules per thread");
-    uint32_t xv[XG], wv[WG], zv[ZG > 0 ? ZG : 1];
-    int xw[XG], ww[WG], zw[ZG > 0 ? ZG : 1];
-#pragma unroll
-    for (int i = 0; i < XG; ++i) {
-      const int e = tid + 512 * i, row = e / GX, g = e % GX;
-      const int gm = m_blk + row < M ? m_blk + row : M - 1;
-      xv[i] = (uint32_t)gm * row_bytes + 16u * (uint32_t)g;
-      xw[i] = row * P::kXRow + 16 * P::xpos(row, g);
-    }
-#pragma unroll
-    for (int i = 0; i < WG; ++i) {
-      const int e0 = tid + 512 * i, e = e0 < WGN ? e0 : WGN - 1;
-      const int row = e / GW, g = e % GW;
-      const int gn = n_blk + row < N ? n_blk + row : N - 1;
-      if constexpr (P::kZRow > 0) {  // int4 nibbles: K / 2 bytes per row
-        wv[i] = (uint32_t)gn * (uint32_t)(K >> 1) + 16u * (uint32_t)g;
-        ww[i] = e0 < WGN ? XB + row * P::kWRow + 16 * pos64(row, g) : -1;
-      } else {
-        wv[i] = (uint32_t)gn * (uint32_t)K + 16u * (uint32_t)g;
-        ww[i] = e0 < WGN ? XB + row * P::kWRow + 16 * P::xpos(row, g) : -1;
-      }
-    }
-    if constexpr (ZG > 0) {
-#pragma unroll
-      for (int i = 0; i < ZG; ++i) {
-        const int e0 = tid + 512 * i, e = e0 < ZGN ? e0 : ZGN - 1;
-        const int row = e >> 2, q = e & 3;
-        const int gn = n_blk + row < N ? n_blk + row : N - 1;
-        zv[i] = pol.zword(gn, q, K);
-        zw[i] = e0 < ZGN ? XB + WB + row * 16 + 4 * posz(row, q) : -1;
-      }
-    }
-    uint4 xr[D][XG], wr[D][WG];
-    uint32_t zr[D][ZG > 0 ? ZG : 1];
-    auto load = [&](int j, uint4 (&xd)[XG], uint4 (&wd)[WG], uint32_t (&zd)[ZG > 0 ? ZG : 1])
-        __attribute__((always_inline)) {
-      const int st = s0 + (j < J ? j : J - 1);
-#pragma unroll
-      for (int i = 0; i < XG; ++i) xd[i] = bload16(xrs, xv[i], (uint32_t)st * P::kXRow);
-#pragma unroll
-      for (int i = 0; i < WG; ++i) wd[i] = bload16<kNT>(wrs, wv[i], pol.wsoff(st));
-      if constexpr (ZG > 0) {
-#pragma unroll
-        for (int i = 0; i < ZG; ++i) zd[i] = bload4<kNT>(zrs, zv[i], pol.zsoff(st));
-      }
-    };
-    auto store = [&](const uint4 (&xd)[XG], const uint4 (&wd)[WG],
-                     const uint32_t (&zd)[ZG > 0 ? ZG : 1], int buf) __attribute__((always_inline)) {
-      uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * STAGE;
-#pragma unroll
-      for (int i = 0; i < XG; ++i) *reinterpret_cast<uint4*>(base + xw[i]) = xd[i];
-#pragma unroll
-      for (int i = 0; i < WG; ++i)
-        if (WGN % 512 == 0 || ww[i] >= 0) *reinterpret_cast<uint4*>(base + ww[i]) = wd[i];
-      if constexpr (ZG > 0) {
-#pragma unroll
-        for (int i = 0; i < ZG; ++i)
-          if (ZGN % 512 == 0 || zw[i] >= 0) *reinterpret_cast<uint32_t*>(base + zw[i]) = zd[i];
-      }
-    };
-    sfor<0, D>([&](auto pc) {
-      constexpr int p = decltype(pc)::value;
-      load(p, xr[p], wr[p], zr[p]);
-    });
-    SF_MARK(1);
-    store(xr[0], wr[0], zr[0], 0);
-    __syncthreads();
-#if TAO_SF_STAMPS
-    SF_MARK(2);
-#endif
-    auto body = [&](auto uc, int j) __attribute__((always_inline)) {
-      constexpr int u = decltype(uc)::value;
-      load(j + D, xr[u], wr[u], zr[u]);  // ring slot u held step j, already in LDS
-      compute(j & 1);
-      if (j + 1 < J) store(xr[(u + 1) % D], wr[(u + 1) % D], zr[(u + 1) % D], (j + 1) & 1);
-      __syncthreads();
-    };
-    int j = 0;
-    for (; j + D <= J; j += D)
-      sfor<0, D>([&](auto uc) { body(uc, j + decltype(uc)::value); });
-    sfor<0, D - 1>([&](auto uc) {
-      if (j + decltype(uc)::value < J) body(uc, j + decltype(uc)::value);
-    });
+    if (j + NS - 1 < J) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
+    compute(j % NS);
   }
   barrier_lgkm();  // all fragment reads done: the LDS is free for the epilogue image
   SF_MARK(3);
 
   // ---- split-K seam -----------------------------------------------------------------------------
+  // Slab: S slices' partial tiles per tile, each in the waves' fragment order (granule
+  // (wave MT NT + a NT + b) 64 + lane). Spread seam: workgroup z owns waves [z W/S, (z+1) W/S)
+  // of the tile (W = 8 waves): it publishes the fragments of the other waves, and its owned
+  // waves sum their fragments over the S slices and run the epilogue for their wave tiles, so
+  // each workgroup takes in (S-1)/S^2 of the slices' partials instead of one reducer taking in
+  // (S-1) whole tiles (the fixed reducer's seam measured 4-11 us at S = 4-8: its intake).
+  const int wpo = kWaves / S;  // waves owned per workgroup (spread)
+  const bool own = S == 1 || !seam || wave / wpo == z;
   if (S > 1) {
     constexpr uint32_t kSlice = kBM * BN * 4;  // bytes of one slice's partial tile
-    const unsigned tile = blockIdx.z * gridDim.x + blockIdx.x;
-    const Rsrc srs = make_rsrc(reinterpret_cast<const uint8_t*>(slab) + (size_t)tile * (S - 1) * kSlice,
-                               (uint32_t)(S - 1) * kSlice);
+    const Rsrc srs = make_rsrc(reinterpret_cast<const uint8_t*>(slab) + (size_t)tile * S * kSlice,
+                               (uint32_t)S * kSlice);
     const uint32_t lo = (uint32_t)((wave * MT * NT * 64 + lane) * 16);
     unsigned* word = reinterpret_cast<unsigned*>(lds);
-    if (!reducer) {
+    if (!reducer && !(seam && own)) {
       // MI355X_MICROARCH.md "Hand-offs measured with sc1 loads in place of the acquire", first row:
       // sc1 16-B stores, every storing wave's vmcnt(0), a workgroup barrier, one agent-scope add
 #pragma unroll
@@ -525,6 +446,8 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
         for (int b = 0; b < NT; ++b)
           bstore16<kSC1>(srs, lo + (a * NT + b) * 1024, (uint32_t)z * kSlice,
                          __builtin_bit_cast(uint4, acc[a][b]));
+    }
+    if (!reducer) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
@@ -534,11 +457,12 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
         }
         (void)__hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+    }
+    if (!seam && !reducer) {
 #if TAO_SF_STAMPS
       SF_MARK(4);
       SF_MARK(5);
       if (tid < 64) {
-        const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
         unsigned long long v = 0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
@@ -547,17 +471,19 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
         }
         if (lane == 6) v = (unsigned long long)z;
         if (lane == 7) v = 0;
-        if (lane < 8 && b < 8192) g_sf_stamps[b * 8 + lane] = v;
+        if (lane < 8 && bid < 8192) g_sf_stamps[bid * 8 + lane] = v;
       }
 #endif
       return;
     }
-    // reducer: one lane polls the ticket (sc1 loads), resets it for the next launch, tells the
-    // workgroup through LDS; every wave then reads the slabs with sc1 loads
+    // fixed reducer: wait for the S-1 publishers, reset the ticket. Spread: every workgroup waits
+    // for all S arrivals, then adds a second arrival; the one that completes 2 S resets the
+    // ticket (every workgroup has left its wait by then). One lane polls with sc1 loads and tells
+    // the workgroup through LDS.
     if (tid == 0) {
+      const unsigned need = seam ? (unsigned)S : (unsigned)(S - 1);
       unsigned it = 0, ok = 1;
-      while (__hip_atomic_load(&cnt[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-             (unsigned)(S - 1)) {
+      while (__hip_atomic_load(&cnt[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
         __builtin_amdgcn_s_sleep(1);
         if (++it > (1u << 22)) {  // ~0.3 s: give up, report (outputs of this tile are invalid)
           ok = 0;
@@ -565,7 +491,14 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
           break;
         }
       }
-      if (ok) __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ok) {
+        if (!seam) {
+          __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (__hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) == 2u * S - 1u) {
+          __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
       if (fenced) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -573,45 +506,49 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
       *word = ok;
     }
     __syncthreads();
-    // slices summed in slice order (publishers 0 .. S-2, then this one): deterministic
-    Acc sum[MT][NT];
+    if (own) {
+      // the other slices' fragments summed with this one's in slice order: deterministic, and
+      // the same additions in the same order under both seams
+      const int zo = seam ? z : S - 1;  // this workgroup's slice
+      Acc sum[MT][NT];
 #pragma unroll
-    for (int a = 0; a < MT; ++a)
+      for (int a = 0; a < MT; ++a)
 #pragma unroll
-      for (int b = 0; b < NT; ++b) sum[a][b] = Acc{0, 0, 0, 0};
-    // up to 4 slabs' loads in flight before their adds (clamped, then masked): one round trip per
-    // 4 publishers instead of one per publisher
-    constexpr int kG = MT * NT <= 4 ? 4 : (MT * NT <= 8 ? 2 : 1);
-    for (int z0 = 0; z0 < S - 1; z0 += kG) {
-      Acc part[kG][MT][NT];
+        for (int b = 0; b < NT; ++b) sum[a][b] = Acc{0, 0, 0, 0};
+      // up to 4 slabs' loads in flight before their adds (clamped, then masked)
+      constexpr int kG = MT * NT <= 4 ? 4 : (MT * NT <= 8 ? 2 : 1);
+      for (int z0 = 0; z0 < S; z0 += kG) {
+        Acc part[kG][MT][NT];
 #pragma unroll
-      for (int gi = 0; gi < kG; ++gi) {
-        const int zz = z0 + gi < S - 1 ? z0 + gi : S - 2;
-#pragma unroll
-        for (int a = 0; a < MT; ++a)
-#pragma unroll
-          for (int b = 0; b < NT; ++b)
-            part[gi][a][b] = __builtin_bit_cast(
-                Acc, bload16<kSC1>(srs, lo + (a * NT + b) * 1024, (uint32_t)zz * kSlice));
-      }
-#pragma unroll
-      for (int gi = 0; gi < kG; ++gi)
-        if (z0 + gi < S - 1) {
+        for (int gi = 0; gi < kG; ++gi) {
+          const int zz = z0 + gi < S ? z0 + gi : S - 1;
 #pragma unroll
           for (int a = 0; a < MT; ++a)
 #pragma unroll
-            for (int b = 0; b < NT; ++b) sum[a][b] += part[gi][a][b];
+            for (int b = 0; b < NT; ++b)
+              part[gi][a][b] = zz == zo ? acc[a][b] : __builtin_bit_cast(
+                  Acc, bload16<kSC1>(srs, lo + (a * NT + b) * 1024, (uint32_t)zz * kSlice));
         }
+#pragma unroll
+        for (int gi = 0; gi < kG; ++gi)
+          if (z0 + gi < S) {
+#pragma unroll
+            for (int a = 0; a < MT; ++a)
+#pragma unroll
+              for (int b = 0; b < NT; ++b) sum[a][b] += part[gi][a][b];
+          }
+      }
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) acc[a][b] = sum[a][b];
     }
-#pragma unroll
-    for (int a = 0; a < MT; ++a)
-#pragma unroll
-      for (int b = 0; b < NT; ++b) acc[a][b] = sum[a][b] + acc[a][b];
     SF_MARK(4);
   }
 
   // ---- epilogue: bf16 tile through an LDS image, rows stored in 16-B pieces ------------------------
   uint16_t* out = reinterpret_cast<uint16_t*>(lds);  // [128][BN]
+  if (own) {
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int c = wn * CN + 16 * nt + fr;
@@ -631,6 +568,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
         out[r * BN + c] = f32_to_bf16(v);
       }
   }
+  }
   __syncthreads();
   constexpr int CPR = BN / 8;  // 16-B pieces per row
   const bool full = n_blk + BN <= N && (N & 7) == 0 && ((uintptr_t)y & 15) == 0;
@@ -639,6 +577,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
     const int r = c / CPR, cc = c % CPR;
     const int m = m_blk + r;
     if (m >= M) continue;
+    if (seam && S > 1 && ((r / RM) * WN + (8 * cc) / CN) / wpo != z) continue;  // not owned
     const uint4 v = reinterpret_cast<const uint4*>(out)[c];
     if (full) {
       *reinterpret_cast<uint4*>(y + (size_t)m * N + n_blk + 8 * cc) = v;
@@ -651,7 +590,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
 #if TAO_SF_STAMPS
   SF_MARK(5);
   if (tid < 64) {
-    const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const unsigned b = bid;
     unsigned long long v = 0;
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
@@ -659,7 +598,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
       if (lane == i) v = ((unsigned long long)h32 << 32) | l32;
     }
     if (lane == 6) v = (unsigned long long)z;
-    if (lane == 7) v = 1;
+    if (lane == 7) v = seam ? 2 : 1;
     if (lane < 8 && b < 8192) g_sf_stamps[b * 8 + lane] = v;
   }
 #endif
@@ -669,20 +608,24 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
 // ---- launch ------------------------------------------------------------------------------------
 struct SfShape {
   int bn, wm, splits, stages, a_steps;
+  int seam;  // 0 fixed reducer, 1 spread (see the kernel)
 };
 
-template <class P, int BN, int WM, int NS, bool REG>
-bool sf_go(dim3 grid, hipStream_t stream, const uint8_t* x, const P& pol, const uint16_t* bias,
-           uint16_t* y, int M, int N, int K, int a, typename P::Acc* slab, unsigned* cnt) {
+template <class P, int BN, int WM, int NS>
+bool sf_go(const SfShape& sh, hipStream_t stream, const uint8_t* x, const P& pol,
+           const uint16_t* bias, uint16_t* y, int M, int N, int K, int a, typename P::Acc* slab,
+           unsigned* cnt) {
   constexpr int STAGE = kBM * P::kXRow + BN * P::kWRow + BN * P::kZRow;
-  constexpr int NB = REG ? 2 : NS;
+  constexpr int NB = NS;
   if constexpr (NB * STAGE <= 160 * 1024 && (kBM * P::kXRow + BN * P::kWRow + BN * P::kZRow) > 0) {
     constexpr int T = (kBM * P::kXRow) / 1024 + (BN * P::kWRow) / 1024 + (BN * P::kZRow) / 256;
     if constexpr (T % kWaves == 0 && (BN * P::kWRow) % 1024 == 0 && (BN * P::kZRow) % 256 == 0 &&
                   BN / (kWaves / WM) >= 16)
     {
-      launch(gemm_sf_kernel<P, BN, WM, NS, REG>, grid, dim3(512), 0, stream, x, pol, bias, y, M,
-             N, K, a, slab, cnt, tuning().splitk_fenced);
+      const int ntn = (N + BN - 1) / BN, mtiles = (M + kBM - 1) / kBM;
+      launch(gemm_sf_kernel<P, BN, WM, NS>, dim3((unsigned)(ntn * sh.splits * mtiles)), dim3(512),
+             0, stream, x, pol, bias, y, M, N, K, a, slab, cnt, tuning().splitk_fenced, sh.splits,
+             ntn, sh.seam);
       return true;
     }
   }
@@ -690,15 +633,13 @@ bool sf_go(dim3 grid, hipStream_t stream, const uint8_t* x, const P& pol, const 
 }
 
 template <class P, int BN>
-int sf_dispatch_wm(const SfShape& sh, dim3 grid, hipStream_t st, const uint8_t* x, const P& pol,
+int sf_dispatch_wm(const SfShape& sh, hipStream_t st, const uint8_t* x, const P& pol,
                    const uint16_t* bias, uint16_t* y, int M, int N, int K, int a,
                    typename P::Acc* slab, unsigned* cnt) {
   bool ok = false;
-  const bool reg = tuning().sf_reg != 0;
   auto go = [&](auto wmc, auto nsc) {
     constexpr int W = decltype(wmc)::value, S_ = decltype(nsc)::value;
-    ok = reg ? sf_go<P, BN, W, S_, true>(grid, st, x, pol, bias, y, M, N, K, a, slab, cnt)
-             : sf_go<P, BN, W, S_, false>(grid, st, x, pol, bias, y, M, N, K, a, slab, cnt);
+    ok = sf_go<P, BN, W, S_>(sh, st, x, pol, bias, y, M, N, K, a, slab, cnt);
   };
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
@@ -728,7 +669,7 @@ static SfShape sf_shape(int path, int M, int N, int K) {
   (void)M;
   const int kstep = path == 0 ? 128 : 256;
   const int nsteps = K / kstep;
-  SfShape sh{path == 0 ? 64 : 32, path == 0 ? 2 : 4, 1, 3, 0};
+  SfShape sh{path == 0 ? 64 : 32, path == 0 ? 2 : 4, 1, 3, 0, 1};
   const Tuning& t = tuning();
   if (t.sf_bn) sh.bn = t.sf_bn;
   if (t.sf_wm) sh.wm = t.sf_wm;
@@ -740,6 +681,10 @@ static SfShape sf_shape(int path, int M, int N, int K) {
   sh.a_steps = nsteps / sh.splits;
   if (t.sf_a_steps) sh.a_steps = t.sf_a_steps;
   if (sh.splits > 1 && sh.a_steps * (sh.splits - 1) >= nsteps) sh.a_steps = nsteps / sh.splits;
+  // the spread seam's S workgroups of a tile wait for one another: S must divide the 8 waves,
+  // and S consecutive workgroups must be resident together (1 per CU: S <= 8 << 256 CUs)
+  sh.seam = t.sf_seam;
+  if (sh.splits != 2 && sh.splits != 4 && sh.splits != 8) sh.seam = 0;
   return sh;
 }
 
@@ -760,13 +705,13 @@ int sf_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uin
                const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream) {
   const SfShape sh = sf_shape(2, M, N, K);
   const int ks = tuning().sf_ks == 128 ? 128 : 256;
-  const dim3 grid((N + sh.bn - 1) / sh.bn, sh.splits, (M + kBM - 1) / kBM);
+  const dim3 grid((N + sh.bn - 1) / sh.bn, 1, (M + kBM - 1) / kBM);  // tiles: grid.x grid.z
   i32x4_t* slab = nullptr;
   unsigned* cnt = nullptr;
   if (sh.splits > 1) {
     void* w = nullptr;
     const size_t tiles = (size_t)grid.x * grid.z;
-    const int rc = split_workspace(stream, tiles * (sh.splits - 1) * kBM * sh.bn * 4, tiles, &w, &cnt);
+    const int rc = split_workspace(stream, tiles * sh.splits * kBM * sh.bn * 4, tiles, &w, &cnt);
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<i32x4_t*>(w);
   }
@@ -775,9 +720,9 @@ int sf_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uin
   auto run = [&](auto pol, int a) -> int {
     typedef decltype(pol) P;
     switch (sh.bn) {
-      case 32: return sf_dispatch_wm<P, 32>(sh, grid, stream, xb, pol, bias, y, M, N, K, a, slab, cnt);
-      case 128: return sf_dispatch_wm<P, 128>(sh, grid, stream, xb, pol, bias, y, M, N, K, a, slab, cnt);
-      default: return sf_dispatch_wm<P, 64>(sh, grid, stream, xb, pol, bias, y, M, N, K, a, slab, cnt);
+      case 32: return sf_dispatch_wm<P, 32>(sh, stream, xb, pol, bias, y, M, N, K, a, slab, cnt);
+      case 128: return sf_dispatch_wm<P, 128>(sh, stream, xb, pol, bias, y, M, N, K, a, slab, cnt);
+      default: return sf_dispatch_wm<P, 64>(sh, stream, xb, pol, bias, y, M, N, K, a, slab, cnt);
     }
   };
   if (ks == 128) {
@@ -798,13 +743,13 @@ int sf_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int l
   if (sh.wm == 1)  // one wave along M: the 32x32x16 kernel (gemm_sf32.hip)
     return sf32_int4(x, packed, sz, lg, bias, y, M, N, K, sh.bn, sh.splits, sh.stages,
                      tuning().sf_a_steps, stream);
-  const dim3 grid((N + sh.bn - 1) / sh.bn, sh.splits, (M + kBM - 1) / kBM);
+  const dim3 grid((N + sh.bn - 1) / sh.bn, 1, (M + kBM - 1) / kBM);  // tiles: grid.x grid.z
   f32x4_t* slab = nullptr;
   unsigned* cnt = nullptr;
   if (sh.splits > 1) {
     void* w = nullptr;
     const size_t tiles = (size_t)grid.x * grid.z;
-    const int rc = split_workspace(stream, tiles * (sh.splits - 1) * kBM * sh.bn * 4, tiles, &w, &cnt);
+    const int rc = split_workspace(stream, tiles * sh.splits * kBM * sh.bn * 4, tiles, &w, &cnt);
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<f32x4_t*>(w);
   }
@@ -814,9 +759,9 @@ int sf_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int l
   const uint8_t* xb = reinterpret_cast<const uint8_t*>(x);
   switch (sh.bn) {
     case 128:
-      return sf_dispatch_wm<SfI4, 128>(sh, grid, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt);
+      return sf_dispatch_wm<SfI4, 128>(sh, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt);
     default:  // 64
-      return sf_dispatch_wm<SfI4, 64>(sh, grid, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt);
+      return sf_dispatch_wm<SfI4, 64>(sh, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt);
   }
 }
 
@@ -846,10 +791,10 @@ extern "C" int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages
   return TAO_OK;
 }
 
-// Register staging instead of LDS-DMA for the single-fetch GEMM (1), or the DMA ring (0, built-in).
-extern "C" int tao_tune_gemm_sf_reg(int reg) {
-  TAO_CHECK_ARG(reg == 0 || reg == 1, "tune: gemm_sf_reg must be 0 or 1");
-  tao::tuning().sf_reg = reg;
+// Split-K seam of the single-fetch GEMM: 1 = spread (built-in), 0 = fixed reducer.
+extern "C" int tao_tune_gemm_sf_seam(int seam) {
+  TAO_CHECK_ARG(seam == 0 || seam == 1, "tune: gemm_sf_seam must be 0 (fixed reducer) or 1 (spread)");
+  tao::tuning().sf_seam = seam;
   return TAO_OK;
 }
 

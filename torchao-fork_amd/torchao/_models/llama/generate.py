@@ -33,16 +33,25 @@ __all__ = ["build_model", "apply_quantization", "prefill", "decode_one_token", "
 
 
 def build_model(name: str, device, dtype=torch.bfloat16, checkpoint_path: Optional[Path] = None,
-                seed: int = 0) -> Transformer:
+                seed: int = 0, tile_format: Optional[str] = None) -> Transformer:
     """Construct on the meta device, materialise on ``device``; load a state dict if given,
-    else random-initialise (nn.Linear default U(-1/sqrt(K), 1/sqrt(K)), embeddings N(0, 0.02))."""
+    else random-initialise (nn.Linear default U(-1/sqrt(K), 1/sqrt(K)), embeddings N(0, 0.02)).
+
+    ``tile_format`` ("cuda" | "rocm") names the nibble map of TensorCoreTiledLayout tensors in
+    the checkpoint (torchao.ops.checkpoint_tile_format); without it such a checkpoint raises."""
     cfg = ModelArgs.from_name(name)
     with torch.device("meta"):
         model = Transformer(cfg)
     model = model.to_empty(device=device).to(dtype)
     if checkpoint_path is not None:
-        state = torch.load(str(checkpoint_path), map_location=device, weights_only=True,
-                           mmap=True)
+        import contextlib
+
+        from torchao.ops import checkpoint_tile_format
+
+        ctx = checkpoint_tile_format(tile_format) if tile_format else contextlib.nullcontext()
+        with ctx:
+            state = torch.load(str(checkpoint_path), map_location=device, weights_only=True,
+                               mmap=True)
         model.load_state_dict(state, assign=True)
         return model.eval()
     gen = torch.Generator(device=device).manual_seed(seed)
@@ -300,6 +309,8 @@ def main(argv=None):
     ap.add_argument("--check_tokens", type=int, default=32,
                     help="after timing, decode this many tokens again eagerly and report their "
                          "agreement with the graph-decoded tokens (0 = skip)")
+    ap.add_argument("--tile_format", choices=("cuda", "rocm"), default=None,
+                    help="nibble map of TensorCoreTiledLayout tensors in --checkpoint_path")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--write_result", type=Path, default=None)
@@ -329,7 +340,7 @@ def main(argv=None):
     device = torch.device(args.device)
     t = time.perf_counter()
     model = build_model(args.model_name, device, checkpoint_path=args.checkpoint_path,
-                        seed=args.seed)
+                        seed=args.seed, tile_format=args.tile_format)
     torch.cuda.synchronize()
     t_build = time.perf_counter() - t
     if not args.no_fuse_w13:

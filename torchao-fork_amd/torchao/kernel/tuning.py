@@ -33,7 +33,7 @@ _KNOBS = {
     "splitk_fenced": ("tao_tune_splitk_fenced", 1),
     "gemm_tile": ("tao_tune_gemm_tile", 2),
     "gemm_sf": ("tao_tune_gemm_sf", 7),
-    "gemm_sf_reg": ("tao_tune_gemm_sf_reg", 1),
+    "gemm_sf_seam": ("tao_tune_gemm_sf_seam", 1),
 }
 
 
