@@ -299,8 +299,8 @@ int tao_rope_kv_bf16(const uint16_t* qkv, const float* freqs, const int64_t* pos
 /* One-query attention over keys 0..pos[0] of the caches, GQA (H % Hkv == 0, H/Hkv <= 8),
  * D == 128: out [B][1][H*D] bf16. partial: fp32 workspace of B*Hkv*ceil(T/64)*(H/Hkv)*(D+2)
  * for the two-launch split (T > 1024, or tao_tune_attn 1); NULL = the library's per-stream
- * workspace (as the one-launch split of tao_tune_attn 2/3 uses: run once eagerly before graph
- * capture). Shorter caches run one single-pass kernel and do not touch it.
+ * workspace (run once eagerly before graph capture). Shorter caches run one single-pass kernel
+ * and do not touch it.
  * Replaces F.scaled_dot_product_attention at decode (model.py:441-476). */
 int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
                          const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
@@ -315,23 +315,9 @@ int tao_attn_prefill_bf16(const uint16_t* q, const uint16_t* k_cache, const uint
                           const int64_t* pos, uint16_t* out, int64_t B, int64_t H, int64_t Hkv,
                           int64_t D, int64_t S, int64_t T, float scale, void* stream);
 
-/* tao_attn_decode_bf16 whose launch also streams up to 4 device regions (pf_ptrs[r], pf_bytes[r]
- * bytes, 16-B aligned) into the MALL with pf_wgs extra workgroups, dropping the data: the
- * harness passes the next linear's weights (wo), so they come from the Infinity Cache instead
- * of HBM. The attention result is identical to tao_attn_decode_bf16's. The prefetch rides only
- * on the single-pass kernel (tao_tune_attn 0, T <= 1024); other modes ignore it. */
-int tao_attn_decode_pf_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
-                            const int64_t* pos, float* partial, uint16_t* out, int64_t B,
-                            int64_t H, int64_t Hkv, int64_t D, int64_t T, float scale,
-                            const void* const* pf_ptrs, const int64_t* pf_bytes, int n_pf,
-                            int pf_wgs, void* stream);
-
 /* Calling thread's choice of the decode-attention kernel: 0 = single-pass workgroup per query head
  * (f32 math, whole-line K loads) for T <= 1024, else the two-launch split (default); 1 = two-launch
- * split; 2 / 3 = one launch over 32 / 64-key chunks merged by the kv head's last arriving chunk;
- * 4 = as 0 with the packed-bf16 single-pass kernel (measured slower); 5 = as 0 with half-line K
- * loads (the round-1 kernel); 6 = as 0 with 32 keys per wave step (one load round trip up to 512
- * keys). */
+ * split. */
 int tao_tune_attn(int mode);
 
 /* Device-side faults of the decode kernels since the last call, read and cleared (synchronous:

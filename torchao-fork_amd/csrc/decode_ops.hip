@@ -11,8 +11,9 @@
 //                a workgroup per query head (online softmax per wave, LDS merge). Longer:
 //                split over 64-key chunks (flash-decoding; GQA: a workgroup serves the G query
 //                heads of one kv head), then a combine kernel merges the chunks' (max, sum, o).
-//                Opt-in (tao_tune_attn 2/3): the split in one launch, merged by the kv head's
-//                last arriving chunk (measured slower end to end, 672 vs 700 tokens/s)
+//                (Variants measured slower and removed in round 4: the split in one launch merged
+//                by the last arriving chunk, 672 vs 700 tokens/s; packed-bf16 math; half-line K
+//                loads; 32 keys per wave step; weight prefetch riding on the launch.)
 //   * SiLU-mul:  y = bf16(bf16(silu(a)) * b)                             (F.silu(w1 x) * w3 x)
 //   * argmax:    greedy next token over bf16 logits, torch.argmax's first-index tie rule
 #include <atomic>
@@ -30,19 +31,10 @@ int attn_prefill_mfma(const uint16_t* q, const uint16_t* k_cache, const uint16_t
 #ifndef TAO_ATTN_WAVES
 #define TAO_ATTN_WAVES 16  // waves per workgroup of the single-pass decode attention
 #endif
-// TAO_ATTN_STAMPS 1 (timing only, experiments/attn_stamps.py): per-workgroup s_memrealtime
-// stamps of attn_single_kernel: first instruction, q in registers, key loop done (per wave 0),
-// end. Never in the product library.
-#ifndef TAO_ATTN_STAMPS
-#define TAO_ATTN_STAMPS 0
-#endif
 
 namespace tao {
 
 TAO_DECODE_ERROR_WORD(decode_ops_status)
-#if TAO_ATTN_STAMPS
-__device__ unsigned long long g_attn_stamps[1024 * 4];
-#endif
 int int4gemv_decode_status(unsigned* bits);
 int int8gemv_decode_status(unsigned* bits);
 int int8dyn_decode_status(unsigned* bits);
@@ -312,312 +304,45 @@ __global__ __launch_bounds__(64) void attn_combine_kernel(const float* __restric
 }
 
 // ---- decode attention in one launch (short caches): one workgroup per (batch, query head) -----
-// NW waves (16; 8 measured 656 vs 682 tokens/s end to end); wave w takes keys w*16 + 16 NW i:
-// 4 lanes per key (lane p holds dims v*32 + 8p + e of q in registers, so each 16-B K load of 4
-// lanes is 64 contiguous bytes), the 16 keys' V rows loaded in the same round trip (lane = dim
-// pair). Online softmax per wave in fp32, waves merged through LDS. Every wave walks
-// ceil((L - 16 w) / (16 NW)) steps, so at T <= 1024 the chain is <= 4 round trips; longer
-// caches take the two-kernel split above.
+// NW waves (16; 8 measured 656 vs 682 tokens/s end to end); wave w takes keys w*16 + 16 NW i.
+// Each K load instruction covers 8 keys x 128 B (whole cache lines; lane l: key t0 + 8 i + l / 8,
+// dims 64 h + 8 (l % 8) ..; half-line loads moved half the bytes per instruction through the L2,
+// profiles/r3_probe_l2_pattern.jsonl), and the 16 keys' V rows are loaded in the same round trip
+// (lane = dim pair). The first step's K/V loads are issued before q's, so q (fresh from the wqkv
+// kernel) and the first keys arrive together; later steps prefetch the next step's K/V before
+// computing the current one. Online softmax per wave in fp32, waves merged through LDS. At
+// T <= 1024 the chain is <= 4 round trips; longer caches take the two-kernel split above.
 constexpr int kSingleMaxT = 1024;
-// tao_tune_attn: 0 = single-pass for T <= 1024 else the two-launch split (default), 1 = the
-// two-launch split, 2 / 3 = attn_chunk_fused_kernel with 32 / 64-key chunks
 constexpr int kSingleWaves = TAO_ATTN_WAVES;
 
-// Weight prefetch riding on the attention launch (tao_attn_decode_pf_bf16): workgroups past the
-// B x H attention workgroups stream up to 4 regions (the next linear's weights) with
-// default-policy 16-B loads and drop the data, so the bytes sit in the MALL when that linear
-// runs. One attention workgroup per head leaves most CUs idle for the launch's ~5 µs.
-struct AttnPf {
-  const uint4* p[4];
-  uint32_t n16[4];  // 16-B units per region
-  int n;            // regions
-  int nbh;          // B x H: the attention workgroups; blockIdx.x >= nbh prefetch
-};
-__device__ unsigned g_attn_pf_sink;
-
-// FULLK: each K load instruction covers 8 keys x 128 B (whole cache lines; lane l: key
-// t0 + 8 i + l / 8, dims 64 h + 8 (l % 8) ..) instead of 16 keys x 64 B (half lines: the L2 moves
-// half the bytes per instruction, profiles/r3_probe_l2_pattern.jsonl); 8 lanes per key.
-// KEYS32 (with FULLK): each wave takes 32 keys per step, both 16-key sets' loads issued at once,
-// so a cache of <= 512 keys is one load round trip per wave instead of two above 256 keys (no
-// cross-step prefetch: the registers hold one step).
-template <int D, int NW, bool FULLK = false, bool KEYS32 = false>
+template <int D, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
-    int H, int Hkv, int T, float scale, int S, AttnPf pf) {
-#if TAO_ATTN_STAMPS
-  const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
-#endif
+    int H, int Hkv, int T, float scale) {
   static_assert(D == 128, "head_dim 128");
   __shared__ float wm[NW], wl[NW];
   __shared__ float wo[NW][D];
-  if (pf.n > 0 && (int)blockIdx.x >= pf.nbh) {  // prefetch role (workgroup-uniform)
-    const uint32_t w = blockIdx.x - pf.nbh, nw = gridDim.x - pf.nbh;
-    constexpr uint32_t kT = NW * 64, kU = 8;  // threads, loads in flight per thread
-    uint32_t acc = 0;
-    for (int r = 0; r < pf.n; ++r) {
-      const uint4* base = pf.p[r];
-      const uint32_t n16 = pf.n16[r];
-      for (uint32_t u0 = w * kT * kU + threadIdx.x; u0 < n16; u0 += nw * kT * kU) {
-        uint4 v[kU];
-#pragma unroll
-        for (uint32_t j = 0; j < kU; ++j) {
-          const uint32_t u = u0 + j * kT;
-          v[j] = base[u < n16 ? u : n16 - 1];
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kU; ++j) acc ^= v[j].x ^ v[j].w;
-      }
-    }
-    if (acc == 0x9E3779B9u) g_attn_pf_sink = acc;  // keeps the loads; the value is irrelevant
-    return;
-  }
-  // S queries per (batch, head) (prefill; decode S = 1): q [B][H][S][D], query s at position
-  // pos[s] attends keys 0..pos[s]; out [B][S][H * D]
-  const int bhs = blockIdx.x;  // (b * H + h) * S + s
-  const int bh = bhs / S, s_q = bhs % S;
+  // q [B][H][1][D]: the query at position pos[0] attends keys 0..pos[0]; out [B][1][H * D]
+  const int bh = blockIdx.x;
   const int b = bh / H, h = bh % H, kvh = h / (H / Hkv);
-  const int L = attn_len(pos[s_q], T);
-  const size_t ooff = ((size_t)(b * S + s_q) * H + h) * (D / 2);  // output dword offset
+  const int L = attn_len(pos[0], T);
+  const size_t ooff = (size_t)bh * (D / 2);  // output dword offset
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int kq = lane >> 2, p = lane & 3;
   const size_t head = (size_t)(b * Hkv + kvh) * T;
   const uint32_t* vb = reinterpret_cast<const uint32_t*>(vc + head * D) + lane;
-  if constexpr (FULLK && KEYS32) {
-    const int g = lane >> 3, p8 = lane & 7;
-    const uint16_t* kbase = kc + head * D + p8 * 8;
-    uint4 ka[2][2], kb2[2][2];
-    uint32_t vv[2][16];
-    auto load_step = [&](int t0) __attribute__((always_inline)) {
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const int t1 = t0 + 16 * st;
-        const int ta = t1 + g < L ? t1 + g : L - 1, tb = t1 + 8 + g < L ? t1 + 8 + g : L - 1;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          ka[st][h] = *reinterpret_cast<const uint4*>(kbase + (size_t)ta * D + 64 * h);
-          kb2[st][h] = *reinterpret_cast<const uint4*>(kbase + (size_t)tb * D + 64 * h);
-        }
-      }
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int tj = t0 + 16 * st + j < L ? t0 + 16 * st + j : L - 1;
-          vv[st][j] = vb[(size_t)tj * (D / 2)];
-        }
-    };
-    const int first = wave * 32;
-    if (first < L) load_step(first);
-    float qr[16];
-    {
-      const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bhs * D + p8 * 8);
-      uint4 qv[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) qv[h] = qp[h * 8];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t w[4] = {qv[h].x, qv[h].y, qv[h].z, qv[h].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          qr[h * 8 + 2 * e] = bf16lo_to_f32(w[e]);
-          qr[h * 8 + 2 * e + 1] = bf16hi_to_f32(w[e]);
-        }
-      }
-    }
-    float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
-    for (int t0 = first; t0 < L; t0 += NW * 32) {
-      if (t0 != first) load_step(t0);
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const int t1 = t0 + 16 * st;
-        if (t1 >= L) break;  // wave-uniform
-        float sa = 0.f, sb = 0.f;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const uint32_t wa[4] = {ka[st][h].x, ka[st][h].y, ka[st][h].z, ka[st][h].w};
-          const uint32_t wb[4] = {kb2[st][h].x, kb2[st][h].y, kb2[st][h].z, kb2[st][h].w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            sa = fmaf(qr[h * 8 + 2 * e], bf16lo_to_f32(wa[e]),
-                      fmaf(qr[h * 8 + 2 * e + 1], bf16hi_to_f32(wa[e]), sa));
-            sb = fmaf(qr[h * 8 + 2 * e], bf16lo_to_f32(wb[e]),
-                      fmaf(qr[h * 8 + 2 * e + 1], bf16hi_to_f32(wb[e]), sb));
-          }
-        }
-        sa = wave_bfly<1, 8>(sa, lane_id(), [](float a, float c) { return a + c; });
-        sb = wave_bfly<1, 8>(sb, lane_id(), [](float a, float c) { return a + c; });
-        const bool va = t1 + g < L, vbk = t1 + 8 + g < L;
-        sa = va ? sa * scale : -INFINITY;
-        sb = vbk ? sb * scale : -INFINITY;
-        float mx = fmaxf(sa, sb);
-        mx = wave_bfly<8, 64>(mx, lane_id(), [](float a, float c) { return fmaxf(a, c); });
-        const float mn = fmaxf(m, mx);  // finite: key t1 < L is valid
-        const float corr = __expf(m - mn);
-        const float ea = va ? __expf(sa - mn) : 0.f, eb = vbk ? __expf(sb - mn) : 0.f;
-        float es = ea + eb;
-        es = wave_bfly<8, 64>(es, lane_id(), [](float a, float c) { return a + c; });
-        l = fmaf(l, corr, es);
-        o0 *= corr;
-        o1 *= corr;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float pa = __shfl(ea, 8 * j, 64), pb = __shfl(eb, 8 * j, 64);
-          o0 = fmaf(pa, bf16lo_to_f32(vv[st][j]), o0);
-          o1 = fmaf(pa, bf16hi_to_f32(vv[st][j]), o1);
-          o0 = fmaf(pb, bf16lo_to_f32(vv[st][j + 8]), o0);
-          o1 = fmaf(pb, bf16hi_to_f32(vv[st][j + 8]), o1);
-        }
-        m = mn;
-      }
-    }
-    if (lane == 0) {
-      wm[wave] = m;
-      wl[wave] = l;
-    }
-    wo[wave][2 * lane] = o0;
-    wo[wave][2 * lane + 1] = o1;
-    __syncthreads();
-    if (wave == 0) {
-      float M = -INFINITY;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w]);
-      float a0 = 0.f, a1 = 0.f, ls = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        const float f = wm[w] == -INFINITY ? 0.f : __expf(wm[w] - M);  // waves with no keys
-        ls = fmaf(wl[w], f, ls);
-        a0 = fmaf(wo[w][2 * lane], f, a0);
-        a1 = fmaf(wo[w][2 * lane + 1], f, a1);
-      }
-      const float inv = 1.f / ls;
-      reinterpret_cast<uint32_t*>(out)[ooff + lane] =
-          (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
-    }
-    return;
-  }
-  if constexpr (FULLK) {
-    // lane (g = l / 8, p8 = l % 8): keys t0 + g and t0 + 8 + g, dims 64 h + 8 p8 + e (h < 2, e < 8)
-    const int g = lane >> 3, p8 = lane & 7;
-    const uint16_t* kbase = kc + head * D + p8 * 8;
-    uint4 ka[2], kb2[2];
-    uint32_t vv[16];
-    auto load_step = [&](int t0) __attribute__((always_inline)) {
-      const int ta = t0 + g < L ? t0 + g : L - 1, tb = t0 + 8 + g < L ? t0 + 8 + g : L - 1;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        ka[h] = *reinterpret_cast<const uint4*>(kbase + (size_t)ta * D + 64 * h);
-        kb2[h] = *reinterpret_cast<const uint4*>(kbase + (size_t)tb * D + 64 * h);
-      }
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int tj = t0 + j < L ? t0 + j : L - 1;
-        vv[j] = vb[(size_t)tj * (D / 2)];
-      }
-    };
-    load_step(wave * 16);
-    float qr[16];
-    {
-      const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bhs * D + p8 * 8);
-      uint4 qv[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) qv[h] = qp[h * 8];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t w[4] = {qv[h].x, qv[h].y, qv[h].z, qv[h].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          qr[h * 8 + 2 * e] = bf16lo_to_f32(w[e]);
-          qr[h * 8 + 2 * e + 1] = bf16hi_to_f32(w[e]);
-        }
-      }
-    }
-    float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
-    for (int t0 = wave * 16; t0 < L; t0 += NW * 16) {
-      float sa = 0.f, sb = 0.f;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t wa[4] = {ka[h].x, ka[h].y, ka[h].z, ka[h].w};
-        const uint32_t wb[4] = {kb2[h].x, kb2[h].y, kb2[h].z, kb2[h].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          sa = fmaf(qr[h * 8 + 2 * e], bf16lo_to_f32(wa[e]),
-                    fmaf(qr[h * 8 + 2 * e + 1], bf16hi_to_f32(wa[e]), sa));
-          sb = fmaf(qr[h * 8 + 2 * e], bf16lo_to_f32(wb[e]),
-                    fmaf(qr[h * 8 + 2 * e + 1], bf16hi_to_f32(wb[e]), sb));
-        }
-      }
-      float vf[32];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        vf[2 * j] = bf16lo_to_f32(vv[j]);
-        vf[2 * j + 1] = bf16hi_to_f32(vv[j]);
-      }
-      if (t0 + NW * 16 < L) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
-      sa = wave_bfly<1, 8>(sa, lane_id(), [](float a, float c) { return a + c; });
-      sb = wave_bfly<1, 8>(sb, lane_id(), [](float a, float c) { return a + c; });
-      const bool va = t0 + g < L, vbk = t0 + 8 + g < L;
-      sa = va ? sa * scale : -INFINITY;
-      sb = vbk ? sb * scale : -INFINITY;
-      float mx = fmaxf(sa, sb);
-      mx = wave_bfly<8, 64>(mx, lane_id(), [](float a, float c) { return fmaxf(a, c); });
-      const float mn = fmaxf(m, mx);  // finite: key t0 < L is valid
-      const float corr = __expf(m - mn);
-      const float ea = va ? __expf(sa - mn) : 0.f, eb = vbk ? __expf(sb - mn) : 0.f;
-      float es = ea + eb;  // each key sits in 8 lanes of one group: xor 8..32 counts it once
-      es = wave_bfly<8, 64>(es, lane_id(), [](float a, float c) { return a + c; });
-      l = fmaf(l, corr, es);
-      o0 *= corr;
-      o1 *= corr;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float pa = __shfl(ea, 8 * j, 64), pb = __shfl(eb, 8 * j, 64);
-        o0 = fmaf(pa, vf[2 * j], o0);
-        o1 = fmaf(pa, vf[2 * j + 1], o1);
-        o0 = fmaf(pb, vf[2 * (j + 8)], o0);
-        o1 = fmaf(pb, vf[2 * (j + 8) + 1], o1);
-      }
-      m = mn;
-    }
-    if (lane == 0) {
-      wm[wave] = m;
-      wl[wave] = l;
-    }
-    wo[wave][2 * lane] = o0;
-    wo[wave][2 * lane + 1] = o1;
-    __syncthreads();
-    if (wave == 0) {
-      float M = -INFINITY;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w]);
-      float a0 = 0.f, a1 = 0.f, ls = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        const float f = wm[w] == -INFINITY ? 0.f : __expf(wm[w] - M);  // waves with no keys
-        ls = fmaf(wl[w], f, ls);
-        a0 = fmaf(wo[w][2 * lane], f, a0);
-        a1 = fmaf(wo[w][2 * lane + 1], f, a1);
-      }
-      const float inv = 1.f / ls;
-      reinterpret_cast<uint32_t*>(out)[ooff + lane] =
-          (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
-    }
-    return;
-  }
-  const uint16_t* kb = kc + head * D + p * 8;
-
-  // One step = 16 keys of this wave: lane (kq, p) loads 4 x 16 B of key t0 + kq, and the 16
-  // keys' V dim pair `lane`. The first step's K/V loads are issued before q's, so q (fresh from
-  // the wqkv kernel) and the first keys arrive in the same round trip; later steps prefetch the
-  // next step's K/V before computing the current one.
-  uint4 kv[4];
+  // lane (g = l / 8, p8 = l % 8): keys t0 + g and t0 + 8 + g, dims 64 h + 8 p8 + e (h < 2, e < 8)
+  const int g = lane >> 3, p8 = lane & 7;
+  const uint16_t* kbase = kc + head * D + p8 * 8;
+  uint4 ka[2], kb2[2];
   uint32_t vv[16];
   auto load_step = [&](int t0) __attribute__((always_inline)) {
-    const int t = t0 + kq;
-    const int tc = t < L ? t : L - 1;  // clamped loads, masked below
+    const int ta = t0 + g < L ? t0 + g : L - 1, tb = t0 + 8 + g < L ? t0 + 8 + g : L - 1;
 #pragma unroll
-    for (int v = 0; v < 4; ++v) kv[v] = *reinterpret_cast<const uint4*>(kb + (size_t)tc * D + v * 32);
+    for (int hh = 0; hh < 2; ++hh) {
+      ka[hh] = *reinterpret_cast<const uint4*>(kbase + (size_t)ta * D + 64 * hh);
+      kb2[hh] = *reinterpret_cast<const uint4*>(kbase + (size_t)tb * D + 64 * hh);
+    }
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int tj = t0 + j < L ? t0 + j : L - 1;
@@ -625,41 +350,36 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     }
   };
   load_step(wave * 16);
-  // lane p holds q dims v*32 + 8p + e (e < 8) in registers: 4 x 16 B straight from global
-  float qr[32];
+  float qr[16];
   {
-    const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bhs * D + p * 8);
-    uint4 qv[4];
+    const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bh * D + p8 * 8);
+    uint4 qv[2];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) qv[v] = qp[v * 4];
+    for (int hh = 0; hh < 2; ++hh) qv[hh] = qp[hh * 8];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const uint32_t w[4] = {qv[v].x, qv[v].y, qv[v].z, qv[v].w};
+    for (int hh = 0; hh < 2; ++hh) {
+      const uint32_t w[4] = {qv[hh].x, qv[hh].y, qv[hh].z, qv[hh].w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        qr[v * 8 + 2 * e] = bf16lo_to_f32(w[e]);
-        qr[v * 8 + 2 * e + 1] = bf16hi_to_f32(w[e]);
+        qr[hh * 8 + 2 * e] = bf16lo_to_f32(w[e]);
+        qr[hh * 8 + 2 * e + 1] = bf16hi_to_f32(w[e]);
       }
     }
   }
-
-#if TAO_ATTN_STAMPS
-  float qsum = 0.f;  // forces the q loads to land before the stamp
-#pragma unroll
-  for (int i = 0; i < 32; ++i) qsum += qr[i];
-  const unsigned long long st1 = __builtin_amdgcn_s_memrealtime() + (qsum == 12345.f ? 1 : 0);
-#endif
   float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
   for (int t0 = wave * 16; t0 < L; t0 += NW * 16) {
-    const int t = t0 + kq;
-    float sc = 0.f;
+    float sa = 0.f, sb = 0.f;
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const uint32_t w[4] = {kv[v].x, kv[v].y, kv[v].z, kv[v].w};
+    for (int hh = 0; hh < 2; ++hh) {
+      const uint32_t wa[4] = {ka[hh].x, ka[hh].y, ka[hh].z, ka[hh].w};
+      const uint32_t wb[4] = {kb2[hh].x, kb2[hh].y, kb2[hh].z, kb2[hh].w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        sc = fmaf(qr[v * 8 + 2 * e], bf16lo_to_f32(w[e]),
-                  fmaf(qr[v * 8 + 2 * e + 1], bf16hi_to_f32(w[e]), sc));
+      for (int e = 0; e < 4; ++e) {
+        sa = fmaf(qr[hh * 8 + 2 * e], bf16lo_to_f32(wa[e]),
+                  fmaf(qr[hh * 8 + 2 * e + 1], bf16hi_to_f32(wa[e]), sa));
+        sb = fmaf(qr[hh * 8 + 2 * e], bf16lo_to_f32(wb[e]),
+                  fmaf(qr[hh * 8 + 2 * e + 1], bf16hi_to_f32(wb[e]), sb));
+      }
     }
     float vf[32];
 #pragma unroll
@@ -668,32 +388,33 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
       vf[2 * j + 1] = bf16hi_to_f32(vv[j]);
     }
     if (t0 + NW * 16 < L) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
-    sc += xor_partner<1>(sc, lane_id());
-    sc += xor_partner<2>(sc, lane_id());
-    sc = t < L ? sc * scale : -INFINITY;
-    float mx = sc;
-    mx = wave_bfly<4, 64>(mx, lane_id(), [](float a, float b) { return fmaxf(a, b); });
+    sa = wave_bfly<1, 8>(sa, lane_id(), [](float a, float c) { return a + c; });
+    sb = wave_bfly<1, 8>(sb, lane_id(), [](float a, float c) { return a + c; });
+    const bool va = t0 + g < L, vbk = t0 + 8 + g < L;
+    sa = va ? sa * scale : -INFINITY;
+    sb = vbk ? sb * scale : -INFINITY;
+    float mx = fmaxf(sa, sb);
+    mx = wave_bfly<8, 64>(mx, lane_id(), [](float a, float c) { return fmaxf(a, c); });
     const float mn = fmaxf(m, mx);  // finite: key t0 < L is valid
     const float corr = __expf(m - mn);
-    const float e = t < L ? __expf(sc - mn) : 0.f;
-    float es = e;  // each key sits in 4 lanes; the xor 4..32 sum counts it once
-    es = wave_bfly<4, 64>(es, lane_id(), [](float a, float b) { return a + b; });
+    const float ea = va ? __expf(sa - mn) : 0.f, eb = vbk ? __expf(sb - mn) : 0.f;
+    float es = ea + eb;  // each key sits in 8 lanes of one group: xor 8..32 counts it once
+    es = wave_bfly<8, 64>(es, lane_id(), [](float a, float c) { return a + c; });
     l = fmaf(l, corr, es);
     o0 *= corr;
     o1 *= corr;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float pj = __shfl(e, j * 4, 64);
-      o0 = fmaf(pj, vf[2 * j], o0);
-      o1 = fmaf(pj, vf[2 * j + 1], o1);
+    for (int j = 0; j < 8; ++j) {
+      const float pa = __shfl(ea, 8 * j, 64), pb = __shfl(eb, 8 * j, 64);
+      o0 = fmaf(pa, vf[2 * j], o0);
+      o1 = fmaf(pa, vf[2 * j + 1], o1);
+      o0 = fmaf(pb, vf[2 * (j + 8)], o0);
+      o1 = fmaf(pb, vf[2 * (j + 8) + 1], o1);
     }
     m = mn;
   }
   if (lane == 0) {
     wm[wave] = m;
-#if TAO_ATTN_STAMPS
-    if (wave == 0) g_attn_stamps[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memrealtime();
-#endif
     wl[wave] = l;
   }
   wo[wave][2 * lane] = o0;
@@ -713,305 +434,6 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     }
     const float inv = 1.f / ls;
     reinterpret_cast<uint32_t*>(out)[ooff + lane] =
-        (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
-#if TAO_ATTN_STAMPS
-    const unsigned long long st3 = __builtin_amdgcn_s_memrealtime();
-    if (lane < 4 && lane != 2 && blockIdx.x < 1024)
-      g_attn_stamps[blockIdx.x * 4 + lane] = lane == 0 ? st0 : lane == 1 ? st1 : st3;
-#endif
-  }
-}
-
-// ---- decode attention, one launch, packed-bf16 math (tao_tune_attn 4; measured slower) -------
-// Same geometry as attn_single_kernel (a workgroup of NW waves per (batch, query head), the
-// waves merged through LDS), rebuilt around what its timeline showed: the key loop was VALU
-// bound (every k and v element converted to f32 and multiplied on its own: ~170 wave
-// instructions per 16 keys, 4 waves a SIMD) and a 300-key cache took two dependent load rounds.
-//   * 32 keys per wave per round (512 per workgroup): at <= 512 keys every load of the launch —
-//     q, and each wave's K rows (4 lanes x 64 B per key, 2 keys a lane) and V rows (a dim pair a
-//     lane) — is issued at once: one round trip;
-//   * scores by v_dot2c_f32_bf16 on the packed bf16 q and k (2 exact products per op, f32 sum):
-//     16 ops per key-quarter instead of 32 multiply-adds and 32 conversions;
-//   * P.V by v_dot2c_f32_bf16 on key pairs: p rounded to bf16 (as flash attention feeds its PV
-//     product) and packed two keys a dword, broadcast by v_readlane (no LDS shuffles), v pairs
-//     formed by v_perm; the softmax denominator sums the same rounded p, so the output is an
-//     exactly normalised weighted mean of the V rows.
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void attn_dot2_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
-    const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
-    int H, int Hkv, int T, float scale) {
-  constexpr int D = 128, KPW = 32, ROUND = NW * KPW;
-  __shared__ float wm[NW], wl[NW];
-  __shared__ float wo[NW][D];
-  const int bh = blockIdx.x;  // b * H + h
-  const int b = bh / H, h = bh % H, kvh = h / (H / Hkv);
-  const int L = attn_len(pos[0], T);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar key indices
-  const int kq = lane >> 2, p = lane & 3;
-  const size_t head = (size_t)(b * Hkv + kvh) * T;
-  const uint16_t* kb = kc + head * D + p * 8;
-  // V rows by buffer loads: the row offset (wave-uniform) in a scalar register, the lane's
-  // dim pair in the vector offset
-  const Rsrc vr = make_rsrc(vc + head * D, (uint32_t)((size_t)L * D * 2));
-
-  uint4 ka[4], kb2[4];  // keys t0 + kq and t0 + 16 + kq: dims v*32 + 8p + e, packed bf16
-  uint32_t vv[KPW];     // the wave's 32 keys' V dim pair `lane`
-  auto load_round = [&](int t0) __attribute__((always_inline)) {
-    const int ta = t0 + kq < L ? t0 + kq : L - 1, tb = t0 + 16 + kq < L ? t0 + 16 + kq : L - 1;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      ka[v] = *reinterpret_cast<const uint4*>(kb + (size_t)ta * D + v * 32);
-      kb2[v] = *reinterpret_cast<const uint4*>(kb + (size_t)tb * D + v * 32);
-    }
-#pragma unroll
-    for (int j = 0; j < KPW; ++j) {
-      const int tj = t0 + j < L ? t0 + j : L - 1;  // clamped, weighted 0 below
-      vv[j] = __builtin_amdgcn_raw_buffer_load_b32(vr, lane * 4, tj * (D * 2), 0);
-    }
-  };
-  uint4 qv[4];  // q dims v*32 + 8p + e, packed bf16 (no conversion)
-  {
-    const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bh * D + p * 8);
-#pragma unroll
-    for (int v = 0; v < 4; ++v) qv[v] = qp[v * 4];
-  }
-
-  // q's loads and the first round's K / V loads are all in flight before the first wait;
-  // caches past 512 keys take one more round trip per round
-  float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
-#pragma unroll 1
-  for (int t0 = wave * KPW; t0 < L; t0 += ROUND) {
-    load_round(t0);
-    float sa = 0.f, sb = 0.f;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const uint32_t qw[4] = {qv[v].x, qv[v].y, qv[v].z, qv[v].w};
-      const uint32_t aw[4] = {ka[v].x, ka[v].y, ka[v].z, ka[v].w};
-      const uint32_t bw[4] = {kb2[v].x, kb2[v].y, kb2[v].z, kb2[v].w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        sa = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, qw[e]),
-                                             __builtin_bit_cast(bf16x2_t, aw[e]), sa, false);
-        sb = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, qw[e]),
-                                             __builtin_bit_cast(bf16x2_t, bw[e]), sb, false);
-      }
-    }
-    sa += xor_partner<1>(sa, lane_id());
-    sb += xor_partner<1>(sb, lane_id());
-    sa += xor_partner<2>(sa, lane_id());
-    sb += xor_partner<2>(sb, lane_id());
-    const bool va = t0 + kq < L, vb_ok = t0 + 16 + kq < L;
-    sa = va ? sa * scale : -INFINITY;
-    sb = vb_ok ? sb * scale : -INFINITY;
-    float mx = fmaxf(sa, sb);
-    mx = wave_bfly<4, 64>(mx, lane_id(), [](float a, float c) { return fmaxf(a, c); });
-    const float mn = fmaxf(m, mx);  // finite: key t0 < L is valid
-    const float corr = __expf(m - mn);
-    // p rounded to bf16; the denominator sums the rounded values
-    const uint16_t pa = va ? f32_to_bf16(__expf(sa - mn)) : (uint16_t)0;
-    const uint16_t pb = vb_ok ? f32_to_bf16(__expf(sb - mn)) : (uint16_t)0;
-    float es = bf16_to_f32(pa) + bf16_to_f32(pb);  // 4 lanes per key: xor 4..32 counts each once
-    es = wave_bfly<4, 64>(es, lane_id(), [](float a, float c) { return a + c; });
-    l = fmaf(l, corr, es);
-    o0 *= corr;
-    o1 *= corr;
-    // pair (key 2i, key 2i + 1) of each half: lanes 8i and 8i + 4 hold them
-    const uint32_t na = (uint32_t)xor_partner<4>((int)pa, lane_id());
-    const uint32_t nb = (uint32_t)xor_partner<4>((int)pb, lane_id());
-    const uint32_t ppa = (uint32_t)pa | (na << 16), ppb = (uint32_t)pb | (nb << 16);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t sA = (uint32_t)__builtin_amdgcn_readlane((int)ppa, 8 * i);
-      const uint32_t sB = (uint32_t)__builtin_amdgcn_readlane((int)ppb, 8 * i);
-      const uint32_t a0 = vv[2 * i], a1 = vv[2 * i + 1];
-      const uint32_t b0 = vv[16 + 2 * i], b1 = vv[16 + 2 * i + 1];
-      o0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, sA),
-                                           __builtin_bit_cast(bf16x2_t, __builtin_amdgcn_perm(a1, a0, 0x05040100u)),
-                                           o0, false);
-      o1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, sA),
-                                           __builtin_bit_cast(bf16x2_t, __builtin_amdgcn_perm(a1, a0, 0x07060302u)),
-                                           o1, false);
-      o0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, sB),
-                                           __builtin_bit_cast(bf16x2_t, __builtin_amdgcn_perm(b1, b0, 0x05040100u)),
-                                           o0, false);
-      o1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, sB),
-                                           __builtin_bit_cast(bf16x2_t, __builtin_amdgcn_perm(b1, b0, 0x07060302u)),
-                                           o1, false);
-    }
-    m = mn;
-  }
-  if (lane == 0) {
-    wm[wave] = m;  // -inf: the wave had no keys
-    wl[wave] = l;
-  }
-  wo[wave][2 * lane] = o0;
-  wo[wave][2 * lane + 1] = o1;
-  __syncthreads();
-  if (wave == 0) {
-    const int nw = (L + KPW - 1) / KPW < NW ? (L + KPW - 1) / KPW : NW;  // waves with keys
-    float M = -INFINITY;
-    for (int w = 0; w < nw; ++w) M = fmaxf(M, wm[w]);
-    float a0 = 0.f, a1 = 0.f, ls = 0.f;
-    for (int w = 0; w < nw; ++w) {
-      const float f = __expf(wm[w] - M);
-      ls = fmaf(wl[w], f, ls);
-      a0 = fmaf(wo[w][2 * lane], f, a0);
-      a1 = fmaf(wo[w][2 * lane + 1], f, a1);
-    }
-    const float inv = 1.f / ls;
-    reinterpret_cast<uint32_t*>(out)[(size_t)bh * (D / 2) + lane] =
-        (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
-  }
-}
-
-// ---- decode attention in one launch, split over key chunks (opt-in, tao_tune_attn 2 / 3) -----
-// Flash-decoding with the merge in the same launch: a workgroup per (batch, kv head, CH-key
-// chunk) serves the G query heads of its kv head (GQA: each K/V byte is read once, not G
-// times), and the chunk's partial (m, l, o) goes to a slab; the chunk whose ticket comes last
-// for its kv head merges all its chunks in chunk order (deterministic) and writes the bf16
-// output. Hand-off as the split-K GEMM's (gemm_mfma.hip): sc1 stores and loads of the partials,
-// every storing wave's vmcnt(0) wait and a workgroup barrier before one lane's agent-scope
-// ticket, no fences. The grid is sized by T; chunks past pos[0] exit without a ticket. Against
-// attn_single_kernel (a workgroup per query head over the whole cache): G x fewer K/V bytes and
-// ~ceil(L / CH) x more workgroups per head, but the hand-off adds three device-scope round trips
-// (sc1 store, ticket, sc1 loads) to a latency-bound launch: Llama-3-8B int4 decode 672 (32-key)
-// / 669 (64-key) vs 700 tokens/s with the single-pass kernel (experiments/ab_attn.py,
-// profiles/r1_ab_attn.jsonl).
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-
-template <int G, int CH>
-__global__ __launch_bounds__(256) void attn_chunk_fused_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
-    const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, float* __restrict__ part,
-    unsigned* __restrict__ cnt, uint16_t* __restrict__ out, int Hkv, int T, float scale) {
-  constexpr int D = 128;
-  constexpr int KPT = 256 / CH;       // threads per key in the score phase
-  constexpr int DPT = D / KPT;        // dims per thread
-  constexpr int KL = DPT / 8;         // 16-B K loads per thread
-  constexpr int PS = D + 2;           // floats per (chunk, head) partial: o[D], m, l
-  static_assert(CH == 32 || CH == 64, "chunk of 32 or 64 keys");
-  __shared__ float qs[G][D];
-  __shared__ float ps[G][CH];
-  __shared__ unsigned flag;
-  const int bk = blockIdx.x;  // b * Hkv + kvh
-  const int b = bk / Hkv, kvh = bk % Hkv;
-  const int c = blockIdx.y, NC = gridDim.y;
-  const int L = attn_len(pos[0], T);
-  const int t0 = c * CH;
-  if (t0 >= L) return;  // uniform; not counted
-  const int nact = (L + CH - 1) / CH;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int H = Hkv * G;
-  const size_t head = (size_t)bk * T;
-
-  // every load of the chunk up front: this thread's K piece, then its V column (dim pair
-  // `lane`, all CH keys; rows past L clamped and weighted 0), then q
-  const int j = tid / KPT, pp = tid % KPT;
-  const int kk = t0 + j;
-  uint4 kv[KL];
-  {
-    const uint4* kr = reinterpret_cast<const uint4*>(
-        kc + (head + (kk < L ? kk : L - 1)) * D + pp * DPT);
-#pragma unroll
-    for (int v = 0; v < KL; ++v) kv[v] = kr[v];
-  }
-  uint32_t vv[CH];
-  {
-    const uint32_t* vb = reinterpret_cast<const uint32_t*>(vc + head * D) + lane;
-#pragma unroll
-    for (int i = 0; i < CH; ++i) vv[i] = vb[(size_t)(t0 + i < L ? t0 + i : L - 1) * (D / 2)];
-  }
-  for (int i = tid; i < G * D / 2; i += 256) {
-    const int g = i / (D / 2), d2 = i % (D / 2);
-    const uint32_t w = reinterpret_cast<const uint32_t*>(q)[((size_t)b * H + kvh * G + g) * (D / 2) + d2];
-    qs[g][2 * d2] = bf16lo_to_f32(w);
-    qs[g][2 * d2 + 1] = bf16hi_to_f32(w);
-  }
-  __syncthreads();
-
-  // scores of key j for the G heads: KPT lanes per key, DPT dims each
-  float sc[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) sc[g] = 0.f;
-#pragma unroll
-  for (int v = 0; v < KL; ++v) {
-    const uint32_t w[4] = {kv[v].x, kv[v].y, kv[v].z, kv[v].w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int d = pp * DPT + v * 8 + 2 * e;
-      const float k0 = bf16lo_to_f32(w[e]), k1 = bf16hi_to_f32(w[e]);
-#pragma unroll
-      for (int g = 0; g < G; ++g) sc[g] = fmaf(qs[g][d], k0, fmaf(qs[g][d + 1], k1, sc[g]));
-    }
-  }
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-    if constexpr (KPT > 1)
-      sc[g] = wave_bfly<1, KPT>(sc[g], lane_id(), [](float a, float b) { return a + b; });
-  if (pp == 0) {
-#pragma unroll
-    for (int g = 0; g < G; ++g) ps[g][j] = kk < L ? sc[g] * scale : -INFINITY;
-  }
-  __syncthreads();
-
-  // per head (wave g, g + 4): chunk softmax, then o = sum_j p_j v_j for dim pair `lane`
-  const Rsrc prs = make_rsrc(part + (size_t)bk * NC * G * PS, (uint32_t)(NC * G * PS * 4));
-  for (int g = wave; g < G; g += 4) {
-    const float s = lane < CH ? ps[g][lane] : -INFINITY;
-    float m = s;
-    m = wave_max(m);  // finite: key t0 < L
-    const float e = s == -INFINITY ? 0.f : __expf(s - m);
-    const float l = wave_sum(e);
-    float o0 = 0.f, o1 = 0.f;
-#pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const float pj = __shfl(e, i, 64);
-      o0 = fmaf(pj, bf16lo_to_f32(vv[i]), o0);
-      o1 = fmaf(pj, bf16hi_to_f32(vv[i]), o1);
-    }
-    const uint32_t base = (uint32_t)((c * G + g) * PS) * 4;
-    const uint2 ov = make_uint2(__float_as_uint(o0), __float_as_uint(o1));
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, ov), prs, base + 8 * lane,
-                                          0, kSC1);
-    if (lane == 0) {
-      const uint2 ml = make_uint2(__float_as_uint(m), __float_as_uint(l));
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, ml), prs, base + 4 * D,
-                                            0, kSC1);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (!last_arriver(&cnt[bk], (unsigned)nact, &flag, 0)) return;
-
-  // merge the kv head's chunks in chunk order, 8 chunks' loads in flight per round
-  for (int g = wave; g < G; g += 4) {
-    float M = -INFINITY, ls = 0.f, a0 = 0.f, a1 = 0.f;
-    for (int c0 = 0; c0 < nact; c0 += 8) {
-      uint2 ml[8], ov[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int cc = c0 + u < nact ? c0 + u : nact - 1;
-        const uint32_t base = (uint32_t)((cc * G + g) * PS) * 4;
-        ml[u] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(prs, base + 4 * D, 0, kSC1));
-        ov[u] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(prs, base + 8 * lane, 0, kSC1));
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (c0 + u < nact) {
-          const float m = __uint_as_float(ml[u].x), l = __uint_as_float(ml[u].y);
-          const float mn = fmaxf(M, m);
-          const float fo = __expf(M - mn), fn = __expf(m - mn);  // M = -inf first: fo = 0
-          ls = ls * fo + l * fn;
-          a0 = a0 * fo + __uint_as_float(ov[u].x) * fn;
-          a1 = a1 * fo + __uint_as_float(ov[u].y) * fn;
-          M = mn;
-        }
-      }
-    }
-    const float inv = 1.f / ls;
-    reinterpret_cast<uint32_t*>(out)[((size_t)b * H + kvh * G + g) * (D / 2) + lane] =
         (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
   }
 }
@@ -1171,66 +593,21 @@ int tao_rope_kv_bf16(const uint16_t* qkv, const float* freqs, const int64_t* pos
 
 static int attn_decode(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
                        const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
-                       int64_t Hkv, int64_t D, int64_t T, float scale, tao::AttnPf pf,
-                       int pf_wgs, void* stream) {
+                       int64_t Hkv, int64_t D, int64_t T, float scale, void* stream) {
   TAO_CHECK_ARG(D == 128, "attn_decode: head_dim must be 128 (got %lld)", (long long)D);
   TAO_CHECK_ARG(B > 0 && Hkv > 0 && H % Hkv == 0 && T > 0, "attn_decode: bad sizes");
   const int G = (int)(H / Hkv);
   TAO_CHECK_ARG(G == 1 || G == 2 || G == 4 || G == 8, "attn_decode: H / Hkv must be 1, 2, 4 or 8");
   TAO_CHECK_ALIGN(k_cache, 16, "k_cache");
+  TAO_CHECK_ALIGN(q, 16, "q");
   hipStream_t st = as_stream(stream);
   const int mode = tao::tuning().attn_mode;
-  if (mode == 2 || mode == 3) {  // one launch, key chunks merged by the last arriver
-    const int CH = mode == 2 ? 32 : 64;
-    const int NC = (int)((T + CH - 1) / CH);
-    void* ws = nullptr;
-    unsigned* cnt = nullptr;
-    const size_t bytes = (size_t)B * Hkv * NC * G * (D + 2) * sizeof(float);
-    TAO_CHECK_ARG(bytes / B / Hkv < (1ull << 31), "attn_decode: cache too long");
-    const int rc = split_workspace(st, bytes, (size_t)(B * Hkv), &ws, &cnt);
-    if (rc != TAO_OK) return rc;
-    float* slab = reinterpret_cast<float*>(ws);
-    const dim3 grid((unsigned)(B * Hkv), (unsigned)NC);
-    switch (G * 100 + CH) {
-#define TAO_ATTN_F(GG, CC)                                                                   \
-  case GG * 100 + CC:                                                                        \
-    launch(attn_chunk_fused_kernel<GG, CC>, grid, dim3(256), 0, st, q, k_cache, v_cache, pos, \
-           slab, cnt, out, (int)Hkv, (int)T, scale);                                         \
-    break;
-      TAO_ATTN_F(1, 32) TAO_ATTN_F(2, 32) TAO_ATTN_F(4, 32) TAO_ATTN_F(8, 32)
-      TAO_ATTN_F(1, 64) TAO_ATTN_F(2, 64) TAO_ATTN_F(4, 64) TAO_ATTN_F(8, 64)
-#undef TAO_ATTN_F
-    }
-    return check_launch("attn_chunk_fused_kernel");
-  }
-  // Single pass, a workgroup per query head. The f32 kernel is the default: the packed-bf16
-  // one (mode 4) loads every key of a <= 512-key cache in one round trip but measured slower
-  // at every length (experiments/attn_time.py, profiles/r3_attn_time_dot2_vs_f32.jsonl: 328
-  // keys 6.20 vs 5.76 µs per graph launch; e2e 662 vs 668 tokens/s).
-  if (T <= kSingleMaxT && mode == 4) {  // partial is not touched
-    launch(attn_dot2_kernel<16>, dim3((unsigned)(B * H)), dim3(64 * 16), 0, st, q, k_cache,
-           v_cache, pos, out, (int)H, (int)Hkv, (int)T, scale);
-    return check_launch("attn_dot2_kernel");
-  }
-  // The f32 kernel with whole-line K loads is the default (per graph launch 3.92 / 5.63 / 7.06 /
-  // 10.21 µs at 128 / 328 / 512 / 900 keys vs 4.07 / 5.72 / 7.13 / 10.32 with the half-line
-  // loads of mode 5; e2e within noise: profiles/r3_attn_time_fullk.jsonl, r3_ab_e2e_attn5.jsonl).
-  if (T <= kSingleMaxT && mode == 0) {  // the f32 single-pass kernel, whole-line K loads
-    launch((attn_single_kernel<128, kSingleWaves, true>), dim3((unsigned)(B * H + pf_wgs)),
-           dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
-           (int)T, scale, 1, pf);
-    return check_launch("attn_single_kernel<fullk>");
-  }
-  if (T <= kSingleMaxT && mode == 6) {  // whole-line K loads, 32 keys per wave step
-    launch((attn_single_kernel<128, kSingleWaves, true, true>), dim3((unsigned)(B * H + pf_wgs)),
-           dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
-           (int)T, scale, 1, pf);
-    return check_launch("attn_single_kernel<fullk, keys32>");
-  }
-  if (T <= kSingleMaxT && mode == 5) {  // the f32 single-pass kernel, 16 keys x 64 B K loads
+  // Single pass, a workgroup per query head, whole-line K loads (per graph launch 3.92 / 5.63 /
+  // 7.06 / 10.21 us at 128 / 328 / 512 / 900 keys: profiles/r3_attn_time_fullk.jsonl)
+  if (T <= kSingleMaxT && mode == 0) {
     launch((attn_single_kernel<128, kSingleWaves>), dim3((unsigned)(B * H)),
            dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
-           (int)T, scale, 1, tao::AttnPf{});
+           (int)T, scale);
     return check_launch("attn_single_kernel");
   }
   const int NC = (int)((T + kChunk - 1) / kChunk);
@@ -1278,47 +655,13 @@ int tao_attn_prefill_bf16(const uint16_t* q, const uint16_t* k_cache, const uint
 int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
                          const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
                          int64_t Hkv, int64_t D, int64_t T, float scale, void* stream) {
-  return attn_decode(q, k_cache, v_cache, pos, partial, out, B, H, Hkv, D, T, scale,
-                     tao::AttnPf{}, 0, stream);
+  return attn_decode(q, k_cache, v_cache, pos, partial, out, B, H, Hkv, D, T, scale, stream);
 }
-
-int tao_attn_decode_pf_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
-                            const int64_t* pos, float* partial, uint16_t* out, int64_t B,
-                            int64_t H, int64_t Hkv, int64_t D, int64_t T, float scale,
-                            const void* const* pf_ptrs, const int64_t* pf_bytes, int n_pf,
-                            int pf_wgs, void* stream) {
-  TAO_CHECK_ARG(n_pf >= 0 && n_pf <= 4, "attn_decode_pf: 0..4 prefetch regions (got %d)", n_pf);
-  TAO_CHECK_ARG(pf_wgs >= 0 && pf_wgs <= 4096, "attn_decode_pf: 0..4096 prefetch workgroups");
-  tao::AttnPf pf{};
-  int n = 0;
-  for (int r = 0; r < n_pf; ++r) {
-    TAO_CHECK_ARG(pf_bytes[r] >= 0 && pf_bytes[r] < (int64_t(1) << 36),
-                  "attn_decode_pf: region %d size out of range", r);
-    TAO_CHECK_ALIGN(pf_ptrs[r], 16, "prefetch region");
-    if (pf_bytes[r] < 16) continue;
-    pf.p[n] = reinterpret_cast<const uint4*>(pf_ptrs[r]);
-    pf.n16[n] = (uint32_t)(pf_bytes[r] / 16);  // a trailing partial 16 B is left out
-    ++n;
-  }
-  pf.n = pf_wgs > 0 ? n : 0;
-  pf.nbh = (int)(B * H);
-  return attn_decode(q, k_cache, v_cache, pos, partial, out, B, H, Hkv, D, T, scale, pf,
-                     pf.n > 0 ? pf_wgs : 0, stream);
-}
-#if TAO_ATTN_STAMPS
-extern "C" int tao_debug_attn_stamps(unsigned long long* out, int n) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tao::g_attn_stamps), (size_t)n * 4 * 8) != hipSuccess)
-    return TAO_ERR_HIP;
-  return TAO_OK;
-}
-#endif
 
 int tao_tune_attn(int mode) {
-  TAO_CHECK_ARG(mode >= 0 && mode <= 6,
-                "tune: attention mode must be 0 (auto: f32 single pass up to 1024 keys, "
-                "else split), 1 (two-launch split), 2 (one launch, 32-key chunks), 3 (one launch, "
-                "64-key chunks), 4 (packed-bf16 single pass up to 1024 keys, else split), 5 "
-                "(f32 single pass with half-line K loads) or 6 (32 keys per wave step)");
+  TAO_CHECK_ARG(mode == 0 || mode == 1,
+                "tune: attention mode must be 0 (auto: single pass up to 1024 keys, else split) "
+                "or 1 (two-launch split)");
   tao::tuning().attn_mode = mode;
   return TAO_OK;
 }

@@ -78,8 +78,6 @@ _SIGNATURES = {
                              ctypes.c_float, _p],
     "tao_attn_prefill_bf16": [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64,
                               ctypes.c_float, _p],
-    "tao_attn_decode_pf_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
-                                ctypes.c_float, _p, _p, _int, _int, _p],
     "tao_tune_attn": [_int],
     "tao_decode_status": [_p],
     "tao_silu_mul_bf16": [_p, _p, _p, _i64, _p],

@@ -297,9 +297,6 @@ def main(argv=None):
                     help="prefill attention on tao_attn_prefill_bf16 (kernels.PREFILL_ATTN = True)")
     ap.add_argument("--head_prologue", action="store_true",
                     help="fuse the final RMSNorm into the output head GEMV (kernels.HEAD_PROLOGUE)")
-    ap.add_argument("--attn_prefetch_wgs", type=int, default=-1,
-                    help="workgroups that stream wo's weights into the MALL beside the decode "
-                         "attention (kernels.ATTN_PREFETCH_WGS; -1 = built-in, 0 = off)")
     ap.add_argument("--steps_per_graph", type=int, default=32,
                     help="decode steps captured back to back in one HIP graph launch (1 = one "
                          "per token; 32: 717.6 vs 710.1 tokens/s, "
@@ -316,7 +313,7 @@ def main(argv=None):
     ap.add_argument("--write_result", type=Path, default=None)
     args = ap.parse_args(argv)
 
-    if (args.head_prologue or args.attn_prefetch_wgs >= 0 or args.sdpa_prefill
+    if (args.head_prologue or args.sdpa_prefill
             or args.native_prefill_attn or args.prefill_add_norm >= 0):
         from torchao._models.llama import kernels
 
@@ -328,8 +325,6 @@ def main(argv=None):
             kernels.PREFILL_ATTN = True
         if args.head_prologue:
             kernels.HEAD_PROLOGUE = True
-        if args.attn_prefetch_wgs >= 0:
-            kernels.ATTN_PREFETCH_WGS = args.attn_prefetch_wgs
     if args.deferred_norm or args.attn_mode >= 0:
         from torchao import _lib
 

@@ -58,16 +58,9 @@ def rope_kv(qkv: torch.Tensor, freqs: torch.Tensor, pos: torch.Tensor, k_cache: 
     return q
 
 
-# Weight prefetch on the decode attention launch (tao_attn_decode_pf_bf16): workgroups beside
-# the attention's B x H stream the next linear's weights into the MALL. 0 = off.
-ATTN_PREFETCH_WGS = 0
-
-
 def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
-                pos: torch.Tensor, scale: float, prefetch=None) -> torch.Tensor:
-    """q [B, H, 1, D] against keys 0..pos[0] -> [B, 1, H * D] bf16. ``prefetch``: up to 4 CUDA
-    tensors (the next linear's weight storage) streamed into the MALL by the same launch when
-    ATTN_PREFETCH_WGS > 0; the attention result does not depend on it."""
+                pos: torch.Tensor, scale: float) -> torch.Tensor:
+    """q [B, H, 1, D] against keys 0..pos[0] -> [B, 1, H * D] bf16."""
     _check(q, torch.bfloat16, "attn_decode q")
     _check(pos, torch.int64, "attn_decode pos")
     B, H, S, D = q.shape
@@ -79,20 +72,6 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
         part = torch.empty(B * Hkv * nc * (H // Hkv) * (D + 2), dtype=torch.float32,
                            device=q.device)
     out = torch.empty(B, 1, H * D, dtype=q.dtype, device=q.device)
-    regions = [t for t in (prefetch or ()) if t is not None and t.is_cuda and t.numel() > 0]
-    if regions and ATTN_PREFETCH_WGS > 0:
-        import ctypes
-
-        n = len(regions)
-        if n > 4:
-            raise RuntimeError(f"attn_decode: at most 4 prefetch regions, got {n}")
-        ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in regions])
-        sizes = (ctypes.c_int64 * n)(*[t.numel() * t.element_size() for t in regions])
-        _lib.call("tao_attn_decode_pf_bf16", q.data_ptr(), k_cache.data_ptr(),
-                  v_cache.data_ptr(), pos.data_ptr(), None if part is None else part.data_ptr(),
-                  out.data_ptr(), B, H, Hkv, D, T, float(scale), ptrs, sizes, n,
-                  int(ATTN_PREFETCH_WGS), _stream(q))
-        return out
     _lib.call("tao_attn_decode_bf16", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
               pos.data_ptr(), None if part is None else part.data_ptr(), out.data_ptr(), B, H,
               Hkv, D, T, float(scale), _stream(q))

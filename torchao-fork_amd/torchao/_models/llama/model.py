@@ -168,21 +168,6 @@ def _linear_plus(x: torch.Tensor, lin: nn.Linear, residual: torch.Tensor) -> tor
     return residual + lin(x)
 
 
-def _weight_storage(lin: Optional[nn.Linear]):
-    """The device tensors a quantized (int4 / int8) linear's kernel streams, for the decode
-    attention's weight prefetch; () for anything else."""
-    w = getattr(lin, "weight", None)
-    impl = getattr(w, "tensor_impl", None)
-    if impl is None:
-        impl = getattr(getattr(w, "original_weight_tensor", None), "tensor_impl", None)
-    if impl is None:
-        return ()
-    names = ("packed_weight", "scale_and_zero") if hasattr(impl, "packed_weight") else (
-        "int_data", "scale")
-    ts = tuple(getattr(impl, n, None) for n in names)
-    return tuple(t for t in ts if isinstance(t, torch.Tensor) and t.is_cuda)
-
-
 def _int4_parts(lin: Optional[nn.Linear]):
     """(packed_weight, scale_and_zero, group_size) of an int4 weight-only linear on the gfx950
     row-stream layout (Int4WeightOnlyConfig), else None: the fused decode kernels read those
@@ -314,7 +299,7 @@ class Attention(nn.Module):
             q = kernels.rope_kv(self.wqkv(x), freqs_table, input_pos, kv.k_cache, kv.v_cache,
                                 self.n_head)
         y = kernels.attn_decode(q, kv.k_cache, kv.v_cache, input_pos,
-                                1.0 / math.sqrt(self.head_dim), prefetch=_weight_storage(self.wo))
+                                1.0 / math.sqrt(self.head_dim))
         return _linear_plus(y, self.wo, residual)
 
 
