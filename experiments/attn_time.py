@@ -4,7 +4,7 @@ in one HIP graph; µs per launch from HIP events on the replay stream, and the k
 durations (dispatch-packet events, tao_profile_*) from one eager pass. One JSON line per
 (mode, keys) to stdout.
 
-    python experiments/attn_time.py [--modes 0,4] [--keys 128,200,256,300,328,512,900]
+    python experiments/attn_time.py [--modes 0,2] [--keys 128,200,256,300,328,512,900]
 """
 import argparse
 import json
@@ -23,7 +23,7 @@ from torchao._models.llama import kernels  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--modes", default="0,4")
+    ap.add_argument("--modes", default="0,2")
     ap.add_argument("--keys", default="128,200,256,300,328,512,900")
     ap.add_argument("--T", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=50)
