@@ -38,6 +38,7 @@ def main():
             continue
         path, M, N, K = cfg.split("_")
         M, N, K = int(M), int(N), int(K)
+        path = {"sfint8": "int8dyn", "sfint4": "int4"}.get(path, path)  # single-fetch shapes
         vals = collections.defaultdict(list)
         for f in glob.glob(os.path.join(d, "p*", "*_counter_collection.csv")):
             for r in csv.DictReader(open(f)):

@@ -2,6 +2,7 @@
 
 python experiments/prof_gemm.py PATH M N K BM KG SPLITS [REPS]
 PATH in {int4, int8wo, int8dyn}; BM/KG/SPLITS 0 = auto. Prints the median kernel time.
+PROF_SF="mode,bn,wm,splits,stages,a_steps,ks" in the environment sets tao_tune_gemm_sf.
 """
 
 import os
@@ -24,6 +25,8 @@ def main():
     mk = {"int4": make_int4, "int8wo": make_int8wo, "int8dyn": make_int8dyn}[path]
     _lib.call("tao_tune_linear_crossover", 1)
     _lib.call("tao_tune_gemm", bm, kg, sp)
+    if os.environ.get("PROF_SF"):  # single-fetch GEMM launch shape: mode,bn,wm,splits,stages,a,ks
+        _lib.call("tao_tune_gemm_sf", *[int(v) for v in os.environ["PROF_SF"].split(",")])
     run, launches = mk(M, N, K)
     us = kernel_us(run, launches, reps)
     torch.cuda.synchronize()
