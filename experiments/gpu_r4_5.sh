@@ -19,4 +19,8 @@ rc=$?; echo "attn time rc=$rc"; cat gpurun_out/r4_attn_time_xcd.jsonl
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 700 bash experiments/ab_e2e_args.sh 2 int4wo-32 "--attn_mode 0" "--attn_mode 2" > gpurun_out/r4_ab_e2e_attn_xcd.jsonl 2> gpurun_out/r4_ab_e2e_attn_xcd.err
 rc=$?; echo "e2e ab rc=$rc"
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 bash experiments/pmc_sf.sh gpurun_out/r4_pmc_sf > gpurun_out/r4_pmc_sf.log 2>&1
+rc=$?; echo "pmc rc=$rc"
+python3 experiments/pmc_prefill_summary.py gpurun_out/r4_pmc_sf > gpurun_out/r4_pmc_sf.jsonl
 exit $rc

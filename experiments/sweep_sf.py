@@ -106,13 +106,19 @@ def main():
     for path in args.paths.split(","):
         for (M, N, K) in shapes:
             run, copies = (int8_case if path == "int8" else int4_case)(M, N, K, gen)
-            _lib.call("tao_tune_reset")
-            sf(1)
-            ref = run(0).clone()
-            base = median(timed(run, copies, args.reps))
-            rec = {"path": path, "M": M, "N": N, "K": K, "cfg": "incumbent", "us": round(base * 1e3, 2)}
-            print(json.dumps(rec), flush=True)
-            out.write(json.dumps(rec) + "\n")
+            base = None
+            for cs in (1, 32):  # split-K tickets packed / one 128-B line per tile
+                _lib.call("tao_tune_reset")
+                sf(1)
+                _lib.call("tao_tune_cnt_stride", cs)
+                if cs == 1:
+                    ref = run(0).clone()
+                t = median(timed(run, copies, args.reps))
+                base = t if base is None else base
+                rec = {"path": path, "M": M, "N": N, "K": K, "cfg": "incumbent", "cs": cs,
+                       "us": round(t * 1e3, 2)}
+                print(json.dumps(rec), flush=True)
+                out.write(json.dumps(rec) + "\n")
             seams = [int(v) for v in args.seams.split(",")]
             todo = [(c, sm) for c in cfgs[path] for sm in seams if sm == 0 or c[2] in (2, 4, 8)]
             for cfg, seam in todo:

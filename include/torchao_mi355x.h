@@ -81,6 +81,10 @@ int tao_tune_splitk_fenced(int fenced);
 /* The calling thread's current split-K hand-off form (0 fence-free, 1 fenced): the built-in
  * choice unless tao_tune_splitk_fenced overrode it. No device work. */
 int tao_query_splitk_fenced(void);
+/* Split-K ticket layout: unsigned words between consecutive tiles' counters, 32 (built-in: each
+ * tile's ticket on its own 128-B line, so the S workgroups of one tile do not contend with other
+ * tiles' arrivals) or 1 (packed). Thread-local; for measurement. */
+int tao_tune_cnt_stride(int stride);
 
 /* Tuning hook (benchmarks / autotuning sweeps): override the M == 1 int4 GEMV launch shape,
  * for the calling thread. rows_per_wave in {1,2,4,8}; waves_k = waves splitting K inside a workgroup

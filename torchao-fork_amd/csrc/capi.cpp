@@ -290,6 +290,12 @@ int tao_tune_splitk_fenced(int fenced) {
 
 int tao_query_splitk_fenced(void) { return tao::tuning().splitk_fenced; }
 
+int tao_tune_cnt_stride(int stride) {
+  TAO_CHECK_ARG(stride == 1 || stride == 32, "tune: cnt_stride must be 1 or 32");
+  tao::tuning().cnt_stride = stride;
+  return TAO_OK;
+}
+
 int tao_profile_begin(int capacity) {
   TAO_CHECK_ARG(capacity > 0 && capacity <= (1 << 20), "profile: capacity out of range");
   tao::profile_release();

@@ -463,7 +463,7 @@ template <int BM, int D, int KG, int NW, class P>
 __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int sps, typename P::Acc* __restrict__ slab,
-    unsigned* __restrict__ cnt, int fenced, int order) {
+    unsigned* __restrict__ cnt, int fenced, int order, int cs) {
 #if TAO_GEMM_STAMPS
   const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();  // before any setup
 #endif
@@ -706,7 +706,7 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const bool last =
-        last_arriver(&cnt[tile], (unsigned)S, reinterpret_cast<unsigned*>(lds), fenced);
+        last_arriver(&cnt[tile * cs], (unsigned)S, reinterpret_cast<unsigned*>(lds), fenced);
     if (!last || kg != 0) {
       mark(4);
       flush(0);
@@ -854,7 +854,8 @@ void launch_one(dim3 grid, hipStream_t stream, const uint8_t* xb, const P& pol,
     constexpr int D = TAO_GEMM_DEPTH > 0 ? TAO_GEMM_DEPTH
                                          : (BM <= 16 ? 4 : (BM <= 32 ? (big ? 3 : 4) : 2));
     launch((gemm_mfma_kernel<BM, D, KG, NW, P>), grid, dim3(256 * KG), 0, stream, xb, pol, bias, y,
-           M, N, K, sps, slab, cnt, tuning().splitk_fenced, tuning().gemm_order);
+           M, N, K, sps, slab, cnt, tuning().splitk_fenced, tuning().gemm_order,
+           tuning().cnt_stride);
   }
 }
 
@@ -887,8 +888,8 @@ int launch_gemm(const void* x, const P& pol, const uint16_t* bias, uint16_t* y, 
   if (S > 1) {
     const size_t tiles = (size_t)grid.x * grid.y;
     void* ws = nullptr;
-    const int rc = split_workspace(stream, tiles * S * sh.bm * bnw * sizeof(float), tiles, &ws,
-                                   &cnt);
+    const int rc = split_workspace(stream, tiles * S * sh.bm * bnw * sizeof(float),
+                                   tiles * tuning().cnt_stride, &ws, &cnt);
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<typename P::Acc*>(ws);
   }
@@ -941,7 +942,7 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
     const int8_t* __restrict__ x, const int8_t* __restrict__ w, const uint16_t* __restrict__ xscale,
     const uint16_t* __restrict__ wscale, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int sps, i32x4_t* __restrict__ slab,
-    unsigned* __restrict__ cnt, int fenced, int order) {
+    unsigned* __restrict__ cnt, int fenced, int order, int cs) {
   constexpr int XL = BM / 32;           // x chunks per thread per step
   constexpr int WL = BN / 32;           // W chunks per thread per step (BN rows x 8 chunks)
   constexpr int MT = BM / 32, NT = BN / 32;  // 16x16 output tiles per wave
@@ -1080,7 +1081,7 @@ __global__ __launch_bounds__(256) void gemm_i8_lds_kernel(
                        __builtin_bit_cast(uint4, acc[a][b]));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (!last_arriver(&cnt[tile], (unsigned)S, reinterpret_cast<unsigned*>(lds), fenced)) return;
+    if (!last_arriver(&cnt[tile * cs], (unsigned)S, reinterpret_cast<unsigned*>(lds), fenced)) return;
 #pragma unroll
     for (int a = 0; a < MT; ++a)
 #pragma unroll
@@ -1162,7 +1163,8 @@ int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const 
   if (S > 1) {
     void* wsp = nullptr;
     const size_t t = (size_t)grid.x * grid.y;
-    const int rc = split_workspace(stream, t * S * bm * bn * sizeof(int), t, &wsp, &cnt);
+    const int rc = split_workspace(stream, t * S * bm * bn * sizeof(int), t * tuning().cnt_stride,
+                                   &wsp, &cnt);
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<i32x4_t*>(wsp);
   }
@@ -1170,7 +1172,7 @@ int launch_i8_lds(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const 
   const int d = td ? td : (bm == 128 ? 3 : 4);
   auto go = [&](auto kern) {
     launch(kern, grid, dim3(256), 0, stream, xq, wq, xs, ws, bias, y, M, N, K, sps, slab, cnt,
-           tuning().splitk_fenced, tuning().gemm_order);
+           tuning().splitk_fenced, tuning().gemm_order, tuning().cnt_stride);
   };
   if (bn == 128) {  // experiment (tao_tune_gemm_bn): ring depth 2 or 3
     if (bm == 128) {
@@ -1220,7 +1222,7 @@ template <int BM, int D, bool G32>
 __global__ __launch_bounds__(256) void gemm32_int4_kernel(
     const uint8_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
     int gshift, const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K,
-    int sps, f32x16_t* __restrict__ slab, unsigned* __restrict__ cnt, int fenced) {
+    int sps, f32x16_t* __restrict__ slab, unsigned* __restrict__ cnt, int fenced, int cs) {
   constexpr int MT = BM / 32;
   constexpr int SLOTS = 32;                  // 16-B x slots per row per step (512 B)
   constexpr int RPP = 256 / SLOTS;           // x rows per 256-thread pass
@@ -1397,7 +1399,7 @@ __global__ __launch_bounds__(256) void gemm32_int4_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const bool last =
-        last_arriver(&cnt[tile], (unsigned)S, reinterpret_cast<unsigned*>(lds), fenced);
+        last_arriver(&cnt[tile * cs], (unsigned)S, reinterpret_cast<unsigned*>(lds), fenced);
     if (!last) return;
 #pragma unroll
     for (int t = 0; t < MT; ++t)
@@ -1457,7 +1459,8 @@ int launch_gemm32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t
   if (S > 1) {
     void* ws = nullptr;
     const size_t t = (size_t)grid.x * grid.y;
-    const int rc = split_workspace(stream, t * S * bm * 128 * sizeof(float), t, &ws, &cnt);
+    const int rc = split_workspace(stream, t * S * bm * 128 * sizeof(float),
+                                   t * tuning().cnt_stride, &ws, &cnt);
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<f32x16_t*>(ws);
   }
@@ -1466,7 +1469,7 @@ int launch_gemm32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t
   const uint32_t* z = reinterpret_cast<const uint32_t*>(sz);
   auto go = [&](auto kern) {
     launch(kern, grid, dim3(256), 0, stream, xb, w, z, gshift, bias, y, M, N, K, sps, slab, cnt,
-           tuning().splitk_fenced);
+           tuning().splitk_fenced, tuning().cnt_stride);
   };
   if (bm == 128) {  // x ring: one step in flight (2 stages, one live)
     if (gshift == 0) go(gemm32_int4_kernel<128, 2, true>);

@@ -199,7 +199,7 @@ template <class P, int BN, int WM, int NS>
 __global__ __launch_bounds__(512) void gemm_sf_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int a_steps, typename P::Acc* __restrict__ slab,
-    unsigned* __restrict__ cnt, int fenced, int S, int ntn, int seam) {
+    unsigned* __restrict__ cnt, int fenced, int S, int ntn, int seam, int cs) {
 #if TAO_SF_STAMPS
   const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
   unsigned long long stamp[6] = {t_entry, 0, 0, 0, 0, 0};
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        (void)__hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        (void)__hip_atomic_fetch_add(&cnt[tile * cs], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     if (!seam && !reducer) {
@@ -483,7 +483,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
     if (tid == 0) {
       const unsigned need = seam ? (unsigned)S : (unsigned)(S - 1);
       unsigned it = 0, ok = 1;
-      while (__hip_atomic_load(&cnt[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+      while (__hip_atomic_load(&cnt[tile * cs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
         __builtin_amdgcn_s_sleep(1);
         if (++it > (1u << 22)) {  // ~0.3 s: give up, report (outputs of this tile are invalid)
           ok = 0;
@@ -493,10 +493,10 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
       }
       if (ok) {
         if (!seam) {
-          __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (__hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED,
+          __hip_atomic_store(&cnt[tile * cs], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (__hip_atomic_fetch_add(&cnt[tile * cs], 1u, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT) == 2u * S - 1u) {
-          __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&cnt[tile * cs], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
       if (fenced) {
@@ -625,7 +625,7 @@ bool sf_go(const SfShape& sh, hipStream_t stream, const uint8_t* x, const P& pol
       const int ntn = (N + BN - 1) / BN, mtiles = (M + kBM - 1) / kBM;
       launch(gemm_sf_kernel<P, BN, WM, NS>, dim3((unsigned)(ntn * sh.splits * mtiles)), dim3(512),
              0, stream, x, pol, bias, y, M, N, K, a, slab, cnt, tuning().splitk_fenced, sh.splits,
-             ntn, sh.seam);
+             ntn, sh.seam, tuning().cnt_stride);
       return true;
     }
   }
@@ -711,7 +711,8 @@ int sf_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uin
   if (sh.splits > 1) {
     void* w = nullptr;
     const size_t tiles = (size_t)grid.x * grid.z;
-    const int rc = split_workspace(stream, tiles * sh.splits * kBM * sh.bn * 4, tiles, &w, &cnt);
+    const int rc = split_workspace(stream, tiles * sh.splits * kBM * sh.bn * 4,
+                                   tiles * tuning().cnt_stride, &w, &cnt);
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<i32x4_t*>(w);
   }
@@ -749,7 +750,8 @@ int sf_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int l
   if (sh.splits > 1) {
     void* w = nullptr;
     const size_t tiles = (size_t)grid.x * grid.z;
-    const int rc = split_workspace(stream, tiles * sh.splits * kBM * sh.bn * 4, tiles, &w, &cnt);
+    const int rc = split_workspace(stream, tiles * sh.splits * kBM * sh.bn * 4,
+                                   tiles * tuning().cnt_stride, &w, &cnt);
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<f32x4_t*>(w);
   }

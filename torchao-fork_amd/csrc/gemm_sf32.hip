@@ -84,7 +84,7 @@ template <int WV, int NS>
 __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
     const uint16_t* __restrict__ x, const uint32_t* __restrict__ wq, const uint32_t* __restrict__ sz,
     int lg, const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K,
-    int a_steps, f32x16_t* __restrict__ slab, unsigned* __restrict__ cnt, int fenced) {
+    int a_steps, f32x16_t* __restrict__ slab, unsigned* __restrict__ cnt, int fenced, int cs) {
   constexpr int BN = 32 * WV;
   constexpr int XB = kBM * kXRow, WB = BN * kWRow, ZB = BN * kZRow;
   constexpr int STAGE = XB + WB + ZB;
@@ -228,13 +228,13 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        (void)__hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        (void)__hip_atomic_fetch_add(&cnt[tile * cs], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return;
     }
     if (tid == 0) {
       unsigned it = 0, ok = 1;
-      while (__hip_atomic_load(&cnt[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+      while (__hip_atomic_load(&cnt[tile * cs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
              (unsigned)(S - 1)) {
         __builtin_amdgcn_s_sleep(1);
         if (++it > (1u << 22)) {
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
           break;
         }
       }
-      if (ok) __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ok) __hip_atomic_store(&cnt[tile * cs], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (fenced) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -324,14 +324,15 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
   if (splits > 1) {
     void* w = nullptr;
     const size_t tiles = (size_t)grid.x * grid.z;
-    const int rc = split_workspace(stream, tiles * (splits - 1) * kBM * bn * 4, tiles, &w, &cnt);
+    const int rc = split_workspace(stream, tiles * (splits - 1) * kBM * bn * 4,
+                                   tiles * tuning().cnt_stride, &w, &cnt);
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<f32x16_t*>(w);
   }
   const int fenced = tuning().splitk_fenced;
   auto go = [&](auto kern, int threads) {
     launch(kern, grid, dim3(threads), 0, stream, x, packed, reinterpret_cast<const uint32_t*>(sz),
-           lg, bias, y, M, N, K, a_steps, slab, cnt, fenced);
+           lg, bias, y, M, N, K, a_steps, slab, cnt, fenced, tuning().cnt_stride);
   };
   if (bn == 128) {
     if (stages == 2) go(gemm_sf32_int4_kernel<4, 2>, 256);

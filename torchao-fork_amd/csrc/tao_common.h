@@ -70,6 +70,7 @@ struct Tuning {
   int gemm_sf = 0;                               // single-fetch GEMM: 0 auto, 1 off, 2 on
   int sf_bn = 0, sf_wm = 0, sf_splits = 0;       // single-fetch GEMM shape overrides
   int sf_stages = 0, sf_a_steps = 0, sf_ks = 0;
+  int cnt_stride = 32;  // split-K tickets: unsigned words between tiles' counters (32 = a 128-B line each)
   int sf_seam = 1;                               // single-fetch GEMM split-K seam: 1 spread, 0 fixed reducer
 };
 Tuning& tuning();

@@ -306,6 +306,9 @@ def main(argv=None):
     ap.add_argument("--check_tokens", type=int, default=32,
                     help="after timing, decode this many tokens again eagerly and report their "
                          "agreement with the graph-decoded tokens (0 = skip)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KNOB=V[,V..]",
+                    help="launch-shape override for this run (torchao.kernel.tuning knobs; A/B "
+                         "measurement only), e.g. --tune cnt_stride=1")
     ap.add_argument("--tile_format", choices=("cuda", "rocm"), default=None,
                     help="nibble map of TensorCoreTiledLayout tensors in --checkpoint_path")
     ap.add_argument("--device", default="cuda")
@@ -332,6 +335,11 @@ def main(argv=None):
             _lib.call("tao_tune_int4_norm", 1)
         if args.attn_mode >= 0:
             _lib.call("tao_tune_attn", args.attn_mode)
+    for kv in args.tune:
+        from torchao.kernel.tuning import apply as tune_apply
+
+        knob, _, vals = kv.partition("=")
+        tune_apply(knob, *[int(v) for v in vals.split(",")])
     device = torch.device(args.device)
     t = time.perf_counter()
     model = build_model(args.model_name, device, checkpoint_path=args.checkpoint_path,

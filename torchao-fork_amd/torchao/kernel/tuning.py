@@ -34,7 +34,19 @@ _KNOBS = {
     "gemm_tile": ("tao_tune_gemm_tile", 2),
     "gemm_sf": ("tao_tune_gemm_sf", 7),
     "gemm_sf_seam": ("tao_tune_gemm_sf_seam", 1),
+    "cnt_stride": ("tao_tune_cnt_stride", 1),
 }
+
+
+def apply(knob: str, *values: int) -> None:
+    """Set one knob for the calling thread until ``reset()`` (measurement CLIs; prefer the scoped
+    ``tuning`` form)."""
+    if knob not in _KNOBS:
+        raise ValueError(f"unknown tuning knob {knob!r}; known: {sorted(_KNOBS)}")
+    name, nargs = _KNOBS[knob]
+    if len(values) != nargs:
+        raise ValueError(f"{knob} takes {nargs} value(s), got {len(values)}")
+    _lib.call(name, *[int(a) for a in values])
 
 
 def reset() -> None:
