@@ -662,20 +662,53 @@ int sf_dispatch_wm(const SfShape& sh, hipStream_t st, const uint8_t* x, const P&
 
 }  // namespace
 
-// Shape for 64 < M <= 128 (per 128-row M tile): the smallest split S (1, 2, 4, 8) whose grid
-// (N / BN tiles x S) reaches 256 workgroups, publishers taking an equal share of the steps.
-// tao_tune_gemm_sf overrides every field.
-static SfShape sf_shape(int path, int M, int N, int K) {
-  (void)M;
+// Routed shapes (64 < M <= 128, one 128-row M tile), from the sweep against the incumbent
+// MFMA GEMM on the same box (experiments/sweep_sf.py, profiles/r4_sf_sweep_cnt_stride.jsonl; us,
+// incumbent -> single-fetch): int8 dyn 6144x4096 15.0 -> 12.8, 28672x4096 38.4 -> 34.3,
+// 4096x14336 23.6 -> 20.4; int4 4096^2 14.6 -> 14.0, 6144x4096 21.6 -> 19.4, 28672x4096
+// 59.9 -> 50.0 (the 32x32x16 kernel, one wave along M), 4096x14336 32.6 -> 31.6. Config 3
+// (int8 dyn 4096^2: 10.4 vs 10.6) and every M <= 64 stay on the incumbent.
+struct SfRoute {
+  int path, n, k;
+  SfShape sh;
+  int ks;
+};
+constexpr SfRoute kSfRoutes[] = {
+    {2, 6144, 4096, {64, 4, 2, 3, 0, 0}, 256},
+    {2, 28672, 4096, {64, 4, 1, 3, 0, 0}, 128},
+    {2, 4096, 14336, {64, 4, 4, 4, 0, 1}, 128},
+    {0, 4096, 4096, {64, 2, 4, 2, 0, 0}, 0},
+    {0, 6144, 4096, {64, 2, 4, 2, 0, 0}, 0},
+    {0, 28672, 4096, {128, 1, 1, 3, 0, 0}, 0},
+    {0, 4096, 14336, {64, 2, 4, 4, 0, 0}, 0},
+};
+
+static const SfRoute* sf_route(int path, int64_t M, int64_t N, int64_t K) {
+  if (M <= 64 || M > 128) return nullptr;
+  for (const SfRoute& r : kSfRoutes)
+    if (r.path == path && r.n == N && r.k == K) return &r;
+  return nullptr;
+}
+
+// Launch shape: the routed entry, else (tao_tune_gemm_sf mode 2 on other shapes) the smallest
+// split S (1, 2, 4, 8) whose grid (N / BN tiles x S) reaches 256 workgroups, publishers taking
+// an equal share of the steps. tao_tune_gemm_sf / _seam override every field.
+static SfShape sf_shape(int path, int M, int N, int K, int* ks_out = nullptr) {
   const int kstep = path == 0 ? 128 : 256;
   const int nsteps = K / kstep;
-  SfShape sh{path == 0 ? 64 : 32, path == 0 ? 2 : 4, 1, 3, 0, 1};
   const Tuning& t = tuning();
+  const SfRoute* r = sf_route(path, M, N, K);
+  SfShape sh{path == 0 ? 64 : 32, path == 0 ? 2 : 4, 1, 3, 0, 0};
+  if (r) sh = r->sh;
+  if (ks_out) *ks_out = t.sf_ks ? t.sf_ks : (r && r->ks ? r->ks : 256);
   if (t.sf_bn) sh.bn = t.sf_bn;
   if (t.sf_wm) sh.wm = t.sf_wm;
   if (t.sf_stages) sh.stages = t.sf_stages;
-  const long tiles = (N + sh.bn - 1) / sh.bn;
-  while (tiles * sh.splits < 256 && sh.splits < 8 && nsteps >= 2 * sh.splits * 2) sh.splits *= 2;
+  if (!r || t.sf_bn) {
+    const long tiles = (N + sh.bn - 1) / sh.bn;
+    sh.splits = 1;
+    while (tiles * sh.splits < 256 && sh.splits < 8 && nsteps >= 2 * sh.splits * 2) sh.splits *= 2;
+  }
   if (t.sf_splits) sh.splits = t.sf_splits;
   if (sh.splits > nsteps) sh.splits = nsteps;
   sh.a_steps = nsteps / sh.splits;
@@ -683,7 +716,7 @@ static SfShape sf_shape(int path, int M, int N, int K) {
   if (sh.splits > 1 && sh.a_steps * (sh.splits - 1) >= nsteps) sh.a_steps = nsteps / sh.splits;
   // the spread seam's S workgroups of a tile wait for one another: S must divide the 8 waves,
   // and S consecutive workgroups must be resident together (1 per CU: S <= 8 << 256 CUs)
-  sh.seam = t.sf_seam;
+  if (t.sf_seam >= 0) sh.seam = t.sf_seam;
   if (sh.splits != 2 && sh.splits != 4 && sh.splits != 8) sh.seam = 0;
   return sh;
 }
@@ -698,13 +731,14 @@ bool use_sf(int path, int64_t M, int64_t N, int64_t K, int64_t group_size) {
     return false;
   if (path == 0 && (group_size < 32 || group_size > 256 || K % group_size != 0)) return false;
   if (mode == 2) return M <= 128;
-  return false;  // auto: not yet routed
+  return sf_route(path, M, N, K) != nullptr;  // auto: the measured shapes
 }
 
 int sf_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uint16_t* ws,
                const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream) {
-  const SfShape sh = sf_shape(2, M, N, K);
-  const int ks = tuning().sf_ks == 128 ? 128 : 256;
+  int ks = 256;
+  const SfShape sh = sf_shape(2, M, N, K, &ks);
+  ks = ks == 128 ? 128 : 256;
   const dim3 grid((N + sh.bn - 1) / sh.bn, 1, (M + kBM - 1) / kBM);  // tiles: grid.x grid.z
   i32x4_t* slab = nullptr;
   unsigned* cnt = nullptr;
@@ -793,9 +827,11 @@ extern "C" int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages
   return TAO_OK;
 }
 
-// Split-K seam of the single-fetch GEMM: 1 = spread (built-in), 0 = fixed reducer.
+// Split-K seam of the single-fetch GEMM: -1 = built-in (per routed shape), 0 = fixed reducer,
+// 1 = spread.
 extern "C" int tao_tune_gemm_sf_seam(int seam) {
-  TAO_CHECK_ARG(seam == 0 || seam == 1, "tune: gemm_sf_seam must be 0 (fixed reducer) or 1 (spread)");
+  TAO_CHECK_ARG(seam >= -1 && seam <= 1,
+                "tune: gemm_sf_seam must be -1 (built-in), 0 (fixed reducer) or 1 (spread)");
   tao::tuning().sf_seam = seam;
   return TAO_OK;
 }

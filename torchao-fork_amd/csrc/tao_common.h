@@ -71,7 +71,7 @@ struct Tuning {
   int sf_bn = 0, sf_wm = 0, sf_splits = 0;       // single-fetch GEMM shape overrides
   int sf_stages = 0, sf_a_steps = 0, sf_ks = 0;
   int cnt_stride = 32;  // split-K tickets: unsigned words between tiles' counters (32 = a 128-B line each)
-  int sf_seam = 1;                               // single-fetch GEMM split-K seam: 1 spread, 0 fixed reducer
+  int sf_seam = -1;  // single-fetch GEMM split-K seam: -1 built-in, 0 fixed reducer, 1 spread
 };
 Tuning& tuning();
 
