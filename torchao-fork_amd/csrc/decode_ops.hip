@@ -319,16 +319,14 @@ template <int D, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
-    int H, int Hkv, int T, float scale, int xcd) {
+    int H, int Hkv, int T, float scale) {
   static_assert(D == 128, "head_dim 128");
   __shared__ float wm[NW], wl[NW];
   __shared__ float wo[NW][D];
   // q [B][H][1][D]: the query at position pos[0] attends keys 0..pos[0]; out [B][1][H * D].
-  // xcd (B H % 8 == 0): workgroup i serves query head (i % 8) (B H / 8) + i / 8, so the G heads
-  // of one kv head have equal i % 8 -- one XCD under round-robin placement (for speed only:
-  // they share that XCD's L2 for their common K/V rows)
-  const int bh = xcd ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8)
-                     : (int)blockIdx.x;
+  // (Dealing the G query heads of one kv head to one XCD, so they share its L2 for their common
+  // K/V rows, measured no faster: profiles/r4_attn_time_xcd.jsonl, r4_ab_e2e_attn_xcd.jsonl.)
+  const int bh = blockIdx.x;
   const int b = bh / H, h = bh % H, kvh = h / (H / Hkv);
   const int L = attn_len(pos[0], T);
   const size_t ooff = (size_t)bh * (D / 2);  // output dword offset
@@ -608,11 +606,10 @@ static int attn_decode(const uint16_t* q, const uint16_t* k_cache, const uint16_
   const int mode = tao::tuning().attn_mode;
   // Single pass, a workgroup per query head, whole-line K loads (per graph launch 3.92 / 5.63 /
   // 7.06 / 10.21 us at 128 / 328 / 512 / 900 keys: profiles/r3_attn_time_fullk.jsonl)
-  if (T <= kSingleMaxT && (mode == 0 || mode == 2)) {
-    const int xcd = mode == 2 && (B * H) % 8 == 0;
+  if (T <= kSingleMaxT && mode == 0) {
     launch((attn_single_kernel<128, kSingleWaves>), dim3((unsigned)(B * H)),
            dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
-           (int)T, scale, xcd);
+           (int)T, scale);
     return check_launch("attn_single_kernel");
   }
   const int NC = (int)((T + kChunk - 1) / kChunk);
@@ -664,9 +661,9 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
 }
 
 int tao_tune_attn(int mode) {
-  TAO_CHECK_ARG(mode >= 0 && mode <= 2,
-                "tune: attention mode must be 0 (auto: single pass up to 1024 keys, else split), "
-                "1 (two-launch split) or 2 (as 0, a kv head's query heads on one XCD)");
+  TAO_CHECK_ARG(mode == 0 || mode == 1,
+                "tune: attention mode must be 0 (auto: single pass up to 1024 keys, else split) "
+                "or 1 (two-launch split)");
   tao::tuning().attn_mode = mode;
   return TAO_OK;
 }
