@@ -479,6 +479,8 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
 
     quant_us, gemm_us = timed(int8dyn, copies, 2)
     xq, xs = torch.ops.torchao.int8_quantize_per_token(x)
+    torch.ops.torchao.int8_scaled_mm(xq, xs, ws[0], wsc, None)
+    kern8 = _lib.lib().tao_last_kernel().decode()
     xs2 = xs.reshape(-1, 1)
 
     def ours8(c):
@@ -499,7 +501,7 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
     att = max(ops / (INT8_PEAK_TOPS * 1e12), nbytes / (HBM_PEAK_GBPS * 1e9)) * 1e6
     out["int8_dyn"] = {
         "config": f"BASELINE config 3: int8 dyn-act int8-weight linear M={M} N={N} K={K}",
-        "kernel": "routed int8 dyn MFMA GEMM (v_mfma_i32_16x16x64_i8)",
+        "kernel": f"routed int8 dyn GEMM: {kern8} (v_mfma_i32_16x16x64_i8)",
         "gemm_us": round(gemm_us, 2), "quant_us": round(quant_us, 2),
         "TOPS": round(ops / (gemm_us * 1e-6) / 1e12, 1),
         "mfma_frac": round(ops / (gemm_us * 1e-6) / 1e12 / INT8_PEAK_TOPS, 4),
@@ -531,6 +533,8 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
         return torch.ops.torchao.int4_weight_only_linear(x, w4[c][0], w4[c][1], g, None)
 
     (us4,) = timed(int4, copies, 1)
+    int4(0)
+    kern4 = _lib.lib().tao_last_kernel().decode()
     ref4_us = ours4_graph_us = ref4_diff = None
     try:
         ours4_graph_us = graph_us_per_call(int4, copies, device)
@@ -545,7 +549,7 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
     att4 = max(ops / (BF16_PEAK_TFLOPS * 1e12), nbytes4 / (HBM_PEAK_GBPS * 1e9)) * 1e6
     out["int4_wo"] = {
         "config": f"int4 g{g} weight-only linear M={M} N={N} K={K} (prefill)",
-        "kernel": "routed int4 MFMA GEMM (v_mfma_f32_16x16x32_bf16)",
+        "kernel": f"routed int4 GEMM: {kern4} (bf16 MFMA)",
         "gemm_us": round(us4, 2),
         "TFLOPS": round(ops / (us4 * 1e-6) / 1e12, 1),
         "mfma_frac": round(ops / (us4 * 1e-6) / 1e12 / BF16_PEAK_TFLOPS, 4),

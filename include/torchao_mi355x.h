@@ -43,6 +43,9 @@ enum {
 const char* tao_version(void);
 /* Message describing the last failed call on this thread ("" if none). */
 const char* tao_last_error(void);
+/* Name of the last kernel this thread launched through the library (its routing decision, for
+ * measurement labels); "" before the first launch. */
+const char* tao_last_kernel(void);
 /* Number of hipDevices visible (0 if no GPU / runtime unavailable). Never fails. */
 int tao_device_count(void);
 

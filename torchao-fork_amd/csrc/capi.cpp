@@ -26,11 +26,16 @@ int set_error(int code, const char* fmt, ...) {
 
 void clear_error() { g_err[0] = 0; }
 
+static thread_local const char* g_last_kernel = "";
+
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(TAO_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+  g_last_kernel = what;
   return TAO_OK;
 }
+
+const char* last_kernel() { return g_last_kernel; }
 
 // ---- per-kernel timing sessions --------------------------------------------------------------
 struct ProfileSession {
@@ -265,6 +270,8 @@ extern "C" {
 const char* tao_version(void) { return "torchao-mi355x 0.1.0 gfx950"; }
 
 const char* tao_last_error(void) { return tao::g_err; }
+
+const char* tao_last_kernel(void) { return tao::last_kernel(); }
 
 int tao_device_count(void) {
   int n = 0;

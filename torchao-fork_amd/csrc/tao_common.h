@@ -25,6 +25,7 @@ void clear_error();
 
 // Check the launch of the kernel just enqueued (no synchronisation: capture-safe).
 int check_launch(const char* what);
+const char* last_kernel();  // name given to the last successful check_launch of this thread
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -30,6 +30,7 @@ _int = ctypes.c_int
 _SIGNATURES = {
     "tao_version": [],
     "tao_last_error": [],
+    "tao_last_kernel": [],
     "tao_device_count": [],
     "tao_profile_begin": [_int],
     "tao_profile_end": [_p, _int, _p],
@@ -93,7 +94,8 @@ _SIGNATURES = {
     "tao_int8dq_decode_bf16": [_p, _p, _p, _i64, _i64, _p, ctypes.c_float, _int, _p, _p, _p, _p, _p,
                                _i64, _i64, _i64, _i64, _p],
 }
-_RESTYPES = {"tao_version": ctypes.c_char_p, "tao_last_error": ctypes.c_char_p}
+_RESTYPES = {"tao_version": ctypes.c_char_p, "tao_last_error": ctypes.c_char_p,
+             "tao_last_kernel": ctypes.c_char_p}
 
 
 def library_path() -> str:
