@@ -325,7 +325,7 @@ int tao_attn_prefill_bf16(const uint16_t* q, const uint16_t* k_cache, const uint
 
 /* Calling thread's choice of the decode-attention kernel: 0 = single-pass workgroup per query head
  * (f32 math, whole-line K loads) for T <= 1024, else the two-launch split (default); 1 = two-launch
- * split; 2 = as 0 with V rows loaded 16 B per lane. */
+ * split. */
 int tao_tune_attn(int mode);
 
 /* Device-side faults of the decode kernels since the last call, read and cleared (synchronous:

@@ -315,12 +315,7 @@ __global__ __launch_bounds__(64) void attn_combine_kernel(const float* __restric
 constexpr int kSingleMaxT = 1024;
 constexpr int kSingleWaves = TAO_ATTN_WAVES;
 
-// V16: V rows loaded 16 B per lane (lane l: key t0 + 4 i + l / 16, dims 8 (l % 16) ..; 4 wave
-// instructions per 16 keys) instead of 4 B per lane (16 instructions, one V row each): the
-// address unit takes a wave instruction in the same cycles whatever its width, so 4-B loads move
-// a quarter of the bytes per cycle into the CU. Each lane keeps 8 dims of its keys' weighted sum;
-// the four lanes of a dim group are summed by two xor exchanges after the key loop.
-template <int D, int NW, bool V16 = false>
+template <int D, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
@@ -338,14 +333,11 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const size_t head = (size_t)(b * Hkv + kvh) * T;
   const uint32_t* vb = reinterpret_cast<const uint32_t*>(vc + head * D) + lane;
-  const int vr = lane >> 4, vcg = lane & 15;  // V16: key sub-row, dim granule
-  const uint4* vb16 = reinterpret_cast<const uint4*>(vc + head * D) + vcg;
   // lane (g = l / 8, p8 = l % 8): keys t0 + g and t0 + 8 + g, dims 64 h + 8 p8 + e (h < 2, e < 8)
   const int g = lane >> 3, p8 = lane & 7;
   const uint16_t* kbase = kc + head * D + p8 * 8;
   uint4 ka[2], kb2[2];
-  uint32_t vv[V16 ? 1 : 16];
-  uint4 vq[V16 ? 4 : 1];
+  uint32_t vv[16];
   auto load_step = [&](int t0) __attribute__((always_inline)) {
     const int ta = t0 + g < L ? t0 + g : L - 1, tb = t0 + 8 + g < L ? t0 + 8 + g : L - 1;
 #pragma unroll
@@ -353,18 +345,10 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
       ka[hh] = *reinterpret_cast<const uint4*>(kbase + (size_t)ta * D + 64 * hh);
       kb2[hh] = *reinterpret_cast<const uint4*>(kbase + (size_t)tb * D + 64 * hh);
     }
-    if constexpr (V16) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int tj = t0 + 4 * i + vr < L ? t0 + 4 * i + vr : L - 1;
-        vq[i] = vb16[(size_t)tj * (D / 8)];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int tj = t0 + j < L ? t0 + j : L - 1;
-        vv[j] = vb[(size_t)tj * (D / 2)];
-      }
+    for (int j = 0; j < 16; ++j) {
+      const int tj = t0 + j < L ? t0 + j : L - 1;
+      vv[j] = vb[(size_t)tj * (D / 2)];
     }
   };
   load_step(wave * 16);
@@ -385,9 +369,6 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     }
   }
   float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
-  float o8[V16 ? 8 : 1];
-#pragma unroll
-  for (int d = 0; d < (V16 ? 8 : 1); ++d) o8[d] = 0.f;
   for (int t0 = wave * 16; t0 < L; t0 += NW * 16) {
     float sa = 0.f, sb = 0.f;
 #pragma unroll
@@ -403,22 +384,10 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
       }
     }
     float vf[32];
-    if constexpr (V16) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t w[4] = {vq[i].x, vq[i].y, vq[i].z, vq[i].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          vf[8 * i + 2 * e] = bf16lo_to_f32(w[e]);
-          vf[8 * i + 2 * e + 1] = bf16hi_to_f32(w[e]);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        vf[2 * j] = bf16lo_to_f32(vv[j]);
-        vf[2 * j + 1] = bf16hi_to_f32(vv[j]);
-      }
+    for (int j = 0; j < 16; ++j) {
+      vf[2 * j] = bf16lo_to_f32(vv[j]);
+      vf[2 * j + 1] = bf16hi_to_f32(vv[j]);
     }
     if (t0 + NW * 16 < L) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
     sa = wave_bfly<1, 8>(sa, lane_id(), [](float a, float c) { return a + c; });
@@ -434,27 +403,15 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     float es = ea + eb;  // each key sits in 8 lanes of one group: xor 8..32 counts it once
     es = wave_bfly<8, 64>(es, lane_id(), [](float a, float c) { return a + c; });
     l = fmaf(l, corr, es);
-    if constexpr (V16) {
-      // key 4 i + vr of the step: its weight sits in lane 8 ((4 i + vr) % 8) of ea (i < 2) / eb
+    o0 *= corr;
+    o1 *= corr;
 #pragma unroll
-      for (int d = 0; d < 8; ++d) o8[d] *= corr;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float pk = __shfl(i < 2 ? ea : eb, 32 * (i & 1) + 8 * vr, 64);
-#pragma unroll
-        for (int d = 0; d < 8; ++d) o8[d] = fmaf(pk, vf[8 * i + d], o8[d]);
-      }
-    } else {
-      o0 *= corr;
-      o1 *= corr;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float pa = __shfl(ea, 8 * j, 64), pb = __shfl(eb, 8 * j, 64);
-        o0 = fmaf(pa, vf[2 * j], o0);
-        o1 = fmaf(pa, vf[2 * j + 1], o1);
-        o0 = fmaf(pb, vf[2 * (j + 8)], o0);
-        o1 = fmaf(pb, vf[2 * (j + 8) + 1], o1);
-      }
+    for (int j = 0; j < 8; ++j) {
+      const float pa = __shfl(ea, 8 * j, 64), pb = __shfl(eb, 8 * j, 64);
+      o0 = fmaf(pa, vf[2 * j], o0);
+      o1 = fmaf(pa, vf[2 * j + 1], o1);
+      o0 = fmaf(pb, vf[2 * (j + 8)], o0);
+      o1 = fmaf(pb, vf[2 * (j + 8) + 1], o1);
     }
     m = mn;
   }
@@ -462,20 +419,8 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     wm[wave] = m;
     wl[wave] = l;
   }
-  if constexpr (V16) {
-#pragma unroll
-    for (int d = 0; d < 8; ++d) {
-      o8[d] += xor_partner<16>(o8[d], lane);
-      o8[d] += xor_partner<32>(o8[d], lane);
-    }
-    if (vr == 0) {
-#pragma unroll
-      for (int d = 0; d < 8; ++d) wo[wave][8 * vcg + d] = o8[d];
-    }
-  } else {
-    wo[wave][2 * lane] = o0;
-    wo[wave][2 * lane + 1] = o1;
-  }
+  wo[wave][2 * lane] = o0;
+  wo[wave][2 * lane + 1] = o1;
   __syncthreads();
   if (wave == 0) {
     float M = -INFINITY;
@@ -667,13 +612,6 @@ static int attn_decode(const uint16_t* q, const uint16_t* k_cache, const uint16_
            (int)T, scale);
     return check_launch("attn_single_kernel");
   }
-  if (T <= kSingleMaxT && mode == 2) {
-    TAO_CHECK_ALIGN(v_cache, 16, "v_cache");
-    launch((attn_single_kernel<128, kSingleWaves, true>), dim3((unsigned)(B * H)),
-           dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
-           (int)T, scale);
-    return check_launch("attn_single_kernel<v16>");
-  }
   const int NC = (int)((T + kChunk - 1) / kChunk);
   const dim3 g1((unsigned)(B * Hkv), (unsigned)NC), g2((unsigned)(B * H));
   if (partial == nullptr) {  // the library's workspace
@@ -723,9 +661,9 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
 }
 
 int tao_tune_attn(int mode) {
-  TAO_CHECK_ARG(mode >= 0 && mode <= 2,
-                "tune: attention mode must be 0 (auto: single pass up to 1024 keys, else split), "
-                "1 (two-launch split) or 2 (as 0 with 16-B V loads)");
+  TAO_CHECK_ARG(mode == 0 || mode == 1,
+                "tune: attention mode must be 0 (auto: single pass up to 1024 keys, else split) "
+                "or 1 (two-launch split)");
   tao::tuning().attn_mode = mode;
   return TAO_OK;
 }
