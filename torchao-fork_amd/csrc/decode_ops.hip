@@ -315,10 +315,12 @@ __global__ __launch_bounds__(64) void attn_combine_kernel(const float* __restric
 constexpr int kSingleMaxT = 1024;
 constexpr int kSingleWaves = TAO_ATTN_WAVES;
 
-// DOT2: scores by v_dot2_f32_bf16 on the packed bf16 q and k words (8 ops per key-lane instead
-// of 16 conversions + 16 fmas; the products are exact in fp32 either way), and the P.V weights
-// broadcast by v_readlane (the source lane is uniform) instead of ds_bpermute shuffles.
-template <int D, int NW, bool DOT2 = false>
+// Scores by v_dot2_f32_bf16 on the packed bf16 q and k words (8 ops per key-lane instead of 16
+// conversions + 16 fmas; the products are exact in fp32 either way) and the P.V weights
+// broadcast by v_readlane (the source lane is uniform) instead of ds_bpermute shuffles: 3.65 /
+// 5.52 / 6.54 / 9.85 us per graph launch at 128 / 328 / 512 / 900 keys against 3.80 / 5.63 /
+// 7.04 / 10.20 for f32 conversions and shuffles (profiles/r4_attn_time_dot2.jsonl).
+template <int D, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
@@ -355,7 +357,6 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     }
   };
   load_step(wave * 16);
-  float qr[DOT2 ? 1 : 16];
   uint32_t qw[8];
   {
     const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bh * D + p8 * 8);
@@ -368,10 +369,6 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         qw[hh * 4 + e] = w[e];
-        if constexpr (!DOT2) {
-          qr[hh * 8 + 2 * e] = bf16lo_to_f32(w[e]);
-          qr[hh * 8 + 2 * e + 1] = bf16hi_to_f32(w[e]);
-        }
       }
     }
   }
@@ -384,15 +381,8 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
       const uint32_t wb[4] = {kb2[hh].x, kb2[hh].y, kb2[hh].z, kb2[hh].w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        if constexpr (DOT2) {
-          sa = dot2_bf16(qw[hh * 4 + e], wa[e], sa);
-          sb = dot2_bf16(qw[hh * 4 + e], wb[e], sb);
-        } else {
-          sa = fmaf(qr[hh * 8 + 2 * e], bf16lo_to_f32(wa[e]),
-                    fmaf(qr[hh * 8 + 2 * e + 1], bf16hi_to_f32(wa[e]), sa));
-          sb = fmaf(qr[hh * 8 + 2 * e], bf16lo_to_f32(wb[e]),
-                    fmaf(qr[hh * 8 + 2 * e + 1], bf16hi_to_f32(wb[e]), sb));
-        }
+        sa = dot2_bf16(qw[hh * 4 + e], wa[e], sa);
+        sb = dot2_bf16(qw[hh * 4 + e], wb[e], sb);
       }
     }
     float vf[32];
@@ -419,14 +409,10 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     o1 *= corr;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float pa, pb;
-      if constexpr (DOT2) {
-        pa = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ea), 8 * j));
-        pb = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, eb), 8 * j));
-      } else {
-        pa = __shfl(ea, 8 * j, 64);
-        pb = __shfl(eb, 8 * j, 64);
-      }
+      const float pa =
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ea), 8 * j));
+      const float pb =
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, eb), 8 * j));
       o0 = fmaf(pa, vf[2 * j], o0);
       o1 = fmaf(pa, vf[2 * j + 1], o1);
       o0 = fmaf(pb, vf[2 * (j + 8)], o0);
@@ -631,12 +617,7 @@ static int attn_decode(const uint16_t* q, const uint16_t* k_cache, const uint16_
            (int)T, scale);
     return check_launch("attn_single_kernel");
   }
-  if (T <= kSingleMaxT && mode == 2) {
-    launch((attn_single_kernel<128, kSingleWaves, true>), dim3((unsigned)(B * H)),
-           dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
-           (int)T, scale);
-    return check_launch("attn_single_kernel<dot2>");
-  }
+
   const int NC = (int)((T + kChunk - 1) / kChunk);
   const dim3 g1((unsigned)(B * Hkv), (unsigned)NC), g2((unsigned)(B * H));
   if (partial == nullptr) {  // the library's workspace
@@ -686,9 +667,9 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
 }
 
 int tao_tune_attn(int mode) {
-  TAO_CHECK_ARG(mode >= 0 && mode <= 2,
-                "tune: attention mode must be 0 (auto: single pass up to 1024 keys, else split), "
-                "1 (two-launch split) or 2 (as 0 with dot2 scores and readlane weights)");
+  TAO_CHECK_ARG(mode == 0 || mode == 1,
+                "tune: attention mode must be 0 (auto: single pass up to 1024 keys, else split) "
+                "or 1 (two-launch split)");
   tao::tuning().attn_mode = mode;
   return TAO_OK;
 }
