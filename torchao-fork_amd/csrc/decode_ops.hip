@@ -320,11 +320,7 @@ constexpr int kSingleWaves = TAO_ATTN_WAVES;
 // broadcast by v_readlane (the source lane is uniform) instead of ds_bpermute shuffles: 3.65 /
 // 5.52 / 6.54 / 9.85 us per graph launch at 128 / 328 / 512 / 900 keys against 3.80 / 5.63 /
 // 7.04 / 10.20 for f32 conversions and shuffles (profiles/r4_attn_time_dot2.jsonl).
-// LDS1: the wave's second step (keys t0 + 16 NW ..) is fetched at launch by LDS-DMA into an 8-KiB
-// slot of its own (lane-linear: each lane later reads back exactly the words it would have
-// loaded), so up to 32 NW keys arrive in one memory round trip; the register chain resumes at the
-// third step (its loads issued while the first step computes).
-template <int D, int NW, bool LDS1 = false>
+template <int D, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
@@ -332,7 +328,6 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
   static_assert(D == 128, "head_dim 128");
   __shared__ float wm[NW], wl[NW];
   __shared__ float wo[NW][D];
-  __shared__ uint4 kvslot[LDS1 ? NW * 512 : 1];  // LDS1: 8 KiB per wave (K 4 x 1 KiB, V 16 x 256 B)
   // q [B][H][1][D]: the query at position pos[0] attends keys 0..pos[0]; out [B][1][H * D].
   // (Dealing the G query heads of one kv head to one XCD, so they share its L2 for their common
   // K/V rows, measured no faster: profiles/r4_attn_time_xcd.jsonl, r4_ab_e2e_attn_xcd.jsonl.)
@@ -340,8 +335,7 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
   const int b = bh / H, h = bh % H, kvh = h / (H / Hkv);
   const int L = attn_len(pos[0], T);
   const size_t ooff = (size_t)bh * (D / 2);  // output dword offset
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const size_t head = (size_t)(b * Hkv + kvh) * T;
   const uint32_t* vb = reinterpret_cast<const uint32_t*>(vc + head * D) + lane;
   // lane (g = l / 8, p8 = l % 8): keys t0 + g and t0 + 8 + g, dims 64 h + 8 p8 + e (h < 2, e < 8)
@@ -362,26 +356,6 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
       vv[j] = vb[(size_t)tj * (D / 2)];
     }
   };
-  uint8_t* slot = reinterpret_cast<uint8_t*>(kvslot) + (LDS1 ? wave * 8192 : 0);
-  if constexpr (LDS1) {
-    const int t1 = wave * 16 + NW * 16;
-    if (t1 < L) {  // wave-uniform
-      const Rsrc krs = make_rsrc(kc + head * D, (uint32_t)T * D * 2);
-      const Rsrc vrs = make_rsrc(vc + head * D, (uint32_t)T * D * 2);
-      const int ta = t1 + g < L ? t1 + g : L - 1, tb = t1 + 8 + g < L ? t1 + 8 + g : L - 1;
-      const uint32_t ko = 16u * (uint32_t)p8;
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        dma_lds<16>(krs, (uint32_t)ta * (D * 2) + ko + 128u * hh, 0, slot + 1024 * hh);
-        dma_lds<16>(krs, (uint32_t)tb * (D * 2) + ko + 128u * hh, 0, slot + 2048 + 1024 * hh);
-      }
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int tj = t1 + j < L ? t1 + j : L - 1;
-        dma_lds<4>(vrs, (uint32_t)tj * (D * 2) + 4u * (uint32_t)lane, 0, slot + 4096 + 256 * j);
-      }
-    }
-  }
   load_step(wave * 16);
   uint32_t qw[8];
   {
@@ -393,18 +367,18 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     for (int hh = 0; hh < 2; ++hh) {
       const uint32_t w[4] = {qv[hh].x, qv[hh].y, qv[hh].z, qv[hh].w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) qw[hh * 4 + e] = w[e];
+      for (int e = 0; e < 4; ++e) {
+        qw[hh * 4 + e] = w[e];
+      }
     }
   }
   float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
-  // one 16-key step: scores of keys t0 + g, t0 + 8 + g from the K words, online softmax, P.V
-  auto step = [&](int t0, const uint4 (&KA)[2], const uint4 (&KB)[2], const uint32_t (&VV)[16],
-                  auto prefetch) __attribute__((always_inline)) {
+  for (int t0 = wave * 16; t0 < L; t0 += NW * 16) {
     float sa = 0.f, sb = 0.f;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const uint32_t wa[4] = {KA[hh].x, KA[hh].y, KA[hh].z, KA[hh].w};
-      const uint32_t wb[4] = {KB[hh].x, KB[hh].y, KB[hh].z, KB[hh].w};
+      const uint32_t wa[4] = {ka[hh].x, ka[hh].y, ka[hh].z, ka[hh].w};
+      const uint32_t wb[4] = {kb2[hh].x, kb2[hh].y, kb2[hh].z, kb2[hh].w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         sa = dot2_bf16(qw[hh * 4 + e], wa[e], sa);
@@ -414,10 +388,10 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     float vf[32];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      vf[2 * j] = bf16lo_to_f32(VV[j]);
-      vf[2 * j + 1] = bf16hi_to_f32(VV[j]);
+      vf[2 * j] = bf16lo_to_f32(vv[j]);
+      vf[2 * j + 1] = bf16hi_to_f32(vv[j]);
     }
-    prefetch();
+    if (t0 + NW * 16 < L) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
     sa = wave_bfly<1, 8>(sa, lane_id(), [](float a, float c) { return a + c; });
     sb = wave_bfly<1, 8>(sb, lane_id(), [](float a, float c) { return a + c; });
     const bool va = t0 + g < L, vbk = t0 + 8 + g < L;
@@ -445,37 +419,7 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
       o1 = fmaf(pb, vf[2 * (j + 8) + 1], o1);
     }
     m = mn;
-  };
-  int t0 = wave * 16;
-  if constexpr (LDS1) {
-    if (t0 < L) {
-      const int t2 = t0 + 2 * NW * 16;
-      step(t0, ka, kb2, vv, [&]() __attribute__((always_inline)) {
-        if (t2 < L) load_step(t2);
-      });
-      const int t1 = t0 + NW * 16;
-      if (t1 < L) {
-        // this wave's DMAs landed: only the third step's 20 register loads may still be in flight
-        if (t2 < L) wait_vmcnt<20>();
-        else wait_vmcnt<0>();
-        uint4 KA[2], KB[2];
-        uint32_t VV[16];
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          KA[hh] = reinterpret_cast<const uint4*>(slot + 1024 * hh)[lane];
-          KB[hh] = reinterpret_cast<const uint4*>(slot + 2048 + 1024 * hh)[lane];
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) VV[j] = reinterpret_cast<const uint32_t*>(slot + 4096 + 256 * j)[lane];
-        step(t1, KA, KB, VV, []() {});
-      }
-    }
-    t0 += 2 * NW * 16;
   }
-  for (; t0 < L; t0 += NW * 16)
-    step(t0, ka, kb2, vv, [&]() __attribute__((always_inline)) {
-      if (t0 + NW * 16 < L) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
-    });
   if (lane == 0) {
     wm[wave] = m;
     wl[wave] = l;
@@ -673,13 +617,6 @@ static int attn_decode(const uint16_t* q, const uint16_t* k_cache, const uint16_
            (int)T, scale);
     return check_launch("attn_single_kernel");
   }
-  if (T <= kSingleMaxT && mode == 2) {
-    TAO_CHECK_ARG((uint64_t)T * D * 2 < (1ull << 32), "attn_decode: cache too long for mode 2");
-    launch((attn_single_kernel<128, kSingleWaves, true>), dim3((unsigned)(B * H)),
-           dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
-           (int)T, scale);
-    return check_launch("attn_single_kernel<lds1>");
-  }
 
   const int NC = (int)((T + kChunk - 1) / kChunk);
   const dim3 g1((unsigned)(B * Hkv), (unsigned)NC), g2((unsigned)(B * H));
@@ -730,9 +667,9 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
 }
 
 int tao_tune_attn(int mode) {
-  TAO_CHECK_ARG(mode >= 0 && mode <= 2,
-                "tune: attention mode must be 0 (auto: single pass up to 1024 keys, else split), "
-                "1 (two-launch split) or 2 (as 0, second step by LDS-DMA)");
+  TAO_CHECK_ARG(mode == 0 || mode == 1,
+                "tune: attention mode must be 0 (auto: single pass up to 1024 keys, else split) "
+                "or 1 (two-launch split)");
   tao::tuning().attn_mode = mode;
   return TAO_OK;
 }
