@@ -69,6 +69,16 @@ int tao_int4wo_linear_bf16(const uint16_t* x, const uint32_t* packed, const uint
                            const uint16_t* bias, uint16_t* y, int64_t M, int64_t N, int64_t K,
                            int64_t group_size, void* stream);
 
+/* tao_int4wo_linear_bf16 (no bias) with the SwiGLU of interleaved (gate, up) output rows folded
+ * into the epilogue: y [M][N/2] = bf16(bf16(silu(a_i)) * b_i), (a_i, b_i) = the bf16 outputs of
+ * rows (2i, 2i+1) (a w1||w3 weight merged row-interleaved; N % 16 == 0). Replaces the prefill's
+ * `F.silu(w1(x)) * w3(x)` (gpt-fast model.py FeedForward.forward) as one launch. Served where
+ * the single-fetch GEMM is routed; TAO_ERR_UNSUPPORTED elsewhere (the caller then runs the linear
+ * and tao_silu_mul_bf16). */
+int tao_int4wo_linear_swiglu_bf16(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
+                                  uint16_t* y, int64_t M, int64_t N, int64_t K,
+                                  int64_t group_size, void* stream);
+
 /* Tuning hooks (tao_tune_*). Every override is THREAD-LOCAL: it re-routes only launches issued
  * from the thread that set it, never another thread's model. tao_tune_reset() restores every
  * built-in choice for the calling thread (torchao.kernel.tuning(...) wraps set + reset). */

@@ -241,3 +241,75 @@ def test_sf_unsupported_shapes_fall_back(sf):
     with pytest.raises(RuntimeError, match="gemm_sf"):
         torch.ops.torchao.int4_weight_only_linear(
             oracle.make_activation(64, 1024, seed=1).to(DEV), packed, sz, 32, None)
+
+
+SW_CFGS = [(0, None), (2, (64, 2, 4, 2, 0)), (2, (64, 2, 2, 3, 0)), (2, (128, 2, 8, 2, 0)),
+           (2, (128, 1, 1, 3, 0)), (2, (64, 1, 2, 3, 0)), (2, (128, 1, 4, 2, 0))]
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 28672, 4096), (100, 1024, 2048), (200, 512, 1024),
+                                   (7, 256, 512)])
+@pytest.mark.parametrize("mode,cfg", SW_CFGS)
+@pytest.mark.parametrize("seam", [0, 1])
+def test_sf_swiglu_epilogue_matches_linear_then_silu_mul(sf, M, N, K, mode, cfg, seam):
+    """tao_int4wo_linear_swiglu_bf16 (the w1||w3 GEMM with the SiLU-mul in its epilogue, both
+    single-fetch kernels, both seams, several M tiles, partial tiles) is bit-identical to the
+    routed linear followed by tao_silu_mul_bf16 on the same launch shape; where no fused kernel
+    serves the shape (auto routing off the measured shapes) the wrapper returns None."""
+    from torchao._models.llama import kernels
+
+    sf(mode, *(cfg or ()))
+    _lib.call("tao_tune_gemm_sf_seam", seam)
+    q, s, z, packed, sz = _int4(N, K, 32, seed=N + K)
+    x = oracle.make_activation(M, K, seed=M).to(DEV)
+    y = kernels.int4_linear_swiglu(x, packed, sz, 32)
+    if mode == 0 and (M, N, K) != (128, 28672, 4096):
+        assert y is None
+        return
+    assert y is not None and y.shape == (M, N // 2)
+    ref = kernels.silu_mul(torch.ops.torchao.int4_weight_only_linear(x, packed, sz, 32, None))
+    assert torch.equal(y, ref)
+
+
+def test_sf_swiglu_prefill_model_matches_unfused():
+    """A small Llama prefill (dim 512, head_dim 128, w1||w3 3072 x 512) with the SwiGLU folded
+    into the w1||w3 GEMM (every linear on the single-fetch kernel) gives bit-identical hidden
+    states to the linear + silu_mul path on the same kernels."""
+    import math
+
+    from torchao._models.llama import model as mdl
+    from torchao._models.llama.generate import apply_quantization
+    from torchao._models.llama.model import ModelArgs, Transformer
+    from torchao.kernel import tuning
+
+    dev = torch.device(DEV)
+    torch.manual_seed(7)
+    m = Transformer(ModelArgs(dim=512, n_layer=2, n_head=4, n_local_heads=2, vocab_size=1000,
+                              block_size=256)).to(dev).to(torch.bfloat16)
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.Linear):
+                b = 1 / math.sqrt(mod.in_features)
+                mod.weight.uniform_(-b, b)
+    m.fuse_w13()
+    apply_quantization(m, "int4wo-32")
+    m.setup_caches(1, 160)
+    assert m.enable_fused_kernels()
+    idx = torch.randint(0, 1000, (1, 128), device=dev,
+                        generator=torch.Generator(device=dev).manual_seed(1))
+    pos = torch.arange(128, device=dev)
+    outs = []
+    with tuning(gemm_sf=(2, 0, 0, 0, 0, 0, 0)):
+        ff = m.layers[0].feed_forward
+        assert ff.swiglu_prefill is not None and mdl._int4_parts(ff.w13) is not None
+        from torchao._models.llama import kernels
+
+        assert kernels.int4_linear_swiglu(torch.zeros(128, 512, device=dev, dtype=torch.bfloat16),
+                                          *mdl._int4_parts(ff.w13)) is not None
+        for fused in (True, False):
+            mdl.PREFILL_SWIGLU = fused
+            try:
+                outs.append(m._layers_prefill(idx, pos).clone())
+            finally:
+                mdl.PREFILL_SWIGLU = True
+    assert torch.equal(outs[0], outs[1])

@@ -61,7 +61,8 @@ bool use_sf(int path, int64_t M, int64_t N, int64_t K, int64_t group_size);
 int sf_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uint16_t* ws,
                const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream);
 int sf_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
-            const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream);
+            const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream,
+            int epi = 0);
 
 namespace {
 

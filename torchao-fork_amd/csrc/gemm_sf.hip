@@ -199,7 +199,7 @@ template <class P, int BN, int WM, int NS>
 __global__ __launch_bounds__(512) void gemm_sf_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int a_steps, typename P::Acc* __restrict__ slab,
-    unsigned* __restrict__ cnt, int fenced, int S, int ntn, int seam, int cs) {
+    unsigned* __restrict__ cnt, int fenced, int S, int ntn, int seam, int cs, int epi) {
 #if TAO_SF_STAMPS
   const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
   unsigned long long stamp[6] = {t_entry, 0, 0, 0, 0, 0};
@@ -570,10 +570,31 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   }
   }
   __syncthreads();
+  if (epi == 1) {  // SwiGLU over interleaved (gate, up) columns: y [M][N / 2]
+    constexpr int OPR = BN / 16;  // 16-B output pieces per row
+    const int N2 = N >> 1;
+    const bool full2 = n_blk + BN <= N && (N2 & 7) == 0 && ((uintptr_t)y & 15) == 0;
+    for (int c = tid; c < kBM * OPR; c += 512) {
+      const int r = c / OPR, cc = c % OPR;
+      const int m = m_blk + r;
+      if (m >= M) continue;
+      if (seam && S > 1 && ((r / RM) * WN + (16 * cc) / CN) / wpo != z) continue;  // not owned
+      const uint4* img = reinterpret_cast<const uint4*>(out) + r * (BN / 8) + 2 * cc;
+      const uint4 v = swiglu_piece(img[0], img[1]);
+      const int n0 = (n_blk >> 1) + 8 * cc;
+      if (full2) {
+        *reinterpret_cast<uint4*>(y + (size_t)m * N2 + n0) = v;
+      } else {
+        const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+        for (int k = 0; k < 8; ++k)
+          if (n0 + k < N2) y[(size_t)m * N2 + n0 + k] = e[k];
+      }
+    }
+  }
   constexpr int CPR = BN / 8;  // 16-B pieces per row
   const bool full = n_blk + BN <= N && (N & 7) == 0 && ((uintptr_t)y & 15) == 0;
 #pragma unroll
-  for (int c = tid; c < kBM * CPR; c += 512) {
+  for (int c = epi == 1 ? kBM * CPR : tid; c < kBM * CPR; c += 512) {
     const int r = c / CPR, cc = c % CPR;
     const int m = m_blk + r;
     if (m >= M) continue;
@@ -614,7 +635,7 @@ struct SfShape {
 template <class P, int BN, int WM, int NS>
 bool sf_go(const SfShape& sh, hipStream_t stream, const uint8_t* x, const P& pol,
            const uint16_t* bias, uint16_t* y, int M, int N, int K, int a, typename P::Acc* slab,
-           unsigned* cnt) {
+           unsigned* cnt, int epi) {
   constexpr int STAGE = kBM * P::kXRow + BN * P::kWRow + BN * P::kZRow;
   constexpr int NB = NS;
   if constexpr (NB * STAGE <= 160 * 1024 && (kBM * P::kXRow + BN * P::kWRow + BN * P::kZRow) > 0) {
@@ -625,7 +646,7 @@ bool sf_go(const SfShape& sh, hipStream_t stream, const uint8_t* x, const P& pol
       const int ntn = (N + BN - 1) / BN, mtiles = (M + kBM - 1) / kBM;
       launch(gemm_sf_kernel<P, BN, WM, NS>, dim3((unsigned)(ntn * sh.splits * mtiles)), dim3(512),
              0, stream, x, pol, bias, y, M, N, K, a, slab, cnt, tuning().splitk_fenced, sh.splits,
-             ntn, sh.seam, tuning().cnt_stride);
+             ntn, sh.seam, tuning().cnt_stride, epi);
       return true;
     }
   }
@@ -635,11 +656,11 @@ bool sf_go(const SfShape& sh, hipStream_t stream, const uint8_t* x, const P& pol
 template <class P, int BN>
 int sf_dispatch_wm(const SfShape& sh, hipStream_t st, const uint8_t* x, const P& pol,
                    const uint16_t* bias, uint16_t* y, int M, int N, int K, int a,
-                   typename P::Acc* slab, unsigned* cnt) {
+                   typename P::Acc* slab, unsigned* cnt, int epi = 0) {
   bool ok = false;
   auto go = [&](auto wmc, auto nsc) {
     constexpr int W = decltype(wmc)::value, S_ = decltype(nsc)::value;
-    ok = sf_go<P, BN, W, S_>(sh, st, x, pol, bias, y, M, N, K, a, slab, cnt);
+    ok = sf_go<P, BN, W, S_>(sh, st, x, pol, bias, y, M, N, K, a, slab, cnt, epi);
   };
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
@@ -770,14 +791,16 @@ int sf_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uin
 
 int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
               const uint16_t* bias, uint16_t* y, int M, int N, int K, int bn, int splits,
-              int stages, int a_steps, hipStream_t stream);
+              int stages, int a_steps, hipStream_t stream, int epi);
 
+// epi 1: y [M][N / 2] = SwiGLU of the interleaved (gate, up) output pairs (bias must be null)
 int sf_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
-            const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream) {
+            const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream,
+            int epi = 0) {
   const SfShape sh = sf_shape(0, M, N, K);
   if (sh.wm == 1)  // one wave along M: the 32x32x16 kernel (gemm_sf32.hip)
     return sf32_int4(x, packed, sz, lg, bias, y, M, N, K, sh.bn, sh.splits, sh.stages,
-                     tuning().sf_a_steps, stream);
+                     tuning().sf_a_steps, stream, epi);
   const dim3 grid((N + sh.bn - 1) / sh.bn, 1, (M + kBM - 1) / kBM);  // tiles: grid.x grid.z
   f32x4_t* slab = nullptr;
   unsigned* cnt = nullptr;
@@ -795,13 +818,43 @@ int sf_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int l
   const uint8_t* xb = reinterpret_cast<const uint8_t*>(x);
   switch (sh.bn) {
     case 128:
-      return sf_dispatch_wm<SfI4, 128>(sh, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt);
+      return sf_dispatch_wm<SfI4, 128>(sh, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt,
+                                       epi);
     default:  // 64
-      return sf_dispatch_wm<SfI4, 64>(sh, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt);
+      return sf_dispatch_wm<SfI4, 64>(sh, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt,
+                                      epi);
   }
 }
 
 }  // namespace tao
+
+// int4 weight-only linear with the SwiGLU of interleaved (gate, up) output rows folded into the
+// epilogue (the w1||w3 linear of a prefill and its SiLU-mul in one launch): y [M][N / 2] =
+// bf16(bf16(silu(a_i)) * b_i), (a_i, b_i) = bf16 outputs of rows (2i, 2i+1). Served by the
+// single-fetch GEMM where it is routed (tao_tune_gemm_sf 2: wherever it applies);
+// TAO_ERR_UNSUPPORTED elsewhere (the caller runs the linear and tao_silu_mul_bf16).
+namespace tao {
+int int4_check_linear_args(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
+                           uint16_t* y, int64_t M, int64_t N, int64_t K, int64_t group_size);
+}  // namespace tao
+
+extern "C" int tao_int4wo_linear_swiglu_bf16(const uint16_t* x, const uint32_t* packed,
+                                             const uint16_t* sz, uint16_t* y, int64_t M,
+                                             int64_t N, int64_t K, int64_t group_size,
+                                             void* stream) {
+  int rc = tao::int4_check_linear_args(x, packed, sz, y, M, N, K, group_size);
+  if (rc != TAO_OK) return rc;
+  TAO_CHECK_ARG(N % 16 == 0, "int4 swiglu linear: N (%lld) must be a multiple of 16",
+                (long long)N);
+  if (M == 0) return TAO_OK;
+  if (!tao::use_sf(0, M, N, K, group_size) || M > (1 << 20))
+    return tao::set_error(TAO_ERR_UNSUPPORTED,
+                          "int4 swiglu linear: no fused kernel for M=%lld N=%lld K=%lld",
+                          (long long)M, (long long)N, (long long)K);
+  const int lg = group_size == 32 ? 5 : group_size == 64 ? 6 : group_size == 128 ? 7 : 8;
+  return tao::sf_int4(x, packed, sz, lg, nullptr, y, (int)M, (int)N, (int)K,
+                      tao::as_stream(stream), 1);
+}
 
 // Single-fetch prefill GEMM routing and launch shape (calling thread only; for A/B measurement):
 // mode 0 = built-in routing, 1 = never, 2 = whenever the shape is supported (M <= 128 per launch

@@ -84,7 +84,8 @@ template <int WV, int NS>
 __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
     const uint16_t* __restrict__ x, const uint32_t* __restrict__ wq, const uint32_t* __restrict__ sz,
     int lg, const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K,
-    int a_steps, f32x16_t* __restrict__ slab, unsigned* __restrict__ cnt, int fenced, int cs) {
+    int a_steps, f32x16_t* __restrict__ slab, unsigned* __restrict__ cnt, int fenced, int cs,
+    int epi) {
   constexpr int BN = 32 * WV;
   constexpr int XB = kBM * kXRow, WB = BN * kWRow, ZB = BN * kZRow;
   constexpr int STAGE = XB + WB + ZB;
@@ -291,6 +292,27 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
       out[r * BN + 32 * wave + r32] = f32_to_bf16(v);
     }
   __syncthreads();
+  if (epi == 1) {  // SwiGLU over interleaved (gate, up) columns: y [M][N / 2]
+    constexpr int OPR = BN / 16;
+    const int N2 = N >> 1;
+    const bool full2 = n_blk + BN <= N && (N2 & 7) == 0 && ((uintptr_t)y & 15) == 0;
+    for (int c = tid; c < kBM * OPR; c += WV * 64) {
+      const int r = c / OPR, cc = c % OPR;
+      const int m = m_blk + r;
+      if (m >= M) continue;
+      const uint4* img = reinterpret_cast<const uint4*>(out) + r * (BN / 8) + 2 * cc;
+      const uint4 v = swiglu_piece(img[0], img[1]);
+      const int n0 = (n_blk >> 1) + 8 * cc;
+      if (full2) {
+        *reinterpret_cast<uint4*>(y + (size_t)m * N2 + n0) = v;
+      } else {
+        const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+        for (int k = 0; k < 8; ++k)
+          if (n0 + k < N2) y[(size_t)m * N2 + n0 + k] = e[k];
+      }
+    }
+    return;
+  }
   constexpr int CPR = BN / 8;
   const bool full = n_blk + BN <= N && (N & 7) == 0 && ((uintptr_t)y & 15) == 0;
   for (int c = tid; c < kBM * CPR; c += WV * 64) {
@@ -313,7 +335,7 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
 // bn 64 (2 waves) or 128 (4 waves); splits S; stages 2-3; a_steps = 128-k steps per publisher
 int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
               const uint16_t* bias, uint16_t* y, int M, int N, int K, int bn, int splits,
-              int stages, int a_steps, hipStream_t stream) {
+              int stages, int a_steps, hipStream_t stream, int epi) {
   const int nsteps = K / 128;
   if (splits > nsteps) splits = nsteps;
   if (splits < 1) splits = 1;
@@ -332,7 +354,7 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
   const int fenced = tuning().splitk_fenced;
   auto go = [&](auto kern, int threads) {
     launch(kern, grid, dim3(threads), 0, stream, x, packed, reinterpret_cast<const uint32_t*>(sz),
-           lg, bias, y, M, N, K, a_steps, slab, cnt, fenced, tuning().cnt_stride);
+           lg, bias, y, M, N, K, a_steps, slab, cnt, fenced, tuning().cnt_stride, epi);
   };
   if (bn == 128) {
     if (stages == 2) go(gemm_sf32_int4_kernel<4, 2>, 256);

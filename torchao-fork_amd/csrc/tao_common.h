@@ -207,6 +207,24 @@ __device__ __forceinline__ void barrier_lgkm() {
   asm volatile("" ::: "memory");
 }
 
+// SwiGLU of an interleaved (gate, up) bf16 pair word: bf16(bf16(silu(a)) * b), the roundings of
+// decode_ops.hip's silu_mul kernel (F.silu(w1 x) * w3 x on bf16 tensors); used by the GEMM
+// epilogues that fold the prefill SiLU-mul into the w1||w3 linear
+__device__ __forceinline__ uint16_t swiglu_pair(uint32_t ab) {
+  const float a = __uint_as_float(ab << 16), b = __uint_as_float(ab & 0xFFFF0000u);
+  const float sa = __uint_as_float((uint32_t)f32_to_bf16(a / (1.f + __expf(-a))) << 16);
+  return f32_to_bf16(sa * b);
+}
+// 16 bf16 columns (8 pairs) of an epilogue image -> 8 bf16 outputs
+__device__ __forceinline__ uint4 swiglu_piece(uint4 lo, uint4 hi) {
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    o[i] = (uint32_t)swiglu_pair(w[2 * i]) | ((uint32_t)swiglu_pair(w[2 * i + 1]) << 16);
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

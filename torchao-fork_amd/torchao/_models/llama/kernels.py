@@ -2,11 +2,13 @@
 include/torchao_mi355x.h). Outputs are allocated with torch (graph-capture safe: inside a
 capture they come from the graph's private pool); launches go on torch's current stream."""
 
+from typing import Optional
+
 import torch
 
 from torchao import _lib
 
-__all__ = ["rmsnorm", "rope_kv", "attn_decode", "silu_mul", "int4_decode", "int8wo_decode", "int8dq_decode", "argmax",
+__all__ = ["rmsnorm", "rope_kv", "attn_decode", "silu_mul", "int4_linear_swiglu", "int4_decode", "int8wo_decode", "int8dq_decode", "argmax",
            "argmax_advance", "check_decode_status"]
 
 
@@ -92,6 +94,29 @@ def attn_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     _lib.call("tao_attn_prefill_bf16", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
               pos.data_ptr(), out.data_ptr(), B, H, Hkv, D, S, T, float(scale), _stream(q))
     return out
+
+
+def int4_linear_swiglu(x: torch.Tensor, packed: torch.Tensor, sz: torch.Tensor,
+                       group_size: int) -> Optional[torch.Tensor]:
+    """silu_mul(x @ W^T) for an int4 w1||w3 weight with interleaved (gate, up) rows, the SiLU-mul
+    folded into the GEMM's epilogue (tao_int4wo_linear_swiglu_bf16): [..., N / 2] bf16, or None
+    where no fused kernel serves the shape (the caller runs the linear and silu_mul)."""
+    _check(x, torch.bfloat16, "int4_linear_swiglu x")
+    x2 = x.reshape(-1, x.shape[-1])
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    M, K = x2.shape
+    N = packed.shape[0]
+    y = torch.empty(*x.shape[:-1], N // 2, dtype=x.dtype, device=x.device)
+    h = _lib.lib()
+    rc = h.tao_int4wo_linear_swiglu_bf16(x2.data_ptr(), packed.data_ptr(), sz.data_ptr(),
+                                         y.data_ptr(), M, N, K, int(group_size), _stream(x))
+    if rc == 2:  # TAO_ERR_UNSUPPORTED
+        return None
+    if rc != 0:
+        raise RuntimeError(f"tao_int4wo_linear_swiglu_bf16 failed (status {rc}): "
+                           + h.tao_last_error().decode(errors="replace"))
+    return y
 
 
 def silu_mul(a: torch.Tensor, b=None) -> torch.Tensor:

@@ -168,6 +168,11 @@ def _linear_plus(x: torch.Tensor, lin: nn.Linear, residual: torch.Tensor) -> tor
     return residual + lin(x)
 
 
+# Prefill: fold the SiLU-mul into the int4 w1||w3 GEMM's epilogue where a fused kernel serves the
+# shape (tao_int4wo_linear_swiglu_bf16); False = the linear then tao_silu_mul_bf16.
+PREFILL_SWIGLU = True
+
+
 def _int4_parts(lin: Optional[nn.Linear]):
     """(packed_weight, scale_and_zero, group_size) of an int4 weight-only linear on the gfx950
     row-stream layout (Int4WeightOnlyConfig), else None: the fused decode kernels read those
@@ -334,6 +339,21 @@ class FeedForward(nn.Module):
         a, b = self._gate_up(x)
         return self.w2(F.silu(a) * b)
 
+    def swiglu_prefill(self, x):
+        """silu(w1 x) * w3 x for S > 1 tokens on the gfx950 kernels: the int4 w1||w3 GEMM with the
+        SiLU-mul in its epilogue where a fused kernel serves the shape, else the linear(s) and
+        tao_silu_mul_bf16."""
+        from torchao._models.llama import kernels
+
+        p4 = _int4_parts(self.w13) if (self.w13 is not None and PREFILL_SWIGLU) else None
+        if p4 is not None:
+            g = kernels.int4_linear_swiglu(x, *p4)
+            if g is not None:
+                return g
+        if self.w13 is not None:
+            return kernels.silu_mul(self.w13(x))
+        return kernels.silu_mul(self.w1(x), self.w3(x))
+
     def forward_fused(self, x, residual, norm=None):
         from torchao._models.llama import kernels
 
@@ -376,9 +396,7 @@ class TransformerBlock(nn.Module):
                                                mask, input_pos)
         ff = self.feed_forward
         xn = kernels.rmsnorm(h, fn.weight, fn.eps)
-        g = kernels.silu_mul(ff.w13(xn)) if ff.w13 is not None else kernels.silu_mul(ff.w1(xn),
-                                                                                     ff.w3(xn))
-        return h + ff.w2(g)
+        return h + ff.w2(ff.swiglu_prefill(xn))
 
 
 class Transformer(nn.Module):
@@ -464,9 +482,7 @@ class Transformer(nn.Module):
                 x, xn = kernels.add_rmsnorm(x, pending, an.weight, an.eps)
             a = blk.attention.forward_prefill(xn, self.freqs, mask, input_pos)
             x, hn = kernels.add_rmsnorm(x, a, fn.weight, fn.eps)
-            g = (kernels.silu_mul(ff.w13(hn)) if ff.w13 is not None
-                 else kernels.silu_mul(ff.w1(hn), ff.w3(hn)))
-            pending = ff.w2(g)
+            pending = ff.w2(ff.swiglu_prefill(hn))
         return x if pending is None else x + pending
 
     def prefill_next(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
