@@ -79,6 +79,19 @@ int tao_int4wo_linear_swiglu_bf16(const uint16_t* x, const uint32_t* packed, con
                                   uint16_t* y, int64_t M, int64_t N, int64_t K,
                                   int64_t group_size, void* stream);
 
+/* The prefill's wqkv linear (int4 weight-only, no bias) with RoPE and the KV-cache write of
+ * tao_rope_kv_bf16 folded into the epilogue: x [B*S][K] bf16; weight [(H + 2 Hkv) D][K]; q
+ * rotated into q_out [B][H][S][D]; k rotated and v written into the caches [B][Hkv][T][D] at row
+ * pos[s] (a position outside [0, T) writes no cache row and sets tao_decode_status bit 1).
+ * D == 128; q_out and the caches 16-B aligned. Replaces wqkv + apply_rotary_emb +
+ * KVCache.update (gpt-fast model.py Attention.forward) at prefill as one launch. Served where
+ * the single-fetch GEMM is routed; TAO_ERR_UNSUPPORTED elsewhere. */
+int tao_int4wo_linear_rope_kv_bf16(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
+                                   int64_t K, int64_t group_size, const float* freqs,
+                                   const int64_t* pos, uint16_t* q_out, uint16_t* k_cache,
+                                   uint16_t* v_cache, int64_t B, int64_t S, int64_t H,
+                                   int64_t Hkv, int64_t D, int64_t T, void* stream);
+
 /* Tuning hooks (tao_tune_*). Every override is THREAD-LOCAL: it re-routes only launches issued
  * from the thread that set it, never another thread's model. tao_tune_reset() restores every
  * built-in choice for the calling thread (torchao.kernel.tuning(...) wraps set + reset). */

@@ -271,10 +271,74 @@ def test_sf_swiglu_epilogue_matches_linear_then_silu_mul(sf, M, N, K, mode, cfg,
     assert torch.equal(y, ref)
 
 
+@pytest.mark.parametrize("B,S,H,Hkv,K,p0,T", [(1, 128, 32, 8, 4096, 0, 200), (1, 100, 4, 2, 512, 7, 160),
+                                              (2, 50, 4, 1, 1024, 0, 64)])
+@pytest.mark.parametrize("mode,cfg", [(0, None), (2, (64, 2, 4, 2, 0)), (2, (128, 2, 2, 3, 0)),
+                                      (2, (64, 4, 1, 3, 0))])
+@pytest.mark.parametrize("seam", [0, 1])
+def test_sf_rope_kv_epilogue_matches_linear_then_rope_kv(sf, B, S, H, Hkv, K, p0, T, mode, cfg,
+                                                        seam):
+    """tao_int4wo_linear_rope_kv_bf16 (wqkv GEMM with RoPE + the KV-cache write in its epilogue)
+    writes the same q and cache rows, bit for bit, as the routed linear followed by
+    tao_rope_kv_bf16; cache rows outside the prompt's positions stay untouched; shapes no fused
+    kernel serves return None."""
+    import math
+
+    from torchao._models.llama import kernels
+    from torchao._models.llama.model import ModelArgs, _rope_freqs
+
+    sf(mode, *(cfg or ()))
+    _lib.call("tao_tune_gemm_sf_seam", seam)
+    D = 128
+    N = (H + 2 * Hkv) * D
+    q, s_, z, packed, sz = _int4(N, K, 32, seed=N + K + S)
+    x = oracle.make_activation(B * S, K, seed=S).reshape(B, S, K).to(DEV)
+    freqs = _rope_freqs(ModelArgs(dim=H * D, n_head=H, n_local_heads=Hkv, block_size=T), T).to(DEV)
+    pos = torch.arange(p0, p0 + S, device=DEV)
+    kc = [torch.full((B, Hkv, T, D), 7, dtype=torch.bfloat16, device=DEV) for _ in range(2)]
+    vc = [torch.full((B, Hkv, T, D), 7, dtype=torch.bfloat16, device=DEV) for _ in range(2)]
+    got = kernels.int4_linear_rope_kv(x, packed, sz, 32, freqs, pos, kc[0], vc[0], H)
+    if B * S > 128 or (mode == 0 and (N, K) != (6144, 4096)) or (mode == 0 and B * S <= 64):
+        assert got is None
+        return
+    assert got is not None
+    qkv = torch.ops.torchao.int4_weight_only_linear(x.reshape(B * S, K), packed, sz, 32, None)
+    ref = kernels.rope_kv(qkv.reshape(B, S, N), freqs, pos, kc[1], vc[1], H)
+    assert torch.equal(got, ref)
+    assert torch.equal(kc[0], kc[1]) and torch.equal(vc[0], vc[1])
+    assert bool((kc[0][:, :, p0 + S:] == 7).all()) and bool((kc[0][:, :, :p0] == 7).all())
+    assert not math.isnan(float(got.float().sum()))
+
+
+def test_sf_rope_kv_epilogue_position_past_cache(sf):
+    """A prompt position outside [0, T) writes no cache row and sets tao_decode_status bit 1,
+    as tao_rope_kv_bf16 does."""
+    from torchao._models.llama import kernels
+    from torchao._models.llama.model import ModelArgs, _rope_freqs
+
+    sf(2, 64, 2, 2, 3, 0)
+    H, Hkv, D, K, S, T = 4, 2, 128, 512, 8, 16
+    N = (H + 2 * Hkv) * D
+    _, _, _, packed, sz = _int4(N, K, 32, seed=5)
+    x = oracle.make_activation(S, K, seed=2).reshape(1, S, K).to(DEV)
+    freqs = _rope_freqs(ModelArgs(dim=H * D, n_head=H, n_local_heads=Hkv, block_size=64), 64).to(DEV)
+    pos = torch.arange(12, 12 + S, device=DEV)  # rows 16.. are past the cache
+    kc = torch.full((1, Hkv, T, D), 7, dtype=torch.bfloat16, device=DEV)
+    vc = kc.clone()
+    st = torch.zeros(1, dtype=torch.int32)
+    _lib.call("tao_decode_status", st.data_ptr())  # clear
+    assert kernels.int4_linear_rope_kv(x, packed, sz, 32, freqs, pos, kc, vc, H) is not None
+    torch.cuda.synchronize()
+    _lib.call("tao_decode_status", st.data_ptr())
+    assert int(st.item()) & 1
+    assert bool((kc[:, :, :12] == 7).all()) and bool((kc[:, :, 12:16] != 7).any())
+
+
 def test_sf_swiglu_prefill_model_matches_unfused():
     """A small Llama prefill (dim 512, head_dim 128, w1||w3 3072 x 512) with the SwiGLU folded
-    into the w1||w3 GEMM (every linear on the single-fetch kernel) gives bit-identical hidden
-    states to the linear + silu_mul path on the same kernels."""
+    into the w1||w3 GEMM and RoPE + the KV write folded into the wqkv GEMM (every linear on the
+    single-fetch kernel) gives bit-identical hidden states and caches to the linear + silu_mul /
+    rope_kv path on the same kernels."""
     import math
 
     from torchao._models.llama import model as mdl
@@ -306,10 +370,16 @@ def test_sf_swiglu_prefill_model_matches_unfused():
 
         assert kernels.int4_linear_swiglu(torch.zeros(128, 512, device=dev, dtype=torch.bfloat16),
                                           *mdl._int4_parts(ff.w13)) is not None
+        assert kernels.int4_linear_rope_kv(
+            torch.zeros(1, 128, 512, device=dev, dtype=torch.bfloat16),
+            *mdl._int4_parts(m.layers[0].attention.wqkv), m.freqs, pos,
+            m.layers[0].attention.kv_cache.k_cache.clone(),
+            m.layers[0].attention.kv_cache.v_cache.clone(), 4) is not None
         for fused in (True, False):
-            mdl.PREFILL_SWIGLU = fused
+            mdl.PREFILL_SWIGLU = mdl.PREFILL_ROPE = fused
             try:
                 outs.append(m._layers_prefill(idx, pos).clone())
+                outs.append(m.layers[1].attention.kv_cache.k_cache.clone())
             finally:
-                mdl.PREFILL_SWIGLU = True
-    assert torch.equal(outs[0], outs[1])
+                mdl.PREFILL_SWIGLU = mdl.PREFILL_ROPE = True
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])

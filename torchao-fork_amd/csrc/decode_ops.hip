@@ -36,6 +36,7 @@ namespace tao {
 
 TAO_DECODE_ERROR_WORD(decode_ops_status)
 int int4gemv_decode_status(unsigned* bits);
+int sf_decode_status(unsigned* bits);
 int int8gemv_decode_status(unsigned* bits);
 int int8dyn_decode_status(unsigned* bits);
 
@@ -717,6 +718,7 @@ extern "C" int tao_decode_status(int* bits) {
   if (rc == TAO_OK) rc = tao::int4gemv_decode_status(&v);
   if (rc == TAO_OK) rc = tao::int8gemv_decode_status(&v);
   if (rc == TAO_OK) rc = tao::int8dyn_decode_status(&v);
+  if (rc == TAO_OK) rc = tao::sf_decode_status(&v);
   *bits = (int)v;
   return rc;
 }

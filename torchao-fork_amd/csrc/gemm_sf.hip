@@ -36,6 +36,8 @@
 
 namespace tao {
 
+TAO_DECODE_ERROR_WORD(sf_decode_status)
+
 namespace {
 
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
@@ -53,6 +55,21 @@ __device__ unsigned long long g_sf_stamps[8192 * 8];
 // reducer poll timeouts (never expected: publishers never wait, and they precede the reducers in
 // every XCD's dispatch order); read and cleared by tao_gemm_sf_status()
 __device__ unsigned g_sf_err = 0;
+
+// Epilogue folded into the GEMM (kind): 0 = y [M][N] bf16 (+ bias); 1 = SwiGLU of interleaved
+// (gate, up) column pairs, y [M][N / 2]; 2 = RoPE + KV-cache write of a wqkv output (the prefill
+// rope_kv kernel's math, decode_ops.hip): rows are tokens (b, s) = (m / S, m % S) at position
+// pos[s]; columns [q heads | k heads | v heads] of D = 128; q rotated into q_out [B][H][S][D],
+// k rotated and v written into the caches [B][Hkv][T][D] at row pos[s].
+struct SfEpi {
+  int kind;
+  const float* freqs;  // [T][D / 2] (cos, sin)
+  const int64_t* pos;  // [S]
+  uint16_t* q_out;
+  uint16_t* kc;
+  uint16_t* vc;
+  int S, H, Hkv, T;
+};
 
 template <int I, int N, class F>
 __device__ __forceinline__ void sfor(F&& f) {
@@ -199,7 +216,8 @@ template <class P, int BN, int WM, int NS>
 __global__ __launch_bounds__(512) void gemm_sf_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int a_steps, typename P::Acc* __restrict__ slab,
-    unsigned* __restrict__ cnt, int fenced, int S, int ntn, int seam, int cs, int epi) {
+    unsigned* __restrict__ cnt, int fenced, int S, int ntn, int seam, int cs, SfEpi ep) {
+  const int epi = ep.kind;
 #if TAO_SF_STAMPS
   const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
   unsigned long long stamp[6] = {t_entry, 0, 0, 0, 0, 0};
@@ -591,10 +609,49 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
       }
     }
   }
+  if (epi == 2) {  // RoPE + KV-cache write (N = (H + 2 Hkv) 128, 16-B aligned destinations)
+    constexpr int CPR = BN / 8;
+    const float2* f2 = reinterpret_cast<const float2*>(ep.freqs);
+    for (int c = tid; c < kBM * CPR; c += 512) {
+      const int r = c / CPR, cc = c % CPR;
+      const int m = m_blk + r, n0 = n_blk + 8 * cc;
+      if (m >= M || n0 >= N) continue;
+      if (seam && S > 1 && ((r / RM) * WN + (8 * cc) / CN) / wpo != z) continue;  // not owned
+      uint4 v = reinterpret_cast<const uint4*>(out)[c];
+      const int b = m / ep.S, s = m % ep.S;
+      int64_t p = ep.pos[s];
+      const bool pok = p >= 0 && p < ep.T;  // KV cache row inside [0, T)
+      if (!pok) {  // report (tao_decode_status) and write no cache row
+        flag_decode_error(kDecodeErrKvPos);
+        p = p < 0 ? 0 : ep.T - 1;
+      }
+      const int head = n0 >> 7, d0 = n0 & 127;
+      if (head < ep.H + ep.Hkv) {  // rotate the 4 interleaved pairs (fp32, bf16 out)
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float2 cs = f2[(size_t)p * 64 + (d0 >> 1) + i];
+          const float x0 = bf16lo_to_f32(w[i]), x1 = bf16hi_to_f32(w[i]);
+          const float o0 = x0 * cs.x - x1 * cs.y, o1 = x1 * cs.x + x0 * cs.y;
+          w[i] = (uint32_t)f32_to_bf16(o0) | ((uint32_t)f32_to_bf16(o1) << 16);
+        }
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      uint16_t* dst = nullptr;
+      if (head < ep.H) {
+        dst = ep.q_out + (((size_t)b * ep.H + head) * ep.S + s) * 128 + d0;
+      } else if (pok) {
+        const bool isk = head < ep.H + ep.Hkv;
+        const int kh = isk ? head - ep.H : head - ep.H - ep.Hkv;
+        dst = (isk ? ep.kc : ep.vc) + (((size_t)b * ep.Hkv + kh) * ep.T + p) * 128 + d0;
+      }
+      if (dst != nullptr) *reinterpret_cast<uint4*>(dst) = v;
+    }
+  }
   constexpr int CPR = BN / 8;  // 16-B pieces per row
   const bool full = n_blk + BN <= N && (N & 7) == 0 && ((uintptr_t)y & 15) == 0;
 #pragma unroll
-  for (int c = epi == 1 ? kBM * CPR : tid; c < kBM * CPR; c += 512) {
+  for (int c = epi != 0 ? kBM * CPR : tid; c < kBM * CPR; c += 512) {
     const int r = c / CPR, cc = c % CPR;
     const int m = m_blk + r;
     if (m >= M) continue;
@@ -635,7 +692,7 @@ struct SfShape {
 template <class P, int BN, int WM, int NS>
 bool sf_go(const SfShape& sh, hipStream_t stream, const uint8_t* x, const P& pol,
            const uint16_t* bias, uint16_t* y, int M, int N, int K, int a, typename P::Acc* slab,
-           unsigned* cnt, int epi) {
+           unsigned* cnt, const SfEpi& ep) {
   constexpr int STAGE = kBM * P::kXRow + BN * P::kWRow + BN * P::kZRow;
   constexpr int NB = NS;
   if constexpr (NB * STAGE <= 160 * 1024 && (kBM * P::kXRow + BN * P::kWRow + BN * P::kZRow) > 0) {
@@ -646,7 +703,7 @@ bool sf_go(const SfShape& sh, hipStream_t stream, const uint8_t* x, const P& pol
       const int ntn = (N + BN - 1) / BN, mtiles = (M + kBM - 1) / kBM;
       launch(gemm_sf_kernel<P, BN, WM, NS>, dim3((unsigned)(ntn * sh.splits * mtiles)), dim3(512),
              0, stream, x, pol, bias, y, M, N, K, a, slab, cnt, tuning().splitk_fenced, sh.splits,
-             ntn, sh.seam, tuning().cnt_stride, epi);
+             ntn, sh.seam, tuning().cnt_stride, ep);
       return true;
     }
   }
@@ -656,11 +713,11 @@ bool sf_go(const SfShape& sh, hipStream_t stream, const uint8_t* x, const P& pol
 template <class P, int BN>
 int sf_dispatch_wm(const SfShape& sh, hipStream_t st, const uint8_t* x, const P& pol,
                    const uint16_t* bias, uint16_t* y, int M, int N, int K, int a,
-                   typename P::Acc* slab, unsigned* cnt, int epi = 0) {
+                   typename P::Acc* slab, unsigned* cnt, const SfEpi& ep = SfEpi{}) {
   bool ok = false;
   auto go = [&](auto wmc, auto nsc) {
     constexpr int W = decltype(wmc)::value, S_ = decltype(nsc)::value;
-    ok = sf_go<P, BN, W, S_>(sh, st, x, pol, bias, y, M, N, K, a, slab, cnt, epi);
+    ok = sf_go<P, BN, W, S_>(sh, st, x, pol, bias, y, M, N, K, a, slab, cnt, ep);
   };
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
@@ -793,14 +850,18 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
               const uint16_t* bias, uint16_t* y, int M, int N, int K, int bn, int splits,
               int stages, int a_steps, hipStream_t stream, int epi);
 
-// epi 1: y [M][N / 2] = SwiGLU of the interleaved (gate, up) output pairs (bias must be null)
-int sf_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
-            const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream,
-            int epi = 0) {
+// ep.kind 1: y [M][N / 2] = SwiGLU of the interleaved (gate, up) output pairs; 2: RoPE + KV
+// write (y unused). Both need bias == nullptr.
+int sf_int4_epi(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
+                const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream,
+                const SfEpi& ep) {
   const SfShape sh = sf_shape(0, M, N, K);
-  if (sh.wm == 1)  // one wave along M: the 32x32x16 kernel (gemm_sf32.hip)
+  if (sh.wm == 1) {  // one wave along M: the 32x32x16 kernel (gemm_sf32.hip)
+    if (ep.kind == 2)
+      return set_error(TAO_ERR_UNSUPPORTED, "gemm_sf: no RoPE epilogue on the 32x32x16 kernel");
     return sf32_int4(x, packed, sz, lg, bias, y, M, N, K, sh.bn, sh.splits, sh.stages,
-                     tuning().sf_a_steps, stream, epi);
+                     tuning().sf_a_steps, stream, ep.kind);
+  }
   const dim3 grid((N + sh.bn - 1) / sh.bn, 1, (M + kBM - 1) / kBM);  // tiles: grid.x grid.z
   f32x4_t* slab = nullptr;
   unsigned* cnt = nullptr;
@@ -819,11 +880,19 @@ int sf_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int l
   switch (sh.bn) {
     case 128:
       return sf_dispatch_wm<SfI4, 128>(sh, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt,
-                                       epi);
+                                       ep);
     default:  // 64
       return sf_dispatch_wm<SfI4, 64>(sh, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt,
-                                      epi);
+                                      ep);
   }
+}
+
+int sf_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
+            const uint16_t* bias, uint16_t* y, int M, int N, int K, hipStream_t stream,
+            int epi = 0) {
+  SfEpi ep{};
+  ep.kind = epi;
+  return sf_int4_epi(x, packed, sz, lg, bias, y, M, N, K, stream, ep);
 }
 
 }  // namespace tao
@@ -838,6 +907,8 @@ int int4_check_linear_args(const uint16_t* x, const uint32_t* packed, const uint
                            uint16_t* y, int64_t M, int64_t N, int64_t K, int64_t group_size);
 }  // namespace tao
 
+static int lg_of(int64_t g) { return g == 32 ? 5 : g == 64 ? 6 : g == 128 ? 7 : 8; }
+
 extern "C" int tao_int4wo_linear_swiglu_bf16(const uint16_t* x, const uint32_t* packed,
                                              const uint16_t* sz, uint16_t* y, int64_t M,
                                              int64_t N, int64_t K, int64_t group_size,
@@ -851,9 +922,48 @@ extern "C" int tao_int4wo_linear_swiglu_bf16(const uint16_t* x, const uint32_t* 
     return tao::set_error(TAO_ERR_UNSUPPORTED,
                           "int4 swiglu linear: no fused kernel for M=%lld N=%lld K=%lld",
                           (long long)M, (long long)N, (long long)K);
-  const int lg = group_size == 32 ? 5 : group_size == 64 ? 6 : group_size == 128 ? 7 : 8;
-  return tao::sf_int4(x, packed, sz, lg, nullptr, y, (int)M, (int)N, (int)K,
+  return tao::sf_int4(x, packed, sz, lg_of(group_size), nullptr, y, (int)M, (int)N, (int)K,
                       tao::as_stream(stream), 1);
+}
+
+// int4 weight-only wqkv linear of a prefill with RoPE and the KV-cache write folded into the
+// epilogue (tao_rope_kv_bf16's math and layouts): x [B S][K]; q_out [B][H][S][D] (rotated);
+// k (rotated), v -> caches [B][Hkv][T][D] at row pos[s]; D == 128; the weight is [(H + 2 Hkv) D][K].
+// Served where the single-fetch GEMM is routed (not its 32x32x16 variant); TAO_ERR_UNSUPPORTED
+// elsewhere (the caller runs the linear and tao_rope_kv_bf16).
+extern "C" int tao_int4wo_linear_rope_kv_bf16(const uint16_t* x, const uint32_t* packed,
+                                              const uint16_t* sz, int64_t K, int64_t group_size,
+                                              const float* freqs, const int64_t* pos,
+                                              uint16_t* q_out, uint16_t* k_cache,
+                                              uint16_t* v_cache, int64_t B, int64_t S, int64_t H,
+                                              int64_t Hkv, int64_t D, int64_t T, void* stream) {
+  TAO_CHECK_ARG(D == 128, "int4 rope linear: head_dim must be 128 (got %lld)", (long long)D);
+  TAO_CHECK_ARG(B > 0 && S > 0 && H > 0 && Hkv > 0 && T > 0 && B * S < (1LL << 30),
+                "int4 rope linear: bad sizes");
+  const int64_t M = B * S, N = (H + 2 * Hkv) * D;
+  int rc = tao::int4_check_linear_args(x, packed, sz, q_out, M, N, K, group_size);
+  if (rc != TAO_OK) return rc;
+  TAO_CHECK_ALIGN(q_out, 16, "q_out");
+  TAO_CHECK_ALIGN(k_cache, 16, "k_cache");
+  TAO_CHECK_ALIGN(v_cache, 16, "v_cache");
+  TAO_CHECK_ALIGN(freqs, 8, "freqs");
+  if (!tao::use_sf(0, M, N, K, group_size))
+    return tao::set_error(TAO_ERR_UNSUPPORTED,
+                          "int4 rope linear: no fused kernel for M=%lld N=%lld K=%lld",
+                          (long long)M, (long long)N, (long long)K);
+  tao::SfEpi ep{};
+  ep.kind = 2;
+  ep.freqs = freqs;
+  ep.pos = pos;
+  ep.q_out = q_out;
+  ep.kc = k_cache;
+  ep.vc = v_cache;
+  ep.S = (int)S;
+  ep.H = (int)H;
+  ep.Hkv = (int)Hkv;
+  ep.T = (int)T;
+  return tao::sf_int4_epi(x, packed, sz, lg_of(group_size), nullptr, q_out, (int)M, (int)N,
+                          (int)K, tao::as_stream(stream), ep);
 }
 
 // Single-fetch prefill GEMM routing and launch shape (calling thread only; for A/B measurement):

@@ -36,6 +36,8 @@ _SIGNATURES = {
     "tao_profile_end": [_p, _int, _p],
     "tao_int4wo_linear_bf16": [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p],
     "tao_int4wo_linear_swiglu_bf16": [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p],
+    "tao_int4wo_linear_rope_kv_bf16": [_p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _i64, _i64,
+                                       _i64, _i64, _i64, _i64, _p],
     "tao_tune_int4_gemv": [_int, _int, _int, _int],
     "tao_tune_linear_crossover": [_int],
     "tao_tune_gemm": [_int, _int, _int],

@@ -290,6 +290,9 @@ def main(argv=None):
     ap.add_argument("--sdpa_prefill", action="store_true",
                     help="prefill attention through torch's masked SDPA instead of "
                          "tao_attn_prefill_bf16 (kernels.PREFILL_ATTN = False)")
+    ap.add_argument("--prefill_rope", type=int, default=-1,
+                    help="1 / 0: fold the prefill RoPE + KV write into the int4 wqkv GEMM's "
+                         "epilogue (model.PREFILL_ROPE; -1 = built-in)")
     ap.add_argument("--prefill_swiglu", type=int, default=-1,
                     help="1 / 0: fold the prefill SiLU-mul into the int4 w1||w3 GEMM's epilogue "
                          "(model.PREFILL_SWIGLU; -1 = built-in)")
@@ -347,6 +350,10 @@ def main(argv=None):
         from torchao._models.llama import model as _mdl
 
         _mdl.PREFILL_SWIGLU = bool(args.prefill_swiglu)
+    if args.prefill_rope >= 0:
+        from torchao._models.llama import model as _mdl
+
+        _mdl.PREFILL_ROPE = bool(args.prefill_rope)
     device = torch.device(args.device)
     t = time.perf_counter()
     model = build_model(args.model_name, device, checkpoint_path=args.checkpoint_path,

@@ -8,7 +8,8 @@ import torch
 
 from torchao import _lib
 
-__all__ = ["rmsnorm", "rope_kv", "attn_decode", "silu_mul", "int4_linear_swiglu", "int4_decode", "int8wo_decode", "int8dq_decode", "argmax",
+__all__ = ["rmsnorm", "rope_kv", "attn_decode", "silu_mul", "int4_linear_swiglu",
+           "int4_linear_rope_kv", "int4_decode", "int8wo_decode", "int8dq_decode", "argmax",
            "argmax_advance", "check_decode_status"]
 
 
@@ -117,6 +118,34 @@ def int4_linear_swiglu(x: torch.Tensor, packed: torch.Tensor, sz: torch.Tensor,
         raise RuntimeError(f"tao_int4wo_linear_swiglu_bf16 failed (status {rc}): "
                            + h.tao_last_error().decode(errors="replace"))
     return y
+
+
+def int4_linear_rope_kv(x: torch.Tensor, packed: torch.Tensor, sz: torch.Tensor,
+                        group_size: int, freqs: torch.Tensor, pos: torch.Tensor,
+                        k_cache: torch.Tensor, v_cache: torch.Tensor,
+                        n_head: int) -> Optional[torch.Tensor]:
+    """rope_kv(x @ Wqkv^T, ...) in one launch (tao_int4wo_linear_rope_kv_bf16): x [B, S, K] ->
+    rotated q [B, H, S, D]; k, v written to the caches at pos. None where no fused kernel serves
+    the shape (the caller runs the linear and rope_kv)."""
+    _check(x, torch.bfloat16, "int4_linear_rope_kv x")
+    _check(freqs, torch.float32, "int4_linear_rope_kv freqs")
+    _check(pos, torch.int64, "int4_linear_rope_kv pos")
+    B, S, K = x.shape
+    _, Hkv, T, D = k_cache.shape
+    if packed.shape[0] != (n_head + 2 * Hkv) * D:
+        return None
+    q = torch.empty(B, n_head, S, D, dtype=x.dtype, device=x.device)
+    h = _lib.lib()
+    rc = h.tao_int4wo_linear_rope_kv_bf16(x.data_ptr(), packed.data_ptr(), sz.data_ptr(), K,
+                                          int(group_size), freqs.data_ptr(), pos.data_ptr(),
+                                          q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), B,
+                                          S, n_head, Hkv, D, T, _stream(x))
+    if rc == 2:  # TAO_ERR_UNSUPPORTED
+        return None
+    if rc != 0:
+        raise RuntimeError(f"tao_int4wo_linear_rope_kv_bf16 failed (status {rc}): "
+                           + h.tao_last_error().decode(errors="replace"))
+    return q
 
 
 def silu_mul(a: torch.Tensor, b=None) -> torch.Tensor:

@@ -171,6 +171,9 @@ def _linear_plus(x: torch.Tensor, lin: nn.Linear, residual: torch.Tensor) -> tor
 # Prefill: fold the SiLU-mul into the int4 w1||w3 GEMM's epilogue where a fused kernel serves the
 # shape (tao_int4wo_linear_swiglu_bf16); False = the linear then tao_silu_mul_bf16.
 PREFILL_SWIGLU = True
+# Prefill: fold RoPE + the KV-cache write into the int4 wqkv GEMM's epilogue where a fused kernel
+# serves the shape (tao_int4wo_linear_rope_kv_bf16); False = the linear then tao_rope_kv_bf16.
+PREFILL_ROPE = True
 
 
 def _int4_parts(lin: Optional[nn.Linear]):
@@ -279,8 +282,14 @@ class Attention(nn.Module):
 
         B, S, _ = x.shape
         kv = self.kv_cache
-        q = kernels.rope_kv(self.wqkv(x), freqs_table, input_pos, kv.k_cache, kv.v_cache,
-                            self.n_head)
+        q = None
+        p4 = _int4_parts(self.wqkv) if PREFILL_ROPE else None
+        if p4 is not None and x.is_contiguous():  # wqkv GEMM with RoPE + KV write (one launch)
+            q = kernels.int4_linear_rope_kv(x, *p4, freqs_table, input_pos, kv.k_cache,
+                                            kv.v_cache, self.n_head)
+        if q is None:
+            q = kernels.rope_kv(self.wqkv(x), freqs_table, input_pos, kv.k_cache, kv.v_cache,
+                                self.n_head)
         if kernels.PREFILL_ATTN and self.head_dim == 128 and q.dtype == torch.bfloat16:
             # the causal mask over the caches is keys 0..input_pos[s] for query s
             y = kernels.attn_prefill(q, kv.k_cache, kv.v_cache, input_pos,
