@@ -95,13 +95,17 @@ def main():
                  (64, 4, 4, 4, 0, 128), (64, 8, 4, 3, 0, 128), (64, 2, 4, 3, 0, 128),
                  (64, 4, 2, 3, 0, 256), (64, 4, 4, 2, 0, 256), (128, 4, 8, 3, 0, 128),
                  (128, 2, 8, 3, 0, 128), (128, 4, 8, 2, 0, 256), (64, 4, 1, 3, 0, 128),
-                 (32, 8, 1, 3, 0, 256), (32, 8, 2, 3, 9, 256), (32, 8, 2, 3, 7, 256)],
+                 (32, 8, 1, 3, 0, 256), (32, 8, 2, 3, 9, 256), (32, 8, 2, 3, 7, 256),
+                 (256, 2, 2, 2, 0, 128), (256, 4, 2, 3, 0, 128), (256, 2, 1, 3, 0, 128),
+                 (256, 4, 4, 2, 0, 128), (256, 2, 4, 3, 0, 128)],
         "int4": [(64, 2, 4, 3, 0), (64, 4, 4, 3, 0), (64, 8, 4, 3, 0), (64, 2, 4, 2, 0),
                  (64, 2, 4, 4, 0), (128, 2, 8, 2, 0), (128, 2, 8, 3, 0), (128, 4, 8, 3, 0),
                  (128, 8, 8, 3, 0), (64, 2, 2, 3, 0), (128, 2, 4, 3, 0), (64, 2, 8, 3, 0),
                  (64, 2, 4, 3, 9), (128, 4, 8, 3, 5), (128, 1, 8, 2, 0), (128, 1, 4, 3, 0),
                  (128, 1, 2, 3, 0), (128, 1, 1, 3, 0), (64, 1, 4, 2, 0), (64, 1, 2, 3, 0),
-                 (64, 1, 8, 2, 0), (128, 1, 8, 3, 0)],
+                 (64, 1, 8, 2, 0), (128, 1, 8, 3, 0),
+                 (256, 2, 2, 2, 0), (256, 2, 2, 3, 0), (256, 2, 1, 3, 0), (256, 4, 2, 2, 0),
+                 (256, 2, 4, 2, 0), (256, 4, 4, 3, 0), (256, 2, 8, 2, 0)],
     }
     for path in args.paths.split(","):
         for (M, N, K) in shapes:

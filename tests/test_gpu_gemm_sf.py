@@ -383,3 +383,26 @@ def test_sf_swiglu_prefill_model_matches_unfused():
             finally:
                 mdl.PREFILL_SWIGLU = mdl.PREFILL_ROPE = True
     assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])
+
+
+@pytest.mark.parametrize("cfg8,cfg4", [((256, 2, 2, 2, 0, 128), (256, 2, 2, 2, 0)),
+                                       ((256, 4, 1, 3, 0, 128), (256, 4, 4, 3, 0)),
+                                       ((256, 2, 4, 3, 0, 128), (256, 2, 1, 3, 0))])
+@pytest.mark.parametrize("M,N,K", [(128, 4096, 4096), (100, 640, 3072), (200, 288, 2048)])
+def test_sf_bn256(sf, cfg8, cfg4, M, N, K):
+    """256-column tiles (x read once per 256 weight columns): int8 dyn bit-exact, int4 within the
+    bars at g = 32 and 128, ragged N tiles and several M tiles, both seams."""
+    for seam in (0, 1):
+        sf(2, *cfg8)
+        _lib.call("tao_tune_gemm_sf_seam", seam)
+        xq, xs, wq, ws = _int8(M, N, K, seed=M + K)
+        y = torch.ops.torchao.int8_scaled_mm(xq.to(DEV), xs.to(DEV), wq.to(DEV), ws.to(DEV), None).cpu()
+        assert torch.equal(y, oracle.int8_scaled_mm(xq, xs, wq, ws, None, epilogue="cpu"))
+        sf(2, *cfg4)
+        _lib.call("tao_tune_gemm_sf_seam", seam)
+        for g in (32, 128):
+            q, s, z, packed, sz = _int4(N, K, g, seed=N + g)
+            x = oracle.make_activation(M, K, seed=g)
+            y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, None).cpu()
+            assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, g)) < TOL_FP32
+            assert oracle.rel_l2(y, oracle.int4_linear(x, q, s, z, g)) < TOL_REF

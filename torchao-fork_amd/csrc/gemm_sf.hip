@@ -835,6 +835,7 @@ int sf_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uin
     switch (sh.bn) {
       case 32: return sf_dispatch_wm<P, 32>(sh, stream, xb, pol, bias, y, M, N, K, a, slab, cnt);
       case 128: return sf_dispatch_wm<P, 128>(sh, stream, xb, pol, bias, y, M, N, K, a, slab, cnt);
+      case 256: return sf_dispatch_wm<P, 256>(sh, stream, xb, pol, bias, y, M, N, K, a, slab, cnt);
       default: return sf_dispatch_wm<P, 64>(sh, stream, xb, pol, bias, y, M, N, K, a, slab, cnt);
     }
   };
@@ -873,11 +874,14 @@ int sf_int4_epi(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, i
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<f32x4_t*>(w);
   }
-  if (sh.bn != 64 && sh.bn != 128)
+  if (sh.bn != 64 && sh.bn != 128 && sh.bn != 256)
     return set_error(TAO_ERR_INVALID_ARGUMENT, "gemm_sf: int4 takes bn 64 or 128 (got %d)", sh.bn);
   SfI4 pol{packed, reinterpret_cast<const uint32_t*>(sz), lg};
   const uint8_t* xb = reinterpret_cast<const uint8_t*>(x);
   switch (sh.bn) {
+    case 256:
+      return sf_dispatch_wm<SfI4, 256>(sh, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt,
+                                       ep);
     case 128:
       return sf_dispatch_wm<SfI4, 128>(sh, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt,
                                        ep);
@@ -972,7 +976,8 @@ extern "C" int tao_int4wo_linear_rope_kv_bf16(const uint16_t* x, const uint32_t*
 extern "C" int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages, int a_steps,
                                 int ks) {
   TAO_CHECK_ARG(mode >= 0 && mode <= 2, "tune: gemm_sf mode must be 0, 1 or 2");
-  TAO_CHECK_ARG(bn == 0 || bn == 32 || bn == 64 || bn == 128, "tune: gemm_sf bn must be 0, 32, 64, 128");
+  TAO_CHECK_ARG(bn == 0 || bn == 32 || bn == 64 || bn == 128 || bn == 256,
+                "tune: gemm_sf bn must be 0, 32, 64, 128, 256");
   TAO_CHECK_ARG(wm == 0 || wm == 1 || wm == 2 || wm == 4 || wm == 8,
                 "tune: gemm_sf wm must be 0, 1 (int4: the 32x32x16 kernel), 2, 4 or 8");
   TAO_CHECK_ARG(splits >= 0 && splits <= 16, "tune: gemm_sf splits must be in [0, 16]");
