@@ -742,7 +742,8 @@ int sf_dispatch_wm(const SfShape& sh, hipStream_t st, const uint8_t* x, const P&
 
 // Routed shapes (64 < M <= 128, one 128-row M tile), from the sweep against the incumbent
 // MFMA GEMM on the same box (experiments/sweep_sf.py, profiles/r4_sf_sweep_cnt_stride.jsonl; us,
-// incumbent -> single-fetch): int8 dyn 6144x4096 15.0 -> 12.8, 28672x4096 38.4 -> 34.3,
+// incumbent -> single-fetch): int8 dyn 6144x4096 15.0 -> 12.8, 28672x4096 37.6 -> 31.1 (256-column
+// tiles, r4_sf_sweep_bn256.jsonl),
 // 4096x14336 23.6 -> 20.4; int4 4096^2 14.6 -> 14.0, 6144x4096 21.6 -> 19.4, 28672x4096
 // 59.9 -> 50.0 (the 32x32x16 kernel, one wave along M), 4096x14336 32.6 -> 31.6. Config 3
 // (int8 dyn 4096^2: 10.4 vs 10.6) and every M <= 64 stay on the incumbent.
@@ -753,7 +754,7 @@ struct SfRoute {
 };
 constexpr SfRoute kSfRoutes[] = {
     {2, 6144, 4096, {64, 4, 2, 3, 0, 0}, 256},
-    {2, 28672, 4096, {64, 4, 1, 3, 0, 0}, 128},
+    {2, 28672, 4096, {256, 4, 2, 3, 0, 1}, 128},
     {2, 4096, 14336, {64, 4, 4, 4, 0, 1}, 128},
     {0, 4096, 4096, {64, 2, 4, 2, 0, 0}, 0},
     {0, 6144, 4096, {64, 2, 4, 2, 0, 0}, 0},
