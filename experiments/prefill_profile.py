@@ -1,7 +1,7 @@
 """Where the config-4 prefill (Llama-3-8B int4wo-32, 128-token prompt) spends its time: one eager
 prefill after warm-up under torch.profiler, GPU kernel time summed per kernel name (top 25).
 
-    PYTHONPATH=torchao-fork_amd python experiments/prefill_profile.py
+    PYTHONPATH=torchao-fork_amd python experiments/prefill_profile.py [--no_fuse_w13]
 """
 import json
 
@@ -19,6 +19,8 @@ def main():
         kernels.PREFILL_ATTN = True
     dev = torch.device("cuda")
     model = build_model("Llama-3-8B", dev, seed=0)
+    if "--no_fuse_w13" not in sys.argv:  # generate.py's default layout
+        model.fuse_w13()
     apply_quantization(model, "int4wo-32")
     P, T = 128, 200
     model.setup_caches(1, P + T)
