@@ -105,7 +105,9 @@ def main():
                  (128, 1, 2, 3, 0), (128, 1, 1, 3, 0), (64, 1, 4, 2, 0), (64, 1, 2, 3, 0),
                  (64, 1, 8, 2, 0), (128, 1, 8, 3, 0),
                  (256, 2, 2, 2, 0), (256, 2, 2, 3, 0), (256, 2, 1, 3, 0), (256, 4, 2, 2, 0),
-                 (256, 2, 4, 2, 0), (256, 4, 4, 3, 0), (256, 2, 8, 2, 0)],
+                 (256, 2, 4, 2, 0), (256, 4, 4, 3, 0), (256, 2, 8, 2, 0),
+                 (128, 1, 1, 3, 0, 2), (128, 1, 1, 2, 0, 2), (128, 1, 2, 3, 0, 2),
+                 (128, 1, 4, 2, 0, 2), (128, 1, 4, 3, 0, 2), (128, 1, 8, 2, 0, 2)],
     }
     for path in args.paths.split(","):
         for (M, N, K) in shapes:

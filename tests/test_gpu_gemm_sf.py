@@ -406,3 +406,29 @@ def test_sf_bn256(sf, cfg8, cfg4, M, N, K):
             y = torch.ops.torchao.int4_weight_only_linear(x.to(DEV), packed, sz, g, None).cpu()
             assert oracle.rel_l2(y, oracle.int4_linear_fp32(x, q, s, z, g)) < TOL_FP32
             assert oracle.rel_l2(y, oracle.int4_linear(x, q, s, z, g)) < TOL_REF
+
+
+@pytest.mark.parametrize("cfg", [(128, 1, 1, 3, 0, 2), (128, 1, 4, 2, 0, 2), (128, 1, 2, 3, 0, 2),
+                                 (128, 1, 8, 2, 3, 2)])
+@pytest.mark.parametrize("M,N,K", [(128, 4096, 4096), (100, 640, 3072), (200, 384, 2048),
+                                   (128, 28672, 4096)])
+def test_sf32_k_halves(sf, cfg, M, N, K):
+    """The 32x32x16 int4 kernel with two waves per column group splitting each step's k (summed
+    through LDS in k-half order): within the bars at g = 32 and 128, run-to-run identical, and its
+    SwiGLU epilogue bit-identical to the linear + silu_mul on the same shape."""
+    from torchao._models.llama import kernels
+
+    sf(2, *cfg)
+    for g in (32, 128):
+        q, s, z, packed, sz = _int4(N, K, g, seed=N + g)
+        x = oracle.make_activation(M, K, seed=g)
+        xd = x.to(DEV)
+        y = torch.ops.torchao.int4_weight_only_linear(xd, packed, sz, g, None)
+        assert torch.equal(y, torch.ops.torchao.int4_weight_only_linear(xd, packed, sz, g, None))
+        if N <= 4096:
+            yc = y.cpu()
+            assert oracle.rel_l2(yc, oracle.int4_linear_fp32(x, q, s, z, g)) < TOL_FP32
+            assert oracle.rel_l2(yc, oracle.int4_linear(x, q, s, z, g)) < TOL_REF
+        if M <= 128:
+            sw = kernels.int4_linear_swiglu(xd, packed, sz, g)
+            assert sw is not None and torch.equal(sw, kernels.silu_mul(y))

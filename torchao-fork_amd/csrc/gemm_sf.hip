@@ -686,7 +686,8 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
 // ---- launch ------------------------------------------------------------------------------------
 struct SfShape {
   int bn, wm, splits, stages, a_steps;
-  int seam;  // 0 fixed reducer, 1 spread (see the kernel)
+  int seam;    // 0 fixed reducer, 1 spread (see the kernel)
+  int kh = 1;  // the 32x32x16 int4 kernel (wm 1): k halves per column group, 1 or 2
 };
 
 template <class P, int BN, int WM, int NS>
@@ -780,6 +781,8 @@ static SfShape sf_shape(int path, int M, int N, int K, int* ks_out = nullptr) {
   SfShape sh{path == 0 ? 64 : 32, path == 0 ? 2 : 4, 1, 3, 0, 0};
   if (r) sh = r->sh;
   if (ks_out) *ks_out = t.sf_ks ? t.sf_ks : (r && r->ks ? r->ks : 256);
+  // int4 (path 0): the route's / tune's ks field is the 32x32x16 kernel's k halves (1, 2)
+  if (path == 0) sh.kh = t.sf_ks == 2 ? 2 : t.sf_ks == 1 ? 1 : (r && r->ks == 2 ? 2 : 1);
   if (t.sf_bn) sh.bn = t.sf_bn;
   if (t.sf_wm) sh.wm = t.sf_wm;
   if (t.sf_stages) sh.stages = t.sf_stages;
@@ -850,7 +853,7 @@ int sf_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const uin
 
 int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
               const uint16_t* bias, uint16_t* y, int M, int N, int K, int bn, int splits,
-              int stages, int a_steps, hipStream_t stream, int epi);
+              int stages, int a_steps, hipStream_t stream, int epi, int kh);
 
 // ep.kind 1: y [M][N / 2] = SwiGLU of the interleaved (gate, up) output pairs; 2: RoPE + KV
 // write (y unused). Both need bias == nullptr.
@@ -862,7 +865,7 @@ int sf_int4_epi(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, i
     if (ep.kind == 2)
       return set_error(TAO_ERR_UNSUPPORTED, "gemm_sf: no RoPE epilogue on the 32x32x16 kernel");
     return sf32_int4(x, packed, sz, lg, bias, y, M, N, K, sh.bn, sh.splits, sh.stages,
-                     tuning().sf_a_steps, stream, ep.kind);
+                     tuning().sf_a_steps, stream, ep.kind, sh.kh);
   }
   const dim3 grid((N + sh.bn - 1) / sh.bn, 1, (M + kBM - 1) / kBM);  // tiles: grid.x grid.z
   f32x4_t* slab = nullptr;
@@ -973,7 +976,8 @@ extern "C" int tao_int4wo_linear_rope_kv_bf16(const uint16_t* x, const uint32_t*
 
 // Single-fetch prefill GEMM routing and launch shape (calling thread only; for A/B measurement):
 // mode 0 = built-in routing, 1 = never, 2 = whenever the shape is supported (M <= 128 per launch
-// tile); bn / wm / splits / stages / a_steps 0 = built-in; ks = int8 k step 128 or 256 (0 = 256).
+// tile); bn / wm / splits / stages / a_steps 0 = built-in; ks = int8 k step 128 or 256 (0 = 256),
+// or for int4 with wm 1 (the 32x32x16 kernel) the k halves per column group, 1 or 2.
 extern "C" int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages, int a_steps,
                                 int ks) {
   TAO_CHECK_ARG(mode >= 0 && mode <= 2, "tune: gemm_sf mode must be 0, 1 or 2");
@@ -984,7 +988,8 @@ extern "C" int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages
   TAO_CHECK_ARG(splits >= 0 && splits <= 16, "tune: gemm_sf splits must be in [0, 16]");
   TAO_CHECK_ARG(stages == 0 || (stages >= 2 && stages <= 4), "tune: gemm_sf stages must be 0, 2, 3, 4");
   TAO_CHECK_ARG(a_steps >= 0, "tune: gemm_sf a_steps must be >= 0");
-  TAO_CHECK_ARG(ks == 0 || ks == 128 || ks == 256, "tune: gemm_sf ks must be 0, 128 or 256");
+  TAO_CHECK_ARG(ks == 0 || ks == 1 || ks == 2 || ks == 128 || ks == 256,
+                "tune: gemm_sf ks must be 0, 128 or 256 (int8 k step) or 1, 2 (int4 wm 1: k halves)");
   tao::Tuning& t = tao::tuning();
   t.gemm_sf = mode;
   t.sf_bn = bn;

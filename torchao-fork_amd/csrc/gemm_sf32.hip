@@ -80,24 +80,30 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
   }
 }
 
-template <int WV, int NS>
-__global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
+// KH = 2: two waves per column group split each step's k (k half kh: MFMA sub-steps 4 kh ..
+// 4 kh + 3, one (scale, zero) group pair), so 2 waves share each SIMD and one's MFMAs and
+// dequantisation cover the other's LDS waits; the halves' accumulators are summed through LDS
+// (in kh order) after the k loop. Same LDS bytes read per step, same dequantisation work.
+template <int WV, int NS, int KH = 1>
+__global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
     const uint16_t* __restrict__ x, const uint32_t* __restrict__ wq, const uint32_t* __restrict__ sz,
     int lg, const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K,
     int a_steps, f32x16_t* __restrict__ slab, unsigned* __restrict__ cnt, int fenced, int cs,
     int epi) {
   constexpr int BN = 32 * WV;
+  constexpr int NW = WV * KH;  // waves
   constexpr int XB = kBM * kXRow, WB = BN * kWRow, ZB = BN * kZRow;
   constexpr int STAGE = XB + WB + ZB;
   constexpr int PX = XB / 1024, PW = WB / 1024, PZ = ZB / 256;
   constexpr int T = PX + PW + PZ;
-  static_assert(T % WV == 0 && PX % WV == 0 && (PW + PZ) % WV == 0, "DMA pieces per wave");
-  constexpr int R = T / WV;
+  static_assert(T % NW == 0 && PX % NW == 0 && (PW + PZ) % NW == 0, "DMA pieces per wave");
+  constexpr int R = T / NW;
   static_assert(NS * STAGE <= 160 * 1024 && kBM * BN * 2 <= NS * STAGE, "LDS");
   __shared__ uint4 lds[NS * STAGE / 16];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cw = wave % WV, kh = wave / WV;  // column group, k half
   const int r32 = lane & 31, h = lane >> 5;
   const int n_blk = blockIdx.x * BN, m_blk = blockIdx.z * kBM;
   const int S = gridDim.y, z = blockIdx.y;
@@ -114,15 +120,15 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
   int dd[R], dk[R];
   sfor<0, R>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
-    if constexpr (r < PX / WV) {  // x: 4 rows x 256 B
-      const int i = r * WV + wave;
+    if constexpr (r < PX / NW) {  // x: 4 rows x 256 B
+      const int i = r * NW + wave;
       const int row = 4 * i + (lane >> 4), p = lane & 15;
       const int gm = m_blk + row < M ? m_blk + row : M - 1;
       dv[r] = (uint32_t)gm * row_bytes + 16u * (uint32_t)xpos(row, p);
       dd[r] = i * 1024;
       dk[r] = 0;
     } else {
-      const int i = (r - PX / WV) * WV + wave;
+      const int i = (r - PX / NW) * NW + wave;
       const int row = 16 * (i < PW ? i : i - PW) + (lane >> 2), p = lane & 3;
       const int gn = n_blk + row < N ? n_blk + row : N - 1;
       if (i < PW) {  // W: 16 rows x 64 B
@@ -141,7 +147,7 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
     uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * STAGE;
     sfor<0, R>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
-      if constexpr (r < PX / WV) {
+      if constexpr (r < PX / NW) {
         dma_lds<16>(xrs, dv[r], (uint32_t)st * kXRow, base + dd[r]);
       } else {
         if (dk[r] == 1) dma_lds<16, kNT>(wrs, dv[r], (uint32_t)st * 64u, base + dd[r]);
@@ -151,7 +157,7 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
   };
 
   // bias of this lane's column (unconditional load: see gemm_sf.hip)
-  const int ncol = n_blk + 32 * wave + r32;
+  const int ncol = n_blk + 32 * cw + r32;
   const uint16_t* bsrc = bias != nullptr ? bias : reinterpret_cast<const uint16_t*>(sz);
   const float bsf = bf16_to_f32(bsrc[ncol < N ? ncol : N - 1]);
 
@@ -161,36 +167,47 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
 
-  const int wrow = 32 * wave + r32;  // this lane's W row in the images
+  const int wrow = 32 * cw + r32;  // this lane's W row in the images
   auto compute = [&](int buf) __attribute__((always_inline)) {
     const uint4* img = lds + buf * (STAGE / 16);
-    const uint4 b0 = img[XB / 16 + wrow * 4 + wpos(wrow, 2 * h)];
-    const uint4 b1 = img[XB / 16 + wrow * 4 + wpos(wrow, 2 * h + 1)];
-    const uint32_t* zi = reinterpret_cast<const uint32_t*>(img) + (XB + WB) / 4 + wrow * 4;
-    const uint32_t z0 = zi[zpos(wrow, 2 * h)], z1 = zi[zpos(wrow, 2 * h + 1)];
-    const float s0f = bf16lo_to_f32(z0), s1f = bf16lo_to_f32(z1);
-    const float c0 = bf16hi_to_f32(z0) - 8.f * s0f, c1 = bf16hi_to_f32(z1) - 8.f * s1f;
-    const uint32_t wd[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    constexpr int KS = 8 / KH;  // MFMA k sub-steps of this wave
+    const int ks0 = KH == 2 ? 4 * kh : 0;
+    uint32_t wd[8];
+    float sf[2], cf[2];
+#pragma unroll
+    for (int u = 0; u < 2 / KH; ++u) {  // the nibble granules / (scale, zero) words this wave uses
+      const int gi = KH == 2 ? kh : u;
+      const uint4 b = img[XB / 16 + wrow * 4 + wpos(wrow, 2 * h + gi)];
+      wd[4 * u] = b.x;
+      wd[4 * u + 1] = b.y;
+      wd[4 * u + 2] = b.z;
+      wd[4 * u + 3] = b.w;
+      const uint32_t zw =
+          reinterpret_cast<const uint32_t*>(img)[(XB + WB) / 4 + wrow * 4 + zpos(wrow, 2 * h + gi)];
+      sf[u] = bf16lo_to_f32(zw);
+      cf[u] = bf16hi_to_f32(zw) - 8.f * sf[u];
+    }
     // A fragments of ks and ks + 1 in flight while ks's MFMAs run
     bf16x8_t af[2][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const int m = 32 * mt + r32;
-      af[0][mt] = __builtin_bit_cast(bf16x8_t, img[m * 16 + xpos(m, 8 * h)]);
+      af[0][mt] = __builtin_bit_cast(bf16x8_t, img[m * 16 + xpos(m, 8 * h + ks0)]);
     }
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      if (ks + 1 < 8) {
+    for (int k = 0; k < KS; ++k) {
+      if (k + 1 < KS) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
           const int m = 32 * mt + r32;
-          af[(ks + 1) & 1][mt] = __builtin_bit_cast(bf16x8_t, img[m * 16 + xpos(m, 8 * h + ks + 1)]);
+          af[(k + 1) & 1][mt] =
+              __builtin_bit_cast(bf16x8_t, img[m * 16 + xpos(m, 8 * h + ks0 + k + 1)]);
         }
       }
-      const bf16x8_t bf = ks < 4 ? deq8s(wd[ks], s0f, c0) : deq8s(wd[ks], s1f, c1);
+      const bf16x8_t bf = deq8s(wd[k], sf[k >> 2], cf[k >> 2]);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
-        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][mt], bf, acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[k & 1][mt], bf, acc[mt], 0, 0, 0);
     }
   };
 
@@ -205,15 +222,42 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
     compute(j % NS);
   }
   barrier_lgkm();
+  if constexpr (KH == 2) {  // k half 1's accumulators into k half 0's, through LDS
+    uint4* red = lds + (cw * 4 * 64 + lane) * 4;  // [cw][t][lane][16 floats]
+    if (kh == 1) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          red[t * 64 * 4 + q] = make_uint4(__float_as_uint(acc[t][4 * q]), __float_as_uint(acc[t][4 * q + 1]),
+                                           __float_as_uint(acc[t][4 * q + 2]), __float_as_uint(acc[t][4 * q + 3]));
+    }
+    __syncthreads();
+    if (kh == 0) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint4 v = red[t * 64 * 4 + q];
+          acc[t][4 * q] += __uint_as_float(v.x);
+          acc[t][4 * q + 1] += __uint_as_float(v.y);
+          acc[t][4 * q + 2] += __uint_as_float(v.z);
+          acc[t][4 * q + 3] += __uint_as_float(v.w);
+        }
+    }
+    __syncthreads();
+  }
+  const bool lead = kh == 0;  // the waves holding the summed tile
 
   if (S > 1) {
     constexpr uint32_t kSlice = kBM * BN * 4;
     const unsigned tile = blockIdx.z * gridDim.x + blockIdx.x;
     const Rsrc srs = make_rsrc(reinterpret_cast<const uint8_t*>(slab) + (size_t)tile * (S - 1) * kSlice,
                                (uint32_t)(S - 1) * kSlice);
-    const uint32_t lo = (uint32_t)((wave * 4 * 64 + lane) * 64);  // 4 x 64 B per lane
+    const uint32_t lo = (uint32_t)((cw * 4 * 64 + lane) * 64);  // 4 x 64 B per lane
     unsigned* word = reinterpret_cast<unsigned*>(lds);
     if (!reducer) {
+      if (lead)
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -257,7 +301,7 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) sum[t][i] = 0.f;
-    for (int zz = 0; zz < S - 1; ++zz) {
+    for (int zz = 0; zz < (lead ? S - 1 : 0); ++zz) {
       uint4 part[4][4];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -282,6 +326,7 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
   // epilogue: bf16 tile [128][BN] through LDS, rows out in 16-B pieces. C map (32x32x16): column
   // lane & 31, row (i & 3) + 8 (i >> 2) + 4 h of accumulator tile t (rows 32 t ..)
   uint16_t* out = reinterpret_cast<uint16_t*>(lds);
+  if (lead)
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -289,14 +334,14 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
       const int r = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
       float v = round_bf16(acc[t][i]);
       if (bias != nullptr) v = round_bf16(v + bsf);
-      out[r * BN + 32 * wave + r32] = f32_to_bf16(v);
+      out[r * BN + 32 * cw + r32] = f32_to_bf16(v);
     }
   __syncthreads();
   if (epi == 1) {  // SwiGLU over interleaved (gate, up) columns: y [M][N / 2]
     constexpr int OPR = BN / 16;
     const int N2 = N >> 1;
     const bool full2 = n_blk + BN <= N && (N2 & 7) == 0 && ((uintptr_t)y & 15) == 0;
-    for (int c = tid; c < kBM * OPR; c += WV * 64) {
+    for (int c = tid; c < kBM * OPR; c += NW * 64) {
       const int r = c / OPR, cc = c % OPR;
       const int m = m_blk + r;
       if (m >= M) continue;
@@ -315,7 +360,7 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
   }
   constexpr int CPR = BN / 8;
   const bool full = n_blk + BN <= N && (N & 7) == 0 && ((uintptr_t)y & 15) == 0;
-  for (int c = tid; c < kBM * CPR; c += WV * 64) {
+  for (int c = tid; c < kBM * CPR; c += NW * 64) {
     const int r = c / CPR, cc = c % CPR;
     const int m = m_blk + r;
     if (m >= M) continue;
@@ -335,7 +380,7 @@ __global__ __launch_bounds__(WV * 64) void gemm_sf32_int4_kernel(
 // bn 64 (2 waves) or 128 (4 waves); splits S; stages 2-3; a_steps = 128-k steps per publisher
 int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
               const uint16_t* bias, uint16_t* y, int M, int N, int K, int bn, int splits,
-              int stages, int a_steps, hipStream_t stream, int epi) {
+              int stages, int a_steps, hipStream_t stream, int epi, int kh) {
   const int nsteps = K / 128;
   if (splits > nsteps) splits = nsteps;
   if (splits < 1) splits = 1;
@@ -356,7 +401,10 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
     launch(kern, grid, dim3(threads), 0, stream, x, packed, reinterpret_cast<const uint32_t*>(sz),
            lg, bias, y, M, N, K, a_steps, slab, cnt, fenced, tuning().cnt_stride, epi);
   };
-  if (bn == 128) {
+  if (bn == 128 && kh == 2) {
+    if (stages == 2) go(gemm_sf32_int4_kernel<4, 2, 2>, 512);
+    else go(gemm_sf32_int4_kernel<4, 3, 2>, 512);
+  } else if (bn == 128) {
     if (stages == 2) go(gemm_sf32_int4_kernel<4, 2>, 256);
     else go(gemm_sf32_int4_kernel<4, 3>, 256);
   } else if (bn == 64) {
