@@ -38,7 +38,7 @@ def main():
             continue
         path, M, N, K = cfg.split("_")
         M, N, K = int(M), int(N), int(K)
-        path = {"sfint8": "int8dyn", "sfint4": "int4"}.get(path, path)  # single-fetch shapes
+        path = "int8dyn" if path.startswith("sfint8") else "int4" if path.startswith("sfint4") else path
         vals = collections.defaultdict(list)
         for f in glob.glob(os.path.join(d, "p*", "*_counter_collection.csv")):
             for r in csv.DictReader(open(f)):

@@ -8,8 +8,8 @@ OUT=$R/$1
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-run() {  # tag path sfcfg
-  local tag=$1 path=$2 sf=$3
+run() {  # tag path sfcfg [N]
+  local tag=$1 path=$2 sf=$3 n=${4:-4096}
   mkdir -p "$OUT/$tag"
   local envs=""
   [ "$sf" != "-" ] && envs="PROF_SF=$sf"
@@ -21,12 +21,16 @@ run() {  # tag path sfcfg
       4) pmc="GRBM_GUI_ACTIVE GRBM_COUNT TA_BUSY_avr TCP_TCC_READ_REQ_sum" ;;
     esac
     env $envs timeout -k 10 120 rocprofv3 -d "$OUT/$tag/p$pass" -o p$pass --output-format csv \
-      --pmc $pmc -- python3 "$R/experiments/prof_gemm.py" $path 128 4096 4096 0 0 0 20 \
+      --pmc $pmc -- python3 "$R/experiments/prof_gemm.py" $path 128 $n 4096 0 0 0 20 \
       > "$OUT/$tag/p$pass.log" 2>&1
   done
 }
-run int8dyn_128_4096_4096 int8dyn -
-run int4_128_4096_4096 int4 -
-run sfint8_128_4096_4096 int8dyn "2,64,4,4,3,0,128"
-run sfint4_128_4096_4096 int4 "2,64,2,4,2,0,0"
+if [ -n "$PMC_SF_SET" ]; then
+  eval "$PMC_SF_SET"
+else
+  run int8dyn_128_4096_4096 int8dyn -
+  run int4_128_4096_4096 int4 -
+  run sfint8_128_4096_4096 int8dyn "2,64,4,4,3,0,128"
+  run sfint4_128_4096_4096 int4 "2,64,2,4,2,0,0"
+fi
 echo done > "$OUT/ok"
