@@ -189,11 +189,12 @@ __device__ __forceinline__ bf16x8_t deq8(uint32_t w, float sc, float zc) {
   const f32x2_t q15 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(lo, 512.f, true);
   const f32x2_t q26 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, false);
   const f32x2_t q37 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, true);
-  const f32x2_t sv = {sc, sc}, zv = {zc, zc};
-  const f32x2_t w04 = q04 * sv + zv, w15 = q15 * sv + zv;
-  const f32x2_t w26 = q26 * sv + zv, w37 = q37 * sv + zv;
-  const u32x4_t v = {pk_bf16(w04[0], w15[0]), pk_bf16(w26[0], w37[0]), pk_bf16(w04[1], w15[1]),
-                     pk_bf16(w26[1], w37[1])};
+  // scalar fmas (the Makefile keeps the SLP vectorizer from pairing them into v_pk_fma_f32)
+  const float w0 = __builtin_fmaf(q04[0], sc, zc), w4 = __builtin_fmaf(q04[1], sc, zc);
+  const float w1 = __builtin_fmaf(q15[0], sc, zc), w5 = __builtin_fmaf(q15[1], sc, zc);
+  const float w2 = __builtin_fmaf(q26[0], sc, zc), w6 = __builtin_fmaf(q26[1], sc, zc);
+  const float w3 = __builtin_fmaf(q37[0], sc, zc), w7 = __builtin_fmaf(q37[1], sc, zc);
+  const u32x4_t v = {pk_bf16(w0, w1), pk_bf16(w2, w3), pk_bf16(w4, w5), pk_bf16(w6, w7)};
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
