@@ -210,7 +210,7 @@ struct Int4WO {
   // in the bytes of w & 0x0F0F0F0F and q2,q6,q3,q7 in those of (w >> 4) & 0x0F0F0F0F. A byte
   // b < 16 read as OCP e4m3 is exactly b / 512 (subnormals for b < 8, exponent 1 above), so
   // one v_cvt_scalef32_pk_f32_fp8 with scale 512 turns two of them into exact fp32 integers;
-  // then two fmas and one v_cvt_pk_bf16_f32 per pair.
+  // then one v_pk_fma_f32 and one v_cvt_pk_bf16_f32 per pair: ~1.9 VALU per weight.
   __device__ __forceinline__ bf16x8_t frag(const Prep& p, int s) const {
     const uint32_t w = p.w[s];
     const float sc = s < 4 ? p.s0 : p.s1, zc = s < 4 ? p.zc0 : p.zc1;
@@ -219,14 +219,11 @@ struct Int4WO {
     const f32x2_t q15 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(lo, 512.f, true);
     const f32x2_t q26 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, false);
     const f32x2_t q37 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, true);
-    // scalar fmas: v_pk_fma_f32 beside MFMAs stalls (MI355X_MICROARCH.md cycle table); the
-    // Makefile builds this file with -fno-slp-vectorize so they are not paired back
-    const float w0 = __builtin_fmaf(q04[0], sc, zc), w4 = __builtin_fmaf(q04[1], sc, zc);
-    const float w1 = __builtin_fmaf(q15[0], sc, zc), w5 = __builtin_fmaf(q15[1], sc, zc);
-    const float w2 = __builtin_fmaf(q26[0], sc, zc), w6 = __builtin_fmaf(q26[1], sc, zc);
-    const float w3 = __builtin_fmaf(q37[0], sc, zc), w7 = __builtin_fmaf(q37[1], sc, zc);
-    return as_bf16x8(pack_bf16x2(w0, w1), pack_bf16x2(w2, w3), pack_bf16x2(w4, w5),
-                     pack_bf16x2(w6, w7));
+    const f32x2_t sv = {sc, sc}, zv = {zc, zc};
+    const f32x2_t w04 = q04 * sv + zv, w15 = q15 * sv + zv;  // v_pk_fma_f32 (contracted)
+    const f32x2_t w26 = q26 * sv + zv, w37 = q37 * sv + zv;
+    return as_bf16x8(pack_bf16x2(w04[0], w15[0]), pack_bf16x2(w26[0], w37[0]),
+                     pack_bf16x2(w04[1], w15[1]), pack_bf16x2(w26[1], w37[1]));
   }
   // MFMA s = 4 h + t takes dword t of chunk 4 h + kq: x slot 4 (4 h + kq) + t
   static __device__ __forceinline__ int slot(int s, int kq) {
@@ -1353,12 +1350,11 @@ __global__ __launch_bounds__(256) void gemm32_int4_kernel(
         const f32x2_t q15 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(lo, 512.f, true);
         const f32x2_t q26 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, false);
         const f32x2_t q37 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(hi, 512.f, true);
-        const float w0 = __builtin_fmaf(q04[0], scl, zcl), w4 = __builtin_fmaf(q04[1], scl, zcl);
-        const float w1 = __builtin_fmaf(q15[0], scl, zcl), w5 = __builtin_fmaf(q15[1], scl, zcl);
-        const float w2 = __builtin_fmaf(q26[0], scl, zcl), w6 = __builtin_fmaf(q26[1], scl, zcl);
-        const float w3 = __builtin_fmaf(q37[0], scl, zcl), w7 = __builtin_fmaf(q37[1], scl, zcl);
-        const bf16x8_t b = as_bf16x8(pack_bf16x2(w0, w1), pack_bf16x2(w2, w3),
-                                     pack_bf16x2(w4, w5), pack_bf16x2(w6, w7));
+        const f32x2_t sv = {scl, scl}, zvv = {zcl, zcl};
+        const f32x2_t w04 = q04 * sv + zvv, w15 = q15 * sv + zvv;
+        const f32x2_t w26 = q26 * sv + zvv, w37 = q37 * sv + zvv;
+        const bf16x8_t b = as_bf16x8(pack_bf16x2(w04[0], w15[0]), pack_bf16x2(w26[0], w37[0]),
+                                     pack_bf16x2(w04[1], w15[1]), pack_bf16x2(w26[1], w37[1]));
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
           const uint4 a = xb[lds_slot<SLOTS>(32 * t + r, 16 * h + s)];
