@@ -26,6 +26,14 @@
 
 #include "tao_common.h"
 
+// Timing-only variant builds (experiments/sf32_debug.sh; never the shipped library; results
+// wrong): 1 no MFMAs (the B fragment folded into one accumulator lane), 2 no dequantisation (the
+// nibble words reinterpreted as bf16), 3 no LDS-DMA after the prologue (steps reuse stale
+// stages), 4 no A-fragment LDS reads (one read per step reused).
+#ifndef TAO_SF32_DEBUG
+#define TAO_SF32_DEBUG 0
+#endif
+
 namespace tao {
 namespace {
 
@@ -197,7 +205,7 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
     }
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
-      if (k + 1 < KS) {
+      if (k + 1 < KS && TAO_SF32_DEBUG != 4) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
           const int m = 32 * mt + r32;
@@ -205,10 +213,19 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
               __builtin_bit_cast(bf16x8_t, img[m * 16 + xpos(m, 8 * h + ks0 + k + 1)]);
         }
       }
+#if TAO_SF32_DEBUG == 2
+      const bf16x8_t bf = __builtin_bit_cast(bf16x8_t, make_uint4(wd[k], wd[k] ^ 1u, wd[k] ^ 2u, wd[k] ^ 3u));
+#else
       const bf16x8_t bf = deq8s(wd[k], sf[k >> 2], cf[k >> 2]);
+#endif
+#if TAO_SF32_DEBUG == 1
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt][k] += (float)af[k & 1][mt][0] + (float)bf[mt];
+#else
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
         acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[k & 1][mt], bf, acc[mt], 0, 0, 0);
+#endif
     }
   };
 
@@ -219,7 +236,7 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
     const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
     wait_ahead<R>(ahead);
     barrier_lgkm();
-    if (j + NS - 1 < J) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
+    if (j + NS - 1 < J && TAO_SF32_DEBUG != 3) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
     compute(j % NS);
   }
   barrier_lgkm();
