@@ -466,6 +466,30 @@ def test_generate_tile_format_flag_reaches_checkpoint_load(tmp_path):
         main(["--tile_format", "cuda11"])
 
 
+def test_tuning_apply_validates_knobs():
+    """torchao.kernel.tuning.apply (generate.py --tune KNOB=V) rejects unknown knobs and wrong
+    arity before touching the library; the scoped form does the same."""
+    from torchao.kernel import tuning as scoped
+    from torchao.kernel.tuning import apply
+
+    with pytest.raises(ValueError, match="unknown tuning knob"):
+        apply("no_such_knob", 1)
+    with pytest.raises(ValueError, match="takes 7 value"):
+        apply("gemm_sf", 2, 64)
+    with pytest.raises(ValueError, match="unknown tuning knob"):
+        with scoped(bogus=1):
+            pass
+
+
+def test_generate_cli_fusion_flags_parse():
+    """generate.py's A/B flags (--tune, --prefill_swiglu, --prefill_rope) are accepted by the
+    parser; a malformed --tune value fails before any model is built."""
+    from torchao._models.llama.generate import main
+
+    with pytest.raises(ValueError, match="unknown tuning knob"):
+        main(["--tune", "nope=1", "--prefill_swiglu", "0", "--prefill_rope", "0"])
+
+
 def _ref_ckpt_cases():
     return sorted(f[len("ref_ckpt_"):-3] for f in os.listdir(os.path.join(ROOT, "tests", "golden"))
                   if f.startswith("ref_ckpt_") and f.endswith(".pt"))
