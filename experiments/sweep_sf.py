@@ -80,6 +80,7 @@ def main():
     ap.add_argument("--shapes", default="")
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--seams", default="1,0", help="split-K seams to time (1 spread, 0 fixed reducer)")
+    ap.add_argument("--cfgs", default="", help="launch shapes to time, ';'-separated (default: the built-in list)")
     args = ap.parse_args()
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     out = open(args.out, "a")
@@ -109,19 +110,23 @@ def main():
                  (128, 1, 1, 3, 0, 2), (128, 1, 1, 2, 0, 2), (128, 1, 2, 3, 0, 2),
                  (128, 1, 4, 2, 0, 2), (128, 1, 4, 3, 0, 2), (128, 1, 8, 2, 0, 2)],
     }
+    if args.cfgs:
+        own = [tuple(int(v) for v in c.split(",")) for c in args.cfgs.split(";")]
+        cfgs = {p: own for p in cfgs}
+    lib = os.path.basename(os.environ.get("TORCHAO_MI355X_LIB", "shipped"))
     for path in args.paths.split(","):
         for (M, N, K) in shapes:
             run, copies = (int8_case if path == "int8" else int4_case)(M, N, K, gen)
             base = None
-            for cs in (1, 32):  # split-K tickets packed / one 128-B line per tile
+            for cs in ((32,) if args.cfgs else (1, 32)):  # split-K tickets packed / one 128-B line per tile
                 _lib.call("tao_tune_reset")
                 sf(1)
                 _lib.call("tao_tune_cnt_stride", cs)
-                if cs == 1:
+                if base is None:
                     ref = run(0).clone()
                 t = median(timed(run, copies, args.reps))
                 base = t if base is None else base
-                rec = {"path": path, "M": M, "N": N, "K": K, "cfg": "incumbent", "cs": cs,
+                rec = {"lib": lib, "path": path, "M": M, "N": N, "K": K, "cfg": "incumbent", "cs": cs,
                        "us": round(t * 1e3, 2)}
                 print(json.dumps(rec), flush=True)
                 out.write(json.dumps(rec) + "\n")
@@ -139,7 +144,7 @@ def main():
                     else:
                         ok = float((y.float() - ref.float()).norm() / ref.float().norm()) < 2e-3
                     us = median(timed(run, copies, args.reps)) * 1e3
-                    rec = {"path": path, "M": M, "N": N, "K": K, "cfg": list(cfg), "seam": seam,
+                    rec = {"lib": lib, "path": path, "M": M, "N": N, "K": K, "cfg": list(cfg), "seam": seam,
                            "us": round(us, 2), "speedup": round(base * 1e3 / us, 3), "ok": ok}
                 except RuntimeError as e:
                     rec = {"path": path, "M": M, "N": N, "K": K, "cfg": list(cfg), "error": str(e)[:120]}

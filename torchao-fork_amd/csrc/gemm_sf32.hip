@@ -33,6 +33,10 @@
 #ifndef TAO_SF32_DEBUG
 #define TAO_SF32_DEBUG 0
 #endif
+// 1: each step's DMA pieces issued between its MFMA k sub-steps (0: all after the step's barrier)
+#ifndef TAO_SF32_IL
+#define TAO_SF32_IL 0
+#endif
 
 namespace tao {
 namespace {
@@ -101,6 +105,7 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
     int epi) {
   constexpr int BN = 32 * WV;
   constexpr int NW = WV * KH;  // waves
+  constexpr bool IL = TAO_SF32_IL != 0;
   constexpr int XB = kBM * kXRow, WB = BN * kWRow, ZB = BN * kZRow;
   constexpr int STAGE = XB + WB + ZB;
   constexpr int PX = XB / 1024, PW = WB / 1024, PZ = ZB / 256;
@@ -152,17 +157,18 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
       }
     }
   });
-  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+  auto issue_piece = [&](auto rc, int st, int buf) __attribute__((always_inline)) {
+    constexpr int r = decltype(rc)::value;
     uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * STAGE;
-    sfor<0, R>([&](auto rc) {
-      constexpr int r = decltype(rc)::value;
-      if constexpr (r < PX / NW) {
-        dma_lds<16>(xrs, dv[r], (uint32_t)st * kXRow, base + dd[r]);
-      } else {
-        if (dk[r] == 1) dma_lds<16, kNT>(wrs, dv[r], (uint32_t)st * 64u, base + dd[r]);
-        else dma_lds<4, kNT>(zrs, dv[r], (uint32_t)(((128 * st) >> lg) * 4), base + dd[r]);
-      }
-    });
+    if constexpr (r < PX / NW) {
+      dma_lds<16>(xrs, dv[r], (uint32_t)st * kXRow, base + dd[r]);
+    } else {
+      if (dk[r] == 1) dma_lds<16, kNT>(wrs, dv[r], (uint32_t)st * 64u, base + dd[r]);
+      else dma_lds<4, kNT>(zrs, dv[r], (uint32_t)(((128 * st) >> lg) * 4), base + dd[r]);
+    }
+  };
+  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+    sfor<0, R>([&](auto rc) { issue_piece(rc, st, buf); });
   };
 
   // bias of this lane's column (unconditional load: see gemm_sf.hip)
@@ -177,7 +183,11 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
 
   const int wrow = 32 * cw + r32;  // this lane's W row in the images
-  auto compute = [&](int buf) __attribute__((always_inline)) {
+  // compute(buf, iss, st, ibuf): one step's MFMAs from stage buf; with IL and iss, stage st's
+  // DMA pieces into ibuf are issued between its k sub-steps (not all ahead of the MFMAs)
+  auto compute = [&](int buf, auto iss, int st, int ibuf) __attribute__((always_inline)) {
+    constexpr bool ISS = decltype(iss)::value;
+    if constexpr (ISS && !IL) issue(st, ibuf);
     const uint4* img = lds + buf * (STAGE / 16);
     constexpr int KS = 8 / KH;  // MFMA k sub-steps of this wave
     const int ks0 = KH == 2 ? 4 * kh : 0;
@@ -203,8 +213,8 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
       const int m = 32 * mt + r32;
       af[0][mt] = __builtin_bit_cast(bf16x8_t, img[m * 16 + xpos(m, 8 * h + ks0)]);
     }
-#pragma unroll
-    for (int k = 0; k < KS; ++k) {
+    sfor<0, KS>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
       if (k + 1 < KS && TAO_SF32_DEBUG != 4) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
@@ -226,18 +236,29 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
       for (int mt = 0; mt < 4; ++mt)
         acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[k & 1][mt], bf, acc[mt], 0, 0, 0);
 #endif
-    }
+      if constexpr (ISS && IL)  // DMA pieces r with r KS / R == k after sub-step k's MFMAs
+        sfor<0, R>([&](auto rc) {
+          constexpr int r = decltype(rc)::value;
+          if constexpr (r * KS / R == k) issue_piece(rc, st, ibuf);
+        });
+    });
   };
 
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < J) issue(s0 + p, p);
-  for (int j = 0; j < J; ++j) {
+  const int jiss = TAO_SF32_DEBUG == 3 ? 0 : J - (NS - 1);  // steps that issue a stage ahead
+  int j = 0;
+  for (; j < jiss; ++j) {
+    wait_ahead<R>(NS - 2);
+    barrier_lgkm();
+    compute(j % NS, std::true_type{}, s0 + j + NS - 1, (j + NS - 1) % NS);
+  }
+  for (; j < J; ++j) {
     const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
     wait_ahead<R>(ahead);
     barrier_lgkm();
-    if (j + NS - 1 < J && TAO_SF32_DEBUG != 3) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
-    compute(j % NS);
+    compute(j % NS, std::false_type{}, 0, 0);
   }
   barrier_lgkm();
   if constexpr (KH == 2) {  // k half 1's accumulators into k half 0's, through LDS
@@ -395,7 +416,7 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
 
 }  // namespace
 
-// bn 64 (2 waves) or 128 (4 waves); splits S; stages 2-3; a_steps = 128-k steps per publisher
+// bn 64 (2 waves), 128 (4 waves) or 256 (8 waves, 2 per SIMD); splits S; stages 2-3; a_steps = 128-k steps per publisher
 int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
               const uint16_t* bias, uint16_t* y, int M, int N, int K, int bn, int splits,
               int stages, int a_steps, hipStream_t stream, int epi, int kh) {
@@ -419,7 +440,10 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
     launch(kern, grid, dim3(threads), 0, stream, x, packed, reinterpret_cast<const uint32_t*>(sz),
            lg, bias, y, M, N, K, a_steps, slab, cnt, fenced, tuning().cnt_stride, epi);
   };
-  if (bn == 128 && kh == 2) {
+  if (bn == 256) {
+    if (stages == 2) go(gemm_sf32_int4_kernel<8, 2>, 512);
+    else go(gemm_sf32_int4_kernel<8, 3>, 512);
+  } else if (bn == 128 && kh == 2) {
     if (stages == 2) go(gemm_sf32_int4_kernel<4, 2, 2>, 512);
     else go(gemm_sf32_int4_kernel<4, 3, 2>, 512);
   } else if (bn == 128) {
@@ -429,7 +453,7 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
     if (stages == 2) go(gemm_sf32_int4_kernel<2, 2>, 128);
     else go(gemm_sf32_int4_kernel<2, 3>, 128);
   } else {
-    return set_error(TAO_ERR_INVALID_ARGUMENT, "gemm_sf32: bn must be 64 or 128 (got %d)", bn);
+    return set_error(TAO_ERR_INVALID_ARGUMENT, "gemm_sf32: bn must be 64, 128 or 256 (got %d)", bn);
   }
   return check_launch("gemm_sf32_int4_kernel");
 }
