@@ -375,7 +375,8 @@ def test_add_rmsnorm_and_fused_prefill_gpu():
     from torchao._models.llama.generate import apply_quantization
 
     dev = torch.device("cuda")
-    for rows, D in ((1, 4096), (128, 4096), (7, 1024)):
+    # register-resident kernel at 1-4 pieces per thread (ragged 2056), the two-pass one past 8192
+    for rows, D in ((1, 4096), (128, 4096), (7, 1024), (3, 8192), (5, 6144), (2, 2056), (2, 16384)):
         g = torch.Generator(device=dev).manual_seed(rows)
         x = torch.randn(rows, D, device=dev, generator=g).to(torch.bfloat16)
         r = torch.randn(rows, D, device=dev, generator=g).to(torch.bfloat16)
