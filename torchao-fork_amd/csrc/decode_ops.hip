@@ -40,11 +40,6 @@ int sf_decode_status(unsigned* bits);
 int int8gemv_decode_status(unsigned* bits);
 int int8dyn_decode_status(unsigned* bits);
 
-// 1: always the two-pass add + RMSNorm kernel (variant builds for A/B timing)
-#ifndef TAO_ADDNORM_LOOP
-#define TAO_ADDNORM_LOOP 0
-#endif
-
 namespace {
 
 __device__ __forceinline__ float block_sum(float v, float* red) {
@@ -140,71 +135,6 @@ __global__ __launch_bounds__(256) void add_rmsnorm_kernel(
       o[j] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
     }
     yr[i] = make_uint4(o[0], o[1], o[2], o[3]);
-  }
-}
-
-// Register-resident form for dim <= 256 * 8 * NV: each thread keeps its NV 16-B pieces of h from
-// the add to the scaling (one pass over x and r, no second read after the reduction), and the
-// norm weight's pieces are loaded before the reduction. Same arithmetic, same bits.
-template <int NV>
-__global__ __launch_bounds__(256) void add_rmsnorm_reg_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
-    const uint16_t* __restrict__ w, uint16_t* __restrict__ h, uint16_t* __restrict__ y, int D,
-    float eps) {
-  __shared__ float red[4];
-  const size_t row = (size_t)blockIdx.x * D;
-  const uint4* xr = reinterpret_cast<const uint4*>(x + row);
-  const uint4* rr = reinterpret_cast<const uint4*>(res + row);
-  const uint4* wr = reinterpret_cast<const uint4*>(w);
-  uint4* hr = reinterpret_cast<uint4*>(h + row);
-  uint4* yr = reinterpret_cast<uint4*>(y + row);
-  const int nv = D / 8;
-  uint4 a[NV], b[NV], g[NV];
-#pragma unroll
-  for (int u = 0; u < NV; ++u) {
-    const int i = threadIdx.x + 256 * u;
-    if (i < nv) {
-      a[u] = xr[i];
-      b[u] = rr[i];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < NV; ++u) {
-    const int i = threadIdx.x + 256 * u;
-    if (i < nv) g[u] = wr[i];
-  }
-  float ss = 0.f;
-#pragma unroll
-  for (int u = 0; u < NV; ++u) {
-    const int i = threadIdx.x + 256 * u;
-    if (i < nv) {
-      a[u] = make_uint4(add_pair_bf16(a[u].x, b[u].x), add_pair_bf16(a[u].y, b[u].y),
-                        add_pair_bf16(a[u].z, b[u].z), add_pair_bf16(a[u].w, b[u].w));
-      hr[i] = a[u];
-      const uint32_t d[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float lo = bf16lo_to_f32(d[j]), hi = bf16hi_to_f32(d[j]);
-        ss = fmaf(lo, lo, fmaf(hi, hi, ss));
-      }
-    }
-  }
-  const float r = rsqrtf(block_sum(ss, red) / (float)D + eps);
-#pragma unroll
-  for (int u = 0; u < NV; ++u) {
-    const int i = threadIdx.x + 256 * u;
-    if (i < nv) {
-      const uint32_t d[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
-      const uint32_t e[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
-      uint32_t o[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float lo = round_bf16(bf16lo_to_f32(d[j]) * r) * bf16lo_to_f32(e[j]);
-        const float hi = round_bf16(bf16hi_to_f32(d[j]) * r) * bf16hi_to_f32(e[j]);
-        o[j] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
-      }
-      yr[i] = make_uint4(o[0], o[1], o[2], o[3]);
-    }
   }
 }
 
@@ -653,20 +583,9 @@ int tao_add_rmsnorm_bf16(const uint16_t* x, const uint16_t* res, const uint16_t*
   TAO_CHECK_ALIGN(w, 16, "w");
   TAO_CHECK_ALIGN(h, 16, "h");
   TAO_CHECK_ALIGN(y, 16, "y");
-  const dim3 grid((unsigned)rows), blk(256);
-  const hipStream_t st = as_stream(stream);
-  const int nvt = (int)((dim / 8 + 255) / 256);  // 16-B pieces per thread
-  if (TAO_ADDNORM_LOOP || nvt > 4) {
-    launch(add_rmsnorm_kernel, grid, blk, 0, st, x, res, w, h, y, (int)dim, eps);
-    return check_launch("add_rmsnorm_kernel");
-  }
-  switch (nvt) {
-    case 1: launch(add_rmsnorm_reg_kernel<1>, grid, blk, 0, st, x, res, w, h, y, (int)dim, eps); break;
-    case 2: launch(add_rmsnorm_reg_kernel<2>, grid, blk, 0, st, x, res, w, h, y, (int)dim, eps); break;
-    case 3: launch(add_rmsnorm_reg_kernel<3>, grid, blk, 0, st, x, res, w, h, y, (int)dim, eps); break;
-    default: launch(add_rmsnorm_reg_kernel<4>, grid, blk, 0, st, x, res, w, h, y, (int)dim, eps); break;
-  }
-  return check_launch("add_rmsnorm_reg_kernel");
+  launch(add_rmsnorm_kernel, dim3((unsigned)rows), dim3(256), 0, as_stream(stream), x, res, w, h,
+         y, (int)dim, eps);
+  return check_launch("add_rmsnorm_kernel");
 }
 
 int tao_rope_kv_bf16(const uint16_t* qkv, const float* freqs, const int64_t* pos,

@@ -29,13 +29,17 @@
 // Timing-only variant builds (experiments/sf32_debug.sh; never the shipped library; results
 // wrong): 1 no MFMAs (the B fragment folded into one accumulator lane), 2 no dequantisation (the
 // nibble words reinterpreted as bf16), 3 no LDS-DMA after the prologue (steps reuse stale
-// stages), 4 no A-fragment LDS reads (one read per step reused).
+// stages), 4 no A-fragment LDS reads (one read per step reused), 5 x read as if step-major
+// ([K / 128][M][128]: each step's x one contiguous block), 6 / 7 no (scale, zero) / W DMA after
+// the prologue (per-instruction vs per-byte cost of the DMA pieces).
 #ifndef TAO_SF32_DEBUG
 #define TAO_SF32_DEBUG 0
 #endif
-// 1: each step's DMA pieces issued between its MFMA k sub-steps (0: all after the step's barrier)
+// 1: with 3+ stages, each step's DMA pieces are issued between its MFMA k sub-steps (0: all after
+// the step's barrier). 2-5% faster at 3 stages, slower at 2 (the stage is needed one step later):
+// profiles/r4_sf32_il.jsonl
 #ifndef TAO_SF32_IL
-#define TAO_SF32_IL 0
+#define TAO_SF32_IL 1
 #endif
 
 namespace tao {
@@ -105,13 +109,16 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
     int epi) {
   constexpr int BN = 32 * WV;
   constexpr int NW = WV * KH;  // waves
-  constexpr bool IL = TAO_SF32_IL != 0;
+  constexpr bool IL = TAO_SF32_IL != 0 && NS >= 3;
   constexpr int XB = kBM * kXRow, WB = BN * kWRow, ZB = BN * kZRow;
   constexpr int STAGE = XB + WB + ZB;
   constexpr int PX = XB / 1024, PW = WB / 1024, PZ = ZB / 256;
   constexpr int T = PX + PW + PZ;
   static_assert(T % NW == 0 && PX % NW == 0 && (PW + PZ) % NW == 0, "DMA pieces per wave");
   constexpr int R = T / NW;
+  // debug 6 / 7 skip each wave's 2 (scale, zero) / 2 W pieces after the prologue
+  constexpr bool DSK = (TAO_SF32_DEBUG == 6 || TAO_SF32_DEBUG == 7) && PW == 2 * NW && PZ == 2 * NW;
+  constexpr int RW = DSK ? R - 2 : R;
   static_assert(NS * STAGE <= 160 * 1024 && kBM * BN * 2 <= NS * STAGE, "LDS");
   __shared__ uint4 lds[NS * STAGE / 16];
 
@@ -138,7 +145,8 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
       const int i = r * NW + wave;
       const int row = 4 * i + (lane >> 4), p = lane & 15;
       const int gm = m_blk + row < M ? m_blk + row : M - 1;
-      dv[r] = (uint32_t)gm * row_bytes + 16u * (uint32_t)xpos(row, p);
+      dv[r] = (TAO_SF32_DEBUG == 5 ? (uint32_t)gm * kXRow : (uint32_t)gm * row_bytes) +
+              16u * (uint32_t)xpos(row, p);
       dd[r] = i * 1024;
       dk[r] = 0;
     } else {
@@ -161,8 +169,11 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
     constexpr int r = decltype(rc)::value;
     uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * STAGE;
     if constexpr (r < PX / NW) {
-      dma_lds<16>(xrs, dv[r], (uint32_t)st * kXRow, base + dd[r]);
+      dma_lds<16>(xrs, dv[r], (uint32_t)st * (TAO_SF32_DEBUG == 5 ? (uint32_t)M * kXRow : kXRow),
+                  base + dd[r]);
     } else {
+      const bool skip = DSK && ((TAO_SF32_DEBUG == 6 && dk[r] == 2) || (TAO_SF32_DEBUG == 7 && dk[r] == 1));
+      if (skip && st >= s0 + NS - 1) return;
       if (dk[r] == 1) dma_lds<16, kNT>(wrs, dv[r], (uint32_t)st * 64u, base + dd[r]);
       else dma_lds<4, kNT>(zrs, dv[r], (uint32_t)(((128 * st) >> lg) * 4), base + dd[r]);
     }
@@ -250,13 +261,13 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
   const int jiss = TAO_SF32_DEBUG == 3 ? 0 : J - (NS - 1);  // steps that issue a stage ahead
   int j = 0;
   for (; j < jiss; ++j) {
-    wait_ahead<R>(NS - 2);
+    wait_ahead<RW>(NS - 2);
     barrier_lgkm();
     compute(j % NS, std::true_type{}, s0 + j + NS - 1, (j + NS - 1) % NS);
   }
   for (; j < J; ++j) {
     const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
-    wait_ahead<R>(ahead);
+    wait_ahead<RW>(ahead);
     barrier_lgkm();
     compute(j % NS, std::false_type{}, 0, 0);
   }
