@@ -27,6 +27,12 @@
 
 #include "tao_common.h"
 
+// 1: with 3+ stages, each step's DMA pieces are issued between its MFMA groups (after group kb,
+// pieces r with r KB / R == kb) instead of all after the step's barrier (gemm_sf32.hip's IL)
+#ifndef TAO_SF_IL
+#define TAO_SF_IL 0
+#endif
+
 // Experiment switch (timing only, experiments/sf_stamps.py): per-workgroup s_memrealtime stamps
 // (100 MHz): 0 entry, 1 prologue DMAs issued, 2 first stage landed, 3 k loop done, 4 publish or
 // poll done, 5 end; 6 = slice, 7 = 1 for the reducer. Never in the product library.
@@ -213,6 +219,13 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
 // so every tile's reducer (slice S-1) is dispatched after all publishers. seam 1 (spread): slice
 // fastest, so a tile's S workgroups are dispatched together (they wait for one another: the
 // launcher takes this seam only when S divides the 8 waves and the grid's resident set holds S).
+// MFMA groups per step: the int8 k blocks, or the 4 nibble dwords of an int4 step
+template <class P>
+constexpr int mfma_groups() {
+  if constexpr (P::kABytes == 1) return P::kKB;
+  else return 4;
+}
+
 template <class P, int BN, int WM, int NS>
 __global__ __launch_bounds__(512) void gemm_sf_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
@@ -241,6 +254,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   static_assert(XB % 1024 == 0 && WB % 1024 == 0 && ZB % 256 == 0, "DMA pieces");
   static_assert(T % kWaves == 0 && PX % kWaves == 0, "DMA pieces per wave");
   constexpr int R = T / kWaves;  // DMA instructions per wave per stage
+  constexpr bool IL = TAO_SF_IL != 0 && NS >= 3;
   constexpr int NB = NS;  // LDS stage buffers
   static_assert(NB * STAGE <= 160 * 1024, "LDS");
   static_assert(kBM * BN * 2 <= NB * STAGE, "epilogue image");
@@ -299,22 +313,34 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
       }
     }
   });
-  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+  constexpr bool kI8 = P::kABytes == 1;
+  auto issue_piece = [&](auto rc, int st, int buf) __attribute__((always_inline)) {
+    constexpr int r = decltype(rc)::value;
     uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * STAGE;
+    if constexpr (r < PX / kWaves) {
+      dma_lds<16>(xrs, dv[r], (uint32_t)st * P::kXRow, base + dd[r]);
+    } else {
+      if (dk[r] == 1) dma_lds<16, kNT>(wrs, dv[r], pol.wsoff(st), base + dd[r]);
+      else if constexpr (PZ > 0) dma_lds<4, kNT>(zrs, dv[r], pol.zsoff(st), base + dd[r]);
+    }
+  };
+  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+    sfor<0, R>([&](auto rc) { issue_piece(rc, st, buf); });
+  };
+  // pieces r with r KB / R == kb, issued after MFMA group kb (IL)
+  auto issue_group = [&](auto kbc, int st, int buf) __attribute__((always_inline)) {
+    constexpr int kb = decltype(kbc)::value;
+    constexpr int KBN = mfma_groups<P>();
+    __builtin_amdgcn_sched_barrier(0);
     sfor<0, R>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
-      if constexpr (r < PX / kWaves) {
-        dma_lds<16>(xrs, dv[r], (uint32_t)st * P::kXRow, base + dd[r]);
-      } else {
-        if (dk[r] == 1) dma_lds<16, kNT>(wrs, dv[r], pol.wsoff(st), base + dd[r]);
-        else if constexpr (PZ > 0) dma_lds<4, kNT>(zrs, dv[r], pol.zsoff(st), base + dd[r]);
-      }
+      if constexpr (r * KBN / R == kb) issue_piece(rc, st, buf);
     });
+    __builtin_amdgcn_sched_barrier(0);
   };
 
   // ---- epilogue operands, loaded ahead of the stream ---------------------------------------------
   // rows of this lane: wm RM + 16 mt + 4 kq + i; columns: wn CN + 16 nt + fr
-  constexpr bool kI8 = P::kABytes == 1;
   float xsf[kI8 ? MT * 4 : 1];
   float wsf[NT], bsf[NT];
   if constexpr (kI8) {
@@ -349,7 +375,9 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   // Every fragment read of the step is issued before the first MFMA (a sched_barrier keeps
   // hipcc from interleaving them one read per MFMA, which exposed each ds_read's latency: one
   // read in flight per wave, lgkmcnt(1) before every MFMA in the first build's ISA).
-  auto compute = [&](int buf) __attribute__((always_inline)) {
+  auto compute = [&](int buf, auto iss, int st, int ibuf) __attribute__((always_inline)) {
+    constexpr bool ISS = decltype(iss)::value;
+    if constexpr (ISS && !IL) issue(st, ibuf);
     const uint4* img = lds + buf * (STAGE / 16);
     if constexpr (kI8) {
       constexpr int G = P::kXRow / 16;  // granules per image row
@@ -369,14 +397,16 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
         }
       }
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int kb = 0; kb < P::kKB; ++kb)
+      sfor<0, P::kKB>([&](auto kbc) {
+        constexpr int kb = decltype(kbc)::value;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt)
             acc[mt][nt] =
                 __builtin_amdgcn_mfma_i32_16x16x64_i8(af[kb][mt], bf[kb][nt], acc[mt][nt], 0, 0, 0);
+        if constexpr (ISS && IL) issue_group(kbc, st, ibuf);
+      });
     } else {
       uint4 wv[NT];
       uint32_t szw[NT];
@@ -403,8 +433,8 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
         sc[nt] = bf16lo_to_f32(szw[nt]);
         zc[nt] = bf16hi_to_f32(szw[nt]) - 8.f * sc[nt];  // q*s + zc == (q - 8)*s + z
       }
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) {
+      sfor<0, 4>([&](auto kbc) {
+        constexpr int kb = decltype(kbc)::value;
         bf16x8_t bf[NT];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
@@ -417,7 +447,8 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
           for (int nt = 0; nt < NT; ++nt)
             acc[mt][nt] =
                 __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kb][mt], bf[nt], acc[mt][nt], 0, 0, 0);
-      }
+        if constexpr (ISS && IL) issue_group(kbc, st, ibuf);
+      });
     }
   };
 
@@ -428,15 +459,24 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   for (int p = 0; p < NS - 1; ++p)
     if (p < J) issue(s0 + p, p);
   SF_MARK(1);
-  for (int j = 0; j < J; ++j) {
-    const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
-    wait_ahead<R>(ahead);  // this wave's DMAs of step j landed
-    barrier_lgkm();        // ... and every wave's; step j - 1's fragment reads are done
+  const int jiss = J - (NS - 1);  // steps that issue a stage ahead
+  int j = 0;
+  for (; j < jiss; ++j) {
+    wait_ahead<R>(NS - 2);  // this wave's DMAs of step j landed
+    barrier_lgkm();         // ... and every wave's; step j - 1's fragment reads are done
 #if TAO_SF_STAMPS
     if (j == 0) SF_MARK(2);
 #endif
-    if (j + NS - 1 < J) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
-    compute(j % NS);
+    compute(j % NS, std::true_type{}, s0 + j + NS - 1, (j + NS - 1) % NS);
+  }
+  for (; j < J; ++j) {
+    const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
+    wait_ahead<R>(ahead);
+    barrier_lgkm();
+#if TAO_SF_STAMPS
+    if (j == 0) SF_MARK(2);
+#endif
+    compute(j % NS, std::false_type{}, 0, 0);
   }
   barrier_lgkm();  // all fragment reads done: the LDS is free for the epilogue image
   SF_MARK(3);
