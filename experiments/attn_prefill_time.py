@@ -57,7 +57,8 @@ def main():
         r = F.scaled_dot_product_attention(q.float(), kc.float(), vc.float(), attn_mask=mask,
                                            enable_gqa=True).transpose(1, 2).reshape(1, S, H * D)
         err = float((y - r).abs().max())
-        print(json.dumps({"S": S, "T": T, "ours_us": round(ours, 2), "sdpa_us": round(sdpa, 2),
+        print(json.dumps({"lib": os.path.basename(os.environ.get("TORCHAO_MI355X_LIB", "shipped")),
+                          "S": S, "T": T, "ours_us": round(ours, 2), "sdpa_us": round(sdpa, 2),
                           "speedup": round(sdpa / ours, 2), "max_abs_err_vs_fp32": round(err, 5)}),
               flush=True)
         del kc, vc, q, mask
