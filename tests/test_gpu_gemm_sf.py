@@ -92,7 +92,8 @@ def test_sf_int8dyn_extreme_values(sf):
 # wm 1: the 32x32x16 kernel (gemm_sf32.hip), 2 or 4 waves of 128 x 32
 I4_CFGS = [(64, 2, 4, 3, 0), (64, 4, 4, 3, 0), (64, 8, 2, 2, 0), (128, 2, 8, 2, 0),
            (128, 4, 8, 3, 0), (128, 2, 1, 3, 0), (64, 2, 4, 4, 0), (128, 1, 8, 2, 0),
-           (128, 1, 4, 3, 0), (128, 1, 1, 3, 0), (64, 1, 4, 2, 0), (64, 1, 2, 3, 0)]
+           (128, 1, 4, 3, 0), (128, 1, 1, 3, 0), (64, 1, 4, 2, 0), (64, 1, 2, 3, 0),
+           (256, 1, 1, 3, 0), (256, 1, 2, 2, 0)]  # wm 1, bn 256: 8 waves, 2 per SIMD
 I4_SHAPES = [(128, 4096, 4096), (17, 128, 1024), (100, 640, 4096), (128, 512, 14336),
              (200, 192, 2048), (64, 96, 768)]
 
@@ -244,7 +245,8 @@ def test_sf_unsupported_shapes_fall_back(sf):
 
 
 SW_CFGS = [(0, None), (2, (64, 2, 4, 2, 0)), (2, (64, 2, 2, 3, 0)), (2, (128, 2, 8, 2, 0)),
-           (2, (128, 1, 1, 3, 0)), (2, (64, 1, 2, 3, 0)), (2, (128, 1, 4, 2, 0))]
+           (2, (128, 1, 1, 3, 0)), (2, (64, 1, 2, 3, 0)), (2, (128, 1, 4, 2, 0)),
+           (2, (256, 1, 1, 3, 0))]
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 28672, 4096), (100, 1024, 2048), (200, 512, 1024),

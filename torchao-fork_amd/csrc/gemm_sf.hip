@@ -805,14 +805,17 @@ constexpr SfRoute kSfRoutes[] = {
     // Llama-3-70B (profiles/r4_sf_sweep_70b.jsonl; us, incumbent -> single-fetch): int8 dyn
     // 10240x8192 42.6 -> 29.6, 8192^2 27.4 -> 21.6, 57344x8192 145.2 -> 99.2, 8192x28672
     // 68.4 -> 55.8; int4 10240x8192 62.2 -> 48.4, 8192^2 37.8 -> 32.9, 57344x8192 225.9 ->
-    // 178.7, 8192x28672 115.1 -> 90.7 (for int4 with wm 1 the ks field is the k halves)
+    // 178.7, 8192x28672 115.1 -> 90.7 (for int4 with wm 1 the ks field is the k halves);
+    // int4 57344x8192 on 256-column tiles of the 32x32x16 kernel (8 waves, 224 tiles: one per
+    // CU) 171.4 against 213.8 / 195.1 for 128 columns with / without k halves
+    // (profiles/r4_sf32_70b.jsonl)
     {2, 10240, 8192, {256, 2, 4, 3, 0, 1}, 128},
     {2, 8192, 8192, {64, 4, 2, 3, 0, 0}, 256},
     {2, 57344, 8192, {256, 2, 1, 3, 0, 0}, 128},
     {2, 8192, 28672, {64, 4, 2, 3, 0, 1}, 256},
     {0, 10240, 8192, {128, 1, 2, 3, 0, 0}, 2},
     {0, 8192, 8192, {64, 2, 2, 3, 0, 0}, 0},
-    {0, 57344, 8192, {128, 1, 1, 3, 0, 0}, 2},
+    {0, 57344, 8192, {256, 1, 1, 3, 0, 0}, 0},
     {0, 8192, 28672, {128, 2, 4, 3, 0, 1}, 0},
 };
 
