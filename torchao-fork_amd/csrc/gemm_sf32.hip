@@ -38,6 +38,10 @@
 // 1: with 3+ stages, each step's DMA pieces are issued between its MFMA k sub-steps (0: all after
 // the step's barrier). 2-5% faster at 3 stages, slower at 2 (the stage is needed one step later):
 // profiles/r4_sf32_il.jsonl
+// 1: 16-B (scale, zero) DMA pieces at group size 32 (the kernel's Z16; 0 for A/B builds)
+#ifndef TAO_SF32_Z16
+#define TAO_SF32_Z16 1
+#endif
 #ifndef TAO_SF32_IL
 #define TAO_SF32_IL 1
 #endif
@@ -101,7 +105,12 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
 // 4 kh + 3, one (scale, zero) group pair), so 2 waves share each SIMD and one's MFMAs and
 // dequantisation cover the other's LDS waits; the halves' accumulators are summed through LDS
 // (in kh order) after the k loop. Same LDS bytes read per step, same dequantisation work.
-template <int WV, int NS, int KH = 1>
+// Z16 (group size 32): a row's 4 (scale, zero) words of a step are 16 contiguous bytes of the
+// [N][K/32][2] array, so they arrive by 16-B DMA, 64 rows per piece, into an unswizzled
+// [BN][16 B] image read with one ds_read_b128 per lane (conflict-free: 8 lanes per 128 B); other
+// group sizes take the 4-B DMA of a swizzled image. The DMA pieces cost per instruction
+// (profiles/r4_sf32_dmacost.jsonl), and Z16 takes a quarter of them for the (scale, zero) words.
+template <int WV, int NS, int KH = 1, bool Z16 = false>
 __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
     const uint16_t* __restrict__ x, const uint32_t* __restrict__ wq, const uint32_t* __restrict__ sz,
     int lg, const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K,
@@ -112,10 +121,11 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
   constexpr bool IL = TAO_SF32_IL != 0 && NS >= 3;
   constexpr int XB = kBM * kXRow, WB = BN * kWRow, ZB = BN * kZRow;
   constexpr int STAGE = XB + WB + ZB;
-  constexpr int PX = XB / 1024, PW = WB / 1024, PZ = ZB / 256;
+  constexpr int PX = XB / 1024, PW = WB / 1024, PZ = Z16 ? ZB / 1024 : ZB / 256;
   constexpr int T = PX + PW + PZ;
-  static_assert(T % NW == 0 && PX % NW == 0 && (PW + PZ) % NW == 0, "DMA pieces per wave");
-  constexpr int R = T / NW;
+  static_assert(PX % NW == 0 && (!Z16 || ZB % 1024 == 0), "DMA pieces per wave");
+  // piece i = r NW + wave: waves below RFULL issue R pieces per stage, the others R - 1
+  constexpr int R = (T + NW - 1) / NW, RFULL = T - (R - 1) * NW;
   // debug 6 / 7 skip each wave's 2 (scale, zero) / 2 W pieces after the prologue
   constexpr bool DSK = (TAO_SF32_DEBUG == 6 || TAO_SF32_DEBUG == 7) && PW == 2 * NW && PZ == 2 * NW;
   constexpr int RW = DSK ? R - 2 : R;
@@ -157,6 +167,16 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
         dv[r] = (uint32_t)gn * (uint32_t)(K >> 1) + 16u * (uint32_t)wpos(row, p);
         dd[r] = XB + i * 1024;
         dk[r] = 1;
+      } else if (i >= PW + PZ) {  // past the last piece (T not a multiple of NW)
+        dv[r] = 0;
+        dd[r] = 0;
+        dk[r] = 3;
+      } else if constexpr (Z16) {  // (scale, zero): 64 rows x 16 B
+        const int zr = 64 * (i - PW) + lane;
+        const int gz = n_blk + zr < N ? n_blk + zr : N - 1;
+        dv[r] = (uint32_t)gz * (uint32_t)(K >> lg) * 4u;
+        dd[r] = XB + WB + (i - PW) * 1024;
+        dk[r] = 2;
       } else {  // (scale, zero): 16 rows x 4 dwords, 4-B DMA; dword q = group of k 32 q
         const int q = zpos(row, p);
         dv[r] = ((uint32_t)gn * (uint32_t)(K >> lg) + (uint32_t)((32 * q) >> lg)) * 4u;
@@ -175,7 +195,10 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
       const bool skip = DSK && ((TAO_SF32_DEBUG == 6 && dk[r] == 2) || (TAO_SF32_DEBUG == 7 && dk[r] == 1));
       if (skip && st >= s0 + NS - 1) return;
       if (dk[r] == 1) dma_lds<16, kNT>(wrs, dv[r], (uint32_t)st * 64u, base + dd[r]);
-      else dma_lds<4, kNT>(zrs, dv[r], (uint32_t)(((128 * st) >> lg) * 4), base + dd[r]);
+      else if (dk[r] == 2) {
+        if constexpr (Z16) dma_lds<16, kNT>(zrs, dv[r], (uint32_t)st * 16u, base + dd[r]);
+        else dma_lds<4, kNT>(zrs, dv[r], (uint32_t)(((128 * st) >> lg) * 4), base + dd[r]);
+      }
     }
   };
   auto issue = [&](int st, int buf) __attribute__((always_inline)) {
@@ -212,8 +235,13 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
       wd[4 * u + 1] = b.y;
       wd[4 * u + 2] = b.z;
       wd[4 * u + 3] = b.w;
-      const uint32_t zw =
-          reinterpret_cast<const uint32_t*>(img)[(XB + WB) / 4 + wrow * 4 + zpos(wrow, 2 * h + gi)];
+      uint32_t zw;
+      if constexpr (Z16) {
+        const uint4 zq = img[(XB + WB) / 16 + wrow];
+        zw = h == 0 ? (gi == 0 ? zq.x : zq.y) : (gi == 0 ? zq.z : zq.w);
+      } else {
+        zw = reinterpret_cast<const uint32_t*>(img)[(XB + WB) / 4 + wrow * 4 + zpos(wrow, 2 * h + gi)];
+      }
       sf[u] = bf16lo_to_f32(zw);
       cf[u] = bf16hi_to_f32(zw) - 8.f * sf[u];
     }
@@ -255,19 +283,28 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
     });
   };
 
+  // this wave's DMAs of the step landed (its own piece count)
+  auto wait_own = [&](int ahead) __attribute__((always_inline)) {
+    if constexpr (RFULL == NW || DSK) {
+      wait_ahead<RW>(ahead);
+    } else {
+      if (wave < RFULL) wait_ahead<R>(ahead);
+      else wait_ahead<R - 1>(ahead);
+    }
+  };
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < J) issue(s0 + p, p);
   const int jiss = TAO_SF32_DEBUG == 3 ? 0 : J - (NS - 1);  // steps that issue a stage ahead
   int j = 0;
   for (; j < jiss; ++j) {
-    wait_ahead<RW>(NS - 2);
+    wait_own(NS - 2);
     barrier_lgkm();
     compute(j % NS, std::true_type{}, s0 + j + NS - 1, (j + NS - 1) % NS);
   }
   for (; j < J; ++j) {
     const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
-    wait_ahead<RW>(ahead);
+    wait_own(ahead);
     barrier_lgkm();
     compute(j % NS, std::false_type{}, 0, 0);
   }
@@ -447,25 +484,32 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
     slab = reinterpret_cast<f32x16_t*>(w);
   }
   const int fenced = tuning().splitk_fenced;
-  auto go = [&](auto kern, int threads) {
+  auto go1 = [&](auto kern, int threads) {
     launch(kern, grid, dim3(threads), 0, stream, x, packed, reinterpret_cast<const uint32_t*>(sz),
            lg, bias, y, M, N, K, a_steps, slab, cnt, fenced, tuning().cnt_stride, epi);
   };
+  // Z16 at one wave per column group only: with k halves (8 waves, 42 pieces, uneven per wave)
+  // it measured 4% slower, at one wave 2-4% faster (profiles/r4_sf32_z16.jsonl)
+  const bool z16 = lg == 5 && TAO_SF32_Z16 != 0 && kh != 2;
+#define SF32_GO(WV, NS, KH)                                            \
+  (z16 ? go1(gemm_sf32_int4_kernel<WV, NS, KH, true>, WV * KH * 64) \
+       : go1(gemm_sf32_int4_kernel<WV, NS, KH, false>, WV * KH * 64))
   if (bn == 256) {
-    if (stages == 2) go(gemm_sf32_int4_kernel<8, 2>, 512);
-    else go(gemm_sf32_int4_kernel<8, 3>, 512);
+    if (stages == 2) SF32_GO(8, 2, 1);
+    else SF32_GO(8, 3, 1);
   } else if (bn == 128 && kh == 2) {
-    if (stages == 2) go(gemm_sf32_int4_kernel<4, 2, 2>, 512);
-    else go(gemm_sf32_int4_kernel<4, 3, 2>, 512);
+    if (stages == 2) SF32_GO(4, 2, 2);
+    else SF32_GO(4, 3, 2);
   } else if (bn == 128) {
-    if (stages == 2) go(gemm_sf32_int4_kernel<4, 2>, 256);
-    else go(gemm_sf32_int4_kernel<4, 3>, 256);
+    if (stages == 2) SF32_GO(4, 2, 1);
+    else SF32_GO(4, 3, 1);
   } else if (bn == 64) {
-    if (stages == 2) go(gemm_sf32_int4_kernel<2, 2>, 128);
-    else go(gemm_sf32_int4_kernel<2, 3>, 128);
+    if (stages == 2) SF32_GO(2, 2, 1);
+    else SF32_GO(2, 3, 1);
   } else {
     return set_error(TAO_ERR_INVALID_ARGUMENT, "gemm_sf32: bn must be 64, 128 or 256 (got %d)", bn);
   }
+#undef SF32_GO
   return check_launch("gemm_sf32_int4_kernel");
 }
 
