@@ -679,6 +679,9 @@ def test_single_fetch_gemm_lds_images_conflict_free():
         for j in range(2):
             assert _b128_conflict_free(lambda l: (32 * t + (l & 31)) * 64
                                        + 16 * _wpos32(32 * t + (l & 31), 2 * (l >> 5) + j))
+        # Z16 (scale, zero) image, unswizzled [BN][16 B]: lane (r, h) reads its row's 16 B (both h
+        # halves the same granule: a broadcast, not a conflict)
+        assert _b128_conflict_free(lambda l: (32 * t + (l & 31)) * 16)
     for f, n in ((_pos256, 16), (_pos256q, 16), (_pos128, 8), (_pos64, 4), (_wpos32, 4)):
         for r in range(64):
             assert sorted(f(r, g) for g in range(n)) == list(range(n))
