@@ -167,12 +167,14 @@ int tao_tune_int4_mfma32(int on);
 int tao_tune_gemm_tile(int mode, int splits);
 
 /* The single-fetch prefill GEMM (csrc/gemm_sf.hip: 128-row tiles so each weight tile is fetched by
- * one workgroup, 8 waves, both operands by LDS-DMA in full lines, K split over workgroups) for
- * the int4 weight-only and int8 dynamic linears. mode 0 = built-in routing (64 < M <= 128 at
- * the Llama-3-8B shapes where it measured faster than the MFMA GEMMs), 1 = never, 2 = wherever
- * the shape is supported (K % 128 (int4) / 256 (int8) == 0; M <= 128 per 128-row tile). bn (32 / 64 / 128), wm (waves along M: 2 / 4 / 8), splits, stages (2-4),
- * a_steps (K steps of each publishing slice) and ks (int8 k step 128 / 256; int4 with wm 1: 1 or
- * 2 waves per 32-column group, splitting each step's k): 0 = built-in.
+ * one workgroup, 8 waves, both operands by LDS-DMA in full lines, K split over workgroups; for
+ * int4 with wm 1 the 32x32x16 kernel of csrc/gemm_sf32.hip) for the int4 weight-only and int8
+ * dynamic linears. mode 0 = built-in routing (64 < M <= 128 at the Llama-3-8B and -70B shapes
+ * where it measured faster than the MFMA GEMMs), 1 = never, 2 = wherever the shape is supported
+ * (K % 128 (int4) / 256 (int8) == 0; M <= 128 per 128-row tile). bn (32 / 64 / 128 / 256), wm
+ * (waves along M: 2 / 4 / 8; int4: 1 = the 32x32x16 kernel, one wave per 32 columns), splits,
+ * stages (2-4), a_steps (K steps of each publishing slice) and ks (int8 k step 128 / 256; int4
+ * with wm 1: 1 or 2 waves per 32-column group, splitting each step's k): 0 = built-in.
  * Thread-local; for measurement. */
 int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages, int a_steps, int ks);
 /* Single-fetch GEMM split-K seam: -1 = built-in (per routed shape), 1 = spread (each of a tile's
