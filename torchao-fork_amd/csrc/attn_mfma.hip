@@ -76,23 +76,33 @@ __global__ __launch_bounds__(64) void attn_prefill_mfma_kernel(
   float m = -INFINITY, l = 0.f;
 
   const uint8_t* vimg_b = reinterpret_cast<const uint8_t*>(vimg);
+  // K A fragments (rows k0 + 16 t + fr, clamped to the cache) and the V block's 16-B pieces. The
+  // next block's are loaded into the same registers once this block's have been consumed (S^T
+  // MFMAs issued, V stored to LDS), so they arrive under this block's softmax and P V.
+  bf16x8_t kf[2][4];
+#define ATTN_LOAD_K(K0)                                                                       \
+  {                                                                                           \
+    _Pragma("unroll") for (int t = 0; t < 2; ++t) {                                           \
+      const int key = (K0) + 16 * t + fr < T ? (K0) + 16 * t + fr : T - 1;                   \
+      const uint4* kp = reinterpret_cast<const uint4*>(kc + (head + key) * kD) + kq;          \
+      _Pragma("unroll") for (int c = 0; c < 4; ++c) kf[t][c] =                                \
+          __builtin_bit_cast(bf16x8_t, kp[4 * c]);                                            \
+    }                                                                                         \
+  }
+  ATTN_LOAD_K(0)
+  // the V block's 16-B pieces (rows k0 + r, clamped to the cache); ext-vector elements, so a
+  // loop-carried copy stays in registers (an array of HIP's uint4 structs went to scratch)
+#define ATTN_LOAD_V(K0)                                                                       \
+  {                                                                                           \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                           \
+      const int r = 4 * i + (lane >> 4);                                                      \
+      const int key = (K0) + r < T ? (K0) + r : T - 1;                                        \
+      vv[i] = reinterpret_cast<const u32x4_t*>(vc + (head + key) * kD)[lane & 15];            \
+    }                                                                                         \
+  }
+  u32x4_t vv[8];
+  ATTN_LOAD_V(0)
   for (int k0 = 0; k0 < Lmax; k0 += kKB) {
-    // K A fragments (rows k0 + 16 t + fr, clamped to the cache) and the V block's 16-B pieces
-    bf16x8_t kf[2][4];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int key = k0 + 16 * t + fr < T ? k0 + 16 * t + fr : T - 1;
-      const uint4* kp = reinterpret_cast<const uint4*>(kc + (head + key) * kD) + kq;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) kf[t][c] = __builtin_bit_cast(bf16x8_t, kp[4 * c]);
-    }
-    uint4 vv[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int r = 4 * i + (lane >> 4);
-      const int key = k0 + r < T ? k0 + r : T - 1;
-      vv[i] = reinterpret_cast<const uint4*>(vc + (head + key) * kD)[lane & 15];
-    }
     // S^T tiles: lane (q, kq) gets keys 16 t + 4 kq + i of query q
     f32x4_t s[2];
 #pragma unroll
@@ -107,8 +117,12 @@ __global__ __launch_bounds__(64) void attn_prefill_mfma_kernel(
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int r = 4 * i + (lane >> 4);
-      *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(vimg) + voff(r, lane & 15)) = vv[i];
+      *reinterpret_cast<u32x4_t*>(reinterpret_cast<uint8_t*>(vimg) + voff(r, lane & 15)) = vv[i];
     }
+    // this block's K and V are consumed (S^T MFMAs issued, V in LDS): the next block's loads
+    // (past the end: clamped rows, unused) arrive under this block's softmax and P V
+    ATTN_LOAD_K(k0 + kKB)
+    ATTN_LOAD_V(k0 + kKB)
     // online softmax over this block's keys, per query (fp32)
     float mx = -INFINITY;
 #pragma unroll
@@ -161,6 +175,8 @@ __global__ __launch_bounds__(64) void attn_prefill_mfma_kernel(
       o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[dt], 0, 0, 0);
     }
   }
+#undef ATTN_LOAD_K
+#undef ATTN_LOAD_V
   // normalise rows 4 kq + i by their query's l, stage the bf16 tile [16][128] in LDS, store rows
   float inv[4];
 #pragma unroll
