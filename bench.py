@@ -347,22 +347,53 @@ def reference_gpu_step(plan, xs, g, device, steps):
     return ms, diff
 
 
-def hbm_copy_gbps(device, nbytes=1 << 30, reps=10):
-    """a copy kernel measured on the box beside the 8 TB/s spec peak (torch's
-    device copy of 1 GiB: read + write bytes / time, HIP events)."""
+def hbm_ceilings(device, nbytes=1 << 30, reps=10):
+    """what the chip streams, measured on the box beside the 8 TB/s spec peak, by
+    the microarch guide's method (MI355X_MICROARCH.md "HBM": one long launch over a buffer far
+    past the 256 MiB Infinity Cache, 16-B accesses). Three numbers, GB/s, HIP events:
+      copy_GBps   tao_hbm_copy_probe over 1 GiB (read + write bytes; the guide's float4 copy row),
+                  best grid of a small sweep;
+      read_GBps   tao_hbm_read_probe over 1 GiB in one launch (the GEMV's own load form: 16-B
+                  non-temporal loads, 512-thread workgroups);
+      torch_copy_GBps  torch's device copy_ of 1 GiB (what rounds 2-4 reported).
+    The per-launch floor of the decode step (pure_read_ms_per_step) is the other ceiling: the
+    same bytes as one read launch per linear."""
+    from torchao import _lib
+
+    lib = _lib.lib()
     a = torch.empty(nbytes // 4, dtype=torch.int32, device=device).fill_(1)
     b = torch.empty_like(a)
-    b.copy_(a)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    e1.synchronize()
-    gbps = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del a, b
+    sink = torch.zeros(1024, dtype=torch.int32, device=device)
+    sp = torch.cuda.current_stream(device).cuda_stream
+
+    def timed(fn):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e-3 / reps
+
+    def copy(grid):
+        rc = lib.tao_hbm_copy_probe(a.data_ptr(), b.data_ptr(), nbytes, grid, sp)
+        if rc:
+            raise RuntimeError(lib.tao_last_error().decode())
+
+    def read():
+        rc = lib.tao_hbm_read_probe(a.data_ptr(), nbytes, sink.data_ptr(), sp)
+        if rc:
+            raise RuntimeError(lib.tao_last_error().decode())
+
+    copy_best = max(2 * nbytes / timed(lambda: copy(gr)) / 1e9 for gr in (1024, 2048, 4096, 8192))
+    out = {"copy_GBps": round(copy_best, 1),
+           "read_GBps": round(nbytes / timed(read) / 1e9, 1),
+           "torch_copy_GBps": round(2 * nbytes / timed(lambda: b.copy_(a)) / 1e9, 1),
+           "bytes": nbytes}
+    del a, b, sink
     torch.cuda.empty_cache()
-    return round(gbps, 1)
+    return out
 
 
 def config2_shapes(device, g=32, copies=32, reps=20):
@@ -969,15 +1000,39 @@ def config5_record(P, rank, g, device, rehearsal, steps, warmup, policy="tp"):
 
 def unfused_record(cfg, g, device, steps):
     """The reference's module layout at P = 1: w1 and w3 as two linears (161 launches, the same
-    bytes as the merged step), one HIP graph, replay GPU time and wall time per step."""
+    bytes as the merged step; what a model quantized unchanged runs,
+    /root/reference/torchao/_models/llama/model.py:481-486), one HIP graph, replay GPU time and
+    wall time per step, its roofline fraction, and per shape the GEMV over a pure read of the
+    same bytes (as the headline's per_shape_graph)."""
     lins = llama_linears(cfg, fuse_w13=False)
     st = LinearStep(lins, ["whole"] * len(lins), 1, 0, g, device, False)
     graph = st.capture()
     ms = st.wall_ms(graph.replay, steps, 3)
-    gpu_ms = st.replay_ms(graph, max(steps, 10))
+    reps = max(steps, 10)
+    gpu_ms = st.replay_ms(graph, reps)
+    gr = st.read_probe_graph()
+    pure_ms = st.replay_ms(gr, reps)
+    del gr
+    per_shape = {}
+    for (n_loc, K) in sorted({(e[1], e[2]) for e in st.plan}):
+        cnt = sum(1 for e in st.plan if (e[1], e[2]) == (n_loc, K))
+        gs_ = st.capture(do_comm=False, only=(n_loc, K))
+        us = st.replay_ms(gs_, reps) * 1e3 / cnt
+        gr_ = st.read_probe_graph(only=(n_loc, K))
+        rus = st.replay_ms(gr_, reps) * 1e3 / cnt
+        b = int4_alg_bytes(n_loc, K, g)
+        per_shape[f"{n_loc}x{K}"] = {
+            "launches": cnt, "us": round(us, 3), "frac": round(b / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+            "pure_read_us": round(rus, 3), "gemv_over_pure_read": round(us / rus, 3)}
+        del gs_, gr_
+    achieved = st.bytes_per_step / (gpu_ms * 1e-3) / 1e9
     rec = {"workload": workload_desc(cfg, False) + f" ({len(st.plan)} GEMV launches/step)",
            "value": round(st.bytes_per_step / (ms * 1e-3) / 1e9, 2), "unit": "GB/s",
            "ms_per_step": round(ms, 4), "kernel_ms_per_step": round(gpu_ms, 4),
+           "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBPS, 4),
+           "pure_read_ms_per_step": round(pure_ms, 4),
+           "gemv_over_pure_read": round(gpu_ms / pure_ms, 3),
+           "per_shape_graph": per_shape,
            "launches": len(st.plan)}
     del graph
     st.release()
@@ -1155,15 +1210,19 @@ def main():
         prefill = prefill_mfma(device)
     extras = P == 1 and not args.no_extras
     config2 = config2_shapes(device) if extras and args.model == "8b" else None
-    copy_gbps = hbm_copy_gbps(device) if extras else None
+    ceil = hbm_ceilings(device) if extras else None
 
     unfused = None
     if P == 1 and args.model == "8b" and not args.no_fuse_w13 and not args.no_extras \
             and graph is not None:
         unfused = unfused_record(cfg, g, device, args.steps)
     config5 = None
+    n_launches, has_graph = len(plan), graph is not None
     if args.model == "8b" and not args.no_config5:
-        # release the 8B step's weights first (the 70B step needs 43 GB / P per rank)
+        # release the 8B step's weights first (the 70B step needs 43 GB / P per rank): the
+        # plan / inputs / graphs bound here hold them too, so drop those references before
+        # st.release() empties the allocator cache
+        plan = xs = graph = groof = run = step = capture = None
         st.release()
         c5 = dict(steps=max(2, min(args.steps, 10)), warmup=min(args.warmup, 2))
         config5 = config5_record(P, rank, g, device, rehearsal, policy="tp", **c5)
@@ -1195,14 +1254,14 @@ def main():
             "config": {
                 "workload": f"{model_name} int4 g{g} weight-only linears, M=1 decode: "
                             + workload_desc(cfg, not args.no_fuse_w13)
-                            + f" ({len(plan)} GEMV launches/step)",
+                            + f" ({n_launches} GEMV launches/step)",
                 "model": f"{model_name} (linears only)",
                 "global_batch": 1,
                 "seq_len": 1,
                 "group_size": g,
                 "bytes_per_step": bytes_per_step,
                 "parallelism": parallelism_desc(st, policy) if P > 1 else "single-gpu",
-                "hip_graph": graph is not None,
+                "hip_graph": has_graph,
             },
             "roofline": {
                 "bound": "hbm",
@@ -1210,10 +1269,16 @@ def main():
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
-                "measured_copy_GBps": copy_gbps,  # 1 GiB device copy on this box (read+write)
+                # what this box streams in one long launch (hbm_ceilings), and the step as a
+                # fraction of each ceiling beside the spec-peak fraction
+                "measured_copy_GBps": ceil["copy_GBps"] if ceil else None,
+                "measured_stream_read_GBps": ceil["read_GBps"] if ceil else None,
+                "torch_copy_GBps": ceil["torch_copy_GBps"] if ceil else None,
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "frac_of_stream_read": round(achieved / ceil["read_GBps"], 4) if ceil else None,
+                "frac_of_copy": round(achieved / ceil["copy_GBps"], 4) if ceil else None,
                 "traffic": traffic,
-                "traffic_unit": f"HBM bytes per step ({len(plan)} launches)",
+                "traffic_unit": f"HBM bytes per step ({n_launches} launches)",
                 "alg_bytes_per_step": bytes_per_step,
                 "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic else None,
                 "launches": len(durs),

@@ -1,0 +1,152 @@
+/*
+ * torchao_mi355x_llama.h — fused kernels of the end-to-end decode / prefill harness
+ * (torchao/_models/llama, BASELINE config 4). They replace the ops around the quantized linears
+ * of the reference's gpt-fast model (torchao/_models/llama/model.py), which the reference gets
+ * from torch.compile (generate.py:865-875). Same conventions as include/torchao_mi355x.h.
+ */
+#ifndef TORCHAO_MI355X_LLAMA_H_
+#define TORCHAO_MI355X_LLAMA_H_
+
+#include "torchao_mi355x.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* tao_int4wo_linear_bf16 (no bias) with the SwiGLU of interleaved (gate, up) output rows folded
+ * into the epilogue: y [M][N/2] = bf16(bf16(silu(a_i)) * b_i), (a_i, b_i) = the bf16 outputs of
+ * rows (2i, 2i+1) (a w1||w3 weight merged row-interleaved; N % 16 == 0). Replaces the prefill's
+ * `F.silu(w1(x)) * w3(x)` (gpt-fast model.py FeedForward.forward) as one launch. Served where
+ * the single-fetch GEMM is routed; TAO_ERR_UNSUPPORTED elsewhere (the caller then runs the linear
+ * and tao_silu_mul_bf16). */
+int tao_int4wo_linear_swiglu_bf16(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
+                                  uint16_t* y, int64_t M, int64_t N, int64_t K,
+                                  int64_t group_size, void* stream);
+
+/* The prefill's wqkv linear (int4 weight-only, no bias) with RoPE and the KV-cache write of
+ * tao_rope_kv_bf16 folded into the epilogue: x [B*S][K] bf16; weight [(H + 2 Hkv) D][K]; q
+ * rotated into q_out [B][H][S][D]; k rotated and v written into the caches [B][Hkv][T][D] at row
+ * pos[s] (a position outside [0, T) writes no cache row and sets tao_decode_status bit 1).
+ * D == 128; q_out and the caches 16-B aligned. Replaces wqkv + apply_rotary_emb +
+ * KVCache.update (gpt-fast model.py Attention.forward) at prefill as one launch. Served where
+ * the single-fetch GEMM is routed; TAO_ERR_UNSUPPORTED elsewhere. */
+int tao_int4wo_linear_rope_kv_bf16(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
+                                   int64_t K, int64_t group_size, const float* freqs,
+                                   const int64_t* pos, uint16_t* q_out, uint16_t* k_cache,
+                                   uint16_t* v_cache, int64_t B, int64_t S, int64_t H,
+                                   int64_t Hkv, int64_t D, int64_t T, void* stream);
+
+/* ---- fused decode-step kernels of the end-to-end harness (torchao/_models/llama) -------------
+ * Not on the int4 path: the fusions the reference gets from torch.compile in its gpt-fast
+ * harness (torchao/_models/llama/generate.py:865-875, model.py:405-501). */
+
+/* y[r] = bf16(bf16(x[r] * rsqrt(mean(x[r]^2) + eps)) * w), rows of `dim` bf16 (dim % 8 == 0).
+ * Replaces RMSNorm.forward (torchao/_models/llama/model.py:489-501). */
+int tao_rmsnorm_bf16(const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t rows,
+                     int64_t dim, float eps, void* stream);
+
+/* h = x + res (bf16, rounded as torch's bf16 add), stored, then y = RMSNorm(h) as
+ * tao_rmsnorm_bf16: the residual add and the next norm of a prefill block in one launch,
+ * bit-identical to the two. rows x dim, dim % 8 == 0. */
+int tao_add_rmsnorm_bf16(const uint16_t* x, const uint16_t* res, const uint16_t* w, uint16_t* h,
+                         uint16_t* y, int64_t rows, int64_t dim, float eps, void* stream);
+
+/* qkv [B*S][(H + 2 Hkv) * D] bf16 -> q_out [B][H][S][D] rotated; k (rotated) and v written to
+ * k_cache / v_cache [B][Hkv][T][D] at positions pos[S] (int64). freqs: rotary table
+ * [rows][D/2][2] fp32 (cos, sin), row pos[s]. Replaces apply_rotary_emb + KVCache.update
+ * (model.py:547-557, 175-196). */
+int tao_rope_kv_bf16(const uint16_t* qkv, const float* freqs, const int64_t* pos,
+                     uint16_t* q_out, uint16_t* k_cache, uint16_t* v_cache, int64_t B, int64_t S,
+                     int64_t H, int64_t Hkv, int64_t D, int64_t T, void* stream);
+
+/* One-query attention over keys 0..pos[0] of the caches, GQA (H % Hkv == 0, H/Hkv <= 8),
+ * D == 128: out [B][1][H*D] bf16. partial: fp32 workspace of B*Hkv*ceil(T/64)*(H/Hkv)*(D+2)
+ * for the two-launch split (T > 1024, or tao_tune_attn 1); NULL = the library's per-stream
+ * workspace (run once eagerly before graph capture). Shorter caches run one single-pass kernel
+ * and do not touch it.
+ * Replaces F.scaled_dot_product_attention at decode (model.py:441-476). */
+int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                         const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
+                         int64_t Hkv, int64_t D, int64_t T, float scale, void* stream);
+
+/* Prefill attention: S queries per (batch, head), q [B][H][S][D] bf16 (RoPE applied), query s at
+ * position pos[s] attending cache keys 0..pos[s] (the causal mask of a prompt written into the
+ * caches at pos), GQA (H % Hkv == 0), D == 128: out [B][S][H*D] bf16, fp32 softmax. Replaces the
+ * masked F.scaled_dot_product_attention over the caches of the reference's Attention.forward
+ * (gpt-fast model.py) at prefill. */
+int tao_attn_prefill_bf16(const uint16_t* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                          const int64_t* pos, uint16_t* out, int64_t B, int64_t H, int64_t Hkv,
+                          int64_t D, int64_t S, int64_t T, float scale, void* stream);
+
+/* y = bf16(bf16(silu(a)) * b) elementwise over n bf16 (n even). Replaces FeedForward's
+ * F.silu(w1(x)) * w3(x) (model.py:485-486). b == NULL: a holds n interleaved (gate, up) pairs
+ * (2n bf16, the output of an interleaved w13 linear) and y[i] = silu(a[2i]) * a[2i+1]. */
+int tao_silu_mul_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t n,
+                      void* stream);
+
+/* out[r] = argmax over n bf16 logits of row r (first index of the maximum; a positive-sign NaN
+ * counts as the maximum, as in torch.argmax) as int64. Replaces logits.argmax(dim=-1) of the greedy decode
+ * (generate.py:111-142, sample with temperature 0). */
+int tao_argmax_bf16(const uint16_t* x, int64_t* out, int64_t rows, int64_t n, void* stream);
+
+/* One decode step's greedy bookkeeping in one launch (batch 1): cur[0] = argmax of x[n] (the
+ * rule of tao_argmax_bf16), then tokens[pos[0] + 1] = cur[0] (when inside [0, max_len)) and
+ * pos[0] += 1. Replaces the harness's argmax + pos.add_ + tokens.index_copy_ + cur.copy_
+ * (torchao/_models/llama/generate.py decode loop, reference generate.py:111-142). */
+int tao_argmax_advance_bf16(const uint16_t* x, int64_t n, int64_t* cur, int64_t* pos,
+                            int64_t* tokens, int64_t max_len, void* stream);
+
+/* One token through an int8 weight-only linear with its decode-step neighbours fused (the
+ * int8 counterpart of tao_int4wo_decode_bf16; csrc/int8_gemv.hip). Operands of
+ * tao_int8wo_linear_bf16 at M == 1 (x [K] bf16, w [N][K] int8, scale [N] bf16, no bias).
+ *   norm_weight  NULL: x as is; else [K] bf16, x -> bf16(bf16(x * rsqrt(mean(x^2) + eps)) * w).
+ *   epilogue 0: y [N] = the linear; 1 (swiglu): rows (2i, 2i+1) = (w1_i, w3_i), y [N/2] =
+ *   bf16(bf16(silu(a)) * b); 2 (rope_kv): rows [q | k | v] heads, y [n_head * head_dim] = rotated
+ *   q, rotated k and v written to k_cache / v_cache [n_kv_head][max_seq][head_dim] at pos[0]
+ *   (outside [0, max_seq): no cache row written, reported by tao_decode_status).
+ * Each result equals rmsnorm -> tao_int8wo_linear_bf16 -> silu_mul / rope_kv. Replaces, at
+ * decode, the RMSNorm / SiLU-mul / RoPE + KVCache.update ops around the reference's int8
+ * weight-only linears (torchao/_models/llama/model.py). */
+int tao_int8wo_decode_bf16(const uint16_t* x, const int8_t* w, const uint16_t* scale, int64_t N,
+                           int64_t K, const uint16_t* norm_weight, float eps, int epilogue,
+                           uint16_t* y, const float* freqs, const int64_t* pos, uint16_t* k_cache,
+                           uint16_t* v_cache, int64_t n_head, int64_t n_kv_head, int64_t head_dim,
+                           int64_t max_seq, void* stream);
+
+/* The same decode-step fusions on the int8 dynamic-activation linear (one token; the per-token
+ * int8 quantisation of the normalised token inside the kernel, as tao_int8_dyn_linear_bf16
+ * does for the plain token). Operands and epilogues as tao_int8wo_decode_bf16; equals
+ * rmsnorm -> tao_int8_dyn_linear_bf16 -> silu_mul / rope_kv up to the norm's fp32 sum order.
+ * K <= 32768 (<= 16384 with norm_weight). Replaces, at decode, the ops around the reference's
+ * Int8DynamicActivationInt8WeightConfig linears (model.py, quant_api.py:1258-1273). */
+int tao_int8dq_decode_bf16(const uint16_t* x, const int8_t* w, const uint16_t* scale, int64_t N,
+                           int64_t K, const uint16_t* norm_weight, float eps, int epilogue,
+                           uint16_t* y, const float* freqs, const int64_t* pos, uint16_t* k_cache,
+                           uint16_t* v_cache, int64_t n_head, int64_t n_kv_head, int64_t head_dim,
+                           int64_t max_seq, void* stream);
+
+/* Decode-step fused int4 linear, M = 1: y = epilogue(rmsnorm(x) W^T) in one launch, with the
+ * operands of tao_int4wo_linear_bf16 (x [K] bf16, packed [N][K/8], scales_and_zeros [N][K/g]).
+ *   norm_weight  NULL: x is used as is; else [K] bf16 and x -> bf16(bf16(x * rsqrt(mean(x^2) +
+ *                eps)) * norm_weight) first (= tao_rmsnorm_bf16; RMSNorm, model.py:489-501).
+ *   epilogue 0   y [N] bf16 (the plain linear).
+ *   epilogue 1   rows (2i, 2i+1) are (w1_i, w3_i): y [N/2] = bf16(bf16(silu(a)) * b)
+ *                (= tao_silu_mul_bf16 over w1 and w3 outputs; FeedForward, model.py:485-486).
+ *   epilogue 2   rows are wqkv's [q | k | v] heads, N = (n_head + 2 n_kv_head) * head_dim:
+ *                y [n_head * head_dim] = rotated q, k rotated and v stored into k_cache /
+ *                v_cache [n_kv_head][max_seq][head_dim] at pos[0] (= tao_rope_kv_bf16 with
+ *                B = S = 1; Attention.forward, model.py:547-557).
+ * freqs/pos/caches/head sizes are read only by epilogue 2. Same bf16 roundings as the unfused
+ * kernels; the one difference is the order of the fp32 sum of squares in the RMSNorm. */
+int tao_int4wo_decode_bf16(const uint16_t* x, const uint32_t* packed,
+                           const uint16_t* scales_and_zeros, int64_t N, int64_t K,
+                           int64_t group_size, const uint16_t* norm_weight, float eps,
+                           int epilogue, uint16_t* y, const float* freqs, const int64_t* pos,
+                           uint16_t* k_cache, uint16_t* v_cache, int64_t n_head,
+                           int64_t n_kv_head, int64_t head_dim, int64_t max_seq, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TORCHAO_MI355X_LLAMA_H_ */

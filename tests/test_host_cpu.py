@@ -39,15 +39,37 @@ from torchao.quantization.quant_primitives import (
 )
 
 HEADER = os.path.join(ROOT, "include", "torchao_mi355x.h")
+# the public boundary, the e2e harness's fused kernels, the internal tuning / measurement entries
+HEADERS = [os.path.join(ROOT, "include", h) for h in
+           ("torchao_mi355x.h", "torchao_mi355x_llama.h", "torchao_mi355x_tune.h")]
 
 
 # ---------------------------------------------------------------------------------------------
 # C-ABI contract
 # ---------------------------------------------------------------------------------------------
-def _declared_functions():
+def _declared_functions(headers=None):
+    names = set()
+    for h in headers or HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(tao_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
+
+
+def test_public_header_is_the_boundary_only():
+    """The drop-in header carries only entries that replace reference calls (plus version /
+    error / status); tuning knobs and measurement hooks live in torchao_mi355x_tune.h."""
+    public = _declared_functions([HEADER])
+    assert not [n for n in public if "tune" in n or "profile" in n or "probe" in n], public
     text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(tao_[a-z0-9_]+)\s*\(", text)))
+    for name in public:
+        if name in ("tao_version", "tao_last_error", "tao_device_count", "tao_decode_status",
+                    "tao_int4_pack_host", "tao_int4_unpack_host",
+                    "tao_unpack_tensor_core_tiled_layout_host"):
+            continue
+        # every boundary entry's comment cites the reference call site it replaces
+        i = text.index(name + "(")
+        block = text[text.rindex("/*", 0, i):i]
+        assert "Replaces" in block or "replaces" in block or ".py:" in block, name
 
 
 def test_library_loads_and_exports_every_declared_symbol():

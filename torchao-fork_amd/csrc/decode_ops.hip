@@ -653,7 +653,10 @@ int tao_attn_prefill_bf16(const uint16_t* q, const uint16_t* k_cache, const uint
                 "attn_prefill: bad sizes");
   TAO_CHECK_ALIGN(q, 16, "q");
   TAO_CHECK_ALIGN(k_cache, 16, "k_cache");
+  TAO_CHECK_ALIGN(v_cache, 16, "v_cache");  // V rows are read with 16-B vector loads
   TAO_CHECK_ALIGN(out, 16, "out");
+  TAO_CHECK_ARG(B * H <= 65535, "attn_prefill: B * H (%lld) exceeds the grid's y extent",
+                (long long)(B * H));
   // MFMA flash-style kernel (attn_mfma.hip): a wave per 16 queries, K / V read once per block of
   // 16 queries instead of once per query (the single-pass decode kernel generalised, which this
   // replaces, re-read the prefix per query: 24 us per layer at S = 128)
@@ -719,6 +722,9 @@ extern "C" int tao_decode_status(int* bits) {
   if (rc == TAO_OK) rc = tao::int8gemv_decode_status(&v);
   if (rc == TAO_OK) rc = tao::int8dyn_decode_status(&v);
   if (rc == TAO_OK) rc = tao::sf_decode_status(&v);
+  unsigned to = 0;  // split-K reducer timeouts of the single-fetch GEMMs (prefill)
+  if (rc == TAO_OK) rc = tao_gemm_sf_status(&to);
+  if (to != 0) v |= tao::kDecodeErrSplitK;
   *bits = (int)v;
   return rc;
 }

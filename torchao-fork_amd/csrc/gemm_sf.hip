@@ -535,10 +535,13 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
 #endif
       return;
     }
-    // fixed reducer: wait for the S-1 publishers, reset the ticket. Spread: every workgroup waits
-    // for all S arrivals, then adds a second arrival; the one that completes 2 S resets the
-    // ticket (every workgroup has left its wait by then). One lane polls with sc1 loads and tells
-    // the workgroup through LDS.
+    // fixed reducer: wait for the S-1 publishers, then take their S-1 arrivals back off the
+    // ticket. Spread: every workgroup waits for all S arrivals, then adds a second arrival; the
+    // one that completes 2 S resets the ticket (every workgroup has left its wait by then). One
+    // lane polls with sc1 loads and tells the workgroup through LDS. A timed-out wait still
+    // settles the ticket the same way (the subtraction, or the second arrival), so once the late
+    // publishers' adds land it is back at 0 for the next launch on this stream's workspace; the
+    // tile itself is skipped and the timeout reported (tao_decode_status bit 2).
     if (tid == 0) {
       const unsigned need = seam ? (unsigned)S : (unsigned)(S - 1);
       unsigned it = 0, ok = 1;
@@ -550,13 +553,12 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
           break;
         }
       }
-      if (ok) {
-        if (!seam) {
-          __hip_atomic_store(&cnt[tile * cs], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (__hip_atomic_fetch_add(&cnt[tile * cs], 1u, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT) == 2u * S - 1u) {
-          __hip_atomic_store(&cnt[tile * cs], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+      if (!seam) {
+        (void)__hip_atomic_fetch_sub(&cnt[tile * cs], need, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+      } else if (__hip_atomic_fetch_add(&cnt[tile * cs], 1u, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT) == 2u * S - 1u) {
+        __hip_atomic_store(&cnt[tile * cs], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (fenced) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -565,6 +567,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
       *word = ok;
     }
     __syncthreads();
+    if (*word == 0) return;  // timed out: write nothing (uniform over the workgroup)
     if (own) {
       // the other slices' fragments summed with this one's in slice order: deterministic, and
       // the same additions in the same order under both seams
@@ -923,6 +926,10 @@ int sf_int4_epi(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, i
     return sf32_int4(x, packed, sz, lg, bias, y, M, N, K, sh.bn, sh.splits, sh.stages,
                      tuning().sf_a_steps, stream, ep.kind, sh.kh);
   }
+  // a column tile only a tuning override can ask for: UNSUPPORTED, so the fused-epilogue callers
+  // fall back to the plain linear + the separate epilogue kernel (checked before any workspace)
+  if (sh.bn != 64 && sh.bn != 128 && sh.bn != 256)
+    return set_error(TAO_ERR_UNSUPPORTED, "gemm_sf: int4 takes bn 64, 128 or 256 (got %d)", sh.bn);
   const dim3 grid((N + sh.bn - 1) / sh.bn, 1, (M + kBM - 1) / kBM);  // tiles: grid.x grid.z
   f32x4_t* slab = nullptr;
   unsigned* cnt = nullptr;
@@ -934,8 +941,6 @@ int sf_int4_epi(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, i
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<f32x4_t*>(w);
   }
-  if (sh.bn != 64 && sh.bn != 128 && sh.bn != 256)
-    return set_error(TAO_ERR_INVALID_ARGUMENT, "gemm_sf: int4 takes bn 64 or 128 (got %d)", sh.bn);
   SfI4 pol{packed, reinterpret_cast<const uint32_t*>(sz), lg};
   const uint8_t* xb = reinterpret_cast<const uint8_t*>(x);
   switch (sh.bn) {

@@ -375,7 +375,10 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
           break;
         }
       }
-      if (ok) __hip_atomic_store(&cnt[tile * cs], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // take the S-1 arrivals back off the ticket, timed out or not: once a late publisher's add
+      // lands the ticket is 0 again for the next launch on this workspace (gemm_sf.hip's seam)
+      (void)__hip_atomic_fetch_sub(&cnt[tile * cs], (unsigned)(S - 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
       if (fenced) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -383,6 +386,7 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
       *word = ok;
     }
     __syncthreads();
+    if (*word == 0) return;  // timed out: write nothing (uniform over the workgroup)
     f32x16_t sum[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)

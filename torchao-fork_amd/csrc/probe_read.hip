@@ -17,8 +17,38 @@ __global__ __launch_bounds__(512) void read_probe_kernel(const uint4* __restrict
   if (acc == 0x9E3779B9u) sink[t & 1023] = acc;  // keeps the load live; never taken in practice
 }
 
+// Streaming copy for the bench's ceiling calibration (MI355X_MICROARCH.md "HBM": a float4 copy
+// measured at 6.29 TB/s read + write): each thread moves 4 x 16 B per grid-stride round with all
+// four loads in flight before the stores; default cache policy on both sides.
+__global__ __launch_bounds__(256) void copy_probe_kernel(const uint4* __restrict__ src,
+                                                         uint4* __restrict__ dst, size_t n16) {
+  const size_t stride = (size_t)gridDim.x * 256 * 4;
+  for (size_t i = (size_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += stride) {
+    uint4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = i + 256 * j < n16 ? src[i + 256 * j] : uint4{};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (i + 256 * j < n16) dst[i + 256 * j] = v[j];
+  }
+}
+
 }  // namespace
 }  // namespace tao
+
+extern "C" int tao_hbm_copy_probe(const void* src, void* dst, int64_t bytes, int grid,
+                                  void* stream) {
+  TAO_CHECK_ARG(src != nullptr && dst != nullptr, "copy probe: null pointer");
+  TAO_CHECK_ARG(bytes > 0 && bytes % 16 == 0, "copy probe: bytes (%lld) must be a positive "
+                "multiple of 16", (long long)bytes);
+  TAO_CHECK_ARG(grid > 0 && grid <= (1 << 20), "copy probe: grid (%d) out of range", grid);
+  TAO_CHECK_ALIGN(src, 16, "src");
+  TAO_CHECK_ALIGN(dst, 16, "dst");
+  tao::launch(tao::copy_probe_kernel, dim3((unsigned)grid), dim3(256), 0, tao::as_stream(stream),
+              reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst),
+              (size_t)(bytes / 16));
+  return tao::check_launch("copy_probe_kernel");
+}
 
 extern "C" int tao_hbm_read_probe(const void* buf, int64_t bytes, void* sink, void* stream) {
   TAO_CHECK_ARG(buf != nullptr && sink != nullptr, "read probe: null pointer");

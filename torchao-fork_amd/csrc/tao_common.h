@@ -7,6 +7,8 @@
 #include <stdint.h>
 
 #include "../../include/torchao_mi355x.h"
+#include "../../include/torchao_mi355x_llama.h"
+#include "../../include/torchao_mi355x_tune.h"
 
 namespace tao {
 
@@ -237,6 +239,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 // tao_decode_status() (a synchronous read, made outside graph capture; the decode harness does
 // it after every generate()). The reference's index_put KV cache device-asserts instead.
 constexpr unsigned kDecodeErrKvPos = 1u;
+// tao_decode_status bit 2: a single-fetch GEMM's split-K reducer timed out waiting for its
+// publishers (that tile was not written; never expected)
+constexpr unsigned kDecodeErrSplitK = 2u;
 #define TAO_DECODE_ERROR_WORD(reader)                                                        \
   static __device__ unsigned g_decode_err = 0;                                                \
   __device__ __forceinline__ void flag_decode_error(unsigned bits) {                          \
