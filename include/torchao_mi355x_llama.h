@@ -69,6 +69,36 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
                          const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
                          int64_t Hkv, int64_t D, int64_t T, float scale, void* stream);
 
+/* Split decode attention (the first half of the decode attention + wo pair): the single-pass
+ * kernel of tao_attn_decode_bf16 over `splits` (2 or 4) key ranges of each query head, one
+ * workgroup per (batch, head, split), each range ceil(L / splits) keys rounded up to 16 (L =
+ * pos[0] + 1 clamped to [1, T]). Writes the unnormalised partials: partial [B * H][splits][132]
+ * fp32 = o[128] (sum over the range of exp(s - m) v), m, l, 2 pad (an empty range: o = 0,
+ * m = -inf, l = 0). D == 128; partial 16-B aligned. tao_attn_merge_bf16 (or the wo linear
+ * tao_int4wo_attn_out_bf16) finishes it. Replaces F.scaled_dot_product_attention at decode
+ * (model.py:441-476), spread over splits x the workgroups of the one-pass kernel. */
+int tao_attn_decode_split_bf16(const uint16_t* q, const uint16_t* k_cache,
+                               const uint16_t* v_cache, const int64_t* pos, float* partial,
+                               int64_t B, int64_t H, int64_t Hkv, int64_t D, int64_t T, float scale,
+                               int64_t splits, void* stream);
+
+/* out [B][1][H * D] bf16 = the merged split partials of tao_attn_decode_split_bf16:
+ * bf16(sum_s o_s w_s * (1 / sum_s l_s w_s)), w_s = exp(m_s - max m). D == 128. */
+int tao_attn_merge_bf16(const float* partial, uint16_t* out, int64_t B, int64_t H, int64_t D,
+                        int64_t splits, void* stream);
+
+/* The attention output linear of a decode step with the split merge folded into its x load: y [N]
+ * = bf16(bf16(W x) + residual[n]) with x = tao_attn_merge_bf16(partial) (batch 1, K = n_head *
+ * 128), W int4 (the operands of tao_int4wo_linear_bf16); residual may be NULL. Every workgroup
+ * merges x into LDS while its first weight slices are in flight. Bit-identical to
+ * tao_attn_merge_bf16 -> tao_int4wo_linear_bf16 (bias = residual) up to the GEMV's launch shape.
+ * Replaces the wo linear + residual add after attention (model.py Attention.forward,
+ * TransformerBlock.forward) at decode. */
+int tao_int4wo_attn_out_bf16(const float* partial, int64_t splits, int64_t n_head,
+                             const uint32_t* packed, const uint16_t* scales_and_zeros, int64_t N,
+                             int64_t K, int64_t group_size, const uint16_t* residual, uint16_t* y,
+                             void* stream);
+
 /* Prefill attention: S queries per (batch, head), q [B][H][S][D] bf16 (RoPE applied), query s at
  * position pos[s] attending cache keys 0..pos[s] (the causal mask of a prompt written into the
  * caches at pos), GQA (H % Hkv == 0), D == 128: out [B][S][H*D] bf16, fp32 softmax. Replaces the

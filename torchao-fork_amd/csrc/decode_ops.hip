@@ -321,11 +321,17 @@ constexpr int kSingleWaves = TAO_ATTN_WAVES;
 // broadcast by v_readlane (the source lane is uniform) instead of ds_bpermute shuffles: 3.65 /
 // 5.52 / 6.54 / 9.85 us per graph launch at 128 / 328 / 512 / 900 keys against 3.80 / 5.63 /
 // 7.04 / 10.20 for f32 conversions and shuffles (profiles/r4_attn_time_dot2.jsonl).
-template <int D, int NW>
+// SPLIT (tao_attn_decode_split_bf16): the same kernel over keys [lo, hi) of split blockIdx.y of
+// gridDim.y (each split ceil(L / NS) keys rounded up to 16), writing the split's unnormalised
+// partial instead of the bf16 output: part [B * H][NS][kPartStride] fp32 = o[D] (sum of
+// exp(s - m) v over the split's keys), m, l. An empty split writes m = -inf, l = 0, o = 0.
+constexpr int kPartStride = 132;  // o[128], m, l, 2 pad: 16-B aligned records
+
+template <int D, int NW, bool SPLIT = false>
 __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int64_t* __restrict__ pos, uint16_t* __restrict__ out,
-    int H, int Hkv, int T, float scale) {
+    int H, int Hkv, int T, float scale, float* __restrict__ part) {
   static_assert(D == 128, "head_dim 128");
   __shared__ float wm[NW], wl[NW];
   __shared__ float wo[NW][D];
@@ -335,6 +341,19 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
   const int bh = blockIdx.x;
   const int b = bh / H, h = bh % H, kvh = h / (H / Hkv);
   const int L = attn_len(pos[0], T);
+  int lo = 0, hi = L;
+  if constexpr (SPLIT) {
+    const int NS = gridDim.y, C = ((L + NS - 1) / NS + 15) & ~15;
+    lo = (int)blockIdx.y * C;
+    hi = lo + C < L ? lo + C : L;
+    if (lo >= hi) {  // no keys in this split (uniform): the empty partial
+      float* pr = part + ((size_t)bh * NS + blockIdx.y) * kPartStride;
+      if (threadIdx.x < D) pr[threadIdx.x] = 0.f;
+      if (threadIdx.x == D) pr[D] = -INFINITY;
+      if (threadIdx.x == D + 1) pr[D + 1] = 0.f;
+      return;
+    }
+  }
   const size_t ooff = (size_t)bh * (D / 2);  // output dword offset
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const size_t head = (size_t)(b * Hkv + kvh) * T;
@@ -345,7 +364,7 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
   uint4 ka[2], kb2[2];
   uint32_t vv[16];
   auto load_step = [&](int t0) __attribute__((always_inline)) {
-    const int ta = t0 + g < L ? t0 + g : L - 1, tb = t0 + 8 + g < L ? t0 + 8 + g : L - 1;
+    const int ta = t0 + g < hi ? t0 + g : hi - 1, tb = t0 + 8 + g < hi ? t0 + 8 + g : hi - 1;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       ka[hh] = *reinterpret_cast<const uint4*>(kbase + (size_t)ta * D + 64 * hh);
@@ -353,11 +372,11 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const int tj = t0 + j < L ? t0 + j : L - 1;
+      const int tj = t0 + j < hi ? t0 + j : hi - 1;
       vv[j] = vb[(size_t)tj * (D / 2)];
     }
   };
-  load_step(wave * 16);
+  load_step(lo + wave * 16);
   uint32_t qw[8];
   {
     const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bh * D + p8 * 8);
@@ -374,7 +393,7 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     }
   }
   float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
-  for (int t0 = wave * 16; t0 < L; t0 += NW * 16) {
+  for (int t0 = lo + wave * 16; t0 < hi; t0 += NW * 16) {
     float sa = 0.f, sb = 0.f;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
@@ -392,10 +411,10 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
       vf[2 * j] = bf16lo_to_f32(vv[j]);
       vf[2 * j + 1] = bf16hi_to_f32(vv[j]);
     }
-    if (t0 + NW * 16 < L) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
+    if (t0 + NW * 16 < hi) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
     sa = wave_bfly<1, 8>(sa, lane_id(), [](float a, float c) { return a + c; });
     sb = wave_bfly<1, 8>(sb, lane_id(), [](float a, float c) { return a + c; });
-    const bool va = t0 + g < L, vbk = t0 + 8 + g < L;
+    const bool va = t0 + g < hi, vbk = t0 + 8 + g < hi;
     sa = va ? sa * scale : -INFINITY;
     sb = vbk ? sb * scale : -INFINITY;
     float mx = fmaxf(sa, sb);
@@ -440,10 +459,41 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
       a0 = fmaf(wo[w][2 * lane], f, a0);
       a1 = fmaf(wo[w][2 * lane + 1], f, a1);
     }
-    const float inv = 1.f / ls;
-    reinterpret_cast<uint32_t*>(out)[ooff + lane] =
-        (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
+    if constexpr (SPLIT) {
+      float* pr = part + ((size_t)bh * gridDim.y + blockIdx.y) * kPartStride;
+      reinterpret_cast<float2*>(pr)[lane] = make_float2(a0, a1);
+      if (lane == 0) reinterpret_cast<float2*>(pr + D)[0] = make_float2(M, ls);
+    } else {
+      const float inv = 1.f / ls;
+      reinterpret_cast<uint32_t*>(out)[ooff + lane] =
+          (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
+    }
   }
+}
+
+// ---- merge of the split partials -> bf16 [B][1][H * D] (tao_attn_merge_bf16) --------------------
+// One wave per (batch, head), lane = dim pair; attn_merge_pair is also the x prologue of the wo
+// GEMV (int4_gemv.hip, tao_int4wo_attn_out_bf16), so both give the same bits.
+template <int NS>
+__global__ __launch_bounds__(64) void attn_merge_kernel(const float* __restrict__ part,
+                                                        uint32_t* __restrict__ out) {
+  const float* pr = part + (size_t)blockIdx.x * NS * kPartStride;
+  float2 ml[NS], o[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    ml[s] = reinterpret_cast<const float2*>(pr + s * kPartStride + 128)[0];
+    o[s] = reinterpret_cast<const float2*>(pr + s * kPartStride)[threadIdx.x];
+  }
+  float wgt[NS], inv;
+  attn_merge_weights<NS>(ml, wgt, inv);
+  float r0 = 0.f, r1 = 0.f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    r0 = fmaf(o[s].x, wgt[s], r0);
+    r1 = fmaf(o[s].y, wgt[s], r1);
+  }
+  out[(size_t)blockIdx.x * 64 + threadIdx.x] =
+      (uint32_t)f32_to_bf16(r0 * inv) | ((uint32_t)f32_to_bf16(r1 * inv) << 16);
 }
 
 // ---- SiLU(a) * b ----------------------------------------------------------------------------
@@ -615,7 +665,7 @@ static int attn_decode(const uint16_t* q, const uint16_t* k_cache, const uint16_
   if (T <= kSingleMaxT && mode == 0) {
     launch((attn_single_kernel<128, kSingleWaves>), dim3((unsigned)(B * H)),
            dim3(64 * kSingleWaves), 0, st, q, k_cache, v_cache, pos, out, (int)H, (int)Hkv,
-           (int)T, scale);
+           (int)T, scale, nullptr);
     return check_launch("attn_single_kernel");
   }
 
@@ -668,6 +718,41 @@ int tao_attn_decode_bf16(const uint16_t* q, const uint16_t* k_cache, const uint1
                          const int64_t* pos, float* partial, uint16_t* out, int64_t B, int64_t H,
                          int64_t Hkv, int64_t D, int64_t T, float scale, void* stream) {
   return attn_decode(q, k_cache, v_cache, pos, partial, out, B, H, Hkv, D, T, scale, stream);
+}
+
+int tao_attn_decode_split_bf16(const uint16_t* q, const uint16_t* k_cache,
+                               const uint16_t* v_cache, const int64_t* pos, float* partial,
+                               int64_t B, int64_t H, int64_t Hkv, int64_t D, int64_t T, float scale,
+                               int64_t splits, void* stream) {
+  TAO_CHECK_ARG(D == 128, "attn_decode_split: head_dim must be 128 (got %lld)", (long long)D);
+  TAO_CHECK_ARG(B > 0 && Hkv > 0 && H % Hkv == 0 && T > 0 && B * H < (1LL << 31),
+                "attn_decode_split: bad sizes");
+  TAO_CHECK_ARG(splits == 2 || splits == 4, "attn_decode_split: splits must be 2 or 4 (got %lld)",
+                (long long)splits);
+  TAO_CHECK_ARG(partial != nullptr, "attn_decode_split: partial is required");
+  TAO_CHECK_ALIGN(q, 16, "q");
+  TAO_CHECK_ALIGN(k_cache, 16, "k_cache");
+  TAO_CHECK_ALIGN(v_cache, 4, "v_cache");
+  TAO_CHECK_ALIGN(partial, 16, "partial");
+  launch((attn_single_kernel<128, kSingleWaves, true>), dim3((unsigned)(B * H), (unsigned)splits),
+         dim3(64 * kSingleWaves), 0, as_stream(stream), q, k_cache, v_cache, pos, nullptr,
+         (int)H, (int)Hkv, (int)T, scale, partial);
+  return check_launch("attn_split_kernel");
+}
+
+int tao_attn_merge_bf16(const float* partial, uint16_t* out, int64_t B, int64_t H, int64_t D,
+                        int64_t splits, void* stream) {
+  TAO_CHECK_ARG(D == 128, "attn_merge: head_dim must be 128 (got %lld)", (long long)D);
+  TAO_CHECK_ARG(B > 0 && H > 0 && B * H < (1LL << 31), "attn_merge: bad sizes");
+  TAO_CHECK_ARG(splits == 2 || splits == 4, "attn_merge: splits must be 2 or 4 (got %lld)",
+                (long long)splits);
+  TAO_CHECK_ALIGN(partial, 16, "partial");
+  TAO_CHECK_ALIGN(out, 4, "out");
+  hipStream_t st = as_stream(stream);
+  uint32_t* o = reinterpret_cast<uint32_t*>(out);
+  if (splits == 2) launch(attn_merge_kernel<2>, dim3((unsigned)(B * H)), dim3(64), 0, st, partial, o);
+  else launch(attn_merge_kernel<4>, dim3((unsigned)(B * H)), dim3(64), 0, st, partial, o);
+  return check_launch("attn_merge_kernel");
 }
 
 int tao_tune_attn(int mode) {

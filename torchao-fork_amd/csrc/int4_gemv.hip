@@ -69,6 +69,7 @@ struct GemvFuse {
   uint16_t* v_cache;
   int H, Hkv, D, T;
   int norm_deferred;  // PRO: 1 = stage bf16(x * w) and scale the outputs by r (see norm_finish)
+  const float* merge;  // MRG: split attention partials [H][MRG][132] (tao_attn_decode_split_bf16)
 };
 
 __device__ __forceinline__ uint32_t mul_pair_bf16(uint32_t xv, uint32_t wv) {
@@ -86,12 +87,15 @@ __device__ __forceinline__ uint32_t rmsnorm_pair(uint32_t xv, uint32_t wv, float
 // WPE: minimum waves per SIMD the register allocation must allow (8 -> <= 64 VGPRs, so four
 // 512-thread workgroups fit on a CU and mid-size grids run in a single resident round).
 // NPT > 0 enables the RMSNorm prologue with NPT 16-B pieces of x per thread (PRO).
-template <int MT, int RPW, int WPE, bool PAIR, int NPT = 0, int EPI = kEpiNone>
+// MRG > 0 (with NPT): x is the merge of MRG split-attention partials per head (fu.merge; head_dim
+// 128), formed in the prologue instead of the RMSNorm: tao_int4wo_attn_out_bf16.
+template <int MT, int RPW, int WPE, bool PAIR, int NPT = 0, int EPI = kEpiNone, int MRG = 0>
 __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     const uint16_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
     const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K, int gshift,
     int Wk, int G, int S, GemvFuse fu) {
   constexpr bool PRO = NPT > 0;
+  static_assert(MRG == 0 || (PRO && EPI == kEpiNone && MT == 1), "merge prologue: M == 1, NPT");
   static_assert(!(PRO || EPI) || (MT == 1 && RPW % 2 == 0), "fusions are M == 1, row pairs");
   constexpr int V = RPW * MT;
   extern __shared__ float red[];  // [G][Wk][V] (PRO: + [8] partial sums, + normalised x [K])
@@ -121,7 +125,28 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
   // ds_read_b128 pass (consecutive chunks) hit 16 distinct 16-B bank groups.
   uint4* xs = reinterpret_cast<uint4*>(red + ((G * Wk * V + 8 + 3) & ~3));
   uint4 xv[NPT > 0 ? NPT : 1], gv[NPT > 0 ? NPT : 1];
+  // MRG: piece i (x[8i .. 8i + 8)) of head i / 16 from the MRG partial records of that head
+  constexpr int kMS = MRG > 0 ? MRG : 1;
+  float2 mlv[NPT > 0 ? NPT : 1][kMS];
+  float4 ov[NPT > 0 ? NPT : 1][kMS][2];
   auto norm_load = [&]() __attribute__((always_inline)) {
+    if constexpr (MRG > 0) {
+      const int nx = K >> 3;
+#pragma unroll
+      for (int u = 0; u < NPT; ++u) {
+        const int i = threadIdx.x + u * (int)blockDim.x;
+        const int ic = i < nx ? i : nx - 1;  // clamped, masked in norm_finish
+        const float* rec = fu.merge + (size_t)(ic >> 4) * MRG * 132;  // head ic / 16
+        const int d0 = (ic & 15) << 3;
+#pragma unroll
+        for (int s = 0; s < MRG; ++s) {
+          mlv[u][s] = *reinterpret_cast<const float2*>(rec + s * 132 + 128);
+          ov[u][s][0] = *reinterpret_cast<const float4*>(rec + s * 132 + d0);
+          ov[u][s][1] = *reinterpret_cast<const float4*>(rec + s * 132 + d0 + 4);
+        }
+      }
+      return;
+    }
     const uint4* xr = reinterpret_cast<const uint4*>(x);
     const uint4* gr = reinterpret_cast<const uint4*>(fu.norm_w);
     const int nx = K >> 3;
@@ -135,6 +160,40 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
   };
   auto norm_finish = [&]() __attribute__((always_inline)) {
     const int nx = K >> 3;
+    if constexpr (MRG > 0) {  // x = the merged attention output, bf16, as attn_merge_kernel
+#pragma unroll
+      for (int u = 0; u < NPT; ++u) {
+        const int i = threadIdx.x + u * (int)blockDim.x;
+        float wgt[MRG], inv;
+        attn_merge_weights<MRG>(mlv[u], wgt, inv);
+        float r[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) r[e] = 0.f;
+#pragma unroll
+        for (int s = 0; s < MRG; ++s) {
+          const float4 a = ov[u][s][0], c = ov[u][s][1];
+          r[0] = fmaf(a.x, wgt[s], r[0]);
+          r[1] = fmaf(a.y, wgt[s], r[1]);
+          r[2] = fmaf(a.z, wgt[s], r[2]);
+          r[3] = fmaf(a.w, wgt[s], r[3]);
+          r[4] = fmaf(c.x, wgt[s], r[4]);
+          r[5] = fmaf(c.y, wgt[s], r[5]);
+          r[6] = fmaf(c.z, wgt[s], r[6]);
+          r[7] = fmaf(c.w, wgt[s], r[7]);
+        }
+        uint32_t pw[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          pw[e] = (uint32_t)f32_to_bf16(r[2 * e] * inv) |
+                  ((uint32_t)f32_to_bf16(r[2 * e + 1] * inv) << 16);
+        if (i < nx) {
+          const int c = i >> 2;
+          xs[c * 4 + (((i & 3) + (c >> 2)) & 3)] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+        }
+      }
+      __syncthreads();
+      return;
+    }
     if (fu.norm_w == nullptr) {  // plain x staged in LDS (tao_tune_int4_xlds), no RMSNorm
 #pragma unroll
       for (int u = 0; u < NPT; ++u) {
@@ -466,7 +525,7 @@ GemvShape default_shape(int S) {
   return {wk, g};
 }
 
-template <int MT, int RPW, int WPE, int NPT = 0, int EPI = kEpiNone>
+template <int MT, int RPW, int WPE, int NPT = 0, int EPI = kEpiNone, int MRG = 0>
 int launch_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
                 const uint16_t* bias, uint16_t* y, int M, int N, int K, int gshift,
                 GemvShape sh, hipStream_t stream, const GemvFuse& fu = GemvFuse{}) {
@@ -481,11 +540,11 @@ int launch_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
                                (size_t)K * 2
                          : (size_t)sh.g * wk * RPW * MT * sizeof(float);
   if (S > wk)
-    launch((int4wo_gemv_kernel<MT, RPW, WPE, true, NPT, EPI>), dim3(grid), dim3(threads), lds,
+    launch((int4wo_gemv_kernel<MT, RPW, WPE, true, NPT, EPI, MRG>), dim3(grid), dim3(threads), lds,
            stream, x, reinterpret_cast<const uint4*>(packed),
            reinterpret_cast<const uint32_t*>(sz), bias, y, M, N, K, gshift, wk, sh.g, S, fu);
   else
-    launch((int4wo_gemv_kernel<MT, RPW, WPE, false, NPT, EPI>), dim3(grid), dim3(threads), lds,
+    launch((int4wo_gemv_kernel<MT, RPW, WPE, false, NPT, EPI, MRG>), dim3(grid), dim3(threads), lds,
            stream, x, reinterpret_cast<const uint4*>(packed),
            reinterpret_cast<const uint32_t*>(sz), bias, y, M, N, K, gshift, wk, sh.g, S, fu);
   return check_launch("int4wo_gemv_kernel");
@@ -568,22 +627,56 @@ int launch_decode_rows(const uint16_t* x, const uint32_t* packed, const uint16_t
   return launch_gemv<1, 4, 8, 0, EPI>(x, packed, sz, nullptr, y, 1, N, K, gs, c.sh, stream, fu);
 }
 
+// Launch shape of the prologue (PRO) paths. Measured (experiments/bench_decode.py,
+// profiles/r1_bench_decode*.jsonl): with the prologue a workgroup should own whole rows (no K
+// split) and 4 waves of them, so the per-workgroup normalisation is amortised over 8-16 rows; 2
+// rows per wave below N = 16384 (Llama-3-70B wqkv 10240x8192: 14.0 vs 18.0 µs at 4 rows).
+M1Shape pro_shape(int N, int K) {
+  const int S = (K / 32 + 63) / 64;
+  M1Shape c = m1_shape(N, S);
+  if (tao::tuning().rpw == 0) c.rpw = N < 16384 ? 2 : 4;
+  if (tao::tuning().wk == 0) c.sh.wk = 1;
+  if (tao::tuning().g == 0) c.sh.g = 4;
+  // enough threads to hold x in the prologue: K <= 8 * NPT * threads, NPT <= kMaxNormPT
+  const int wk = c.sh.wk < S ? c.sh.wk : S;
+  while (64 * wk * c.sh.g * 8 * kMaxNormPT < K && wk * c.sh.g * 2 <= 8) c.sh.g *= 2;
+  return c;
+}
+
+// tao_int4wo_attn_out_bf16: the wo GEMV with the split-attention merge as its x prologue, on the
+// launch shape of the PRO paths (so tao_tune_int4_xlds 1 gives the unfused reference the same
+// per-element sums), bias = the residual
+template <int MRG>
+int launch_attn_out(const float* part, const uint32_t* packed, const uint16_t* sz,
+                    const uint16_t* bias, uint16_t* y, int N, int K, int gs, hipStream_t stream) {
+  const M1Shape c = pro_shape(N, K);
+  const int wk = c.sh.wk < (K / 32 + 63) / 64 ? c.sh.wk : (K / 32 + 63) / 64;
+  const int threads = 64 * wk * c.sh.g;
+  GemvFuse fu{};
+  fu.merge = part;
+  const uint16_t* xn = reinterpret_cast<const uint16_t*>(part);  // unread (the prologue forms x)
+  if (threads * 8 * 2 >= K) {
+    if (c.rpw <= 2)
+      return launch_gemv<1, 2, 4, 2, kEpiNone, MRG>(xn, packed, sz, bias, y, 1, N, K, gs, c.sh,
+                                                    stream, fu);
+    return launch_gemv<1, 4, 4, 2, kEpiNone, MRG>(xn, packed, sz, bias, y, 1, N, K, gs, c.sh,
+                                                  stream, fu);
+  }
+  if (c.rpw <= 2)
+    return launch_gemv<1, 2, 4, 4, kEpiNone, MRG>(xn, packed, sz, bias, y, 1, N, K, gs, c.sh,
+                                                  stream, fu);
+  return launch_gemv<1, 4, 4, 4, kEpiNone, MRG>(xn, packed, sz, bias, y, 1, N, K, gs, c.sh,
+                                                stream, fu);
+}
+
 template <bool PRO, int EPI>
 int launch_decode(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, uint16_t* y,
                   int N, int K, int gs, hipStream_t stream, const GemvFuse& fu) {
   const int S = (K / 32 + 63) / 64;
   M1Shape c = m1_shape(N, S);
   if constexpr (PRO) {
-    // Measured (experiments/bench_decode.py, profiles/r1_bench_decode*.jsonl): with the
-    // prologue a workgroup should own whole rows (no K split) and 4 waves of them, so the
-    // per-workgroup normalisation is amortised over 8-16 rows; 2 rows per wave below
-    // N = 16384 (Llama-3-70B wqkv 10240x8192: 14.0 vs 18.0 µs at 4 rows).
-    if (tao::tuning().rpw == 0) c.rpw = N < 16384 ? 2 : 4;
-    if (tao::tuning().wk == 0) c.sh.wk = 1;
-    if (tao::tuning().g == 0) c.sh.g = 4;
-    // enough threads to hold x in the prologue: K <= 8 * NPT * threads, NPT <= kMaxNormPT
+    c = pro_shape(N, K);
     const int wk = c.sh.wk < S ? c.sh.wk : S;
-    while (64 * wk * c.sh.g * 8 * kMaxNormPT < K && wk * c.sh.g * 2 <= 8) c.sh.g *= 2;
     const int threads = 64 * wk * c.sh.g;
     if (threads * 8 * 2 >= K)
       return launch_decode_rows<2, EPI>(x, packed, sz, y, N, K, gs, stream, fu, c);
@@ -748,4 +841,29 @@ extern "C" int tao_int4wo_decode_bf16(const uint16_t* x, const uint32_t* packed,
       TAO_DEC(false, tao::kEpiNone);
   }
 #undef TAO_DEC
+}
+
+extern "C" int tao_int4wo_attn_out_bf16(const float* partial, int64_t splits, int64_t n_head,
+                                        const uint32_t* packed, const uint16_t* scales_and_zeros,
+                                        int64_t N, int64_t K, int64_t group_size,
+                                        const uint16_t* residual, uint16_t* y, void* stream) {
+  TAO_CHECK_ARG(partial != nullptr, "int4 attn_out: partial is required");
+  TAO_CHECK_ARG(splits == 2 || splits == 4, "int4 attn_out: splits must be 2 or 4 (got %lld)",
+                (long long)splits);
+  TAO_CHECK_ARG(n_head > 0 && K == n_head * 128,
+                "int4 attn_out: K (%lld) must be n_head * 128", (long long)K);
+  TAO_CHECK_ALIGN(partial, 16, "partial");
+  int rc = tao::int4_check_linear_args(reinterpret_cast<const uint16_t*>(partial), packed,
+                                       scales_and_zeros, y, 1, N, K, group_size);
+  if (rc != TAO_OK) return rc;
+  TAO_CHECK_ARG(K <= 8 * tao::kMaxNormPT * 512, "int4 attn_out: K must be <= %d",
+                8 * tao::kMaxNormPT * 512);
+  if (N == 0) return TAO_OK;
+  const int gs = tao::gshift_of(group_size);
+  hipStream_t st = tao::as_stream(stream);
+  if (splits == 2)
+    return tao::launch_attn_out<2>(partial, packed, scales_and_zeros, residual, y, (int)N, (int)K,
+                                   gs, st);
+  return tao::launch_attn_out<4>(partial, packed, scales_and_zeros, residual, y, (int)N, (int)K,
+                                 gs, st);
 }

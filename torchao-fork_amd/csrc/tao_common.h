@@ -257,6 +257,24 @@ constexpr unsigned kDecodeErrSplitK = 2u;
     return TAO_OK;                                                                            \
   }
 
+// Split decode attention: the merge weights of NS partials (m_s, l_s) of one head (an empty split
+// has m = -inf, l = 0; split 0 is never empty): wgt_s = exp(m_s - max m), inv = 1 / sum l_s wgt_s.
+// Shared by the merge kernel (decode_ops.hip) and the wo GEMV's merge prologue (int4_gemv.hip).
+template <int NS>
+__device__ __forceinline__ void attn_merge_weights(const float2 (&ml)[NS], float (&wgt)[NS],
+                                                   float& inv) {
+  float M = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) M = fmaxf(M, ml[s].x);
+  float L = 0.f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    wgt[s] = ml[s].x == -INFINITY ? 0.f : __expf(ml[s].x - M);
+    L = fmaf(ml[s].y, wgt[s], L);
+  }
+  inv = 1.f / L;
+}
+
 // keys attended at query position p of a cache of T rows: p + 1, clamped to [1, T] (a p
 // outside [0, T) was reported by the KV-writing kernel of the same step)
 __device__ __forceinline__ int attn_len(int64_t p, int T) {

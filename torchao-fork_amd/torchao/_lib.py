@@ -80,6 +80,10 @@ _SIGNATURES = {
     "tao_rmsnorm_bf16": [_p, _p, _p, _i64, _i64, ctypes.c_float, _p],
     "tao_add_rmsnorm_bf16": [_p, _p, _p, _p, _p, _i64, _i64, ctypes.c_float, _p],
     "tao_rope_kv_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p],
+    "tao_attn_decode_split_bf16": [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
+                                   ctypes.c_float, _i64, _p],
+    "tao_attn_merge_bf16": [_p, _p, _i64, _i64, _i64, _i64, _p],
+    "tao_int4wo_attn_out_bf16": [_p, _i64, _i64, _p, _p, _i64, _i64, _i64, _p, _p, _p],
     "tao_attn_decode_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
                              ctypes.c_float, _p],
     "tao_attn_prefill_bf16": [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64,

@@ -81,6 +81,54 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     return out
 
 
+# Decode attention split over key ranges (tao_attn_decode_split_bf16) with the merge folded into
+# an int4 wo linear (tao_int4wo_attn_out_bf16): the splits per head (2 or 4; 0 = off, the one-pass
+# kernel then the linear), used for caches of at most ATTN_SPLIT_MAX_T rows.
+ATTN_SPLITS = 2
+ATTN_SPLIT_MAX_T = 1024
+PART_STRIDE = 132  # fp32 per (head, split) record: o[128], m, l, 2 pad
+
+
+def attn_decode_split(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                      pos: torch.Tensor, scale: float, splits: int) -> torch.Tensor:
+    """q [B, H, 1, D] against keys 0..pos[0], the keys split `splits` ways per head ->
+    unnormalised partials [B * H, splits, 132] fp32 (attn_merge or int4_attn_out finish it)."""
+    _check(q, torch.bfloat16, "attn_decode q")
+    _check(pos, torch.int64, "attn_decode pos")
+    B, H, S, D = q.shape
+    assert S == 1, "attn_decode takes one query per (batch, head)"
+    _, Hkv, T, _ = k_cache.shape
+    part = torch.empty(B * H, splits, PART_STRIDE, dtype=torch.float32, device=q.device)
+    _lib.call("tao_attn_decode_split_bf16", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+              pos.data_ptr(), part.data_ptr(), B, H, Hkv, D, T, float(scale), splits, _stream(q))
+    return part
+
+
+def attn_merge(part: torch.Tensor, B: int, H: int, D: int = 128) -> torch.Tensor:
+    """The split partials merged -> [B, 1, H * D] bf16 (the one-pass kernel's output form)."""
+    _check(part, torch.float32, "attn_merge partial")
+    out = torch.empty(B, 1, H * D, dtype=torch.bfloat16, device=part.device)
+    _lib.call("tao_attn_merge_bf16", part.data_ptr(), out.data_ptr(), B, H, D, part.shape[1],
+              _stream(part))
+    return out
+
+
+def int4_attn_out(part: torch.Tensor, n_head: int, packed: torch.Tensor, sz: torch.Tensor,
+                  group_size: int, residual=None) -> torch.Tensor:
+    """wo at decode with the split merge as its x prologue: [1, 1, N] = bf16(bf16(W x) +
+    residual), x = attn_merge(part) (batch 1)."""
+    _check(part, torch.float32, "int4_attn_out partial")
+    N, K = packed.shape[0], packed.shape[1] * 8
+    y = torch.empty(1, 1, N, dtype=torch.bfloat16, device=part.device)
+    if residual is not None:
+        _check(residual, torch.bfloat16, "int4_attn_out residual")
+        assert residual.numel() == N
+    _lib.call("tao_int4wo_attn_out_bf16", part.data_ptr(), part.shape[1], n_head,
+              packed.data_ptr(), sz.data_ptr(), N, K, group_size,
+              None if residual is None else residual.data_ptr(), y.data_ptr(), _stream(part))
+    return y
+
+
 def attn_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                  pos: torch.Tensor, scale: float) -> torch.Tensor:
     """q [B, H, S, D] (query s at position pos[s]) against cache keys 0..pos[s] -> [B, S, H * D]

@@ -312,8 +312,16 @@ class Attention(nn.Module):
                 x = kernels.rmsnorm(x, norm.weight, norm.eps)
             q = kernels.rope_kv(self.wqkv(x), freqs_table, input_pos, kv.k_cache, kv.v_cache,
                                 self.n_head)
-        y = kernels.attn_decode(q, kv.k_cache, kv.v_cache, input_pos,
-                                1.0 / math.sqrt(self.head_dim))
+        scale = 1.0 / math.sqrt(self.head_dim)
+        # int4 wo at batch 1: the attention split over key ranges (more workgroups than heads),
+        # its merge folded into wo's x load (one launch each, as the unsplit pair)
+        p4 = _int4_parts(self.wo)
+        if (p4 is not None and kernels.ATTN_SPLITS and q.shape[0] == 1 and self.head_dim == 128
+                and kv.k_cache.shape[2] <= kernels.ATTN_SPLIT_MAX_T):
+            part = kernels.attn_decode_split(q, kv.k_cache, kv.v_cache, input_pos, scale,
+                                             kernels.ATTN_SPLITS)
+            return kernels.int4_attn_out(part, self.n_head, *p4, residual=residual)
+        y = kernels.attn_decode(q, kv.k_cache, kv.v_cache, input_pos, scale)
         return _linear_plus(y, self.wo, residual)
 
 
