@@ -89,11 +89,13 @@ __device__ __forceinline__ uint32_t rmsnorm_pair(uint32_t xv, uint32_t wv, float
 // NPT > 0 enables the RMSNorm prologue with NPT 16-B pieces of x per thread (PRO).
 // MRG > 0 (with NPT): x is the merge of MRG split-attention partials per head (fu.merge; head_dim
 // 128), formed in the prologue instead of the RMSNorm: tao_int4wo_attn_out_bf16.
-template <int MT, int RPW, int WPE, bool PAIR, int NPT = 0, int EPI = kEpiNone, int MRG = 0>
-__global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
+// The body of one workgroup: rows row_base + rg RPW .. of row group rg (int4wo_gemv_kernel and
+// the tail-light kernel below call it).
+template <int MT, int RPW, bool PAIR, int NPT = 0, int EPI = kEpiNone, int MRG = 0>
+__device__ __forceinline__ void gemv_body(
     const uint16_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
     const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K, int gshift,
-    int Wk, int G, int S, GemvFuse fu) {
+    int Wk, int G, int S, const GemvFuse& fu, int row_base) {
   constexpr bool PRO = NPT > 0;
   static_assert(MRG == 0 || (PRO && EPI == kEpiNone && MT == 1), "merge prologue: M == 1, NPT");
   static_assert(!(PRO || EPI) || (MT == 1 && RPW % 2 == 0), "fusions are M == 1, row pairs");
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int wk = wave % Wk;
   const int rg = wave / Wk;
-  const int row0 = (blockIdx.x * G + rg) * RPW;
+  const int row0 = row_base + rg * RPW;
   const int nchunk = K >> 5;               // 32-k chunks per row
   const int ngroups = K >> (5 + gshift);   // quantisation groups per row
 
@@ -503,6 +505,31 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
   }
 }
 
+template <int MT, int RPW, int WPE, bool PAIR, int NPT = 0, int EPI = kEpiNone, int MRG = 0>
+__global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
+    const uint16_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
+    const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K, int gshift,
+    int Wk, int G, int S, GemvFuse fu) {
+  gemv_body<MT, RPW, PAIR, NPT, EPI, MRG>(x, wq, sz, bias, y, M, N, K, gshift, Wk, G, S, fu,
+                                          (int)blockIdx.x * G * RPW);
+}
+
+// Tail-light M == 1 GEMV (tao_tune_int4_tail): workgroups [0, B1) own G x RPW rows each, the
+// ones dispatched after them G x RPWL rows (RPWL < RPW), so the last-dispatched waves, whose
+// arithmetic and reduction nothing overlaps, carry RPWL / RPW of the work.
+template <int RPW, int RPWL, int WPE, bool PAIR>
+__global__ __launch_bounds__(512, WPE) void int4wo_gemv_tail_kernel(
+    const uint16_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
+    const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K, int gshift,
+    int Wk, int G, int S, GemvFuse fu, int B1) {
+  const int b = (int)blockIdx.x;
+  if (b < B1)
+    gemv_body<1, RPW, PAIR>(x, wq, sz, bias, y, M, N, K, gshift, Wk, G, S, fu, b * G * RPW);
+  else
+    gemv_body<1, RPWL, PAIR>(x, wq, sz, bias, y, M, N, K, gshift, Wk, G, S, fu,
+                             B1 * G * RPW + (b - B1) * G * RPWL);
+}
+
 int gshift_of(int64_t g) {
   switch (g) {
     case 32: return 0;
@@ -602,6 +629,43 @@ M1Shape m1_shape(int N, int S) {
   if (twk > 0) c.sh.wk = twk;
   if (tg > 0) c.sh.g = tg;
   return c;
+}
+
+// The tail-light launch: the last `pct` % of the rows (rounded to whole light workgroups) on
+// workgroups of G x RPWL rows, dispatched after the G x 4-row ones.
+int launch_gemv_tail(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
+                     const uint16_t* bias, uint16_t* y, int N, int K, int gshift, const M1Shape& c,
+                     int pct, int rpwl, hipStream_t stream) {
+  const int nchunk = K / 32;
+  const int S = (nchunk + 63) / 64;
+  const int wk = c.sh.wk < S ? c.sh.wk : S, G = c.sh.g;
+  const int light_rows = G * rpwl;
+  int tail = (int)((int64_t)N * pct / 100);
+  tail = (tail + light_rows - 1) / light_rows * light_rows;
+  if (tail > N) tail = N;
+  const int heavy_rows = G * 4;
+  const int B1 = (N - tail) / heavy_rows;  // heavy workgroups (whole)
+  const int rest = N - B1 * heavy_rows;    // rows left for the light ones
+  const int B2 = (rest + light_rows - 1) / light_rows;
+  const int threads = 64 * wk * G;
+  const size_t lds = (size_t)G * wk * 4 * sizeof(float);
+  const uint4* wq = reinterpret_cast<const uint4*>(packed);
+  const uint32_t* szp = reinterpret_cast<const uint32_t*>(sz);
+  const GemvFuse fu{};
+#define TAO_TAIL(RL, WPE)                                                                       \
+  if (S > wk)                                                                                   \
+    launch((int4wo_gemv_tail_kernel<4, RL, WPE, true>), dim3(B1 + B2), dim3(threads), lds,      \
+           stream, x, wq, szp, bias, y, 1, N, K, gshift, wk, G, S, fu, B1);                    \
+  else                                                                                          \
+    launch((int4wo_gemv_tail_kernel<4, RL, WPE, false>), dim3(B1 + B2), dim3(threads), lds,     \
+           stream, x, wq, szp, bias, y, 1, N, K, gshift, wk, G, S, fu, B1);
+  if (c.occ == 4) {
+    if (rpwl == 1) { TAO_TAIL(1, 4) } else { TAO_TAIL(2, 4) }
+  } else {
+    if (rpwl == 1) { TAO_TAIL(1, 8) } else { TAO_TAIL(2, 8) }
+  }
+#undef TAO_TAIL
+  return check_launch("int4wo_gemv_tail_kernel");
 }
 
 template <int NPT, int EPI>
@@ -709,6 +773,9 @@ int int4wo_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
   if (M <= 1) {
     const M1Shape c = m1_shape(iN, S);
     sh = c.sh;
+    const int tail_frac = tao::tuning().tail_pct, tail_rpw = tao::tuning().tail_rpw;
+    if (tail_frac > 0 && c.rpw == 4 && (tail_rpw == 1 || tail_rpw == 2))
+      return launch_gemv_tail(x, packed, sz, bias, y, iN, iK, gs, c, tail_frac, tail_rpw, stream);
     if (c.rpw == 1) return launch_gemv<1, 1, 8>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
     if (c.rpw == 2) return launch_gemv<1, 2, 8>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
     if (c.rpw == 8) return launch_gemv<1, 8, 4>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
@@ -866,4 +933,13 @@ extern "C" int tao_int4wo_attn_out_bf16(const float* partial, int64_t splits, in
                                    gs, st);
   return tao::launch_attn_out<4>(partial, packed, scales_and_zeros, residual, y, (int)N, (int)K,
                                  gs, st);
+}
+
+extern "C" int tao_tune_int4_tail(int pct, int light_rows_per_wave) {
+  TAO_CHECK_ARG(pct >= 0 && pct <= 100, "tune: int4_tail pct must be 0..100");
+  TAO_CHECK_ARG(light_rows_per_wave == 0 || light_rows_per_wave == 1 || light_rows_per_wave == 2,
+                "tune: int4_tail light rows per wave must be 0, 1 or 2");
+  tao::tuning().tail_pct = pct;
+  tao::tuning().tail_rpw = light_rows_per_wave;
+  return TAO_OK;
 }
