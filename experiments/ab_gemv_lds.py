@@ -1,10 +1,10 @@
-"""A/B of the tail-light int4 M = 1 GEMV (tao_tune_int4_tail) on the bench step's 4-row shapes:
-per shape, 32 launches over distinct weights (past the MALL) in one HIP graph, µs per launch
-from HIP events on the replay stream; each setting's output checked bit-identical to the
-built-in launch (the per-row sums do not depend on which workgroup owns a row). Settings are
-interleaved and repeated (--passes) so box drift shows. One JSON line per (shape, setting, pass).
+"""Occupancy cap of the int4 M = 1 GEMV by reserved LDS (tao_tune_int4_lds): per shape, 32
+launches over distinct weights (past the MALL) in one HIP graph, µs per launch from HIP events on
+the replay stream; settings interleaved and repeated (--passes); outputs checked bit-identical to
+the built-in launch (same launch shape, only residency changes). One JSON line per (shape,
+setting, pass).
 
-    python experiments/ab_gemv_tail.py [--settings 0:0,10:1,10:2,20:2] [--passes 2]
+    python experiments/ab_gemv_lds.py [--lds 0,27000,40960,54000,81920] [--passes 2]
 """
 import argparse
 import json
@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.join(ROOT, "torchao-fork_amd"))
 
 from torchao import _lib  # noqa: E402
 
-SHAPES = [(28672, 4096), (4096, 14336), (128256, 4096), (14336, 4096)]
+SHAPES = [(28672, 4096), (4096, 14336), (6144, 4096), (4096, 4096), (128256, 4096)]
 
 
 def graph_us(fn, n, reps=20):
@@ -42,13 +42,13 @@ def graph_us(fn, n, reps=20):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--settings", default="0:0,5:1,10:1,10:2,20:2,30:2")
+    ap.add_argument("--lds", default="0,20480,27000,32768,40960,54000,81920")
     ap.add_argument("--passes", type=int, default=2)
     ap.add_argument("--shapes", default="")
     a = ap.parse_args()
     dev = torch.device("cuda")
     lib = _lib.lib()
-    settings = [tuple(int(v) for v in t.split(":")) for t in a.settings.split(",")]
+    settings = [int(v) for v in a.lds.split(",")]
     shapes = ([tuple(int(v) for v in t.split("x")) for t in a.shapes.split(",")] if a.shapes
               else SHAPES)
     gen = torch.Generator(device=dev).manual_seed(0)
@@ -72,19 +72,18 @@ def main():
 
         ref = None
         for ps in range(a.passes):
-            for pct, rl in settings:
-                _lib.call("tao_tune_int4_tail", pct, rl)
+            for lds in settings:
+                _lib.call("tao_tune_int4_lds", lds)
                 us = graph_us(run, copies)
                 run()
                 torch.cuda.synchronize()
                 out = torch.stack([y.clone() for y in ys])
                 if ref is None:
                     ref = out
-                same = bool(torch.equal(out, ref))
-                print(json.dumps({"N": N, "K": K, "tail_pct": pct, "light_rpw": rl, "pass": ps,
-                                  "us": round(us, 3), "launches": copies,
-                                  "bit_identical": same}), flush=True)
-        _lib.call("tao_tune_int4_tail", 0, 0)
+                print(json.dumps({"N": N, "K": K, "lds": lds, "pass": ps, "us": round(us, 3),
+                                  "launches": copies, "bit_identical": bool(torch.equal(out, ref))}),
+                      flush=True)
+        _lib.call("tao_tune_int4_lds", 0)
         del ws, ys
 
 

@@ -11,6 +11,7 @@
 #   round_end TAG                tests + smoke + bench + prof (experiments/round_end.sh)
 #   pmc_prefill TAG              counter passes of the M = 128 prefill GEMMs (pmc_prefill.sh)
 #   py TAG SCRIPT [args]         python experiments/SCRIPT args > gpurun_out/TAG.jsonl
+#   rehearse TAG P               bench.py --gpus P --backend gloo on this one GPU (all ranks on it)
 #   ab TAG LIB_B SCRIPT [args]   same-box A/B: SCRIPT with the in-tree library, then with LIB_B
 #                                (TORCHAO_MI355X_LIB), alternated twice -> gpurun_out/TAG.jsonl
 # Several recipes in one call: separate them with "--", e.g.
@@ -65,6 +66,12 @@ run_one() {
           >> $O/$tag.jsonl 2>> $O/$tag.err || return $?
       done
       tail -c 1500 $O/$tag.jsonl ;;
+    rehearse)  # rehearse TAG P: bench.py's P-rank path on this one GPU (gloo, all ranks on card 0)
+      local P=$1
+      timeout -k 10 1100 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$P" \
+        --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus "$P" --backend gloo \
+        --steps 3 --warmup 1 > $O/rehearsal_$tag.jsonl 2> $O/rehearsal_$tag.err
+      local rc=$?; grep '^{' $O/rehearsal_$tag.jsonl | head -c 800; echo; return $rc ;;
     *)
       echo "unknown recipe $recipe" >&2; return 2 ;;
   esac

@@ -53,10 +53,10 @@ int tao_tune_cnt_stride(int stride);
  * = minimum waves per SIMD the register budget targets (rows_per_wave 4 only).
  * 0 for any field keeps the built-in choice; all zeros restores the defaults. */
 int tao_tune_int4_gemv(int rows_per_wave, int waves_k, int row_groups, int occupancy);
-/* Tail-light M == 1 int4 GEMV (the 4-rows-per-wave shapes): the last `pct` % of the rows go to
- * workgroups of light_rows_per_wave (1 or 2) rows per wave, dispatched after the 4-row ones, so
- * the final wave round carries less arithmetic. 0 = off (built-in). Calling thread only. */
-int tao_tune_int4_tail(int pct, int light_rows_per_wave);
+/* int4 GEMV launches: reserve at least `bytes` of LDS per workgroup (0 = built-in: what the kernel
+ * uses), which caps the workgroups resident per CU at 160 KiB / bytes and with them the weight
+ * bytes each CU has in flight. Calling thread only; for measurement. */
+int tao_tune_int4_lds(int bytes);
 
 /* Tuning hook: the weight-only linears (int4 and int8) use the GEMV kernels for M <= max_gemv_m
  * and the MFMA skinny GEMM above it. 0 restores the built-in crossover (M <= 2, or M <= 4 for

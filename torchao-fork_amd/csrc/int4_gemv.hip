@@ -89,8 +89,8 @@ __device__ __forceinline__ uint32_t rmsnorm_pair(uint32_t xv, uint32_t wv, float
 // NPT > 0 enables the RMSNorm prologue with NPT 16-B pieces of x per thread (PRO).
 // MRG > 0 (with NPT): x is the merge of MRG split-attention partials per head (fu.merge; head_dim
 // 128), formed in the prologue instead of the RMSNorm: tao_int4wo_attn_out_bf16.
-// The body of one workgroup: rows row_base + rg RPW .. of row group rg (int4wo_gemv_kernel and
-// the tail-light kernel below call it).
+// The body of one workgroup: rows row_base + rg RPW .. of row group rg (int4wo_gemv_kernel
+// calls it).
 template <int MT, int RPW, bool PAIR, int NPT = 0, int EPI = kEpiNone, int MRG = 0>
 __device__ __forceinline__ void gemv_body(
     const uint16_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
@@ -514,22 +514,6 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
                                           (int)blockIdx.x * G * RPW);
 }
 
-// Tail-light M == 1 GEMV (tao_tune_int4_tail): workgroups [0, B1) own G x RPW rows each, the
-// ones dispatched after them G x RPWL rows (RPWL < RPW), so the last-dispatched waves, whose
-// arithmetic and reduction nothing overlaps, carry RPWL / RPW of the work.
-template <int RPW, int RPWL, int WPE, bool PAIR>
-__global__ __launch_bounds__(512, WPE) void int4wo_gemv_tail_kernel(
-    const uint16_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
-    const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K, int gshift,
-    int Wk, int G, int S, GemvFuse fu, int B1) {
-  const int b = (int)blockIdx.x;
-  if (b < B1)
-    gemv_body<1, RPW, PAIR>(x, wq, sz, bias, y, M, N, K, gshift, Wk, G, S, fu, b * G * RPW);
-  else
-    gemv_body<1, RPWL, PAIR>(x, wq, sz, bias, y, M, N, K, gshift, Wk, G, S, fu,
-                             B1 * G * RPW + (b - B1) * G * RPWL);
-}
-
 int gshift_of(int64_t g) {
   switch (g) {
     case 32: return 0;
@@ -563,9 +547,13 @@ int launch_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
   const int grid = (N + rows_per_wg - 1) / rows_per_wg;
   const int threads = 64 * wk * sh.g;
   constexpr bool PRO = NPT > 0;
-  const size_t lds = PRO ? (((size_t)sh.g * wk * RPW * MT + 8 + 3) & ~(size_t)3) * sizeof(float) +
-                               (size_t)K * 2
-                         : (size_t)sh.g * wk * RPW * MT * sizeof(float);
+  size_t lds = PRO ? (((size_t)sh.g * wk * RPW * MT + 8 + 3) & ~(size_t)3) * sizeof(float) +
+                         (size_t)K * 2
+                   : (size_t)sh.g * wk * RPW * MT * sizeof(float);
+  // tao_tune_int4_lds: dynamic LDS of at least this many bytes per workgroup, which caps the
+  // workgroups resident per CU (160 KiB / bytes) and so the weight bytes in flight per CU
+  if (tao::tuning().gemv_lds > 0 && (size_t)tao::tuning().gemv_lds > lds)
+    lds = (size_t)tao::tuning().gemv_lds;
   if (S > wk)
     launch((int4wo_gemv_kernel<MT, RPW, WPE, true, NPT, EPI, MRG>), dim3(grid), dim3(threads), lds,
            stream, x, reinterpret_cast<const uint4*>(packed),
@@ -629,43 +617,6 @@ M1Shape m1_shape(int N, int S) {
   if (twk > 0) c.sh.wk = twk;
   if (tg > 0) c.sh.g = tg;
   return c;
-}
-
-// The tail-light launch: the last `pct` % of the rows (rounded to whole light workgroups) on
-// workgroups of G x RPWL rows, dispatched after the G x 4-row ones.
-int launch_gemv_tail(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
-                     const uint16_t* bias, uint16_t* y, int N, int K, int gshift, const M1Shape& c,
-                     int pct, int rpwl, hipStream_t stream) {
-  const int nchunk = K / 32;
-  const int S = (nchunk + 63) / 64;
-  const int wk = c.sh.wk < S ? c.sh.wk : S, G = c.sh.g;
-  const int light_rows = G * rpwl;
-  int tail = (int)((int64_t)N * pct / 100);
-  tail = (tail + light_rows - 1) / light_rows * light_rows;
-  if (tail > N) tail = N;
-  const int heavy_rows = G * 4;
-  const int B1 = (N - tail) / heavy_rows;  // heavy workgroups (whole)
-  const int rest = N - B1 * heavy_rows;    // rows left for the light ones
-  const int B2 = (rest + light_rows - 1) / light_rows;
-  const int threads = 64 * wk * G;
-  const size_t lds = (size_t)G * wk * 4 * sizeof(float);
-  const uint4* wq = reinterpret_cast<const uint4*>(packed);
-  const uint32_t* szp = reinterpret_cast<const uint32_t*>(sz);
-  const GemvFuse fu{};
-#define TAO_TAIL(RL, WPE)                                                                       \
-  if (S > wk)                                                                                   \
-    launch((int4wo_gemv_tail_kernel<4, RL, WPE, true>), dim3(B1 + B2), dim3(threads), lds,      \
-           stream, x, wq, szp, bias, y, 1, N, K, gshift, wk, G, S, fu, B1);                    \
-  else                                                                                          \
-    launch((int4wo_gemv_tail_kernel<4, RL, WPE, false>), dim3(B1 + B2), dim3(threads), lds,     \
-           stream, x, wq, szp, bias, y, 1, N, K, gshift, wk, G, S, fu, B1);
-  if (c.occ == 4) {
-    if (rpwl == 1) { TAO_TAIL(1, 4) } else { TAO_TAIL(2, 4) }
-  } else {
-    if (rpwl == 1) { TAO_TAIL(1, 8) } else { TAO_TAIL(2, 8) }
-  }
-#undef TAO_TAIL
-  return check_launch("int4wo_gemv_tail_kernel");
 }
 
 template <int NPT, int EPI>
@@ -773,9 +724,6 @@ int int4wo_gemv(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
   if (M <= 1) {
     const M1Shape c = m1_shape(iN, S);
     sh = c.sh;
-    const int tail_frac = tao::tuning().tail_pct, tail_rpw = tao::tuning().tail_rpw;
-    if (tail_frac > 0 && c.rpw == 4 && (tail_rpw == 1 || tail_rpw == 2))
-      return launch_gemv_tail(x, packed, sz, bias, y, iN, iK, gs, c, tail_frac, tail_rpw, stream);
     if (c.rpw == 1) return launch_gemv<1, 1, 8>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
     if (c.rpw == 2) return launch_gemv<1, 2, 8>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
     if (c.rpw == 8) return launch_gemv<1, 8, 4>(x, packed, sz, bias, y, iM, iN, iK, gs, sh, stream);
@@ -935,11 +883,9 @@ extern "C" int tao_int4wo_attn_out_bf16(const float* partial, int64_t splits, in
                                  gs, st);
 }
 
-extern "C" int tao_tune_int4_tail(int pct, int light_rows_per_wave) {
-  TAO_CHECK_ARG(pct >= 0 && pct <= 100, "tune: int4_tail pct must be 0..100");
-  TAO_CHECK_ARG(light_rows_per_wave == 0 || light_rows_per_wave == 1 || light_rows_per_wave == 2,
-                "tune: int4_tail light rows per wave must be 0, 1 or 2");
-  tao::tuning().tail_pct = pct;
-  tao::tuning().tail_rpw = light_rows_per_wave;
+
+extern "C" int tao_tune_int4_lds(int bytes) {
+  TAO_CHECK_ARG(bytes >= 0 && bytes <= 160 * 1024, "tune: int4_lds bytes must be 0..163840");
+  tao::tuning().gemv_lds = bytes;
   return TAO_OK;
 }

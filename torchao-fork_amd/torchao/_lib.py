@@ -39,7 +39,7 @@ _SIGNATURES = {
     "tao_int4wo_linear_rope_kv_bf16": [_p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _i64, _i64,
                                        _i64, _i64, _i64, _i64, _p],
     "tao_tune_int4_gemv": [_int, _int, _int, _int],
-    "tao_tune_int4_tail": [_int, _int],
+    "tao_tune_int4_lds": [_int],
     "tao_tune_linear_crossover": [_int],
     "tao_tune_gemm": [_int, _int, _int],
     "tao_tune_gemm_algo": [_int],

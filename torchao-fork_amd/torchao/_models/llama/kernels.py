@@ -83,8 +83,13 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
 
 # Decode attention split over key ranges (tao_attn_decode_split_bf16) with the merge folded into
 # an int4 wo linear (tao_int4wo_attn_out_bf16): the splits per head (2 or 4; 0 = off, the one-pass
-# kernel then the linear), used for caches of at most ATTN_SPLIT_MAX_T rows.
-ATTN_SPLITS = 2
+# kernel then the linear), taken for caches of ATTN_SPLIT_MIN_T..ATTN_SPLIT_MAX_T rows. Measured
+# per layer (attention + wo, graph of 32 layers; profiles/r5a_attn_pair.jsonl): the split saves
+# 1.1-4.4 us on the attention but the merge prologue costs wo ~1.5 us (every wo workgroup merges
+# all heads' partials), so the pair pays only past ~600 keys: 328 keys one-pass 9.98 us vs
+# 10.33 / 11.16 split 2 / 4; 512 keys 10.98 vs 10.83 / 11.38; 900 keys 14.29 vs 12.69 / 12.30.
+ATTN_SPLITS = 4
+ATTN_SPLIT_MIN_T = 768
 ATTN_SPLIT_MAX_T = 1024
 PART_STRIDE = 132  # fp32 per (head, split) record: o[128], m, l, 2 pad
 

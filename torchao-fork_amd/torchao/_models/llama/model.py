@@ -316,8 +316,9 @@ class Attention(nn.Module):
         # int4 wo at batch 1: the attention split over key ranges (more workgroups than heads),
         # its merge folded into wo's x load (one launch each, as the unsplit pair)
         p4 = _int4_parts(self.wo)
+        T = kv.k_cache.shape[2]
         if (p4 is not None and kernels.ATTN_SPLITS and q.shape[0] == 1 and self.head_dim == 128
-                and kv.k_cache.shape[2] <= kernels.ATTN_SPLIT_MAX_T):
+                and kernels.ATTN_SPLIT_MIN_T <= T <= kernels.ATTN_SPLIT_MAX_T):
             part = kernels.attn_decode_split(q, kv.k_cache, kv.v_cache, input_pos, scale,
                                              kernels.ATTN_SPLITS)
             return kernels.int4_attn_out(part, self.n_head, *p4, residual=residual)

@@ -16,7 +16,7 @@ from torchao import _lib
 # keyword -> (entry point, number of int arguments)
 _KNOBS = {
     "int4_gemv": ("tao_tune_int4_gemv", 4),
-    "int4_tail": ("tao_tune_int4_tail", 2),
+    "int4_lds": ("tao_tune_int4_lds", 1),
     "linear_crossover": ("tao_tune_linear_crossover", 1),
     "gemm": ("tao_tune_gemm", 3),
     "gemm_algo": ("tao_tune_gemm_algo", 1),
