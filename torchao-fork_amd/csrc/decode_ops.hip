@@ -53,18 +53,97 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
-// ---- RMSNorm: one workgroup per row, 8 bf16 per thread per pass --------------------------------
-__global__ __launch_bounds__(256) void rmsnorm_kernel(const uint16_t* __restrict__ x,
-                                                      const uint16_t* __restrict__ w,
-                                                      uint16_t* __restrict__ y, int D, float eps) {
+// ---- RMSNorm (+ residual add): one workgroup per row, 8 bf16 per 16-B piece ---------------------
+// The row's pieces stay in registers from the load to the normalised store (NP pieces per thread,
+// D <= 8 NP 256), so a row costs one global round trip, the block sum and the stores; the first
+// versions re-read x (and the residual) after the block sum, a second dependent round trip in
+// every launch. ADD: h = bf16(x + r) stored first (torch's bf16 `x + r`: fp32 sum, RNE), then the
+// norm of h; the pair is bit-identical to the two launches it replaces. y = bf16(bf16(h * r) * w).
+__device__ __forceinline__ uint32_t add_pair_bf16(uint32_t a, uint32_t b) {
+  const float lo = bf16lo_to_f32(a) + bf16lo_to_f32(b);
+  const float hi = bf16hi_to_f32(a) + bf16hi_to_f32(b);
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+
+template <int NP, bool ADD>
+__global__ __launch_bounds__(256) void rmsnorm_rows_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+    const uint16_t* __restrict__ w, uint16_t* __restrict__ h, uint16_t* __restrict__ y, int D,
+    float eps) {
   __shared__ float red[4];
-  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)blockIdx.x * D);
+  const size_t row = (size_t)blockIdx.x * D;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + row);
+  const uint4* rr = reinterpret_cast<const uint4*>(ADD ? res + row : x + row);
   const uint4* wr = reinterpret_cast<const uint4*>(w);
-  uint4* yr = reinterpret_cast<uint4*>(y + (size_t)blockIdx.x * D);
   const int nv = D / 8;
+  uint4 v[NP], g[NP];
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {  // every load of the row (and its norm weights) in one round trip
+    const int i = threadIdx.x + 256 * u, ic = i < nv ? i : nv - 1;
+    v[u] = xr[ic];
+    g[u] = wr[ic];
+    if constexpr (ADD) {
+      const uint4 b = rr[ic];
+      v[u] = make_uint4(add_pair_bf16(v[u].x, b.x), add_pair_bf16(v[u].y, b.y),
+                        add_pair_bf16(v[u].z, b.z), add_pair_bf16(v[u].w, b.w));
+    }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    if (i >= nv) continue;
+    if constexpr (ADD) reinterpret_cast<uint4*>(h + row)[i] = v[u];
+    const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a = bf16lo_to_f32(d[j]), b = bf16hi_to_f32(d[j]);
+      ss = fmaf(a, a, fmaf(b, b, ss));
+    }
+  }
+  const float r = rsqrtf(block_sum(ss, red) / (float)D + eps);
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    if (i >= nv) continue;
+    const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+    const uint32_t e[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float lo = round_bf16(bf16lo_to_f32(d[j]) * r) * bf16lo_to_f32(e[j]);
+      const float hi = round_bf16(bf16hi_to_f32(d[j]) * r) * bf16hi_to_f32(e[j]);
+      o[j] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+    }
+    reinterpret_cast<uint4*>(y + row)[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// Rows wider than 8 x 4 x 256 bf16: the streaming form (x and the residual re-read after the sum)
+template <bool ADD>
+__global__ __launch_bounds__(256) void rmsnorm_wide_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+    const uint16_t* __restrict__ w, uint16_t* __restrict__ h, uint16_t* __restrict__ y, int D,
+    float eps) {
+  __shared__ float red[4];
+  const size_t row = (size_t)blockIdx.x * D;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + row);
+  const uint4* rr = reinterpret_cast<const uint4*>(ADD ? res + row : x + row);
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
+  const int nv = D / 8;
+  auto piece = [&](int i) __attribute__((always_inline)) {
+    uint4 a = xr[i];
+    if constexpr (ADD) {
+      const uint4 b = rr[i];
+      a = make_uint4(add_pair_bf16(a.x, b.x), add_pair_bf16(a.y, b.y), add_pair_bf16(a.z, b.z),
+                     add_pair_bf16(a.w, b.w));
+    }
+    return a;
+  };
   float ss = 0.f;
   for (int i = threadIdx.x; i < nv; i += 256) {
-    const uint4 v = xr[i];
+    const uint4 v = piece(i);
+    if constexpr (ADD) reinterpret_cast<uint4*>(h + row)[i] = v;
     const uint32_t d[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -74,7 +153,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const uint16_t* __restrict
   }
   const float r = rsqrtf(block_sum(ss, red) / (float)D + eps);
   for (int i = threadIdx.x; i < nv; i += 256) {
-    const uint4 v = xr[i], g = wr[i];
+    const uint4 v = piece(i), g = wr[i];
     const uint32_t d[4] = {v.x, v.y, v.z, v.w}, e[4] = {g.x, g.y, g.z, g.w};
     uint32_t o[4];
 #pragma unroll
@@ -83,59 +162,19 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const uint16_t* __restrict
       const float hi = round_bf16(bf16hi_to_f32(d[j]) * r) * bf16hi_to_f32(e[j]);
       o[j] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
     }
-    yr[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    reinterpret_cast<uint4*>(y + row)[i] = make_uint4(o[0], o[1], o[2], o[3]);
   }
 }
 
-// ---- residual add + RMSNorm (prefill): h = bf16(x + r) stored, then y = RMSNorm(h) -----------
-// The add rounds as torch's bf16 `x + r` does (fp32 sum, RNE), the norm as rmsnorm_kernel, so the
-// pair is bit-identical to the two launches it replaces. One workgroup per row.
-__device__ __forceinline__ uint32_t add_pair_bf16(uint32_t a, uint32_t b) {
-  const float lo = bf16lo_to_f32(a) + bf16lo_to_f32(b);
-  const float hi = bf16hi_to_f32(a) + bf16hi_to_f32(b);
-  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
-}
-
-__global__ __launch_bounds__(256) void add_rmsnorm_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
-    const uint16_t* __restrict__ w, uint16_t* __restrict__ h, uint16_t* __restrict__ y, int D,
-    float eps) {
-  __shared__ float red[4];
-  const size_t row = (size_t)blockIdx.x * D;
-  const uint4* xr = reinterpret_cast<const uint4*>(x + row);
-  const uint4* rr = reinterpret_cast<const uint4*>(res + row);
-  const uint4* wr = reinterpret_cast<const uint4*>(w);
-  uint4* hr = reinterpret_cast<uint4*>(h + row);
-  uint4* yr = reinterpret_cast<uint4*>(y + row);
-  const int nv = D / 8;
-  float ss = 0.f;
-  for (int i = threadIdx.x; i < nv; i += 256) {
-    const uint4 a = xr[i], b = rr[i];
-    const uint4 v = make_uint4(add_pair_bf16(a.x, b.x), add_pair_bf16(a.y, b.y),
-                               add_pair_bf16(a.z, b.z), add_pair_bf16(a.w, b.w));
-    hr[i] = v;
-    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float lo = bf16lo_to_f32(d[j]), hi = bf16hi_to_f32(d[j]);
-      ss = fmaf(lo, lo, fmaf(hi, hi, ss));
-    }
-  }
-  const float r = rsqrtf(block_sum(ss, red) / (float)D + eps);
-  for (int i = threadIdx.x; i < nv; i += 256) {
-    const uint4 a = xr[i], b = rr[i], g = wr[i];
-    const uint32_t d[4] = {add_pair_bf16(a.x, b.x), add_pair_bf16(a.y, b.y),
-                           add_pair_bf16(a.z, b.z), add_pair_bf16(a.w, b.w)};
-    const uint32_t e[4] = {g.x, g.y, g.z, g.w};
-    uint32_t o[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float lo = round_bf16(bf16lo_to_f32(d[j]) * r) * bf16lo_to_f32(e[j]);
-      const float hi = round_bf16(bf16hi_to_f32(d[j]) * r) * bf16hi_to_f32(e[j]);
-      o[j] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
-    }
-    yr[i] = make_uint4(o[0], o[1], o[2], o[3]);
-  }
+template <bool ADD>
+void launch_rmsnorm(const uint16_t* x, const uint16_t* res, const uint16_t* w, uint16_t* h,
+                    uint16_t* y, int64_t rows, int64_t dim, float eps, hipStream_t st) {
+  const dim3 grid((unsigned)rows), blk(256);
+  const int D = (int)dim, nv = D / 8;
+  if (nv <= 256) launch(rmsnorm_rows_kernel<1, ADD>, grid, blk, 0, st, x, res, w, h, y, D, eps);
+  else if (nv <= 512) launch(rmsnorm_rows_kernel<2, ADD>, grid, blk, 0, st, x, res, w, h, y, D, eps);
+  else if (nv <= 1024) launch(rmsnorm_rows_kernel<4, ADD>, grid, blk, 0, st, x, res, w, h, y, D, eps);
+  else launch(rmsnorm_wide_kernel<ADD>, grid, blk, 0, st, x, res, w, h, y, D, eps);
 }
 
 // ---- RoPE on q, k + KV-cache write: one workgroup per token, one thread per pair -------------
@@ -618,8 +657,7 @@ int tao_rmsnorm_bf16(const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t 
   TAO_CHECK_ALIGN(x, 16, "x");
   TAO_CHECK_ALIGN(w, 16, "w");
   TAO_CHECK_ALIGN(y, 16, "y");
-  launch(rmsnorm_kernel, dim3((unsigned)rows), dim3(256), 0, as_stream(stream), x, w, y,
-         (int)dim, eps);
+  launch_rmsnorm<false>(x, nullptr, w, nullptr, y, rows, dim, eps, as_stream(stream));
   return check_launch("rmsnorm_kernel");
 }
 
@@ -633,8 +671,7 @@ int tao_add_rmsnorm_bf16(const uint16_t* x, const uint16_t* res, const uint16_t*
   TAO_CHECK_ALIGN(w, 16, "w");
   TAO_CHECK_ALIGN(h, 16, "h");
   TAO_CHECK_ALIGN(y, 16, "y");
-  launch(add_rmsnorm_kernel, dim3((unsigned)rows), dim3(256), 0, as_stream(stream), x, res, w, h,
-         y, (int)dim, eps);
+  launch_rmsnorm<true>(x, res, w, h, y, rows, dim, eps, as_stream(stream));
   return check_launch("add_rmsnorm_kernel");
 }
 
