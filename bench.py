@@ -1218,6 +1218,7 @@ def main():
         unfused = unfused_record(cfg, g, device, args.steps)
     config5 = None
     n_launches, has_graph = len(plan), graph is not None
+    par_desc = parallelism_desc(st, policy) if P > 1 else "single-gpu"
     if args.model == "8b" and not args.no_config5:
         # release the 8B step's weights first (the 70B step needs 43 GB / P per rank): the
         # plan / inputs / graphs bound here hold them too, so drop those references before
@@ -1260,7 +1261,7 @@ def main():
                 "seq_len": 1,
                 "group_size": g,
                 "bytes_per_step": bytes_per_step,
-                "parallelism": parallelism_desc(st, policy) if P > 1 else "single-gpu",
+                "parallelism": par_desc,
                 "hip_graph": has_graph,
             },
             "roofline": {

@@ -87,10 +87,12 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
 # per layer (attention + wo, graph of 32 layers; profiles/r5a_attn_pair.jsonl): the split saves
 # 1.1-4.4 us on the attention but the merge prologue costs wo ~1.5 us (every wo workgroup merges
 # all heads' partials), so the pair pays only past ~600 keys: 328 keys one-pass 9.98 us vs
-# 10.33 / 11.16 split 2 / 4; 512 keys 10.98 vs 10.83 / 11.38; 900 keys 14.29 vs 12.69 / 12.30.
+# 10.33 / 11.16 split 2 / 4; 512 keys 10.98 vs 10.83 / 11.38; 900 keys 14.29 vs 12.69 / 12.30;
+# past 1024 rows against the two-launch chunk split: 1500 keys 23.3 vs 14.5, 3000 keys 35.1 vs
+# 18.5 (split 4; profiles/r5b_attn_pair_long.jsonl).
 ATTN_SPLITS = 4
 ATTN_SPLIT_MIN_T = 768
-ATTN_SPLIT_MAX_T = 1024
+ATTN_SPLIT_MAX_T = 8192
 PART_STRIDE = 132  # fp32 per (head, split) record: o[128], m, l, 2 pad
 
 
