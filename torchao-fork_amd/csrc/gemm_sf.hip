@@ -318,10 +318,10 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
     constexpr int r = decltype(rc)::value;
     uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * STAGE;
     if constexpr (r < PX / kWaves) {
-      dma_lds<16>(xrs, dv[r], (uint32_t)st * P::kXRow, base + dd[r]);
+      dma_lds_ring<16>(xrs, dv[r], (uint32_t)st * P::kXRow, base + dd[r]);
     } else {
-      if (dk[r] == 1) dma_lds<16, kNT>(wrs, dv[r], pol.wsoff(st), base + dd[r]);
-      else if constexpr (PZ > 0) dma_lds<4, kNT>(zrs, dv[r], pol.zsoff(st), base + dd[r]);
+      if (dk[r] == 1) dma_lds_ring<16, kNT>(wrs, dv[r], pol.wsoff(st), base + dd[r]);
+      else if constexpr (PZ > 0) dma_lds_ring<4, kNT>(zrs, dv[r], pol.zsoff(st), base + dd[r]);
     }
   };
   auto issue = [&](int st, int buf) __attribute__((always_inline)) {

@@ -179,6 +179,35 @@ constexpr int kWave = 64;
 // touches and waits vmcnt(0) before the first read of every step, which drains a ring. The caller
 // waits for its DMAs by hand (counted vmcnt before a barrier). M0 is saved and restored.
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+// dma_lds_ring: the same DMA without the asm's "memory" clobber, for rings whose every refill
+// targets a stage no ds_read of the current barrier interval touches (the stage was last read
+// before the barrier_lgkm() that precedes the refill, and barrier_lgkm() is itself a compiler
+// memory barrier; volatile asm statements keep their order). The clobber otherwise pins every
+// LDS fragment read of the step on one side of every DMA piece, so hipcc cannot issue a step's
+// reads ahead of the MFMAs that need them.
+template <int SIZE, int AUX = 0>
+__device__ __forceinline__ void dma_lds_ring(Rsrc r, uint32_t voff, uint32_t soff, void* dst) {
+  static_assert((SIZE == 16 || SIZE == 4) && (AUX == 0 || AUX == kNT), "dma_lds: 16 / 4 B, nt or not");
+  const uint32_t lds_addr = (uint32_t)(uintptr_t)(lds_ptr_t)dst;
+  uint32_t keep;
+  if constexpr (SIZE == 16 && AUX == 0)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "s"(lds_addr), "v"(voff), "s"(r), "s"(soff));
+  else if constexpr (SIZE == 16)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %2, %3, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "s"(lds_addr), "v"(voff), "s"(r), "s"(soff));
+  else if constexpr (AUX == 0)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "buffer_load_dword %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "s"(lds_addr), "v"(voff), "s"(r), "s"(soff));
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "buffer_load_dword %2, %3, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "s"(lds_addr), "v"(voff), "s"(r), "s"(soff));
+}
+
 template <int SIZE, int AUX = 0>
 __device__ __forceinline__ void dma_lds(Rsrc r, uint32_t voff, uint32_t soff, void* dst) {
   static_assert((SIZE == 16 || SIZE == 4) && (AUX == 0 || AUX == kNT), "dma_lds: 16 / 4 B, nt or not");
