@@ -45,14 +45,6 @@
 #ifndef TAO_SF32_IL
 #define TAO_SF32_IL 1
 #endif
-// 1: software-pipelined sub-steps (KH = 1): A fragments two k sub-steps ahead, the B fragment of
-// sub-step k + 1 dequantised while sub-step k's MFMAs run, and the issue order pinned per
-// sub-step by sched_group_barrier (4 DS reads, then MFMA / 6 VALU alternating), so no MFMA waits
-// on the LDS read or the dequantisation it consumes. 0: the plain order (A one sub-step ahead,
-// dequantisation just before its MFMAs).
-#ifndef TAO_SF32_PIPE
-#define TAO_SF32_PIPE 1
-#endif
 
 namespace tao {
 namespace {
@@ -252,48 +244,6 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
       }
       sf[u] = bf16lo_to_f32(zw);
       cf[u] = bf16hi_to_f32(zw) - 8.f * sf[u];
-    }
-    if constexpr (TAO_SF32_PIPE != 0 && KH == 1 && TAO_SF32_DEBUG == 0) {
-      bf16x8_t af[3][4];
-#pragma unroll
-      for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const int m = 32 * mt + r32;
-          af[p][mt] = __builtin_bit_cast(bf16x8_t, img[m * 16 + xpos(m, 8 * h + p)]);
-        }
-      bf16x8_t bfc = deq8s(wd[0], sf[0], cf[0]);
-      sfor<0, 8>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        if constexpr (k + 2 < 8) {
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt) {
-            const int m = 32 * mt + r32;
-            af[(k + 2) % 3][mt] = __builtin_bit_cast(bf16x8_t, img[m * 16 + xpos(m, 8 * h + k + 2)]);
-          }
-        }
-        // the reads stay above this sub-step's MFMAs (hipcc otherwise sinks each one to just before
-        // its MFMA, which then waits out the LDS latency)
-        __builtin_amdgcn_sched_barrier(0);
-        bf16x8_t bfn = bfc;
-        if constexpr (k + 1 < 8) bfn = deq8s(wd[k + 1], sf[(k + 1) >> 2], cf[(k + 1) >> 2]);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-          acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[k % 3][mt], bfc, acc[mt], 0, 0, 0);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // up to 6 VALU
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        bfc = bfn;
-        if constexpr (ISS && IL)  // DMA pieces r with r KS / R == k after sub-step k's MFMAs
-          sfor<0, R>([&](auto rc) {
-            constexpr int r = decltype(rc)::value;
-            if constexpr (r * KS / R == k) issue_piece(rc, st, ibuf);
-          });
-      });
-      return;
     }
     // A fragments of ks and ks + 1 in flight while ks's MFMAs run
     bf16x8_t af[2][4];
