@@ -45,6 +45,12 @@
 #ifndef TAO_SF32_IL
 #define TAO_SF32_IL 1
 #endif
+// Timing-only build (experiments/sf32_steps.py; never the shipped library): s_memtime (shader
+// clock) of every wave of workgroups 0..7 at each k step: step top, own DMAs landed, barrier
+// passed, MFMAs issued; and the s_memrealtime / s_memtime pair at entry and exit.
+#ifndef TAO_SF32_STEPSTAMPS
+#define TAO_SF32_STEPSTAMPS 0
+#endif
 
 namespace tao {
 namespace {
@@ -58,6 +64,10 @@ constexpr int kBM = 128;
 constexpr int kXRow = 256, kWRow = 64, kZRow = 16;  // bytes per row per 128-k step
 
 __device__ unsigned g_sf32_err = 0;
+#if TAO_SF32_STEPSTAMPS
+// [wg 8][wave 8][step 64][4] + [wg 8][wave 8][4] (entry / exit memtime, memrealtime)
+__device__ unsigned long long g_sf32_ts[8 * 8 * 64 * 4 + 8 * 8 * 4];
+#endif
 
 template <int I, int N, class F>
 __device__ __forceinline__ void sfor(F&& f) {
@@ -297,17 +307,48 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
     if (p < J) issue(s0 + p, p);
   const int jiss = TAO_SF32_DEBUG == 3 ? 0 : J - (NS - 1);  // steps that issue a stage ahead
   int j = 0;
+#if TAO_SF32_STEPSTAMPS
+  const int flat_wg = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+  const bool stamp = flat_wg < 8 && lane == 0;
+  unsigned long long* tsb = g_sf32_ts + ((size_t)flat_wg * 8 + wave) * 64 * 4;
+  unsigned long long* tse = g_sf32_ts + 8 * 8 * 64 * 4 + ((size_t)flat_wg * 8 + wave) * 4;
+  if (stamp) {
+    tse[0] = __builtin_amdgcn_s_memtime();
+    tse[1] = __builtin_amdgcn_s_memrealtime();
+  }
+#define SF32_TS(i) \
+  if (stamp && j < 64) tsb[j * 4 + (i)] = __builtin_amdgcn_s_memtime()
+#else
+#define SF32_TS(i) \
+  do {             \
+  } while (0)
+#endif
   for (; j < jiss; ++j) {
+    SF32_TS(0);
     wait_own(NS - 2);
+    SF32_TS(1);
     barrier_lgkm();
+    SF32_TS(2);
     compute(j % NS, std::true_type{}, s0 + j + NS - 1, (j + NS - 1) % NS);
+    SF32_TS(3);
   }
   for (; j < J; ++j) {
     const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
+    SF32_TS(0);
     wait_own(ahead);
+    SF32_TS(1);
     barrier_lgkm();
+    SF32_TS(2);
     compute(j % NS, std::false_type{}, 0, 0);
+    SF32_TS(3);
   }
+#if TAO_SF32_STEPSTAMPS
+  if (stamp) {
+    tse[2] = __builtin_amdgcn_s_memtime();
+    tse[3] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
+#undef SF32_TS
   barrier_lgkm();
   if constexpr (KH == 2) {  // k half 1's accumulators into k half 0's, through LDS
     uint4* red = lds + (cw * 4 * 64 + lane) * 4;  // [cw][t][lane][16 floats]
@@ -516,6 +557,16 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
 #undef SF32_GO
   return check_launch("gemm_sf32_int4_kernel");
 }
+
+#if TAO_SF32_STEPSTAMPS
+extern "C" int tao_debug_sf32_steps(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sf32_ts), sizeof(g_sf32_ts)) != hipSuccess)
+    return TAO_ERR_HIP;
+  static unsigned long long zero[8 * 8 * 64 * 4 + 8 * 8 * 4];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sf32_ts), zero, sizeof(zero)) == hipSuccess ? TAO_OK
+                                                                                    : TAO_ERR_HIP;
+}
+#endif
 
 int sf32_status(unsigned* bits) {
   unsigned v = 0, zero = 0;
