@@ -19,14 +19,17 @@ from torchao import _lib  # noqa: E402
 
 def main():
     path, shape, cfg = sys.argv[1], sys.argv[2], sys.argv[3]
+    loaders = int(sys.argv[4]) if len(sys.argv) > 4 else 0  # tao_tune_gemm_sf_loaders
     M, N, K = (int(v) for v in shape.split("x"))
     cfg = [int(v) for v in cfg.split(",")]
     gen = torch.Generator(device="cuda").manual_seed(0)
     run, copies = (int8_case if path == "int8" else int4_case)(M, N, K, gen)
     sf(2, *cfg)
+    _lib.call("tao_tune_gemm_sf_loaders", loaders)
     us = median(timed(run, copies, 30)) * 1e3
     print(json.dumps({"lib": os.path.basename(os.environ.get("TORCHAO_MI355X_LIB", "shipped")),
-                      "path": path, "shape": shape, "cfg": cfg, "us": round(us, 2)}), flush=True)
+                      "path": path, "shape": shape, "cfg": cfg, "loaders": loaders,
+                      "us": round(us, 2)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -434,3 +434,30 @@ def test_sf32_k_halves(sf, cfg, M, N, K):
         if M <= 128:
             sw = kernels.int4_linear_swiglu(xd, packed, sz, g)
             assert sw is not None and torch.equal(sw, kernels.silu_mul(y))
+
+
+@pytest.mark.parametrize("cfg", [(128, 1, 1, 3, 0, 0), (128, 1, 4, 3, 0, 0), (64, 1, 2, 3, 0, 0),
+                                 (128, 1, 2, 3, 5, 0)])
+@pytest.mark.parametrize("M,N,K", [(128, 4096, 4096), (100, 640, 3072), (200, 384, 2048),
+                                   (128, 28672, 4096), (1, 96, 512)])
+def test_sf32_loader_waves_bit_identical(sf, cfg, M, N, K):
+    """Dedicated LDS-DMA loader waves (tao_tune_gemm_sf_loaders 2) change who issues the DMA
+    pieces and when, not what any compute wave reads or sums: outputs bit-identical to the
+    one-wave-per-column-group kernel, its SwiGLU epilogue too, at g = 32 (16-B (scale, zero)
+    pieces) and 128 (4-B pieces), split or not, ragged M / N, several M tiles."""
+    from torchao._models.llama import kernels
+
+    sf(2, *cfg)
+    for g in (32, 128):
+        q, s, z, packed, sz = _int4(N, K, g, seed=N + g)
+        x = oracle.make_activation(M, K, seed=g).to(DEV)
+        _lib.call("tao_tune_gemm_sf_loaders", 1)
+        ref = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)
+        ref_sw = kernels.int4_linear_swiglu(x, packed, sz, g) if M <= 128 else None
+        _lib.call("tao_tune_gemm_sf_loaders", 2)
+        got = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)
+        assert torch.equal(got, ref)
+        if ref_sw is not None:
+            assert torch.equal(kernels.int4_linear_swiglu(x, packed, sz, g), ref_sw)
+        if N <= 4096:
+            assert oracle.rel_l2(got.cpu(), oracle.int4_linear(x.cpu(), q, s, z, g)) < TOL_REF

@@ -1062,6 +1062,13 @@ extern "C" int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages
   return TAO_OK;
 }
 
+// Loader waves of the 32x32x16 int4 kernel: 0 = built-in, 1 = off, 2 = on.
+extern "C" int tao_tune_gemm_sf_loaders(int mode) {
+  TAO_CHECK_ARG(mode >= 0 && mode <= 2, "tune: gemm_sf_loaders must be 0, 1 or 2");
+  tao::tuning().sf_loaders = mode;
+  return TAO_OK;
+}
+
 // Split-K seam of the single-fetch GEMM: -1 = built-in (per routed shape), 0 = fixed reducer,
 // 1 = spread.
 extern "C" int tao_tune_gemm_sf_seam(int seam) {

@@ -120,22 +120,32 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
 // [BN][16 B] image read with one ds_read_b128 per lane (conflict-free: 8 lanes per 128 B); other
 // group sizes take the 4-B DMA of a swizzled image. The DMA pieces cost per instruction
 // (profiles/r4_sf32_dmacost.jsonl), and Z16 takes a quarter of them for the (scale, zero) words.
-template <int WV, int NS, int KH = 1, bool Z16 = false>
-__global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
+// LDW > 0 (KH = 1): LDW dedicated loader waves issue every LDS-DMA piece (they wait for their own
+// pieces, join the step barrier and refill the freed stage) and the WV compute waves only read
+// LDS, dequantise and issue MFMAs. The per-step stamps (TAO_SF32_STEPSTAMPS) put the one-wave
+// kernel at ~2350 of ~2760 cycles per step in its compute phase (32 MFMAs = 1024 cycles), of
+// which the DMA pieces issued between the MFMA sub-steps are ~640 (the no-DMA timing build):
+// a loader wave on each SIMD takes that issue off the MFMA stream (VMEM and VALU / MFMA issue
+// from different waves of a SIMD proceed in parallel).
+template <int WV, int NS, int KH = 1, bool Z16 = false, int LDW = 0>
+__global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
     const uint16_t* __restrict__ x, const uint32_t* __restrict__ wq, const uint32_t* __restrict__ sz,
     int lg, const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K,
     int a_steps, f32x16_t* __restrict__ slab, unsigned* __restrict__ cnt, int fenced, int cs,
     int epi) {
   constexpr int BN = 32 * WV;
-  constexpr int NW = WV * KH;  // waves
-  constexpr bool IL = TAO_SF32_IL != 0 && NS >= 3;
+  constexpr int NW = WV * KH;  // compute waves
+  static_assert(LDW == 0 || KH == 1, "loader waves with one compute wave per column group");
+  constexpr int NWT = NW + LDW;            // waves of the workgroup
+  constexpr int DW = LDW > 0 ? LDW : NW;   // waves that issue the DMA pieces
+  constexpr bool IL = TAO_SF32_IL != 0 && NS >= 3 && LDW == 0;
   constexpr int XB = kBM * kXRow, WB = BN * kWRow, ZB = BN * kZRow;
   constexpr int STAGE = XB + WB + ZB;
   constexpr int PX = XB / 1024, PW = WB / 1024, PZ = Z16 ? ZB / 1024 : ZB / 256;
   constexpr int T = PX + PW + PZ;
-  static_assert(PX % NW == 0 && (!Z16 || ZB % 1024 == 0), "DMA pieces per wave");
-  // piece i = r NW + wave: waves below RFULL issue R pieces per stage, the others R - 1
-  constexpr int R = (T + NW - 1) / NW, RFULL = T - (R - 1) * NW;
+  static_assert(PX % DW == 0 && (!Z16 || ZB % 1024 == 0), "DMA pieces per wave");
+  // piece i = r DW + dma wave: waves below RFULL issue R pieces per stage, the others R - 1
+  constexpr int R = (T + DW - 1) / DW, RFULL = T - (R - 1) * DW;
   // debug 6 / 7 skip each wave's 2 (scale, zero) / 2 W pieces after the prologue
   constexpr bool DSK = (TAO_SF32_DEBUG == 6 || TAO_SF32_DEBUG == 7) && PW == 2 * NW && PZ == 2 * NW;
   constexpr int RW = DSK ? R - 2 : R;
@@ -144,7 +154,9 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cw = wave % WV, kh = wave / WV;  // column group, k half
+  const bool loader = LDW > 0 && wave >= NW;
+  const int dwv = LDW > 0 ? wave - NW : wave;       // index among the DMA-issuing waves
+  const int cw = loader ? 0 : wave % WV, kh = loader ? 0 : wave / WV;  // column group, k half
   const int r32 = lane & 31, h = lane >> 5;
   const int n_blk = blockIdx.x * BN, m_blk = blockIdx.z * kBM;
   const int S = gridDim.y, z = blockIdx.y;
@@ -161,8 +173,8 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
   int dd[R], dk[R];
   sfor<0, R>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
-    if constexpr (r < PX / NW) {  // x: 4 rows x 256 B
-      const int i = r * NW + wave;
+    if constexpr (r < PX / DW) {  // x: 4 rows x 256 B
+      const int i = r * DW + dwv;
       const int row = 4 * i + (lane >> 4), p = lane & 15;
       const int gm = m_blk + row < M ? m_blk + row : M - 1;
       dv[r] = (TAO_SF32_DEBUG == 5 ? (uint32_t)gm * kXRow : (uint32_t)gm * row_bytes) +
@@ -170,7 +182,7 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
       dd[r] = i * 1024;
       dk[r] = 0;
     } else {
-      const int i = (r - PX / NW) * NW + wave;
+      const int i = (r - PX / DW) * DW + dwv;
       const int row = 16 * (i < PW ? i : i - PW) + (lane >> 2), p = lane & 3;
       const int gn = n_blk + row < N ? n_blk + row : N - 1;
       if (i < PW) {  // W: 16 rows x 64 B
@@ -198,7 +210,7 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
   auto issue_piece = [&](auto rc, int st, int buf) __attribute__((always_inline)) {
     constexpr int r = decltype(rc)::value;
     uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * STAGE;
-    if constexpr (r < PX / NW) {
+    if constexpr (r < PX / DW) {
       dma_lds_ring<16>(xrs, dv[r], (uint32_t)st * (TAO_SF32_DEBUG == 5 ? (uint32_t)M * kXRow : kXRow),
                   base + dd[r]);
     } else {
@@ -295,13 +307,32 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
 
   // this wave's DMAs of the step landed (its own piece count)
   auto wait_own = [&](int ahead) __attribute__((always_inline)) {
-    if constexpr (RFULL == NW || DSK) {
+    if constexpr (RFULL == DW || DSK) {
       wait_ahead<RW>(ahead);
     } else {
-      if (wave < RFULL) wait_ahead<R>(ahead);
+      if (dwv < RFULL) wait_ahead<R>(ahead);
       else wait_ahead<R - 1>(ahead);
     }
   };
+  if constexpr (LDW > 0) {
+    if (loader) {
+#pragma unroll
+      for (int p = 0; p < NS - 1; ++p)
+        if (p < J) issue(s0 + p, p);
+      for (int j = 0; j < J; ++j) {
+        const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
+        wait_own(ahead);  // this loader's pieces of stage j landed
+        barrier_lgkm();   // ... every loader's; the compute waves are done with stage j - 1
+        if (j + NS - 1 < J) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
+      }
+    } else {
+      for (int j = 0; j < J; ++j) {
+        barrier_lgkm();
+        compute(j % NS, std::false_type{}, 0, 0);
+      }
+    }
+  }
+  if constexpr (LDW == 0) {
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < J) issue(s0 + p, p);
@@ -349,6 +380,7 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
   }
 #endif
 #undef SF32_TS
+  }  // LDW == 0
   barrier_lgkm();
   if constexpr (KH == 2) {  // k half 1's accumulators into k half 0's, through LDS
     uint4* red = lds + (cw * 4 * 64 + lane) * 4;  // [cw][t][lane][16 floats]
@@ -375,7 +407,7 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
     }
     __syncthreads();
   }
-  const bool lead = kh == 0;  // the waves holding the summed tile
+  const bool lead = kh == 0 && !loader;  // the waves holding the summed tile
 
   if (S > 1) {
     constexpr uint32_t kSlice = kBM * BN * 4;
@@ -473,7 +505,7 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
     constexpr int OPR = BN / 16;
     const int N2 = N >> 1;
     const bool full2 = n_blk + BN <= N && (N2 & 7) == 0 && ((uintptr_t)y & 15) == 0;
-    for (int c = tid; c < kBM * OPR; c += NW * 64) {
+    for (int c = tid; c < kBM * OPR; c += NWT * 64) {
       const int r = c / OPR, cc = c % OPR;
       const int m = m_blk + r;
       if (m >= M) continue;
@@ -492,7 +524,7 @@ __global__ __launch_bounds__(WV * KH * 64) void gemm_sf32_int4_kernel(
   }
   constexpr int CPR = BN / 8;
   const bool full = n_blk + BN <= N && (N & 7) == 0 && ((uintptr_t)y & 15) == 0;
-  for (int c = tid; c < kBM * CPR; c += NW * 64) {
+  for (int c = tid; c < kBM * CPR; c += NWT * 64) {
     const int r = c / CPR, cc = c % CPR;
     const int m = m_blk + r;
     if (m >= M) continue;
@@ -539,6 +571,19 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
 #define SF32_GO(WV, NS, KH)                                            \
   (z16 ? go1(gemm_sf32_int4_kernel<WV, NS, KH, true>, WV * KH * 64) \
        : go1(gemm_sf32_int4_kernel<WV, NS, KH, false>, WV * KH * 64))
+  // dedicated loader waves (one per SIMD): tao_tune_gemm_sf_loaders 2 = on, 1 = off, 0 = built-in
+  const int ldm = tuning().sf_loaders;
+  const bool loaders = kh == 1 && (bn == 128 || bn == 64) && ldm == 2;
+  if (loaders) {
+    if (bn == 128) {
+      if (z16) go1(gemm_sf32_int4_kernel<4, 3, 1, true, 4>, 8 * 64);
+      else go1(gemm_sf32_int4_kernel<4, 3, 1, false, 4>, 8 * 64);
+    } else {
+      if (z16) go1(gemm_sf32_int4_kernel<2, 3, 1, true, 2>, 4 * 64);
+      else go1(gemm_sf32_int4_kernel<2, 3, 1, false, 2>, 4 * 64);
+    }
+    return check_launch("gemm_sf32_int4_kernel");
+  }
   if (bn == 256) {
     if (stages == 2) SF32_GO(8, 2, 1);
     else SF32_GO(8, 3, 1);

@@ -35,6 +35,7 @@ _KNOBS = {
     "gemm_tile": ("tao_tune_gemm_tile", 2),
     "gemm_sf": ("tao_tune_gemm_sf", 7),
     "gemm_sf_seam": ("tao_tune_gemm_sf_seam", 1),
+    "gemm_sf_loaders": ("tao_tune_gemm_sf_loaders", 1),
     "cnt_stride": ("tao_tune_cnt_stride", 1),
 }
 
