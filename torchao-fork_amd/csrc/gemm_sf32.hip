@@ -572,8 +572,11 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
   (z16 ? go1(gemm_sf32_int4_kernel<WV, NS, KH, true>, WV * KH * 64) \
        : go1(gemm_sf32_int4_kernel<WV, NS, KH, false>, WV * KH * 64))
   // dedicated loader waves (one per SIMD): tao_tune_gemm_sf_loaders 2 = on, 1 = off, 0 = built-in
+  // (on for 128-column tiles at 3 stages: w1||w3 28672x4096 M = 128 47.4-48.5 -> 39.6 us,
+  // 10240x8192 S = 2 48.9 -> 48.7; profiles/r5e_sf32_loaders.jsonl)
   const int ldm = tuning().sf_loaders;
-  const bool loaders = kh == 1 && (bn == 128 || bn == 64) && ldm == 2;
+  const bool loaders = kh == 1 && ((ldm == 2 && (bn == 128 || bn == 64)) ||
+                                   (ldm == 0 && bn == 128 && stages == 3));
   if (loaders) {
     if (bn == 128) {
       if (z16) go1(gemm_sf32_int4_kernel<4, 3, 1, true, 4>, 8 * 64);
