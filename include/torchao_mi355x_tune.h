@@ -120,10 +120,14 @@ int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages, int a_ste
  * S workgroups sums and stores 1/S of the tile; splits 2 / 4 / 8 only, others take 0), 0 = fixed
  * reducer (slice S-1 sums the whole tile). Thread-local; for measurement. */
 int tao_tune_gemm_sf_seam(int seam);
-/* 32x32x16 int4 kernel of the single-fetch GEMM: dedicated LDS-DMA loader waves, one per SIMD,
- * beside the compute waves (0 = built-in, 1 = off, 2 = on; bn 64 / 128, one wave per column
- * group). Thread-local; for measurement. */
+/* Single-fetch GEMMs: dedicated LDS-DMA loader waves beside the compute waves (0 = built-in,
+ * 1 = off, 2 = on). 32x32x16 int4 kernel: one per SIMD, bn 64 / 128, one wave per column group;
+ * 16x16 kernel: 4 beside its 8 compute waves, 64-column tiles. Thread-local; for measurement. */
 int tao_tune_gemm_sf_loaders(int mode);
+/* Single-fetch GEMM, fixed-reducer seam: place each K slice's workgroups on their own XCDs
+ * (slice z on XCDs [8z/S, 8(z+1)/S)), so each XCD's L2 takes in 1/S of x. 0 = built-in,
+ * 1 = off, 2 = on. */
+int tao_tune_gemm_sf_xmap(int mode);
 /* Reducer poll timeouts of the single-fetch GEMM since the last call (*bits != 0: some split
  * launch's outputs are invalid; never expected, see gemm_sf.hip). Synchronous. */
 int tao_gemm_sf_status(unsigned* bits);

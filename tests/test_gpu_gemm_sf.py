@@ -461,3 +461,60 @@ def test_sf32_loader_waves_bit_identical(sf, cfg, M, N, K):
             assert torch.equal(kernels.int4_linear_swiglu(x, packed, sz, g), ref_sw)
         if N <= 4096:
             assert oracle.rel_l2(got.cpu(), oracle.int4_linear(x.cpu(), q, s, z, g)) < TOL_REF
+
+
+@pytest.mark.parametrize("seam", [0, 1])
+@pytest.mark.parametrize("cfg", [(64, 2, 4, 2, 0, 0), (64, 4, 1, 3, 0, 0), (64, 8, 2, 4, 0, 0),
+                                 (64, 2, 8, 3, 0, 0)])
+@pytest.mark.parametrize("M,N,K", [(128, 4096, 4096), (100, 640, 3072), (200, 384, 2048),
+                                   (1, 96, 512)])
+def test_sf16_loader_waves_bit_identical(sf, seam, cfg, M, N, K):
+    """The 16x16x32 kernel with 4 dedicated LDS-DMA loader waves beside its 8 compute waves
+    (tao_tune_gemm_sf_loaders 2, 64-column tiles): int4 (g 32 / 128) and int8 dynamic outputs
+    bit-identical to the kernel whose compute waves issue the DMA pieces themselves, under both
+    split-K seams (fixed reducer, spread)."""
+    sf(2, *cfg)
+    _lib.call("tao_tune_gemm_sf_seam", seam)
+    for g in (32, 128):
+        q, s, z, packed, sz = _int4(N, K, g, seed=N + g)
+        x = oracle.make_activation(M, K, seed=g).to(DEV)
+        _lib.call("tao_tune_gemm_sf_loaders", 1)
+        ref = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)
+        _lib.call("tao_tune_gemm_sf_loaders", 2)
+        got = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, g, None)
+        assert torch.equal(got, ref)
+    xq, xs, wq, ws = (t.to(DEV) for t in _int8(M, N, K, seed=M + N))
+    sf(2, *cfg[:5], 128)
+    _lib.call("tao_tune_gemm_sf_loaders", 1)
+    ref = torch.ops.torchao.int8_scaled_mm(xq, xs, wq, ws, None)
+    _lib.call("tao_tune_gemm_sf_loaders", 2)
+    got = torch.ops.torchao.int8_scaled_mm(xq, xs, wq, ws, None)
+    assert torch.equal(got, ref)
+    assert torch.equal(got.cpu(), oracle.int8_scaled_mm(xq.cpu(), xs.cpu(), wq.cpu(), ws.cpu(),
+                                                       None, epilogue="cpu"))
+
+
+@pytest.mark.parametrize("cfg", [(64, 2, 4, 2, 0, 0), (64, 4, 2, 3, 0, 0), (128, 2, 8, 2, 0, 0),
+                                 (64, 2, 4, 4, 3, 0)])
+@pytest.mark.parametrize("M,N,K", [(128, 4096, 4096), (200, 1024, 2048), (100, 4096, 14336)])
+def test_sf_xcd_slice_map_bit_identical(sf, cfg, M, N, K):
+    """K slice -> XCD placement (tao_tune_gemm_sf_xmap 2) only renumbers the workgroups: int4 and
+    int8 dynamic outputs bit-identical to the default numbering, asymmetric slices and several
+    M tiles included; N / 64 not a multiple of 8 / S falls back to the default numbering."""
+    sf(2, *cfg)
+    _lib.call("tao_tune_gemm_sf_seam", 0)
+    q, s, z, packed, sz = _int4(N, K, 32, seed=N)
+    x = oracle.make_activation(M, K, seed=5).to(DEV)
+    _lib.call("tao_tune_gemm_sf_xmap", 1)
+    ref = torch.ops.torchao.int4_weight_only_linear(x, packed, sz, 32, None)
+    _lib.call("tao_tune_gemm_sf_xmap", 2)
+    assert torch.equal(torch.ops.torchao.int4_weight_only_linear(x, packed, sz, 32, None), ref)
+    xq, xs, wq, ws = (t.to(DEV) for t in _int8(M, N, K, seed=M + N))
+    sf(2, *cfg[:5], 128)
+    _lib.call("tao_tune_gemm_sf_xmap", 1)
+    ref = torch.ops.torchao.int8_scaled_mm(xq, xs, wq, ws, None)
+    _lib.call("tao_tune_gemm_sf_xmap", 2)
+    got = torch.ops.torchao.int8_scaled_mm(xq, xs, wq, ws, None)
+    assert torch.equal(got, ref)
+    assert torch.equal(got.cpu(), oracle.int8_scaled_mm(xq.cpu(), xs.cpu(), wq.cpu(), ws.cpu(),
+                                                       None, epilogue="cpu"))

@@ -226,11 +226,14 @@ constexpr int mfma_groups() {
   else return 4;
 }
 
-template <class P, int BN, int WM, int NS>
-__global__ __launch_bounds__(512) void gemm_sf_kernel(
+// LDW > 0: LDW dedicated loader waves (one per SIMD) issue every LDS-DMA piece and the 8 compute
+// waves only read fragments, dequantise and issue MFMAs (gemm_sf32.hip measured the same split
+// 17% faster on its 128-column tile).
+template <class P, int BN, int WM, int NS, int LDW = 0>
+__global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int a_steps, typename P::Acc* __restrict__ slab,
-    unsigned* __restrict__ cnt, int fenced, int S, int ntn, int seam, int cs, SfEpi ep) {
+    unsigned* __restrict__ cnt, int fenced, int S, int ntn, int seam, int cs, SfEpi ep, int xmap) {
   const int epi = ep.kind;
 #if TAO_SF_STAMPS
   const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
@@ -252,9 +255,11 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   constexpr int PX = XB / 1024, PW = WB / 1024, PZ = ZB / 256;
   constexpr int T = PX + PW + PZ;
   static_assert(XB % 1024 == 0 && WB % 1024 == 0 && ZB % 256 == 0, "DMA pieces");
-  static_assert(T % kWaves == 0 && PX % kWaves == 0, "DMA pieces per wave");
-  constexpr int R = T / kWaves;  // DMA instructions per wave per stage
-  constexpr bool IL = TAO_SF_IL != 0 && NS >= 3;
+  constexpr int DW = LDW > 0 ? LDW : kWaves;  // waves that issue the DMA pieces
+  constexpr int NTH = (kWaves + LDW) * 64;      // threads
+  static_assert(T % DW == 0 && PX % DW == 0, "DMA pieces per wave");
+  constexpr int R = T / DW;  // DMA instructions per DMA wave per stage
+  constexpr bool IL = TAO_SF_IL != 0 && NS >= 3 && LDW == 0;
   constexpr int NB = NS;  // LDS stage buffers
   static_assert(NB * STAGE <= 160 * 1024, "LDS");
   static_assert(kBM * BN * 2 <= NB * STAGE, "epilogue image");
@@ -262,7 +267,9 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
+  const bool loader = LDW > 0 && wave >= kWaves;
+  const int dwv = LDW > 0 ? wave - kWaves : wave;  // index among the DMA-issuing waves
+  const int wm = loader ? 0 : wave / WN, wn = loader ? 0 : wave % WN;
   const int fr = lane & 15, kq = lane >> 4;
   const int bid = blockIdx.x;
   int z, nb, mb;
@@ -270,6 +277,11 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
     z = bid % S;
     nb = (bid / S) % ntn;
     mb = bid / (S * ntn);
+  } else if (xmap) {  // slice z on XCDs [z G, (z + 1) G), G = 8 / S (dispatch: block b on XCD b % 8)
+    const int G = 8 / S, b = bid % (S * ntn), xcd = b & 7;  // (runtime divisions: VALU, so
+    z = __builtin_amdgcn_readfirstlane(xcd / G);            // pinned back to SGPRs)
+    nb = __builtin_amdgcn_readfirstlane((b >> 3) * G + xcd % G);
+    mb = __builtin_amdgcn_readfirstlane(bid / (S * ntn));
   } else {
     nb = bid % ntn;
     z = (bid / ntn) % S;
@@ -292,16 +304,16 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   int dd[R], dk[R];
   sfor<0, R>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
-    if constexpr (r < PX / kWaves) {
+    if constexpr (r < PX / DW) {
       constexpr int G = P::kXRow / 16;
-      const int i = r * kWaves + wave;
+      const int i = r * DW + dwv;
       const int row = i * (1024 / P::kXRow) + lane / G, p = lane % G;
       const int gm = m_blk + row < M ? m_blk + row : M - 1;
       dv[r] = (uint32_t)gm * row_bytes + 16u * (uint32_t)P::xpos(row, p);
       dd[r] = i * 1024;
       dk[r] = 0;
     } else {
-      const int i = (r - PX / kWaves) * kWaves + wave;
+      const int i = (r - PX / DW) * DW + dwv;
       if (i < PW) {
         dv[r] = pol.wsrc(i, lane, n_blk, N, K);
         dd[r] = XB + i * 1024;
@@ -317,7 +329,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   auto issue_piece = [&](auto rc, int st, int buf) __attribute__((always_inline)) {
     constexpr int r = decltype(rc)::value;
     uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * STAGE;
-    if constexpr (r < PX / kWaves) {
+    if constexpr (r < PX / DW) {
       dma_lds_ring<16>(xrs, dv[r], (uint32_t)st * P::kXRow, base + dd[r]);
     } else {
       if (dk[r] == 1) dma_lds_ring<16, kNT>(wrs, dv[r], pol.wsoff(st), base + dd[r]);
@@ -455,6 +467,23 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   // ---- the k loop: LDS-DMA, NS-1 stages in flight, one barrier per step ----------------------------
   // (a register-staged variant -- 16-B loads into a register ring, two LDS buffers -- measured
   // 5-15% slower at every swept shape: profiles/r4_sf_sweep_reg.jsonl)
+  if constexpr (LDW > 0) {  // loaders wait for their pieces, join the barrier, refill; compute
+    if (loader) {            // waves only read and compute
+#pragma unroll
+      for (int p = 0; p < NS - 1; ++p)
+        if (p < J) issue(s0 + p, p);
+      for (int j = 0; j < J; ++j) {
+        wait_ahead<R>(J - 1 - j < NS - 2 ? J - 1 - j : NS - 2);
+        barrier_lgkm();
+        if (j + NS - 1 < J) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
+      }
+    } else {
+      for (int j = 0; j < J; ++j) {
+        barrier_lgkm();
+        compute(j % NS, std::false_type{}, 0, 0);
+      }
+    }
+  } else {
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < J) issue(s0 + p, p);
@@ -478,6 +507,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
 #endif
     compute(j % NS, std::false_type{}, 0, 0);
   }
+  }  // LDW == 0
   barrier_lgkm();  // all fragment reads done: the LDS is free for the epilogue image
   SF_MARK(3);
 
@@ -489,14 +519,14 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   // each workgroup takes in (S-1)/S^2 of the slices' partials instead of one reducer taking in
   // (S-1) whole tiles (the fixed reducer's seam measured 4-11 us at S = 4-8: its intake).
   const int wpo = kWaves / S;  // waves owned per workgroup (spread)
-  const bool own = S == 1 || !seam || wave / wpo == z;
+  const bool own = !loader && (S == 1 || !seam || wave / wpo == z);
   if (S > 1) {
     constexpr uint32_t kSlice = kBM * BN * 4;  // bytes of one slice's partial tile
     const Rsrc srs = make_rsrc(reinterpret_cast<const uint8_t*>(slab) + (size_t)tile * S * kSlice,
                                (uint32_t)S * kSlice);
     const uint32_t lo = (uint32_t)((wave * MT * NT * 64 + lane) * 16);
     unsigned* word = reinterpret_cast<unsigned*>(lds);
-    if (!reducer && !(seam && own)) {
+    if (!reducer && !(seam && own) && !loader) {
       // MI355X_MICROARCH.md "Hand-offs measured with sc1 loads in place of the acquire", first row:
       // sc1 16-B stores, every storing wave's vmcnt(0), a workgroup barrier, one agent-scope add
 #pragma unroll
@@ -636,7 +666,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
     constexpr int OPR = BN / 16;  // 16-B output pieces per row
     const int N2 = N >> 1;
     const bool full2 = n_blk + BN <= N && (N2 & 7) == 0 && ((uintptr_t)y & 15) == 0;
-    for (int c = tid; c < kBM * OPR; c += 512) {
+    for (int c = tid; c < kBM * OPR; c += NTH) {
       const int r = c / OPR, cc = c % OPR;
       const int m = m_blk + r;
       if (m >= M) continue;
@@ -656,7 +686,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   if (epi == 2) {  // RoPE + KV-cache write (N = (H + 2 Hkv) 128, 16-B aligned destinations)
     constexpr int CPR = BN / 8;
     const float2* f2 = reinterpret_cast<const float2*>(ep.freqs);
-    for (int c = tid; c < kBM * CPR; c += 512) {
+    for (int c = tid; c < kBM * CPR; c += NTH) {
       const int r = c / CPR, cc = c % CPR;
       const int m = m_blk + r, n0 = n_blk + 8 * cc;
       if (m >= M || n0 >= N) continue;
@@ -695,7 +725,7 @@ __global__ __launch_bounds__(512) void gemm_sf_kernel(
   constexpr int CPR = BN / 8;  // 16-B pieces per row
   const bool full = n_blk + BN <= N && (N & 7) == 0 && ((uintptr_t)y & 15) == 0;
 #pragma unroll
-  for (int c = epi != 0 ? kBM * CPR : tid; c < kBM * CPR; c += 512) {
+  for (int c = epi != 0 ? kBM * CPR : tid; c < kBM * CPR; c += NTH) {
     const int r = c / CPR, cc = c % CPR;
     const int m = m_blk + r;
     if (m >= M) continue;
@@ -732,12 +762,14 @@ struct SfShape {
   int bn, wm, splits, stages, a_steps;
   int seam;    // 0 fixed reducer, 1 spread (see the kernel)
   int kh = 1;  // the 32x32x16 int4 kernel (wm 1): k halves per column group, 1 or 2
+  int ld = 0;  // 16x16x32 kernel, 64-column tiles: 4 dedicated LDS-DMA loader waves
+  int xm = 0;  // fixed-reducer seam: each K slice's workgroups on their own XCDs (sf_xmap)
 };
 
 template <class P, int BN, int WM, int NS>
 bool sf_go(const SfShape& sh, hipStream_t stream, const uint8_t* x, const P& pol,
            const uint16_t* bias, uint16_t* y, int M, int N, int K, int a, typename P::Acc* slab,
-           unsigned* cnt, const SfEpi& ep) {
+           unsigned* cnt, const SfEpi& ep, bool loaders) {
   constexpr int STAGE = kBM * P::kXRow + BN * P::kWRow + BN * P::kZRow;
   constexpr int NB = NS;
   if constexpr (NB * STAGE <= 160 * 1024 && (kBM * P::kXRow + BN * P::kWRow + BN * P::kZRow) > 0) {
@@ -746,9 +778,21 @@ bool sf_go(const SfShape& sh, hipStream_t stream, const uint8_t* x, const P& pol
                   BN / (kWaves / WM) >= 16)
     {
       const int ntn = (N + BN - 1) / BN, mtiles = (M + kBM - 1) / kBM;
-      launch(gemm_sf_kernel<P, BN, WM, NS>, dim3((unsigned)(ntn * sh.splits * mtiles)), dim3(512),
-             0, stream, x, pol, bias, y, M, N, K, a, slab, cnt, tuning().splitk_fenced, sh.splits,
-             ntn, sh.seam, tuning().cnt_stride, ep);
+      const dim3 grid((unsigned)(ntn * sh.splits * mtiles));
+      const int xm = tuning().sf_xmap ? tuning().sf_xmap == 2 : sh.xm;
+      const int xmap = xm && !sh.seam && (sh.splits == 2 || sh.splits == 4 || sh.splits == 8) &&
+                       ntn % (8 / sh.splits) == 0;
+      if constexpr (BN <= 64 && T % 4 == 0 && ((kBM * P::kXRow) / 1024) % 4 == 0) {  // wider: spills
+        if (loaders) {  // 4 loader waves beside the 8 compute waves
+          launch(gemm_sf_kernel<P, BN, WM, NS, 4>, grid, dim3(768), 0, stream, x, pol, bias, y, M,
+                 N, K, a, slab, cnt, tuning().splitk_fenced, sh.splits, ntn, sh.seam,
+                 tuning().cnt_stride, ep, xmap);
+          return true;
+        }
+      }
+      launch(gemm_sf_kernel<P, BN, WM, NS>, grid, dim3(512), 0, stream, x, pol, bias, y, M, N, K,
+             a, slab, cnt, tuning().splitk_fenced, sh.splits, ntn, sh.seam, tuning().cnt_stride,
+             ep, xmap);
       return true;
     }
   }
@@ -762,7 +806,8 @@ int sf_dispatch_wm(const SfShape& sh, hipStream_t st, const uint8_t* x, const P&
   bool ok = false;
   auto go = [&](auto wmc, auto nsc) {
     constexpr int W = decltype(wmc)::value, S_ = decltype(nsc)::value;
-    ok = sf_go<P, BN, W, S_>(sh, st, x, pol, bias, y, M, N, K, a, slab, cnt, ep);
+    ok = sf_go<P, BN, W, S_>(sh, st, x, pol, bias, y, M, N, K, a, slab, cnt, ep,
+                             tuning().sf_loaders ? tuning().sf_loaders == 2 : sh.ld != 0);
   };
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
@@ -791,7 +836,9 @@ int sf_dispatch_wm(const SfShape& sh, hipStream_t st, const uint8_t* x, const P&
 // tiles, r4_sf_sweep_bn256.jsonl),
 // 4096x14336 23.6 -> 20.4; int4 4096^2 14.6 -> 14.0, 6144x4096 21.6 -> 19.4, 28672x4096
 // 59.9 -> 50.0 (the 32x32x16 kernel, one wave along M), 4096x14336 32.6 -> 31.6. Config 3
-// (int8 dyn 4096^2: 10.4 vs 10.6) and every M <= 64 stay on the incumbent.
+// (int8 dyn 4096^2: 10.4 vs 10.6) and every M <= 64 stay on the incumbent. Round 5: 4 dedicated
+// loader waves on the 64-column int4 tiles where they measured faster (profiles/r5f_ab_loaders*.jsonl,
+// same-process alternation; slower at 6144x4096, neutral at 4096^2 and for int8 dyn).
 struct SfRoute {
   int path, n, k;
   SfShape sh;
@@ -804,7 +851,7 @@ constexpr SfRoute kSfRoutes[] = {
     {0, 4096, 4096, {64, 2, 4, 2, 0, 0}, 0},
     {0, 6144, 4096, {64, 2, 4, 2, 0, 0}, 0},
     {0, 28672, 4096, {128, 1, 1, 3, 0, 0}, 0},
-    {0, 4096, 14336, {64, 2, 4, 4, 0, 0}, 0},
+    {0, 4096, 14336, {64, 2, 4, 4, 0, 0, 1, 1}, 0},  // loader waves: 31.9 -> 28.7 us
     // Llama-3-70B (profiles/r4_sf_sweep_70b.jsonl; us, incumbent -> single-fetch): int8 dyn
     // 10240x8192 42.6 -> 29.6, 8192^2 27.4 -> 21.6, 57344x8192 145.2 -> 99.2, 8192x28672
     // 68.4 -> 55.8; int4 10240x8192 62.2 -> 48.4, 8192^2 37.8 -> 32.9, 57344x8192 225.9 ->
@@ -817,7 +864,7 @@ constexpr SfRoute kSfRoutes[] = {
     {2, 57344, 8192, {256, 2, 1, 3, 0, 0}, 128},
     {2, 8192, 28672, {64, 4, 2, 3, 0, 1}, 256},
     {0, 10240, 8192, {128, 1, 2, 3, 0, 0}, 2},
-    {0, 8192, 8192, {64, 2, 2, 3, 0, 0}, 0},
+    {0, 8192, 8192, {64, 2, 2, 3, 0, 0, 1, 1}, 0},  // loader waves: 36.6 -> 33.0 us
     {0, 57344, 8192, {256, 1, 1, 3, 0, 0}, 0},
     {0, 8192, 28672, {128, 2, 4, 3, 0, 1}, 0},
 };
@@ -1062,10 +1109,17 @@ extern "C" int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages
   return TAO_OK;
 }
 
-// Loader waves of the 32x32x16 int4 kernel: 0 = built-in, 1 = off, 2 = on.
+// Dedicated loader waves of the single-fetch kernels: 0 = built-in, 1 = off, 2 = on.
 extern "C" int tao_tune_gemm_sf_loaders(int mode) {
   TAO_CHECK_ARG(mode >= 0 && mode <= 2, "tune: gemm_sf_loaders must be 0, 1 or 2");
   tao::tuning().sf_loaders = mode;
+  return TAO_OK;
+}
+
+// K slice -> XCD block mapping under the fixed-reducer seam: 0 = built-in, 1 = off, 2 = on.
+extern "C" int tao_tune_gemm_sf_xmap(int mode) {
+  TAO_CHECK_ARG(mode >= 0 && mode <= 2, "tune: gemm_sf_xmap must be 0, 1 or 2");
+  tao::tuning().sf_xmap = mode;
   return TAO_OK;
 }
 

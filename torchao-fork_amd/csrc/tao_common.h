@@ -75,6 +75,7 @@ struct Tuning {
   int sf_stages = 0, sf_a_steps = 0, sf_ks = 0;
   int cnt_stride = 32;  // split-K tickets: unsigned words between tiles' counters (32 = a 128-B line each)
   int sf_seam = -1;  // single-fetch GEMM split-K seam: -1 built-in, 0 fixed reducer, 1 spread
+  int sf_xmap = 0;     // fixed-reducer seam: K slices on their own XCDs (0 built-in, 1 off, 2 on)
   int sf_loaders = 0;  // 32x32x16 int4 GEMM: dedicated LDS-DMA loader waves (0 built-in, 1 off, 2 on)
   int gemv_lds = 0;  // int4 GEMV: minimum dynamic LDS per workgroup (caps residency; tao_tune_int4_lds)
 };

@@ -36,6 +36,7 @@ _KNOBS = {
     "gemm_sf": ("tao_tune_gemm_sf", 7),
     "gemm_sf_seam": ("tao_tune_gemm_sf_seam", 1),
     "gemm_sf_loaders": ("tao_tune_gemm_sf_loaders", 1),
+    "gemm_sf_xmap": ("tao_tune_gemm_sf_xmap", 1),
     "cnt_stride": ("tao_tune_cnt_stride", 1),
 }
 
