@@ -848,8 +848,8 @@ constexpr SfRoute kSfRoutes[] = {
     {2, 6144, 4096, {64, 4, 2, 3, 0, 0}, 256},
     {2, 28672, 4096, {256, 4, 2, 3, 0, 1}, 128},
     {2, 4096, 14336, {64, 4, 4, 4, 0, 1}, 128},
-    {0, 4096, 4096, {64, 2, 4, 2, 0, 0}, 0},
-    {0, 6144, 4096, {64, 2, 4, 2, 0, 0}, 0},
+    {0, 4096, 4096, {64, 2, 4, 4, 0, 0, 1, 1}, 0},  // r5: 4 stages + loaders 14.6 -> 14.0
+    {0, 6144, 4096, {64, 2, 2, 3, 0, 0, 1, 1}, 0},  // r5: S 2, 3 stages + loaders 19.7 -> 18.2
     {0, 28672, 4096, {128, 1, 1, 3, 0, 0}, 0},
     {0, 4096, 14336, {64, 2, 4, 4, 0, 0, 1, 1}, 0},  // loader waves: 31.9 -> 28.7 us
     // Llama-3-70B (profiles/r4_sf_sweep_70b.jsonl; us, incumbent -> single-fetch): int8 dyn
