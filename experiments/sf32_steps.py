@@ -27,14 +27,17 @@ NWG, NWV, NST = 8, 8, 64
 
 
 def main():
-    cases = [("128x28672x4096", (128, 1, 1, 3, 0, 0)), ("128x28672x4096", (128, 1, 1, 3, 0, 2)),
-             ("128x57344x8192", (256, 1, 1, 3, 0, 0))]
+    # (shape, launch shape, tao_tune_gemm_sf_loaders): with loaders (2) waves 0-3 compute and
+    # 4-7 load; their phases are reported separately
+    cases = [("128x28672x4096", (128, 1, 1, 3, 0, 0), 1), ("128x28672x4096", (128, 1, 1, 3, 0, 0), 2),
+             ("128x28672x4096", (128, 1, 1, 3, 0, 2), 1), ("128x57344x8192", (256, 1, 1, 3, 0, 0), 1)]
     gen = torch.Generator(device="cuda").manual_seed(0)
     buf = np.zeros(NWG * NWV * NST * 4 + NWG * NWV * 4, dtype=np.uint64)
-    for shape, cfg in cases:
+    for shape, cfg, ld in cases:
         M, N, K = (int(v) for v in shape.split("x"))
         run, copies = int4_case(M, N, K, gen)
         sf(2, *cfg)
+        lib.tao_tune_gemm_sf_loaders(ld)
         for c in range(copies):
             run(c)
         torch.cuda.synchronize()
@@ -54,7 +57,14 @@ def main():
         span_cyc = te[:, :waves, 2] - te[:, :waves, 0]
         span_rt = (te[:, :waves, 3] - te[:, :waves, 1]) * 10.0  # ns (100 MHz)
         clk = float(np.median(span_cyc / np.maximum(span_rt, 1)))  # GHz
-        rec = {"shape": shape, "cfg": list(cfg), "waves": waves, "steps": nsteps,
+        if ld == 2:
+            lt = ts[:, waves:2 * waves, 1:min(nsteps, NST) - 1, :]
+            loader = {"loader_wait_dma_cyc": float(np.median(lt[..., 1] - lt[..., 0])),
+                      "loader_barrier_cyc": float(np.median(lt[..., 2] - lt[..., 1])),
+                      "loader_issue_cyc": float(np.median(lt[..., 3] - lt[..., 2]))}
+        else:
+            loader = {}
+        rec = {"shape": shape, "cfg": list(cfg), "loaders": ld, "waves": waves, "steps": nsteps,
                "clock_GHz": round(clk, 3),
                "cyc_per_step_median": float(np.median(step)),
                "wait_dma_cyc": float(np.median(wait)), "barrier_cyc": float(np.median(bar)),
@@ -62,9 +72,11 @@ def main():
                "wait_dma_p90": float(np.percentile(wait, 90)),
                "barrier_p90": float(np.percentile(bar, 90)),
                "span_us_median": round(float(np.median(span_rt)) / 1e3, 2),
-               "first_step_wait_cyc": float(np.median(ts[:, :waves, 0, 1] - ts[:, :waves, 0, 0]))}
+               "first_step_wait_cyc": float(np.median(ts[:, :waves, 0, 1] - ts[:, :waves, 0, 0])),
+               **loader}
         print(json.dumps(rec), flush=True)
         sf(0)
+        lib.tao_tune_gemm_sf_loaders(0)
         del run
 
 

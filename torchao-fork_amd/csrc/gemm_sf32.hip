@@ -314,30 +314,6 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
       else wait_ahead<R - 1>(ahead);
     }
   };
-  if constexpr (LDW > 0) {
-    if (loader) {
-#pragma unroll
-      for (int p = 0; p < NS - 1; ++p)
-        if (p < J) issue(s0 + p, p);
-      for (int j = 0; j < J; ++j) {
-        const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
-        wait_own(ahead);  // this loader's pieces of stage j landed
-        barrier_lgkm();   // ... every loader's; the compute waves are done with stage j - 1
-        if (j + NS - 1 < J) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
-      }
-    } else {
-      for (int j = 0; j < J; ++j) {
-        barrier_lgkm();
-        compute(j % NS, std::false_type{}, 0, 0);
-      }
-    }
-  }
-  if constexpr (LDW == 0) {
-#pragma unroll
-  for (int p = 0; p < NS - 1; ++p)
-    if (p < J) issue(s0 + p, p);
-  const int jiss = TAO_SF32_DEBUG == 3 ? 0 : J - (NS - 1);  // steps that issue a stage ahead
-  int j = 0;
 #if TAO_SF32_STEPSTAMPS
   const int flat_wg = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
   const bool stamp = flat_wg < 8 && lane == 0;
@@ -354,6 +330,38 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
   do {             \
   } while (0)
 #endif
+  if constexpr (LDW > 0) {
+    if (loader) {
+#pragma unroll
+      for (int p = 0; p < NS - 1; ++p)
+        if (p < J) issue(s0 + p, p);
+      for (int j = 0; j < J; ++j) {
+        const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
+        SF32_TS(0);
+        wait_own(ahead);  // this loader's pieces of stage j landed
+        SF32_TS(1);
+        barrier_lgkm();   // ... every loader's; the compute waves are done with stage j - 1
+        SF32_TS(2);
+        if (j + NS - 1 < J) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
+        SF32_TS(3);
+      }
+    } else {
+      for (int j = 0; j < J; ++j) {
+        SF32_TS(0);
+        SF32_TS(1);
+        barrier_lgkm();
+        SF32_TS(2);
+        compute(j % NS, std::false_type{}, 0, 0);
+        SF32_TS(3);
+      }
+    }
+  }
+  if constexpr (LDW == 0) {
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < J) issue(s0 + p, p);
+  const int jiss = TAO_SF32_DEBUG == 3 ? 0 : J - (NS - 1);  // steps that issue a stage ahead
+  int j = 0;
   for (; j < jiss; ++j) {
     SF32_TS(0);
     wait_own(NS - 2);
@@ -373,6 +381,7 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
     compute(j % NS, std::false_type{}, 0, 0);
     SF32_TS(3);
   }
+  }  // LDW == 0
 #if TAO_SF32_STEPSTAMPS
   if (stamp) {
     tse[2] = __builtin_amdgcn_s_memtime();
@@ -380,7 +389,6 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
   }
 #endif
 #undef SF32_TS
-  }  // LDW == 0
   barrier_lgkm();
   if constexpr (KH == 2) {  // k half 1's accumulators into k half 0's, through LDS
     uint4* red = lds + (cw * 4 * 64 + lane) * 4;  // [cw][t][lane][16 floats]
