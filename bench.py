@@ -352,7 +352,7 @@ def hbm_ceilings(device, nbytes=1 << 30, reps=10):
     the microarch guide's method (MI355X_MICROARCH.md "HBM": one long launch over a buffer far
     past the 256 MiB Infinity Cache, 16-B accesses). Three numbers, GB/s, HIP events:
       copy_GBps   tao_hbm_copy_probe over 1 GiB (read + write bytes; the guide's float4 copy row),
-                  best grid of a small sweep;
+                  best of a small sweep (grid x cache policy, and a one-pass form);
       read_GBps   tao_hbm_read_probe over 1 GiB in one launch (the GEMV's own load form: 16-B
                   non-temporal loads, 512-thread workgroups);
       torch_copy_GBps  torch's device copy_ of 1 GiB (what rounds 2-4 reported).
@@ -376,8 +376,8 @@ def hbm_ceilings(device, nbytes=1 << 30, reps=10):
         e1.synchronize()
         return e0.elapsed_time(e1) * 1e-3 / reps
 
-    def copy(grid):
-        rc = lib.tao_hbm_copy_probe(a.data_ptr(), b.data_ptr(), nbytes, grid, sp)
+    def copy(grid, mode):
+        rc = lib.tao_hbm_copy_probe(a.data_ptr(), b.data_ptr(), nbytes, grid, mode, sp)
         if rc:
             raise RuntimeError(lib.tao_last_error().decode())
 
@@ -386,8 +386,14 @@ def hbm_ceilings(device, nbytes=1 << 30, reps=10):
         if rc:
             raise RuntimeError(lib.tao_last_error().decode())
 
-    copy_best = max(2 * nbytes / timed(lambda: copy(gr)) / 1e9 for gr in (1024, 2048, 4096, 8192))
-    out = {"copy_GBps": round(copy_best, 1),
+    copies = {(gr, mode): 2 * nbytes / timed(lambda: copy(gr, mode)) / 1e9
+              for mode in (0, 1) for gr in (1024, 2048, 4096, 8192)}
+    copies[(0, 2)] = 2 * nbytes / timed(lambda: copy(0, 2)) / 1e9
+    best = max(copies, key=copies.get)
+    out = {"copy_GBps": round(copies[best], 1),
+           "copy_best": {"grid": best[0], "mode": ["default policy", "nt", "nt one pass"][best[1]]},
+           "copy_sweep_GBps": {f"{['def', 'nt', 'nt1'][m]}_{gr}": round(v, 1)
+                               for (gr, m), v in copies.items()},
            "read_GBps": round(nbytes / timed(read) / 1e9, 1),
            "torch_copy_GBps": round(2 * nbytes / timed(lambda: b.copy_(a)) / 1e9, 1),
            "bytes": nbytes}
@@ -1275,6 +1281,8 @@ def main():
                 "measured_copy_GBps": ceil["copy_GBps"] if ceil else None,
                 "measured_stream_read_GBps": ceil["read_GBps"] if ceil else None,
                 "torch_copy_GBps": ceil["torch_copy_GBps"] if ceil else None,
+                "copy_probe": ({"best": ceil["copy_best"], "sweep_GBps": ceil["copy_sweep_GBps"]}
+                               if ceil else None),
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "frac_of_stream_read": round(achieved / ceil["read_GBps"], 4) if ceil else None,
                 "frac_of_copy": round(achieved / ceil["copy_GBps"], 4) if ceil else None,

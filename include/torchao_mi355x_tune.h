@@ -137,9 +137,11 @@ int tao_gemm_sf_status(unsigned* bits);
  * >= 4 KiB of device memory the kernel may write (it never does in practice). Graph-capturable. */
 int tao_hbm_read_probe(const void* buf, int64_t bytes, void* sink, void* stream);
 /* Measurement kernel (bench.py ceiling calibration): dst <- src, `bytes` (multiple of 16), 16-B
- * loads and stores, `grid` 256-thread workgroups striding over the buffer (4 x 16 B in flight per
- * thread). Graph-capturable. */
-int tao_hbm_copy_probe(const void* src, void* dst, int64_t bytes, int grid, void* stream);
+ * loads and stores. mode 0: `grid` 256-thread workgroups striding over the buffer (4 x 16 B in
+ * flight per thread), default cache policy; 1: the same, non-temporal loads and stores; 2: one
+ * 16-B element per thread, one pass (`grid` ignored), non-temporal. Graph-capturable. */
+int tao_hbm_copy_probe(const void* src, void* dst, int64_t bytes, int grid, int mode,
+                       void* stream);
 /* Number of split-K workspaces currently owned by captured graphs (each is released with its
  * graph). Diagnostic for tests; never fails. */
 int tao_graph_workspace_count(void);

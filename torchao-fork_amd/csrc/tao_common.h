@@ -136,6 +136,12 @@ __device__ __forceinline__ uint4 ld_nt_u4(const uint4* p) {
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
+__device__ __forceinline__ void st_nt_u4(uint4* p, uint4 v) {  // 16-B non-temporal vector store
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+}
+
 // ---- buffer resources --------------------------------------------------------------------------
 // All operand loads are raw buffer loads: a wave-uniform 128-bit descriptor, a per-lane 32-bit
 // voffset fixed for the whole launch and a per-step wave-uniform soffset, so the k loop spends
