@@ -406,3 +406,50 @@ def test_add_rmsnorm_and_fused_prefill_gpu():
         assert torch.equal(outs[0], outs[1])
     finally:
         kernels.PREFILL_ADD_NORM = old
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("quant,fuse", [(None, True), ("int4wo-32", True), ("int4wo-32", False),
+                                        ("int8wo", True)])
+def test_prefill_last_row_gpu(quant, fuse):
+    """Greedy prefill's last block past wqkv on the one-token kernels (kernels.PREFILL_LAST_ROW):
+    the last position's hidden state within bf16 re-association of the all-rows prefill (the
+    one-token GEMVs sum K in another order than the M = S GEMMs), the KV caches of every layer
+    bit-identical (wqkv still runs over every row), and the same next token where the top-2
+    margin of the all-rows logits is decided."""
+    from torchao._models.llama import kernels
+    from torchao._models.llama.generate import apply_quantization
+
+    dev = torch.device("cuda")
+    model = _tiny(dev)
+    if fuse:
+        model.fuse_w13()
+    if quant:
+        apply_quantization(model, quant)
+    model.setup_caches(1, 64)
+    model.enable_fused_kernels()
+    pos = torch.arange(40, device=dev)
+    prompt = torch.randint(0, model.config.vocab_size, (1, 40), device=dev,
+                           generator=torch.Generator(device=dev).manual_seed(5))
+    with torch.no_grad():
+        full = model._layers_prefill(prompt, pos)[:, -1:].clone()
+        caches = [t.clone() for b in model.layers for t in (b.attention.kv_cache.k_cache,
+                                                            b.attention.kv_cache.v_cache)]
+        last = model._layers_prefill(prompt, pos, last_only=True)
+        assert last.shape == full.shape
+        assert torch.equal(torch.cat([t.flatten() for b in model.layers for t in (
+            b.attention.kv_cache.k_cache, b.attention.kv_cache.v_cache)]),
+            torch.cat([t.flatten() for t in caches]))
+        rel = ((last.float() - full.float()).norm() / full.float().norm()).item()
+        assert rel < 1e-2, rel
+        logits = model.output(kernels.rmsnorm(full, model.norm.weight, model.norm.eps)).float()
+        top2 = logits[0, -1].topk(2)
+        tok = model.prefill_next(prompt, pos)
+        if (top2.values[0] - top2.values[1]).item() > 0.05 * top2.values[0].abs().item():
+            assert int(tok.item()) == int(top2.indices[0].item())
+        old = kernels.PREFILL_LAST_ROW
+        try:
+            kernels.PREFILL_LAST_ROW = False
+            assert torch.equal(model._layers_prefill(prompt, pos, last_only=True)[:, -1:], full)
+        finally:
+            kernels.PREFILL_LAST_ROW = old

@@ -225,6 +225,11 @@ _EPILOGUES = {"none": 0, "swiglu": 1, "rope_kv": 2}
 PREFILL_ATTN = True
 # Prefill residual adds fused with the following RMSNorm (tao_add_rmsnorm_bf16).
 PREFILL_ADD_NORM = True
+# Greedy prefill (Transformer.prefill_next) reads only the last position's hidden state: the last
+# block runs wqkv + RoPE + KV write over every row (the caches need them) and everything after it
+# for the last row only, on the one-token kernels (attention, wo + residual, RMSNorm + w1||w3 +
+# SwiGLU, w2 + residual).
+PREFILL_LAST_ROW = True
 
 # Output heads (N >= HEAD_ROWS) normalise in their own RMSNorm launch unless HEAD_PROLOGUE.
 HEAD_ROWS = 65536

@@ -299,6 +299,23 @@ class Attention(nn.Module):
                                            enable_gqa=True)
         return self.wo(y.transpose(1, 2).reshape(B, S, self.n_head * self.head_dim))
 
+    def prefill_last(self, x, freqs_table, input_pos):
+        """forward_prefill's q / K / V for every row (the KV caches need them all), then the
+        attention of the LAST query only -> [B, 1, H * D] (the greedy prefill's last block)."""
+        from torchao._models.llama import kernels
+
+        kv = self.kv_cache
+        q = None
+        p4 = _int4_parts(self.wqkv) if PREFILL_ROPE else None
+        if p4 is not None and x.is_contiguous():
+            q = kernels.int4_linear_rope_kv(x, *p4, freqs_table, input_pos, kv.k_cache,
+                                            kv.v_cache, self.n_head)
+        if q is None:
+            q = kernels.rope_kv(self.wqkv(x), freqs_table, input_pos, kv.k_cache, kv.v_cache,
+                                self.n_head)
+        return kernels.attn_decode(q[:, :, -1:].contiguous(), kv.k_cache, kv.v_cache,
+                                   input_pos[-1:], 1.0 / math.sqrt(self.head_dim))
+
     def forward_fused(self, x, freqs_table, input_pos, residual, norm=None):
         from torchao._models.llama import kernels
 
@@ -480,11 +497,17 @@ class Transformer(nn.Module):
             return y
         return self.output(kernels.rmsnorm(x, self.norm.weight, self.norm.eps))
 
-    def _layers_prefill(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
+    def _layers_prefill(self, idx: torch.Tensor, input_pos: torch.Tensor,
+                        last_only: bool = False) -> torch.Tensor:
+        """The blocks over S > 1 tokens -> hidden states [B, S, dim]; last_only (greedy prefill,
+        kernels.PREFILL_LAST_ROW): [B, 1, dim] of the last position, the last block past its
+        wqkv run on the one-token kernels."""
         from torchao._models.llama import kernels
 
         mask = self.causal_mask[None, None, input_pos]  # [1, 1, S, T]
         x = self.tok_embeddings(idx)
+        last_only = (last_only and kernels.PREFILL_LAST_ROW and kernels.PREFILL_ADD_NORM
+                     and self.config.head_dim == 128 and x.dtype == torch.bfloat16)
         if not kernels.PREFILL_ADD_NORM:
             for blk in self.layers:
                 x = blk.forward_prefill(x, self.freqs, mask, input_pos)
@@ -492,12 +515,16 @@ class Transformer(nn.Module):
         # each residual add fused with the RMSNorm that follows it (tao_add_rmsnorm_bf16): the
         # w2 output of block i is added at block i + 1's attention norm, the last one at the end
         pending = None
-        for blk in self.layers:
+        for i, blk in enumerate(self.layers):
             an, fn, ff = blk.attention_norm, blk.ffn_norm, blk.feed_forward
             if pending is None:
                 xn = kernels.rmsnorm(x, an.weight, an.eps)
             else:
                 x, xn = kernels.add_rmsnorm(x, pending, an.weight, an.eps)
+            if last_only and i == len(self.layers) - 1:
+                y = blk.attention.prefill_last(xn, self.freqs, input_pos)
+                h = _linear_plus(y, blk.attention.wo, x[:, -1:].contiguous())
+                return ff.forward_fused(h, h, fn)
             a = blk.attention.forward_prefill(xn, self.freqs, mask, input_pos)
             x, hn = kernels.add_rmsnorm(x, a, fn.weight, fn.eps)
             pending = ff.w2(ff.swiglu_prefill(hn))
@@ -511,7 +538,7 @@ class Transformer(nn.Module):
             return self(idx, input_pos)[:, -1].argmax(dim=-1, keepdim=True).to(idx.dtype)
         from torchao._models.llama import kernels
 
-        x = self._layers_prefill(idx, input_pos)[:, -1:].contiguous()  # [B, 1, dim]
+        x = self._layers_prefill(idx, input_pos, last_only=True)[:, -1:].contiguous()  # [B, 1, dim]
         return kernels.argmax(self._head_fused(x)[:, -1]).to(idx.dtype)
 
     def decode_next(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
