@@ -74,7 +74,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E, spec (MI355X_MICROARCH.md chip table)
-PMC_FILE = os.path.join(ROOT, "profiles", "r4e_pmc_fetch_bench.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r5f_pmc_fetch_bench.json")
 
 LLAMA3_8B = dict(dim=4096, n_layer=32, n_head=32, n_kv_head=8, head_dim=128,
                  intermediate=14336, vocab=128256)
@@ -608,8 +608,9 @@ def e2e_decode(timeout_s=240):
     model and weights; this process only waits). Its JSON line, trimmed."""
     import subprocess
 
+    # 5 timed samples: generate.py reports the median of each phase (of 2 it took the slower)
     cmd = [sys.executable, "-m", "torchao._models.llama.generate", "-q", "int4wo-32",
-           "--num_samples", "2"]
+           "--num_samples", "5"]
     try:
         out = subprocess.run(cmd, cwd=os.path.join(ROOT, "torchao-fork_amd"), capture_output=True,
                              text=True, timeout=timeout_s, check=True).stdout
