@@ -128,6 +128,11 @@ int tao_tune_gemm_sf_loaders(int mode);
  * (slice z on XCDs [8z/S, 8(z+1)/S)), so each XCD's L2 takes in 1/S of x. 0 = built-in,
  * 1 = off, 2 = on. */
 int tao_tune_gemm_sf_xmap(int mode);
+/* Test hook for the single-fetch split-K seam (fixed reducer): with `on` = 1, slice-0 publishers
+ * add their ticket only after a reducer has given up waiting (0.25 s) or 2 s passed, so tests can
+ * check that a timed-out launch is reported (tao_gemm_sf_status, tao_decode_status bits & 2), writes
+ * nothing for its tiles, and leaves the tickets at 0 for the next launch. Thread-local. */
+int tao_debug_sf_late_publisher(int on);
 /* Reducer poll timeouts of the single-fetch GEMM since the last call (*bits != 0: some split
  * launch's outputs are invalid; never expected, see gemm_sf.hip). Synchronous. */
 int tao_gemm_sf_status(unsigned* bits);

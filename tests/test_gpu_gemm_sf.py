@@ -518,3 +518,44 @@ def test_sf_xcd_slice_map_bit_identical(sf, cfg, M, N, K):
     assert torch.equal(got, ref)
     assert torch.equal(got.cpu(), oracle.int8_scaled_mm(xq.cpu(), xs.cpu(), wq.cpu(), ws.cpu(),
                                                        None, epilogue="cpu"))
+
+
+@pytest.mark.parametrize("path,cfg", [("int4", (64, 2, 4, 2, 0, 0)), ("int4", (128, 1, 4, 3, 0, 0)),
+                                      ("int8", (64, 4, 4, 3, 0, 128))])
+def test_sf_reducer_timeout_recovers(sf, path, cfg):
+    """A split-K launch whose reducers time out (tao_debug_sf_late_publisher: slice-0 publishers
+    add their ticket only after a reducer gave up) is reported through tao_decode_status (bits & 2),
+    and leaves every tile's ticket at 0: the following launches on the same stream's workspace
+    are bit-identical to the ones before it, and report nothing."""
+    sf(2, *cfg)
+    _lib.call("tao_tune_gemm_sf_seam", 0)
+    M, N, K = 128, 512, 2048
+    if path == "int4":
+        q, s, z, packed, sz = _int4(N, K, 32, seed=11)
+        x = oracle.make_activation(M, K, seed=12).to(DEV)
+
+        def run():
+            return torch.ops.torchao.int4_weight_only_linear(x, packed, sz, 32, None)
+    else:
+        xq, xs, wq, ws = (t.to(DEV) for t in _int8(M, N, K, seed=13))
+
+        def run():
+            return torch.ops.torchao.int8_scaled_mm(xq, xs, wq, ws, None)
+    bits = torch.zeros(1, dtype=torch.int32)
+    ref = run()
+    torch.cuda.synchronize()
+    _lib.call("tao_decode_status", bits.data_ptr())
+    assert int(bits.item()) == 0
+    _lib.call("tao_debug_sf_late_publisher", 1)
+    try:
+        run()
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("tao_debug_sf_late_publisher", 0)
+    _lib.call("tao_decode_status", bits.data_ptr())
+    assert int(bits.item()) & 2, "timed-out reducers were not reported"
+    for _ in range(3):
+        assert torch.equal(run(), ref)
+    torch.cuda.synchronize()
+    _lib.call("tao_decode_status", bits.data_ptr())
+    assert int(bits.item()) == 0

@@ -540,10 +540,11 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        if (fenced) {
+        if (fenced & 1) {
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        if ((fenced & 2) && z == 0 && !seam) late_publisher_hold(&g_sf_err);
         (void)__hip_atomic_fetch_add(&cnt[tile * cs], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -571,13 +572,14 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
     // lane polls with sc1 loads and tells the workgroup through LDS. A timed-out wait still
     // settles the ticket the same way (the subtraction, or the second arrival), so once the late
     // publishers' adds land it is back at 0 for the next launch on this stream's workspace; the
-    // tile itself is skipped and the timeout reported (tao_decode_status bit 2).
+    // tile itself is skipped and the timeout reported (tao_decode_status bits & 2).
     if (tid == 0) {
       const unsigned need = seam ? (unsigned)S : (unsigned)(S - 1);
-      unsigned it = 0, ok = 1;
+      unsigned ok = 1;
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load(&cnt[tile * cs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
         __builtin_amdgcn_s_sleep(1);
-        if (++it > (1u << 22)) {  // ~0.3 s: give up, report (outputs of this tile are invalid)
+        if (seam_timed_out(t0)) {  // give up, report (outputs of this tile are invalid)
           ok = 0;
           (void)__hip_atomic_fetch_or(&g_sf_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
@@ -590,7 +592,7 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
                                         __HIP_MEMORY_SCOPE_AGENT) == 2u * S - 1u) {
         __hip_atomic_store(&cnt[tile * cs], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (fenced) {
+      if (fenced & 1) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -758,6 +760,10 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
 }
 
 // ---- launch ------------------------------------------------------------------------------------
+// the kernels' `fenced` argument: bit 0 agent fences on the hand-off, bit 1 the late-publisher
+// test hook (tao_debug_sf_late_publisher)
+inline int sk_flags() { return tuning().splitk_fenced | (tuning().sf_late_pub ? 2 : 0); }
+
 struct SfShape {
   int bn, wm, splits, stages, a_steps;
   int seam;    // 0 fixed reducer, 1 spread (see the kernel)
@@ -785,13 +791,13 @@ bool sf_go(const SfShape& sh, hipStream_t stream, const uint8_t* x, const P& pol
       if constexpr (BN <= 64 && T % 4 == 0 && ((kBM * P::kXRow) / 1024) % 4 == 0) {  // wider: spills
         if (loaders) {  // 4 loader waves beside the 8 compute waves
           launch(gemm_sf_kernel<P, BN, WM, NS, 4>, grid, dim3(768), 0, stream, x, pol, bias, y, M,
-                 N, K, a, slab, cnt, tuning().splitk_fenced, sh.splits, ntn, sh.seam,
+                 N, K, a, slab, cnt, sk_flags(), sh.splits, ntn, sh.seam,
                  tuning().cnt_stride, ep, xmap);
           return true;
         }
       }
       launch(gemm_sf_kernel<P, BN, WM, NS>, grid, dim3(512), 0, stream, x, pol, bias, y, M, N, K,
-             a, slab, cnt, tuning().splitk_fenced, sh.splits, ntn, sh.seam, tuning().cnt_stride,
+             a, slab, cnt, sk_flags(), sh.splits, ntn, sh.seam, tuning().cnt_stride,
              ep, xmap);
       return true;
     }
@@ -1113,6 +1119,14 @@ extern "C" int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages
 extern "C" int tao_tune_gemm_sf_loaders(int mode) {
   TAO_CHECK_ARG(mode >= 0 && mode <= 2, "tune: gemm_sf_loaders must be 0, 1 or 2");
   tao::tuning().sf_loaders = mode;
+  return TAO_OK;
+}
+
+// Test hook: split-K publishers of slice 0 add their ticket only after a reducer has timed out
+// (both single-fetch kernels, fixed-reducer seam). 1 = on, 0 = off. Thread-local.
+extern "C" int tao_debug_sf_late_publisher(int on) {
+  TAO_CHECK_ARG(on == 0 || on == 1, "debug: sf_late_publisher must be 0 or 1");
+  tao::tuning().sf_late_pub = on;
   return TAO_OK;
 }
 

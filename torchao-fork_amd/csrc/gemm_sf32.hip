@@ -437,20 +437,22 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        if (fenced) {
+        if (fenced & 1) {
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        if ((fenced & 2) && z == 0) late_publisher_hold(&g_sf32_err);
         (void)__hip_atomic_fetch_add(&cnt[tile * cs], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return;
     }
     if (tid == 0) {
-      unsigned it = 0, ok = 1;
+      unsigned ok = 1;
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load(&cnt[tile * cs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
              (unsigned)(S - 1)) {
         __builtin_amdgcn_s_sleep(1);
-        if (++it > (1u << 22)) {
+        if (seam_timed_out(t0)) {
           ok = 0;
           (void)__hip_atomic_fetch_or(&g_sf32_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
@@ -460,7 +462,7 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
       // lands the ticket is 0 again for the next launch on this workspace (gemm_sf.hip's seam)
       (void)__hip_atomic_fetch_sub(&cnt[tile * cs], (unsigned)(S - 1), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-      if (fenced) {
+      if (fenced & 1) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -568,7 +570,7 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
     if (rc != TAO_OK) return rc;
     slab = reinterpret_cast<f32x16_t*>(w);
   }
-  const int fenced = tuning().splitk_fenced;
+  const int fenced = tuning().splitk_fenced | (tuning().sf_late_pub ? 2 : 0);
   auto go1 = [&](auto kern, int threads) {
     launch(kern, grid, dim3(threads), 0, stream, x, packed, reinterpret_cast<const uint32_t*>(sz),
            lg, bias, y, M, N, K, a_steps, slab, cnt, fenced, tuning().cnt_stride, epi);

@@ -75,6 +75,7 @@ struct Tuning {
   int sf_stages = 0, sf_a_steps = 0, sf_ks = 0;
   int cnt_stride = 32;  // split-K tickets: unsigned words between tiles' counters (32 = a 128-B line each)
   int sf_seam = -1;  // single-fetch GEMM split-K seam: -1 built-in, 0 fixed reducer, 1 spread
+  int sf_late_pub = 0;  // robustness test hook: slice-0 publishers add after the reducer timed out
   int sf_xmap = 0;     // fixed-reducer seam: K slices on their own XCDs (0 built-in, 1 off, 2 on)
   int sf_loaders = 0;  // 32x32x16 int4 GEMM: dedicated LDS-DMA loader waves (0 built-in, 1 off, 2 on)
   int gemv_lds = 0;  // int4 GEMV: minimum dynamic LDS per workgroup (caps residency; tao_tune_int4_lds)
@@ -140,6 +141,25 @@ __device__ __forceinline__ void st_nt_u4(uint4* p, uint4 v) {  // 16-B non-tempo
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   u32x4 w = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+}
+
+// ---- split-K seam waits ------------------------------------------------------------------------
+// A reducer gives up on its tile's publishers after kSeamTimeoutTicks of the 100 MHz
+// s_memrealtime clock (0.25 s), reports, and writes nothing for that tile.
+constexpr unsigned long long kSeamTimeoutTicks = 25000000ull;
+
+__device__ __forceinline__ bool seam_timed_out(unsigned long long t0) {
+  return __builtin_amdgcn_s_memrealtime() - t0 > kSeamTimeoutTicks;
+}
+
+// Test hook (tao_debug_sf_late_publisher): a slice-0 publisher holds its ticket add until some
+// reducer has timed out (its error word set) or 2 s passed, so a test can check that the
+// ticket is back at 0 after such a launch.
+__device__ __forceinline__ void late_publisher_hold(const unsigned* err) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+         __builtin_amdgcn_s_memrealtime() - t0 < 8 * kSeamTimeoutTicks)
+    __builtin_amdgcn_s_sleep(127);
 }
 
 // ---- buffer resources --------------------------------------------------------------------------
@@ -277,7 +297,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 // tao_decode_status() (a synchronous read, made outside graph capture; the decode harness does
 // it after every generate()). The reference's index_put KV cache device-asserts instead.
 constexpr unsigned kDecodeErrKvPos = 1u;
-// tao_decode_status bit 2: a single-fetch GEMM's split-K reducer timed out waiting for its
+// tao_decode_status bits & 2: a single-fetch GEMM's split-K reducer timed out waiting for its
 // publishers (that tile was not written; never expected)
 constexpr unsigned kDecodeErrSplitK = 2u;
 #define TAO_DECODE_ERROR_WORD(reader)                                                        \
