@@ -1,11 +1,14 @@
-"""Same-process A/B of the greedy prefill's last block on the one-token kernels
-(kernels.PREFILL_LAST_ROW) at BASELINE config 4 (Llama-3-8B int4wo-32, fused w1||w3, 128-token
-prompt): two prefill graphs captured with the flag off / on, replayed alternately; ms per replay
-(HIP events around each replay), median of each, and the first tokens of both.
+"""Same-process A/B of a prefill flag of torchao/_models/llama/kernels.py (default
+PREFILL_LAST_ROW: the greedy prefill's last block on the one-token kernels; PREFILL_PARTIALS: wo /
+w2's K slices summed by the following add + RMSNorm) at BASELINE config 4 (Llama-3-8B int4wo-32,
+fused w1||w3, 128-token prompt): two prefill graphs captured with the flag off / on, replayed
+alternately; ms per replay (HIP events around each replay), median of each, and the first tokens
+of both.
 
-    PYTHONPATH=torchao-fork_amd python experiments/ab_prefill_last.py
+    PYTHONPATH=torchao-fork_amd python experiments/ab_prefill_last.py [FLAG]
 """
 import json
+import sys
 
 import torch
 
@@ -22,12 +25,13 @@ def main():
     model.setup_caches(1, P + 200)
     model.enable_fused_kernels()
     gen = torch.Generator(device="cpu").manual_seed(1)
+    name = sys.argv[1] if len(sys.argv) > 1 else "PREFILL_LAST_ROW"
     pres = {}
     for flag in (False, True):
-        kernels.PREFILL_LAST_ROW = flag
+        setattr(kernels, name, flag)
         pres[flag] = GraphPrefill(model, (1, P), dev)
         pres[flag].capture(torch.randint(0, model.config.vocab_size, (1, P), generator=gen).to(dev))
-    kernels.PREFILL_LAST_ROW = True
+    setattr(kernels, name, True)
     times = {False: [], True: []}
     toks = {False: [], True: []}
     for rep in range(8):
@@ -43,7 +47,7 @@ def main():
             toks[flag].append(int(tok.item()))
     for flag in (False, True):
         v = sorted(times[flag])
-        print(json.dumps({"prefill_last_row": flag, "ms_median": round(v[len(v) // 2], 4),
+        print(json.dumps({"flag": name, "on": flag, "ms_median": round(v[len(v) // 2], 4),
                           "ms_min": round(v[0], 4), "n": len(v)}), flush=True)
     print(json.dumps({"first_tokens_equal": toks[False] == toks[True], "off": toks[False],
                       "on": toks[True]}), flush=True)

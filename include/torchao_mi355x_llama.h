@@ -50,6 +50,23 @@ int tao_rmsnorm_bf16(const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t 
  * bit-identical to the two. rows x dim, dim % 8 == 0. */
 int tao_add_rmsnorm_bf16(const uint16_t* x, const uint16_t* res, const uint16_t* w, uint16_t* h,
                          uint16_t* y, int64_t rows, int64_t dim, float eps, void* stream);
+/* The residual add + RMSNorm after a linear whose K slices were NOT reduced in-kernel
+ * (tao_int4wo_linear_partials_f32): part [splits][rows][dim] fp32; the linear's output is
+ * bf16(sum over slices, in slice order) (bit-identical to the single-fetch GEMM's own bf16
+ * output), h = bf16(x + it), y = RMSNorm(h) * w as tao_add_rmsnorm_bf16. dim <= 8192. */
+int tao_add_rmsnorm_partials_bf16(const uint16_t* x, const float* part, int64_t splits,
+                                  const uint16_t* w, uint16_t* h, uint16_t* y, int64_t rows,
+                                  int64_t dim, float eps, void* stream);
+/* int4 weight-only linear (x [M][K] bf16, the library's packed layout) whose K slices write fp32
+ * partial tiles part [S][M][N] for the NEXT launch to sum instead of meeting at an in-kernel
+ * split-K seam; S from tao_int4wo_linear_partial_slices (0 = not served for this shape: run the
+ * plain linear). Replaces the prefill's wo / w2 `F.linear` + residual add
+ * (torchao/_models/llama/model.py TransformerBlock.forward) together with the add + norm above. */
+int tao_int4wo_linear_partial_slices(int64_t M, int64_t N, int64_t K, int64_t group_size,
+                                     int* slices);
+int tao_int4wo_linear_partials_f32(const uint16_t* x, const uint32_t* packed, const uint16_t* sz,
+                                   float* part, int64_t M, int64_t N, int64_t K,
+                                   int64_t group_size, void* stream);
 
 /* qkv [B*S][(H + 2 Hkv) * D] bf16 -> q_out [B][H][S][D] rotated; k (rotated) and v written to
  * k_cache / v_cache [B][Hkv][T][D] at positions pos[S] (int64). freqs: rotary table

@@ -559,3 +559,42 @@ def test_sf_reducer_timeout_recovers(sf, path, cfg):
     torch.cuda.synchronize()
     _lib.call("tao_decode_status", bits.data_ptr())
     assert int(bits.item()) == 0
+
+
+@pytest.mark.parametrize("cfg", [None, (64, 2, 1, 3, 0, 0), (64, 2, 2, 3, 0, 0), (64, 4, 4, 2, 0, 0),
+                                 (64, 2, 8, 3, 5, 0), (128, 2, 4, 3, 0, 0)])
+@pytest.mark.parametrize("M,N,K", [(128, 4096, 4096), (100, 640, 3072), (128, 4096, 14336),
+                                   (77, 512, 2048)])
+def test_sf_partials_then_add_rmsnorm_bit_identical(sf, cfg, M, N, K):
+    """The prefill's wo / w2 without an in-kernel split-K seam: every K slice writes its fp32
+    partial tile (int4_linear_partials) and the residual add + RMSNorm sums them in slice order
+    (add_rmsnorm_partials): h and y bit-identical to add_rmsnorm(x, linear(...)) on the same
+    launch shape, whatever the split (1-8 slices, uneven slices, several M tiles, ragged M)."""
+    from torchao._models.llama import kernels
+
+    if cfg is None:  # the built-in route (served at M = 128 for the two Llama shapes only)
+        if M != 128 or N != 4096:
+            pytest.skip("no built-in route")
+    else:
+        sf(2, *cfg)
+    q, s, z, packed, sz = _int4(N, K, 32, seed=N + K)
+    a = oracle.make_activation(M, K, seed=M).to(DEV)
+    x = oracle.make_activation(M, N, seed=M + 1).to(DEV)
+    w = (torch.rand(N, generator=torch.Generator().manual_seed(3)) + 0.5).to(torch.bfloat16).to(DEV)
+    part = kernels.int4_linear_partials(a, packed, sz, 32)
+    assert part is not None and part.shape[1:] == (M, N)
+    lin = torch.ops.torchao.int4_weight_only_linear(a, packed, sz, 32, None)
+    h0, y0 = kernels.add_rmsnorm(x, lin, w, 1e-5)
+    h1, y1 = kernels.add_rmsnorm_partials(x, part, w, 1e-5)
+    assert torch.equal(h1, h0) and torch.equal(y1, y0)
+
+
+def test_sf_partials_not_served_on_the_32x32_route(sf):
+    """Shapes routed to the 32x32x16 kernel (one wave along M) have no partials-out form: None,
+    and the caller keeps the plain linear."""
+    from torchao._models.llama import kernels
+
+    sf(2, 128, 1, 2, 3, 0, 0)
+    q, s, z, packed, sz = _int4(512, 1024, 32, seed=9)
+    a = oracle.make_activation(128, 1024, seed=1).to(DEV)
+    assert kernels.int4_linear_partials(a, packed, sz, 32) is None

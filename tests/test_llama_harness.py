@@ -453,3 +453,39 @@ def test_prefill_last_row_gpu(quant, fuse):
             assert torch.equal(model._layers_prefill(prompt, pos, last_only=True)[:, -1:], full)
         finally:
             kernels.PREFILL_LAST_ROW = old
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fuse", [True, False])
+def test_prefill_partials_bit_identical_gpu(fuse):
+    """The prefill with wo / w2's K slices summed by the following add + RMSNorm
+    (kernels.PREFILL_PARTIALS) gives hidden states and KV caches bit-identical to the in-kernel
+    split-K seam (single-fetch GEMM forced on this small model's shapes with 4 K slices)."""
+    from torchao import _lib
+    from torchao._models.llama import kernels
+    from torchao._models.llama.generate import apply_quantization
+
+    dev = torch.device("cuda")
+    model = _tiny(dev)
+    if fuse:
+        model.fuse_w13()
+    apply_quantization(model, "int4wo-32")
+    model.setup_caches(1, 160)
+    model.enable_fused_kernels()
+    pos = torch.arange(100, device=dev)
+    prompt = torch.randint(0, model.config.vocab_size, (1, 100), device=dev,
+                           generator=torch.Generator(device=dev).manual_seed(7))
+    old = kernels.PREFILL_PARTIALS
+    _lib.call("tao_tune_gemm_sf", 2, 64, 2, 4, 3, 0, 0)
+    try:
+        outs = []
+        for flag in (False, True):
+            kernels.PREFILL_PARTIALS = flag
+            with torch.no_grad():
+                outs.append(model._layers_prefill(prompt, pos).clone())
+                outs.append(torch.cat([t.flatten() for b in model.layers for t in (
+                    b.attention.kv_cache.k_cache, b.attention.kv_cache.v_cache)]))
+        assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])
+    finally:
+        kernels.PREFILL_PARTIALS = old
+        _lib.call("tao_tune_reset")

@@ -119,6 +119,91 @@ __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(
   }
 }
 
+// The residual add of a linear whose K slices were NOT reduced in-kernel
+// (tao_int4wo_linear_partials_f32): the linear's output is formed here as bf16(sum_z part[z]) in
+// slice order from 0 (the single-fetch reducer's order and rounding, so bit-identical to its bf16
+// output), then h = bf16(x + that), y = RMSNorm(h) as rmsnorm_rows_kernel<NP, true>.
+template <int NP>
+__global__ __launch_bounds__(256) void rmsnorm_part_kernel(
+    const uint16_t* __restrict__ x, const float* __restrict__ part, int S, size_t plane,
+    const uint16_t* __restrict__ w, uint16_t* __restrict__ h, uint16_t* __restrict__ y, int D,
+    float eps) {
+  __shared__ float red[4];
+  const size_t row = (size_t)blockIdx.x * D;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + row);
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
+  const int nv = D / 8;
+  uint4 v[NP], g[NP];
+  float a[NP][8];
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {
+    const int i = threadIdx.x + 256 * u, ic = i < nv ? i : nv - 1;
+    v[u] = xr[ic];
+    g[u] = wr[ic];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[u][e] = 0.f;
+  }
+  for (int z = 0; z < S; ++z) {  // every slice's loads of the row in flight before the adds
+    float4 p[NP][2];
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+      const int i = threadIdx.x + 256 * u, ic = i < nv ? i : nv - 1;
+      const float4* pr = reinterpret_cast<const float4*>(part + (size_t)z * plane + row) + 2 * ic;
+      p[u][0] = pr[0];
+      p[u][1] = pr[1];
+    }
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+      a[u][0] += p[u][0].x;
+      a[u][1] += p[u][0].y;
+      a[u][2] += p[u][0].z;
+      a[u][3] += p[u][0].w;
+      a[u][4] += p[u][1].x;
+      a[u][5] += p[u][1].y;
+      a[u][6] += p[u][1].z;
+      a[u][7] += p[u][1].w;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      o[e] = (uint32_t)f32_to_bf16(a[u][2 * e]) | ((uint32_t)f32_to_bf16(a[u][2 * e + 1]) << 16);
+    v[u] = make_uint4(add_pair_bf16(v[u].x, o[0]), add_pair_bf16(v[u].y, o[1]),
+                      add_pair_bf16(v[u].z, o[2]), add_pair_bf16(v[u].w, o[3]));
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    if (i >= nv) continue;
+    reinterpret_cast<uint4*>(h + row)[i] = v[u];
+    const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float p = bf16lo_to_f32(d[j]), q = bf16hi_to_f32(d[j]);
+      ss = fmaf(p, p, fmaf(q, q, ss));
+    }
+  }
+  const float r = rsqrtf(block_sum(ss, red) / (float)D + eps);
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    if (i >= nv) continue;
+    const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+    const uint32_t e[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float lo = round_bf16(bf16lo_to_f32(d[j]) * r) * bf16lo_to_f32(e[j]);
+      const float hi = round_bf16(bf16hi_to_f32(d[j]) * r) * bf16hi_to_f32(e[j]);
+      o[j] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+    }
+    reinterpret_cast<uint4*>(y + row)[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // Rows wider than 8 x 4 x 256 bf16: the streaming form (x and the residual re-read after the sum)
 template <bool ADD>
 __global__ __launch_bounds__(256) void rmsnorm_wide_kernel(
@@ -673,6 +758,30 @@ int tao_add_rmsnorm_bf16(const uint16_t* x, const uint16_t* res, const uint16_t*
   TAO_CHECK_ALIGN(y, 16, "y");
   launch_rmsnorm<true>(x, res, w, h, y, rows, dim, eps, as_stream(stream));
   return check_launch("add_rmsnorm_kernel");
+}
+
+int tao_add_rmsnorm_partials_bf16(const uint16_t* x, const float* part, int64_t splits,
+                                  const uint16_t* w, uint16_t* h, uint16_t* y, int64_t rows,
+                                  int64_t dim, float eps, void* stream) {
+  TAO_CHECK_ARG(rows >= 0 && dim > 0 && dim % 8 == 0 && dim <= 8192,
+                "add_rmsnorm_partials: dim (%lld) must be a positive multiple of 8, <= 8192",
+                (long long)dim);
+  TAO_CHECK_ARG(splits >= 1 && splits <= 64, "add_rmsnorm_partials: splits (%lld) out of range",
+                (long long)splits);
+  if (rows == 0) return TAO_OK;
+  TAO_CHECK_ALIGN(x, 16, "x");
+  TAO_CHECK_ALIGN(part, 16, "part");
+  TAO_CHECK_ALIGN(w, 16, "w");
+  TAO_CHECK_ALIGN(h, 16, "h");
+  TAO_CHECK_ALIGN(y, 16, "y");
+  const dim3 grid((unsigned)rows), blk(256);
+  const int D = (int)dim, nv = D / 8, S = (int)splits;
+  const size_t plane = (size_t)rows * dim;
+  hipStream_t st = as_stream(stream);
+  if (nv <= 256) launch(rmsnorm_part_kernel<1>, grid, blk, 0, st, x, part, S, plane, w, h, y, D, eps);
+  else if (nv <= 512) launch(rmsnorm_part_kernel<2>, grid, blk, 0, st, x, part, S, plane, w, h, y, D, eps);
+  else launch(rmsnorm_part_kernel<4>, grid, blk, 0, st, x, part, S, plane, w, h, y, D, eps);
+  return check_launch("rmsnorm_part_kernel");
 }
 
 int tao_rope_kv_bf16(const uint16_t* qkv, const float* freqs, const int64_t* pos,

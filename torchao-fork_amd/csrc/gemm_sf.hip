@@ -66,9 +66,12 @@ __device__ unsigned g_sf_err = 0;
 // (gate, up) column pairs, y [M][N / 2]; 2 = RoPE + KV-cache write of a wqkv output (the prefill
 // rope_kv kernel's math, decode_ops.hip): rows are tokens (b, s) = (m / S, m % S) at position
 // pos[s]; columns [q heads | k heads | v heads] of D = 128; q rotated into q_out [B][H][S][D],
-// k rotated and v written into the caches [B][Hkv][T][D] at row pos[s].
+// k rotated and v written into the caches [B][Hkv][T][D] at row pos[s]; 3 = int4 only: no seam
+// and no bf16 output, every K slice z writes its fp32 partial tile row-major into
+// part[z][M][N] (the consumer sums the slices in slice order: tao_add_rmsnorm_partials_bf16).
 struct SfEpi {
   int kind;
+  float* part;         // kind 3: [S][M][N] fp32
   const float* freqs;  // [T][D / 2] (cos, sin)
   const int64_t* pos;  // [S]
   uint16_t* q_out;
@@ -510,6 +513,25 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
   }  // LDW == 0
   barrier_lgkm();  // all fragment reads done: the LDS is free for the epilogue image
   SF_MARK(3);
+  if constexpr (!kI8) {
+    if (epi == 3) {  // partials out: this slice's fp32 tile, row-major, no hand-off
+      if (!loader) {
+        float* dst = ep.part + (size_t)z * M * N;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int c = n_blk + wn * CN + 16 * nt + fr;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int r = m_blk + wm * RM + 16 * mt + 4 * kq + i;
+              if (r < M && c < N) dst[(size_t)r * N + c] = acc[mt][nt][i];
+            }
+        }
+      }
+      return;
+    }
+  }
 
   // ---- split-K seam -----------------------------------------------------------------------------
   // Slab: S slices' partial tiles per tile, each in the waves' fragment order (granule
@@ -986,7 +1008,7 @@ int sf_int4_epi(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, i
   const dim3 grid((N + sh.bn - 1) / sh.bn, 1, (M + kBM - 1) / kBM);  // tiles: grid.x grid.z
   f32x4_t* slab = nullptr;
   unsigned* cnt = nullptr;
-  if (sh.splits > 1) {
+  if (sh.splits > 1 && ep.kind != 3) {  // (the partials-out launch has no seam)
     void* w = nullptr;
     const size_t tiles = (size_t)grid.x * grid.z;
     const int rc = split_workspace(stream, tiles * sh.splits * kBM * sh.bn * 4,
@@ -1007,6 +1029,13 @@ int sf_int4_epi(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, i
       return sf_dispatch_wm<SfI4, 64>(sh, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt,
                                       ep);
   }
+}
+
+// K slices the partials-out launch of this int4 shape writes (0: not served, the 32x32x16 route)
+int sf_int4_partial_slices(int M, int N, int K) {
+  const SfShape sh = sf_shape(0, M, N, K);
+  if (sh.wm == 1 || (sh.bn != 64 && sh.bn != 128 && sh.bn != 256)) return 0;
+  return sh.splits;
 }
 
 int sf_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int lg,
@@ -1085,6 +1114,41 @@ extern "C" int tao_int4wo_linear_rope_kv_bf16(const uint16_t* x, const uint32_t*
   ep.Hkv = (int)Hkv;
   ep.T = (int)T;
   return tao::sf_int4_epi(x, packed, sz, lg_of(group_size), nullptr, q_out, (int)M, (int)N,
+                          (int)K, tao::as_stream(stream), ep);
+}
+
+// int4 weight-only linear whose K slices hand their fp32 partial tiles to the NEXT launch instead
+// of reducing them in-kernel (no split-K seam): part [S][M][N] fp32, S = the routed split count
+// (tao_int4wo_linear_partial_slices). The residual add + RMSNorm that follows wo / w2 in a prefill
+// sums them (tao_add_rmsnorm_partials_bf16): bf16(sum in slice order) is bit-identical to the
+// linear's bf16 output. TAO_ERR_UNSUPPORTED where the shape is not routed to the 16x16 kernel.
+extern "C" int tao_int4wo_linear_partial_slices(int64_t M, int64_t N, int64_t K,
+                                                int64_t group_size, int* slices) {
+  TAO_CHECK_ARG(slices != nullptr, "int4 partials: null output");
+  *slices = 0;
+  if (M > 0 && M <= (1 << 20) && N > 0 && K > 0 && tao::use_sf(0, M, N, K, group_size))
+    *slices = tao::sf_int4_partial_slices((int)M, (int)N, (int)K);
+  return TAO_OK;
+}
+
+extern "C" int tao_int4wo_linear_partials_f32(const uint16_t* x, const uint32_t* packed,
+                                              const uint16_t* sz, float* part, int64_t M,
+                                              int64_t N, int64_t K, int64_t group_size,
+                                              void* stream) {
+  int rc = tao::int4_check_linear_args(x, packed, sz, reinterpret_cast<uint16_t*>(part), M, N, K,
+                                       group_size);
+  if (rc != TAO_OK) return rc;
+  if (M == 0) return TAO_OK;
+  int S = 0;
+  tao_int4wo_linear_partial_slices(M, N, K, group_size, &S);
+  if (S == 0)
+    return tao::set_error(TAO_ERR_UNSUPPORTED,
+                          "int4 partials: no 16x16 single-fetch route for M=%lld N=%lld K=%lld",
+                          (long long)M, (long long)N, (long long)K);
+  tao::SfEpi ep{};
+  ep.kind = 3;
+  ep.part = part;
+  return tao::sf_int4_epi(x, packed, sz, lg_of(group_size), nullptr, nullptr, (int)M, (int)N,
                           (int)K, tao::as_stream(stream), ep);
 }
 

@@ -83,6 +83,9 @@ _SIGNATURES = {
     "tao_tune_int8_quant": [_int],
     "tao_rmsnorm_bf16": [_p, _p, _p, _i64, _i64, ctypes.c_float, _p],
     "tao_add_rmsnorm_bf16": [_p, _p, _p, _p, _p, _i64, _i64, ctypes.c_float, _p],
+    "tao_add_rmsnorm_partials_bf16": [_p, _p, _i64, _p, _p, _p, _i64, _i64, ctypes.c_float, _p],
+    "tao_int4wo_linear_partial_slices": [_i64, _i64, _i64, _i64, _p],
+    "tao_int4wo_linear_partials_f32": [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p],
     "tao_rope_kv_bf16": [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p],
     "tao_attn_decode_split_bf16": [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
                                    ctypes.c_float, _i64, _p],

@@ -47,6 +47,54 @@ def add_rmsnorm(x: torch.Tensor, res: torch.Tensor, weight: torch.Tensor, eps: f
     return h, y
 
 
+def add_rmsnorm_partials(x: torch.Tensor, part: torch.Tensor, weight: torch.Tensor, eps: float):
+    """(h, rmsnorm(h)) with h = x + bf16(sum of the fp32 partial planes part [S, *x.shape]) in one
+    launch (tao_add_rmsnorm_partials_bf16): bit-identical to add_rmsnorm(x, linear(...)) when
+    part comes from int4_linear_partials of that linear."""
+    _check(x, torch.bfloat16, "add_rmsnorm_partials x")
+    _check(part, torch.float32, "add_rmsnorm_partials part")
+    _check(weight, torch.bfloat16, "add_rmsnorm_partials weight")
+    if tuple(part.shape[1:]) != tuple(x.shape):
+        raise RuntimeError(f"add_rmsnorm_partials: part {tuple(part.shape)} does not hold planes "
+                           f"of x {tuple(x.shape)}")
+    h, y = torch.empty_like(x), torch.empty_like(x)
+    D = x.shape[-1]
+    _lib.call("tao_add_rmsnorm_partials_bf16", x.data_ptr(), part.data_ptr(), part.shape[0],
+              weight.data_ptr(), h.data_ptr(), y.data_ptr(), x.numel() // D, D, float(eps),
+              _stream(x))
+    return h, y
+
+
+def int4_linear_partials(x: torch.Tensor, packed: torch.Tensor, sz: torch.Tensor,
+                         group_size: int) -> Optional[torch.Tensor]:
+    """x @ W^T of an int4 linear as fp32 partial planes [S, *x.shape[:-1], N], one per K slice of
+    the single-fetch GEMM, left for add_rmsnorm_partials to sum (no in-kernel split-K seam;
+    tao_int4wo_linear_partials_f32), or None where the shape is not served that way."""
+    import ctypes
+
+    _check(x, torch.bfloat16, "int4_linear_partials x")
+    x2 = x.reshape(-1, x.shape[-1])
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    M, K = x2.shape
+    N = packed.shape[0]
+    S = ctypes.c_int(0)
+    _lib.call("tao_int4wo_linear_partial_slices", M, N, K, int(group_size),
+              ctypes.cast(ctypes.pointer(S), ctypes.c_void_p))
+    if S.value == 0:
+        return None
+    part = torch.empty(S.value, *x.shape[:-1], N, dtype=torch.float32, device=x.device)
+    h = _lib.lib()
+    rc = h.tao_int4wo_linear_partials_f32(x2.data_ptr(), packed.data_ptr(), sz.data_ptr(),
+                                          part.data_ptr(), M, N, K, int(group_size), _stream(x))
+    if rc == 2:  # TAO_ERR_UNSUPPORTED
+        return None
+    if rc != 0:
+        raise RuntimeError(f"tao_int4wo_linear_partials_f32 failed (status {rc}): "
+                           + h.tao_last_error().decode(errors="replace"))
+    return part
+
+
 def rope_kv(qkv: torch.Tensor, freqs: torch.Tensor, pos: torch.Tensor, k_cache: torch.Tensor,
             v_cache: torch.Tensor, n_head: int) -> torch.Tensor:
     """qkv [B, S, (H + 2 Hkv) D] -> rotated q [B, H, S, D]; k, v written to the caches at pos."""
@@ -230,6 +278,10 @@ PREFILL_ADD_NORM = True
 # for the last row only, on the one-token kernels (attention, wo + residual, RMSNorm + w1||w3 +
 # SwiGLU, w2 + residual).
 PREFILL_LAST_ROW = True
+# Prefill wo / w2 (int4, where the 16x16 single-fetch GEMM serves them): the K slices' fp32
+# partial tiles are summed by the residual add + RMSNorm launch that follows instead of at an
+# in-kernel split-K seam (int4_linear_partials + add_rmsnorm_partials; bit-identical).
+PREFILL_PARTIALS = True
 
 # Output heads (N >= HEAD_ROWS) normalise in their own RMSNorm launch unless HEAD_PROLOGUE.
 HEAD_ROWS = 65536

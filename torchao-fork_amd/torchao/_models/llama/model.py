@@ -161,6 +161,29 @@ def kernels_rmsnorm(x: torch.Tensor, norm: "RMSNorm") -> torch.Tensor:
     return kernels.rmsnorm(x, norm.weight, norm.eps)
 
 
+def _linear_or_partials(x: torch.Tensor, lin: nn.Linear):
+    """lin(x), or for an int4 linear the single-fetch GEMM's unreduced K-slice partials
+    (kernels.PREFILL_PARTIALS) wrapped as ("partials", part) for _add_norm to sum."""
+    from torchao._models.llama import kernels
+
+    p4 = _int4_parts(lin) if kernels.PREFILL_PARTIALS else None
+    if p4 is not None and x.dtype == torch.bfloat16:
+        part = kernels.int4_linear_partials(x, *p4)
+        if part is not None:
+            return ("partials", part)
+    return lin(x)
+
+
+def _add_norm(x: torch.Tensor, pending, norm: "RMSNorm"):
+    """(x + pending, RMSNorm(x + pending)) in one launch; pending is a bf16 linear output or
+    _linear_or_partials' partials."""
+    from torchao._models.llama import kernels
+
+    if isinstance(pending, tuple):
+        return kernels.add_rmsnorm_partials(x, pending[1], norm.weight, norm.eps)
+    return kernels.add_rmsnorm(x, pending, norm.weight, norm.eps)
+
+
 def _linear_plus(x: torch.Tensor, lin: nn.Linear, residual: torch.Tensor) -> torch.Tensor:
     """residual + lin(x); at one token the add rides on the linear's bias epilogue."""
     if x.numel() == x.shape[-1]:
@@ -275,9 +298,10 @@ class Attention(nn.Module):
         y = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, enable_gqa=True)
         return self.wo(y.transpose(1, 2).reshape(B, S, q_sz))
 
-    def forward_prefill(self, x, freqs_table, mask, input_pos):
+    def forward_prefill(self, x, freqs_table, mask, input_pos, wo=True):
         """S > 1 tokens on the gfx950 kernels: wqkv (MFMA GEMM), RoPE + KV-cache write in one
-        launch, then F.scaled_dot_product_attention over the caches (forward's math)."""
+        launch, then F.scaled_dot_product_attention over the caches (forward's math). wo=False:
+        the attention output [B, S, H * D] before the wo linear."""
         from torchao._models.llama import kernels
 
         B, S, _ = x.shape
@@ -294,10 +318,11 @@ class Attention(nn.Module):
             # the causal mask over the caches is keys 0..input_pos[s] for query s
             y = kernels.attn_prefill(q, kv.k_cache, kv.v_cache, input_pos,
                                      1.0 / math.sqrt(self.head_dim))
-            return self.wo(y)
+            return self.wo(y) if wo else y
         y = F.scaled_dot_product_attention(q, kv.k_cache, kv.v_cache, attn_mask=mask,
                                            enable_gqa=True)
-        return self.wo(y.transpose(1, 2).reshape(B, S, self.n_head * self.head_dim))
+        y = y.transpose(1, 2).reshape(B, S, self.n_head * self.head_dim)
+        return self.wo(y) if wo else y
 
     def prefill_last(self, x, freqs_table, input_pos):
         """forward_prefill's q / K / V for every row (the KV caches need them all), then the
@@ -520,15 +545,19 @@ class Transformer(nn.Module):
             if pending is None:
                 xn = kernels.rmsnorm(x, an.weight, an.eps)
             else:
-                x, xn = kernels.add_rmsnorm(x, pending, an.weight, an.eps)
+                x, xn = _add_norm(x, pending, an)
             if last_only and i == len(self.layers) - 1:
                 y = blk.attention.prefill_last(xn, self.freqs, input_pos)
                 h = _linear_plus(y, blk.attention.wo, x[:, -1:].contiguous())
                 return ff.forward_fused(h, h, fn)
-            a = blk.attention.forward_prefill(xn, self.freqs, mask, input_pos)
-            x, hn = kernels.add_rmsnorm(x, a, fn.weight, fn.eps)
-            pending = ff.w2(ff.swiglu_prefill(hn))
-        return x if pending is None else x + pending
+            y = blk.attention.forward_prefill(xn, self.freqs, mask, input_pos, wo=False)
+            x, hn = _add_norm(x, _linear_or_partials(y, blk.attention.wo), fn)
+            pending = _linear_or_partials(ff.swiglu_prefill(hn), ff.w2)
+        if pending is None:
+            return x
+        if isinstance(pending, tuple):  # the last w2's partials: h only (its norm is unused)
+            return _add_norm(x, pending, self.norm)[0]
+        return x + pending
 
     def prefill_next(self, idx: torch.Tensor, input_pos: torch.Tensor) -> torch.Tensor:
         """Greedy next token [B, 1] after the prompt ``idx`` [B, S] (the reference's prefill:
