@@ -4,6 +4,9 @@ distinct weights replayed back to back; the last launch's stamps (s_memrealtime,
 every workgroup's wave 0: first instruction, slices done, end.
 
     TORCHAO_MI355X_LIB=experiments/build/libgstamps.so python experiments/gemv_stamps.py
+
+Also per shape: end-time percentiles, the most workgroups running at once, and a pure 16-B read
+of the same bytes (tao_hbm_read_probe) replayed the same way, for the per-launch gap to it.
 """
 import ctypes
 import json
@@ -58,6 +61,32 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         per_launch = e0.elapsed_time(e1) * 1e3 / 10 / 32
+        nbytes = (N * K // 2 + N * (K // G) * 4 + 8191) // 8192 * 8192
+        rb = [torch.empty(nbytes, dtype=torch.uint8, device=dev).fill_(7) for _ in range(32)]
+        sink = torch.zeros(1024, dtype=torch.int32, device=dev)
+
+        def rrun():
+            sp = torch.cuda.current_stream().cuda_stream
+            for b in rb:
+                assert lib.tao_hbm_read_probe(b.data_ptr(), nbytes, sink.data_ptr(), sp) == 0
+        with torch.cuda.stream(s):
+            rrun()
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, stream=s):
+                rrun()
+        torch.cuda.current_stream().wait_stream(s)
+        for _ in range(3):
+            gr.replay()
+        e0.record()
+        for _ in range(10):
+            gr.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        read_per_launch = e0.elapsed_time(e1) * 1e3 / 10 / 32
+        del gr, rb
+        # the GEMV graph once more, so the stamps are the GEMV's
+        g.replay()
+        torch.cuda.synchronize()
         buf = np.zeros(NB * 4, dtype=np.uint64)
         assert lib.tao_debug_gemv_stamps(buf.ctypes.data, NB) == 0
         st = buf.reshape(NB, 4)
@@ -73,7 +102,13 @@ def main():
                                     round(float(us((st[:, 1] - st[:, 0]).max())), 2)],
                "tail_us": [round(float(us(np.median(st[:, 2] - st[:, 1]))), 2),
                            round(float(us((st[:, 2] - st[:, 1]).max())), 2)],
-               "last_end_minus_p90_end_us": round(float(us(st[:, 2].max() - np.percentile(st[:, 2], 90))), 2)}
+               "last_end_minus_p90_end_us": round(float(us(st[:, 2].max() - np.percentile(st[:, 2], 90))), 2),
+               "end_pct_us": [round(float(us(np.percentile(st[:, 2], q) - e)), 2)
+                              for q in (10, 50, 90, 99)],
+               "max_concurrent_wgs": int(max(
+                   ((st[:, 0] <= t) & (st[:, 2] > t)).sum() for t in np.linspace(e, st[:, 2].max(), 200))),
+               "pure_read_us_per_launch": round(read_per_launch, 3),
+               "bytes": nbytes}
         print(json.dumps(rec), flush=True)
         del g, ws
 
