@@ -36,6 +36,11 @@
 #define TAO_GEMV_STAMPS 0
 #endif
 // TAO_NORM_DEBUG 1 (timing only): the RMSNorm prologue skips its cross-wave exchange.
+// 1 (variant builds for A/B): M = 1 slices load their x pieces with their weights, and a wave's
+// two paired slices are both issued before the first is consumed (see load_slice)
+#ifndef GEMV_XPRE
+#define GEMV_XPRE 0
+#endif
 #ifndef TAO_NORM_DEBUG
 #define TAO_NORM_DEBUG 0
 #endif
@@ -278,11 +283,27 @@ __device__ __forceinline__ void gemv_body(
   // PAIR (waves owning >= 2 slices): slices are processed two at a time, both slices' weight
   // and (scale, zero) loads issued before either is consumed, so a wave walking two slices pays
   // one memory round trip, not two.
-  auto load_slice = [&](int s, uint4 (&wv)[RPW], uint32_t (&szv)[RPW], int& cc, bool& cval)
-      __attribute__((always_inline)) {
+  // XPRE (M == 1 without the LDS prologue, tao_tune_int4_xpre): a slice's x pieces are loaded
+  // with its weights, so a wave holding two slices in flight can consume the first while the
+  // second's loads are still out (in-order vmcnt: the first slice's loads are all older)
+  constexpr bool kXPre = GEMV_XPRE && MT == 1 && !PRO;
+  auto load_slice = [&](int s, uint4 (&wv)[RPW], uint32_t (&szv)[RPW], uint4 (&xv)[4], int& cc,
+                        bool& cval) __attribute__((always_inline)) {
     const int c = s * 64 + lane;
     cval = s < S && c < nchunk;
     cc = c < nchunk ? c : nchunk - 1;  // clamped: every load stays in bounds, no branches
+    if constexpr (kXPre) {
+      const uint4* xp = reinterpret_cast<const uint4*>(x + (size_t)cc * 32);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#if TAO_GEMV_DEBUG == 1 || TAO_GEMV_DEBUG == 6
+        xv[j] = make_uint4(0x3F803F80u + cc + j, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+        (void)xp;
+#else
+        xv[j] = xp[j];
+#endif
+      }
+    }
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
       const int n = row0 + r;
@@ -295,8 +316,8 @@ __device__ __forceinline__ void gemv_body(
 #endif
     }
   };
-  auto do_slice = [&](const uint4 (&wv)[RPW], const uint32_t (&szv)[RPW], int cc, bool cval)
-      __attribute__((always_inline)) {
+  auto do_slice = [&](const uint4 (&wv)[RPW], const uint32_t (&szv)[RPW], const uint4 (&xv)[4],
+                      int cc, bool cval) __attribute__((always_inline)) {
     // Lanes past K contribute nothing: zero their (s, z) so the chunk term vanishes.
     float sc[RPW], zp[RPW];
 #pragma unroll
@@ -318,8 +339,9 @@ __device__ __forceinline__ void gemv_body(
 #if TAO_GEMV_DEBUG == 1 || TAO_GEMV_DEBUG == 6
         const uint4 t4 = make_uint4(0x3F803F80u + cc + j, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
         (void)xp;
+        (void)xv;
 #else
-        const uint4 t4 = PRO ? xs[cc * 4 + ((j + (cc >> 2)) & 3)] : xp[j];
+        const uint4 t4 = kXPre ? xv[j] : PRO ? xs[cc * 4 + ((j + (cc >> 2)) & 3)] : xp[j];
 #endif
         xd[j][0] = t4.x;
         xd[j][1] = t4.y;
@@ -352,52 +374,59 @@ __device__ __forceinline__ void gemv_body(
   // With PRO the first slice (every wave has one: Wk <= S) is peeled so the RMSNorm prologue
   // can sit around its loads.
   auto pair_step = [&](int s, auto first) __attribute__((always_inline)) {
-    uint4 wv0[RPW], wv1[RPW];
+    uint4 wv0[RPW], wv1[RPW], xv0[4], xv1[4];
     uint32_t szv0[RPW], szv1[RPW];
     int cc0, cc1;
     bool cv0, cv1;
     if constexpr (PRO && decltype(first)::value) norm_load();
-    load_slice(s, wv0, szv0, cc0, cv0);
-    load_slice(s + Wk, wv1, szv1, cc1, cv1);
+    load_slice(s, wv0, szv0, xv0, cc0, cv0);
+    load_slice(s + Wk, wv1, szv1, xv1, cc1, cv1);
     if constexpr (PRO && decltype(first)::value) norm_finish();
-    do_slice(wv0, szv0, cc0, cv0);
-    if (s + Wk < S) do_slice(wv1, szv1, cc1, cv1);  // wave-uniform
+    do_slice(wv0, szv0, xv0, cc0, cv0);
+    if (s + Wk < S) do_slice(wv1, szv1, xv1, cc1, cv1);  // wave-uniform
   };
   auto single_step = [&](int s, auto first) __attribute__((always_inline)) {
-    uint4 wv0[RPW];
+    uint4 wv0[RPW], xv0[4];
     uint32_t szv0[RPW];
     int cc0;
     bool cv0;
     if constexpr (PRO && decltype(first)::value) norm_load();
-    load_slice(s, wv0, szv0, cc0, cv0);
+    load_slice(s, wv0, szv0, xv0, cc0, cv0);
     if constexpr (PRO && decltype(first)::value) norm_finish();
-    do_slice(wv0, szv0, cc0, cv0);
+    do_slice(wv0, szv0, xv0, cc0, cv0);
   };
   if constexpr (PAIR && PRO) {
     pair_step(wk, std::true_type{});
     for (int s = wk + 2 * Wk; s < S; s += 2 * Wk) pair_step(s, std::false_type{});
   } else if constexpr (PAIR) {
     for (int s = wk; s < S; s += 2 * Wk) {
-      uint4 wv0[RPW], wv1[RPW];
+      uint4 wv0[RPW], wv1[RPW], xv0[4], xv1[4];
       uint32_t szv0[RPW], szv1[RPW];
       int cc0, cc1;
       bool cv0, cv1;
-      load_slice(s, wv0, szv0, cc0, cv0);
-      load_slice(s + Wk, wv1, szv1, cc1, cv1);
-      do_slice(wv0, szv0, cc0, cv0);
-      if (s + Wk < S) do_slice(wv1, szv1, cc1, cv1);  // wave-uniform
+      load_slice(s, wv0, szv0, xv0, cc0, cv0);
+      load_slice(s + Wk, wv1, szv1, xv1, cc1, cv1);
+      if constexpr (kXPre) __builtin_amdgcn_sched_barrier(0);  // both slices' loads issued first
+      do_slice(wv0, szv0, xv0, cc0, cv0);
+      // wave-uniform. hipcc sinks slice s + Wk's loads into this branch, behind slice s's
+      // arithmetic; issuing both slices' loads first (the second do_slice unconditional) measured
+      // SLOWER: 28672x4096 14.6-15.0 -> 16.0 us, 4096x14336 9.3 -> 11.4 (every grid is resident
+      // at once, and a wave holding less in flight computes while the others' loads stream;
+      // profiles/r5g_ab_gemv_pair.jsonl)
+      if (GEMV_XPRE) do_slice(wv1, szv1, xv1, cc1, cv1);  // (past S: cv1 false, zero terms)
+      else if (s + Wk < S) do_slice(wv1, szv1, xv1, cc1, cv1);
     }
   } else if constexpr (PRO) {
     single_step(wk, std::true_type{});
     for (int s = wk + Wk; s < S; s += Wk) single_step(s, std::false_type{});
   } else {
     for (int s = wk; s < S; s += Wk) {
-      uint4 wv0[RPW];
+      uint4 wv0[RPW], xv0[4];
       uint32_t szv0[RPW];
       int cc0;
       bool cv0;
-      load_slice(s, wv0, szv0, cc0, cv0);
-      do_slice(wv0, szv0, cc0, cv0);
+      load_slice(s, wv0, szv0, xv0, cc0, cv0);
+      do_slice(wv0, szv0, xv0, cc0, cv0);
     }
   }
 
