@@ -42,7 +42,12 @@ def graph_us(launch, copies=32):
 
 def main():
     tag = os.path.basename(os.environ.get("TORCHAO_MI355X_LIB", "") or "shipped")
-    for N, K in ((4096, 4096), (6144, 4096), (28672, 4096), (4096, 14336)):
+    tune = os.environ.get("TUNE")  # "rpw,wk,g,occ" -> tao_tune_int4_gemv (0 = built-in)
+    if tune:
+        _lib.call("tao_tune_int4_gemv", *[int(v) for v in tune.split(",")])
+        tag += f" tune={tune}"
+    shapes = os.environ.get("SHAPES", "4096x4096,6144x4096,28672x4096,4096x14336")
+    for N, K in (tuple(int(v) for v in sh.split("x")) for sh in shapes.split(",")):
         ws = []
         for _ in range(32):
             q = torch.randint(0, 16, (N, K), dtype=torch.int32, device=dev)
