@@ -1138,7 +1138,8 @@ extern "C" int tao_int4wo_linear_partials_f32(const uint16_t* x, const uint32_t*
   int rc = tao::int4_check_linear_args(x, packed, sz, reinterpret_cast<uint16_t*>(part), M, N, K,
                                        group_size);
   if (rc != TAO_OK) return rc;
-  if (M == 0) return TAO_OK;
+  if (M == 0 || N == 0) return TAO_OK;
+  TAO_CHECK_ALIGN(part, 4, "part");
   int S = 0;
   tao_int4wo_linear_partial_slices(M, N, K, group_size, &S);
   if (S == 0)
