@@ -245,17 +245,19 @@ def test_fused_decode_matches_unfused_gpu(quant, split, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("P", [37, 200])
 @pytest.mark.parametrize("quant,fuse", [(None, True), ("int4wo-32", True), ("int4wo-32", False)])
-def test_fused_prefill_matches_torch_ops_gpu(quant, fuse):
+def test_fused_prefill_matches_torch_ops_gpu(quant, fuse, P):
     """S > 1 tokens on the fused kernels (RMSNorm, RoPE + KV write, SiLU-mul) track the torch-op
     forward: all positions' logits and the KV caches; prefill_next (head at the last position
-    only) takes the same greedy token wherever the top-2 margin decides it."""
+    only, the last block past wqkv on the one-token kernels) takes the same greedy token wherever
+    the top-2 margin decides it. P = 200: more than one 128-row M tile (the single-fetch GEMMs and
+    their partials path do not serve it; the MFMA GEMMs do)."""
     dev = torch.device("cuda")
     model = _tiny(dev, seed=7)
     if fuse:
         model.fuse_w13()
     apply_quantization(model, quant)
-    P = 37
     model.setup_caches(2, P + 3)
     prompt = torch.randint(0, 1000, (2, P), device=dev)
     pos = torch.arange(P, device=dev)
