@@ -437,14 +437,16 @@ def test_sf32_k_halves(sf, cfg, M, N, K):
 
 
 @pytest.mark.parametrize("cfg", [(128, 1, 1, 3, 0, 0), (128, 1, 4, 3, 0, 0), (64, 1, 2, 3, 0, 0),
-                                 (128, 1, 2, 3, 5, 0)])
+                                 (128, 1, 2, 3, 5, 0), (128, 1, 1, 3, 0, 2), (128, 1, 4, 3, 0, 2),
+                                 (128, 1, 2, 3, 5, 2)])
 @pytest.mark.parametrize("M,N,K", [(128, 4096, 4096), (100, 640, 3072), (200, 384, 2048),
                                    (128, 28672, 4096), (1, 96, 512)])
 def test_sf32_loader_waves_bit_identical(sf, cfg, M, N, K):
     """Dedicated LDS-DMA loader waves (tao_tune_gemm_sf_loaders 2) change who issues the DMA
     pieces and when, not what any compute wave reads or sums: outputs bit-identical to the
-    one-wave-per-column-group kernel, its SwiGLU epilogue too, at g = 32 (16-B (scale, zero)
-    pieces) and 128 (4-B pieces), split or not, ragged M / N, several M tiles."""
+    kernel without them, its SwiGLU epilogue too, at g = 32 (16-B (scale, zero) pieces) and 128
+    (4-B pieces), split or not, ragged M / N, several M tiles; one or two compute waves per
+    column group (k halves, ks 2)."""
     from torchao._models.llama import kernels
 
     sf(2, *cfg)

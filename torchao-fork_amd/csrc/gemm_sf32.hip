@@ -135,7 +135,6 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
     int epi) {
   constexpr int BN = 32 * WV;
   constexpr int NW = WV * KH;  // compute waves
-  static_assert(LDW == 0 || KH == 1, "loader waves with one compute wave per column group");
   constexpr int NWT = NW + LDW;            // waves of the workgroup
   constexpr int DW = LDW > 0 ? LDW : NW;   // waves that issue the DMA pieces
   constexpr bool IL = TAO_SF32_IL != 0 && NS >= 3 && LDW == 0;
@@ -267,8 +266,11 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
       sf[u] = bf16lo_to_f32(zw);
       cf[u] = bf16hi_to_f32(zw) - 8.f * sf[u];
     }
-    // A fragments of ks and ks + 1 in flight while ks's MFMAs run
-    bf16x8_t af[2][4];
+    // A fragments of ks and ks + 1 in flight while ks's MFMAs run (one buffer with k halves and
+    // loader waves: 12 waves cap a wave at 170 VGPRs, and the SIMD's other compute wave covers
+    // the read latency)
+    constexpr int AB = (LDW > 0 && KH == 2) ? 1 : 2;
+    bf16x8_t af[AB][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const int m = 32 * mt + r32;
@@ -276,7 +278,15 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
     }
     sfor<0, KS>([&](auto kc) {
       constexpr int k = decltype(kc)::value;
-      if (k + 1 < KS && TAO_SF32_DEBUG != 4) {
+      if constexpr (AB == 1) {
+        if (k > 0) {
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            const int m = 32 * mt + r32;
+            af[0][mt] = __builtin_bit_cast(bf16x8_t, img[m * 16 + xpos(m, 8 * h + ks0 + k)]);
+          }
+        }
+      } else if (k + 1 < KS && TAO_SF32_DEBUG != 4) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
           const int m = 32 * mt + r32;
@@ -291,11 +301,11 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
 #endif
 #if TAO_SF32_DEBUG == 1
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[mt][k] += (float)af[k & 1][mt][0] + (float)bf[mt];
+      for (int mt = 0; mt < 4; ++mt) acc[mt][k] += (float)af[k & (AB - 1)][mt][0] + (float)bf[mt];
 #else
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
-        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[k & 1][mt], bf, acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[k & (AB - 1)][mt], bf, acc[mt], 0, 0, 0);
 #endif
       if constexpr (ISS && IL)  // DMA pieces r with r KS / R == k after sub-step k's MFMAs
         sfor<0, R>([&](auto rc) {
@@ -470,6 +480,30 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
     }
     __syncthreads();
     if (*word == 0) return;  // timed out: write nothing (uniform over the workgroup)
+    if constexpr (LDW > 0 && KH == 2) {  // one accumulator tile at a time (the 170-VGPR cap of
+      // 12 waves), the same additions in the same order as below
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        f32x16_t st;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) st[i] = 0.f;
+        for (int zz = 0; zz < (lead ? S - 1 : 0); ++zz) {
+          uint4 pt[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            pt[q] = bload16<kSC1>(srs, lo + t * 64 * 64 + 16 * q, (uint32_t)zz * kSlice);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            st[4 * q] += __uint_as_float(pt[q].x);
+            st[4 * q + 1] += __uint_as_float(pt[q].y);
+            st[4 * q + 2] += __uint_as_float(pt[q].z);
+            st[4 * q + 3] += __uint_as_float(pt[q].w);
+          }
+        }
+        acc[t] = st + acc[t];
+      }
+      __syncthreads();  // `word` lives where the output image goes
+    } else {
     f32x16_t sum[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -495,6 +529,7 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = sum[t] + acc[t];
     __syncthreads();  // `word` lives where the output image goes
+    }
   }
 
   // epilogue: bf16 tile [128][BN] through LDS, rows out in 16-B pieces. C map (32x32x16): column
@@ -585,10 +620,16 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
   // (on for 128-column tiles at 3 stages: w1||w3 28672x4096 M = 128 47.4-48.5 -> 39.6 us,
   // 10240x8192 S = 2 48.9 -> 48.7; profiles/r5e_sf32_loaders.jsonl)
   const int ldm = tuning().sf_loaders;
-  const bool loaders = kh == 1 && ((ldm == 2 && (bn == 128 || bn == 64)) ||
-                                   (ldm == 0 && bn == 128 && stages == 3));
+  // (k halves + loaders, 12 waves: 70B's 10240x8192 49.4 -> 45.4 us; w1||w3 42.6 -> 44.8, so the
+  // one-compute-wave form stays there: profiles/r5g_ab_kh2_loaders.jsonl)
+  const bool loaders = (kh == 1 && ((ldm == 2 && (bn == 128 || bn == 64)) ||
+                                    (ldm == 0 && bn == 128 && stages == 3))) ||
+                       (kh == 2 && bn == 128 && (ldm == 2 || (ldm == 0 && stages == 3)));
   if (loaders) {
-    if (bn == 128) {
+    if (kh == 2) {  // two compute waves per column group (k halves) + 4 loader waves
+      if (z16) go1(gemm_sf32_int4_kernel<4, 3, 2, true, 4>, 12 * 64);
+      else go1(gemm_sf32_int4_kernel<4, 3, 2, false, 4>, 12 * 64);
+    } else if (bn == 128) {
       if (z16) go1(gemm_sf32_int4_kernel<4, 3, 1, true, 4>, 8 * 64);
       else go1(gemm_sf32_int4_kernel<4, 3, 1, false, 4>, 8 * 64);
     } else {
