@@ -48,6 +48,9 @@
 // Timing-only build (experiments/sf32_steps.py; never the shipped library): s_memtime (shader
 // clock) of every wave of workgroups 0..7 at each k step: step top, own DMAs landed, barrier
 // passed, MFMAs issued; and the s_memrealtime / s_memtime pair at entry and exit.
+#ifndef TAO_SF32_ABUF
+#define TAO_SF32_ABUF 2
+#endif
 #ifndef TAO_SF32_STEPSTAMPS
 #define TAO_SF32_STEPSTAMPS 0
 #endif
@@ -266,10 +269,9 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
       sf[u] = bf16lo_to_f32(zw);
       cf[u] = bf16hi_to_f32(zw) - 8.f * sf[u];
     }
-    // A fragments of ks and ks + 1 in flight while ks's MFMAs run (one buffer with k halves and
-    // loader waves: 12 waves cap a wave at 170 VGPRs, and the SIMD's other compute wave covers
-    // the read latency)
-    constexpr int AB = (LDW > 0 && KH == 2) ? 1 : 2;
+    // A fragments of ks and ks + 1 in flight while ks's MFMAs run (TAO_SF32_ABUF 1, variant
+    // builds: one buffer, each sub-step's fragments read at its top)
+    constexpr int AB = TAO_SF32_ABUF;
     bf16x8_t af[AB][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
