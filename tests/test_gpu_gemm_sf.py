@@ -600,3 +600,57 @@ def test_sf_partials_not_served_on_the_32x32_route(sf):
     q, s, z, packed, sz = _int4(512, 1024, 32, seed=9)
     a = oracle.make_activation(128, 1024, seed=1).to(DEV)
     assert kernels.int4_linear_partials(a, packed, sz, 32) is None
+
+
+def _rand_cases(seed, n):
+    """Seeded random (M, N, K, launch shape) cases for the single-fetch GEMMs."""
+    import random
+
+    r = random.Random(seed)
+    out = []
+    for _ in range(n):
+        M = r.choice([1, 7, 33, 64, 65, 100, 127, 128])
+        N = 64 * r.randint(1, 24) + r.choice([0, 0, 16, 48])
+        K = 128 * r.randint(2, 24)
+        bn = r.choice([64, 64, 128])
+        wm = r.choice([2, 4, 8]) if bn == 64 else r.choice([2, 4])
+        S = r.choice([1, 2, 4, 8])
+        stages = r.choice([2, 3, 4]) if bn == 64 else r.choice([2, 3])
+        out.append((M, N, K, (bn, wm, S, stages, 0, 0)))
+    return out
+
+
+@pytest.mark.parametrize("case", _rand_cases(2025, 24))
+def test_sf_random_shapes_all_forms_agree(sf, case):
+    """Seeded random shapes and launch shapes through every int4 form of the 16x16 single-fetch
+    GEMM that round 5 added beside the plain one: loader waves (4 DMA waves, 64-column tiles),
+    the K-slice -> XCD numbering, and the partials-out epilogue summed by add_rmsnorm_partials:
+    each bit-identical to the plain launch of the same shape, which is within the oracle bar."""
+    from torchao._models.llama import kernels
+
+    M, N, K, cfg = case
+    sf(2, *cfg)
+    _lib.call("tao_tune_gemm_sf_seam", 0)
+    q, s, z, packed, sz = _int4(N, K, 32, seed=N * 7 + K)
+    a = oracle.make_activation(M, K, seed=M + K).to(DEV)
+    _lib.call("tao_tune_gemm_sf_loaders", 1)
+    ref = torch.ops.torchao.int4_weight_only_linear(a, packed, sz, 32, None)
+    if cfg[0] == 64:
+        _lib.call("tao_tune_gemm_sf_loaders", 2)
+        assert torch.equal(torch.ops.torchao.int4_weight_only_linear(a, packed, sz, 32, None), ref)
+        _lib.call("tao_tune_gemm_sf_loaders", 1)
+    _lib.call("tao_tune_gemm_sf_xmap", 2)
+    assert torch.equal(torch.ops.torchao.int4_weight_only_linear(a, packed, sz, 32, None), ref)
+    _lib.call("tao_tune_gemm_sf_xmap", 1)
+    part = kernels.int4_linear_partials(a, packed, sz, 32)
+    if M <= 2:  # the plain linear runs the skinny-M GEMV there: no partials form
+        assert part is None
+    elif N % 8 == 0:
+        assert part is not None
+        x = oracle.make_activation(M, N, seed=3).to(DEV)
+        w = torch.ones(N, dtype=torch.bfloat16, device=DEV)
+        h0, y0 = kernels.add_rmsnorm(x, ref, w, 1e-5)
+        h1, y1 = kernels.add_rmsnorm_partials(x, part, w, 1e-5)
+        assert torch.equal(h1, h0) and torch.equal(y1, y0)
+    if N * K <= 4096 * 4096:
+        assert oracle.rel_l2(ref.cpu(), oracle.int4_linear(a.cpu(), q, s, z, 32)) < TOL_REF

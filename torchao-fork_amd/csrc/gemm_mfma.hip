@@ -1506,6 +1506,10 @@ int gshift_of(int64_t g) {
 
 }  // namespace
 
+// the skinny-M crossover, for the single-fetch partials entry (gemm_sf.hip), which serves only
+// shapes the plain linear runs on the single-fetch kernel
+bool int4_linear_takes_gemv(int64_t M, int64_t N, int64_t K) { return use_gemv(M, N, K); }
+
 int int8_scaled_mm_launch(const int8_t* xq, const uint16_t* xs, const int8_t* wq,
                           const uint16_t* ws, const uint16_t* bias, uint16_t* y, int M, int N,
                           int K, hipStream_t stream) {

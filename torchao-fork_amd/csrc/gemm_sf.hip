@@ -1058,6 +1058,10 @@ int int4_check_linear_args(const uint16_t* x, const uint32_t* packed, const uint
                            uint16_t* y, int64_t M, int64_t N, int64_t K, int64_t group_size);
 }  // namespace tao
 
+namespace tao {
+bool int4_linear_takes_gemv(int64_t M, int64_t N, int64_t K);
+}  // namespace tao
+
 static int lg_of(int64_t g) { return g == 32 ? 5 : g == 64 ? 6 : g == 128 ? 7 : 8; }
 
 extern "C" int tao_int4wo_linear_swiglu_bf16(const uint16_t* x, const uint32_t* packed,
@@ -1126,7 +1130,10 @@ extern "C" int tao_int4wo_linear_partial_slices(int64_t M, int64_t N, int64_t K,
                                                 int64_t group_size, int* slices) {
   TAO_CHECK_ARG(slices != nullptr, "int4 partials: null output");
   *slices = 0;
-  if (M > 0 && M <= (1 << 20) && N > 0 && K > 0 && tao::use_sf(0, M, N, K, group_size))
+  // served only where the plain linear takes this same kernel (not the skinny-M GEMV), so
+  // summing the partials reproduces its output bit for bit
+  if (M > 0 && M <= (1 << 20) && N > 0 && K > 0 && !tao::int4_linear_takes_gemv(M, N, K) &&
+      tao::use_sf(0, M, N, K, group_size))
     *slices = tao::sf_int4_partial_slices((int)M, (int)N, (int)K);
   return TAO_OK;
 }
