@@ -5,8 +5,9 @@ fused w1||w3, 128-token prompt): two prefill graphs captured with the flag off /
 alternately; ms per replay (HIP events around each replay), median of each, and the first tokens
 of both.
 
-    PYTHONPATH=torchao-fork_amd python experiments/ab_prefill_last.py [FLAG]
+    PYTHONPATH=torchao-fork_amd python experiments/ab_prefill_last.py [FLAG | tune:KNOB=OFF,ON]
 """
+import contextlib
 import json
 import sys
 
@@ -14,6 +15,7 @@ import torch
 
 from torchao._models.llama import kernels
 from torchao._models.llama.generate import GraphPrefill, apply_quantization, build_model
+from torchao.kernel.tuning import tuning
 
 
 def main():
@@ -28,10 +30,18 @@ def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "PREFILL_LAST_ROW"
     pres = {}
     for flag in (False, True):
-        setattr(kernels, name, flag)
-        pres[flag] = GraphPrefill(model, (1, P), dev)
-        pres[flag].capture(torch.randint(0, model.config.vocab_size, (1, P), generator=gen).to(dev))
-    setattr(kernels, name, True)
+        if name.startswith("tune:"):  # tune:KNOB=OFF,ON -- the knob's values for off / on
+            knob, vals = name[5:].split("=")
+            ctx = tuning(**{knob: int(vals.split(",")[int(flag)])})
+        else:
+            setattr(kernels, name, flag)
+            ctx = contextlib.nullcontext()
+        with ctx:
+            pres[flag] = GraphPrefill(model, (1, P), dev)
+            pres[flag].capture(torch.randint(0, model.config.vocab_size, (1, P),
+                                             generator=gen).to(dev))
+    if not name.startswith("tune:"):
+        setattr(kernels, name, True)
     times = {False: [], True: []}
     toks = {False: [], True: []}
     for rep in range(8):

@@ -20,6 +20,32 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "torchao-fork_amd"))
 
 from torchao._models.llama import kernels  # noqa: E402
+from torchao.kernel.tuning import tuning  # noqa: E402
+
+
+def graph_timed(fn, reps=20):
+    """us per call from a HIP graph of `reps` calls (no host launch cost between them)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(reps):
+                fn()
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for _ in range(5):
+        e0.record()
+        g.replay()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e3 / reps)
+    return sorted(ts)[2]
 
 
 def timed(fn, reps=20):
@@ -51,6 +77,11 @@ def main():
         mask = torch.ones(T, T, dtype=torch.bool, device=dev).tril()[pos].view(1, 1, S, T)
         scale = 1.0 / math.sqrt(D)
         ours = timed(lambda: kernels.attn_prefill(q, kc, vc, pos, scale))
+        by_nw = {}
+        for nw in (1, 2, 4):  # waves per query block (key blocks split round-robin)
+            with tuning(attn_prefill_nw=nw):
+                by_nw[nw] = round(graph_timed(lambda: kernels.attn_prefill(q, kc, vc, pos,
+                                                                            scale)), 2)
         sdpa = timed(lambda: F.scaled_dot_product_attention(q, kc, vc, attn_mask=mask,
                                                             enable_gqa=True))
         y = kernels.attn_prefill(q, kc, vc, pos, scale).float()
@@ -58,7 +89,7 @@ def main():
                                            enable_gqa=True).transpose(1, 2).reshape(1, S, H * D)
         err = float((y - r).abs().max())
         print(json.dumps({"lib": os.path.basename(os.environ.get("TORCHAO_MI355X_LIB", "shipped")),
-                          "S": S, "T": T, "ours_us": round(ours, 2), "sdpa_us": round(sdpa, 2),
+                          "S": S, "T": T, "ours_us": round(ours, 2), "graph_us_by_nw": by_nw, "sdpa_us": round(sdpa, 2),
                           "speedup": round(sdpa / ours, 2), "max_abs_err_vs_fp32": round(err, 5)}),
               flush=True)
         del kc, vc, q, mask

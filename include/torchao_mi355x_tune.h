@@ -128,6 +128,10 @@ int tao_tune_gemm_sf_loaders(int mode);
  * (slice z on XCDs [8z/S, 8(z+1)/S)), so each XCD's L2 takes in 1/S of x. 0 = built-in,
  * 1 = off, 2 = on. */
 int tao_tune_gemm_sf_xmap(int mode);
+/* Prefill attention: waves per 16-query block, each taking every nw-th 32-key block, partial
+ * softmax states merged through LDS (0 = built-in: 2 for 513-1024 query blocks, else 4;
+ * 1, 2 or 4). Thread-local; for measurement. */
+int tao_tune_attn_prefill_nw(int nw);
 /* Test hook for the single-fetch split-K seam (fixed reducer): with `on` = 1, slice-0 publishers
  * add their ticket only after a reducer has given up waiting (0.25 s) or 2 s passed, so tests can
  * check that a timed-out launch is reported (tao_gemm_sf_status, tao_decode_status bits & 2), writes

@@ -374,6 +374,13 @@ def test_attn_prefill_gpu(G, S, p0, T):
     ref = ref.transpose(1, 2).reshape(B, S, H * D)
     torch.testing.assert_close(got.float(), ref, rtol=2e-2, atol=2e-2)
     assert torch.equal(kernels.attn_prefill(q, kc, vc, pos, 1 / math.sqrt(D)), got)
+    # each key-split width (waves per query block; wave w takes key blocks w, w + nw, ...; waves
+    # past the last block merge an empty state) against the same reference
+    from torchao.kernel.tuning import tuning
+    for nw in (1, 2, 4):
+        with tuning(attn_prefill_nw=nw):
+            alt = kernels.attn_prefill(q, kc, vc, pos, 1 / math.sqrt(D))
+        torch.testing.assert_close(alt.float(), ref, rtol=2e-2, atol=2e-2)
 
 
 @pytest.mark.gpu

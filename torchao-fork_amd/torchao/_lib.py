@@ -60,6 +60,7 @@ _SIGNATURES = {
     "tao_tune_gemm_sf_seam": [_int],
     "tao_tune_gemm_sf_loaders": [_int],
     "tao_tune_gemm_sf_xmap": [_int],
+    "tao_tune_attn_prefill_nw": [_int],
     "tao_debug_sf_late_publisher": [_int],
     "tao_tune_cnt_stride": [_int],
     "tao_hbm_read_probe": [_p, _i64, _p, _p],

@@ -37,6 +37,7 @@ _KNOBS = {
     "gemm_sf_seam": ("tao_tune_gemm_sf_seam", 1),
     "gemm_sf_loaders": ("tao_tune_gemm_sf_loaders", 1),
     "gemm_sf_xmap": ("tao_tune_gemm_sf_xmap", 1),
+    "attn_prefill_nw": ("tao_tune_attn_prefill_nw", 1),
     "cnt_stride": ("tao_tune_cnt_stride", 1),
 }
 
