@@ -192,6 +192,25 @@ int tao_int4wo_decode_bf16(const uint16_t* x, const uint32_t* packed,
                            uint16_t* k_cache, uint16_t* v_cache, int64_t n_head,
                            int64_t n_kv_head, int64_t head_dim, int64_t max_seq, void* stream);
 
+/* Decode step, batch 1: RMSNorm -> int4 wqkv -> RoPE + KV-cache write (= tao_int4wo_decode_bf16
+ * with norm_weight and epilogue 2, q into `q` [n_head * 128]) AND the decode attention of the
+ * rotated q over cache keys 0..pos[0] (= tao_attn_decode_bf16) in ONE launch: out [n_head * 128]
+ * bf16. Replaces, at decode, the Attention.forward sequence wqkv -> apply_rotary_emb ->
+ * KVCache.update -> F.scaled_dot_product_attention (model.py:547-562). The attention workgroups
+ * (n_head x `splits` key ranges, splits 2 or 4) follow the GEMV's in the grid and start on
+ * per-head tickets; a ticket wait that times out sets tao_decode_status bit 2. head_dim 128,
+ * caches [1][n_kv_head][max_seq][128]; shapes tao_int4wo_qkv_attn_supported() accepts (returns
+ * 1 / 0, not a status). */
+int tao_int4wo_qkv_attn_supported(int64_t N, int64_t K, int64_t n_head, int64_t n_kv_head,
+                                  int64_t head_dim);
+int tao_int4wo_qkv_attn_bf16(const uint16_t* x, const uint32_t* packed,
+                             const uint16_t* scales_and_zeros, int64_t N, int64_t K,
+                             int64_t group_size, const uint16_t* norm_weight, float eps,
+                             uint16_t* q, uint16_t* out, const float* freqs, const int64_t* pos,
+                             uint16_t* k_cache, uint16_t* v_cache, int64_t n_head,
+                             int64_t n_kv_head, int64_t head_dim, int64_t max_seq, float scale,
+                             int64_t splits, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -211,12 +211,16 @@ def test_attn_decode_modes_gpu(mode, G):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("quant,split", [(None, 0), ("int4wo-32", 0), ("int4wo-32", 2),
-                                         ("int4wo-32", 4)])
+                                         ("int4wo-32", 4), ("int4wo-32", "qkv")])
 def test_fused_decode_matches_unfused_gpu(quant, split, monkeypatch):
     """Fused decode (one-pass attention, or with `split` the split attention + merged int4 wo,
-    forced for this small cache) against the torch-op forward; graph replay == eager."""
+    forced for this small cache; "qkv": wqkv + RoPE/KV + attention in one launch,
+    kernels.DECODE_QKV_ATTN) against the torch-op forward; graph replay == eager."""
     from torchao._models.llama import kernels
 
+    if split == "qkv":
+        monkeypatch.setattr(kernels, "DECODE_QKV_ATTN", True)
+        split = 0
     monkeypatch.setattr(kernels, "ATTN_SPLITS", split)
     monkeypatch.setattr(kernels, "ATTN_SPLIT_MIN_T", 0)
     dev = torch.device("cuda")

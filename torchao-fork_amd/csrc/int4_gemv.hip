@@ -96,7 +96,17 @@ __device__ __forceinline__ uint32_t rmsnorm_pair(uint32_t xv, uint32_t wv, float
 // 128), formed in the prologue instead of the RMSNorm: tao_int4wo_attn_out_bf16.
 // The body of one workgroup: rows row_base + rg RPW .. of row group rg (int4wo_gemv_kernel
 // calls it).
-template <int MT, int RPW, bool PAIR, int NPT = 0, int EPI = kEpiNone, int MRG = 0>
+// COH (tao_int4wo_qkv_attn_bf16): the RoPE epilogue's q and cache stores are agent-scope (sc1)
+// stores, read by the same launch's attention workgroups after their ticket wait.
+__device__ __forceinline__ void st_coh(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_coh(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int MT, int RPW, bool PAIR, int NPT = 0, int EPI = kEpiNone, int MRG = 0,
+          bool COH = false>
 __device__ __forceinline__ void gemv_body(
     const uint16_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
     const uint16_t* __restrict__ bias, uint16_t* __restrict__ y, int M, int N, int K, int gshift,
@@ -522,12 +532,14 @@ __device__ __forceinline__ void gemv_body(
           ov = (uint32_t)f32_to_bf16(o0) | ((uint32_t)f32_to_bf16(o1) << 16);
         }
         if (n < HD) {
-          reinterpret_cast<uint32_t*>(y)[n >> 1] = ov;
+          if constexpr (COH) st_coh(reinterpret_cast<uint32_t*>(y) + (n >> 1), ov);
+          else reinterpret_cast<uint32_t*>(y)[n >> 1] = ov;
         } else if (pok) {
           const int nk = n < HD + KD ? n - HD : n - HD - KD;
           uint16_t* cache = n < HD + KD ? fu.k_cache : fu.v_cache;
           const size_t off = ((size_t)(nk / D) * fu.T + p) * D + nk % D;
-          reinterpret_cast<uint32_t*>(cache)[off >> 1] = ov;
+          if constexpr (COH) st_coh(reinterpret_cast<uint32_t*>(cache) + (off >> 1), ov);
+          else reinterpret_cast<uint32_t*>(cache)[off >> 1] = ov;
         }
       }
     }
@@ -541,6 +553,243 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
     int Wk, int G, int S, GemvFuse fu) {
   gemv_body<MT, RPW, PAIR, NPT, EPI, MRG>(x, wq, sz, bias, y, M, N, K, gshift, Wk, G, S, fu,
                                           (int)blockIdx.x * G * RPW);
+}
+
+// ---- wqkv + RoPE / KV write + decode attention in one launch (tao_int4wo_qkv_attn_bf16) -------
+// Workgroups [0, ngemv) are the RMSNorm -> wqkv -> RoPE + KV GEMV (kEpiRopeKV, stores agent-scope);
+// each then adds one ticket for the q / k / v head its rows belong to. Workgroups past them (the
+// grid's tail, so on every XCD they are dispatched after all of that XCD's GEMV workgroups) are
+// the decode attention: one per (query head, key split), NW waves. A consumer loads its first
+// key step of cache history (rows < pos, written by earlier launches) before its wait, waits for
+// the q head's and the kv head's tickets, then reads q and the new row pos with agent-scope loads,
+// runs the one-pass attention of decode_ops.hip's attn_single_kernel over its key range, stores
+// its split's unnormalised partial (sc1) and the split whose ticket comes last merges the head
+// (attn_merge_weights) into the bf16 output. No stream-ordered launch between wqkv and the
+// attention: the attention launch's fixed cost and its cold history loads overlap the GEMV.
+// Tickets: producer counters go back to zero when the last consumer of a kv-head group has passed
+// its wait (it subtracts what each counter was owed), so a timed-out wait (reported through
+// tao_decode_status bits & 2, that head's output unspecified) still leaves them at zero once
+// the late producers have added.
+struct QkvAttn {
+  uint16_t* out;  // [H * D] bf16 attention output
+  float* part;    // [H][NS][kQaRec] fp32 split partials (split workspace slab)
+  unsigned* cnt;  // workspace counters, cs words apart: [0, H + 2 Hkv) tickets of the q | k | v
+                  // heads, [H + 2 Hkv, + Hkv) consumer arrivals per kv head, then H merge tickets
+  int ngemv, need, cs, fenced;
+  float scale;
+};
+constexpr int kQaRec = 132;  // o[128], m, l, 2 pad
+
+template <int NW, int NS>
+__device__ __forceinline__ void qkv_attn_tail(const GemvFuse& fu, const QkvAttn& qa,
+                                              const uint16_t* __restrict__ qbuf) {
+  constexpr int D = 128;
+  extern __shared__ float red[];  // [NW] m, [NW] l, [NW][D] o, one flag word
+  float* wm = red;
+  float* wl = red + NW;
+  float* wo = red + 2 * NW;
+  unsigned* flag = reinterpret_cast<unsigned*>(red + 2 * NW + NW * D);
+  const int c = (int)blockIdx.x - qa.ngemv;
+  const int h = c / NS, sp = c % NS;
+  const int G = fu.H / fu.Hkv, kvh = h / G, T = fu.T;
+  const int64_t p64 = fu.pos[0];
+  const int L = attn_len(p64, T);
+  const int pk = p64 >= 0 && p64 < T ? (int)p64 : -1;  // the cache row this launch writes
+  const int Cn = ((L + NS - 1) / NS + 15) & ~15;
+  const int lo = sp * Cn, hi = lo + Cn < L ? lo + Cn : L;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const size_t head = (size_t)kvh * T;  // batch 1
+  const uint32_t* vb = reinterpret_cast<const uint32_t*>(fu.v_cache + head * D) + lane;
+  // lane (g = l / 8, p8 = l % 8): keys t0 + g and t0 + 8 + g, dims 64 hh + 8 p8 + e
+  const int g = lane >> 3, p8 = lane & 7;
+  const uint16_t* kbase = fu.k_cache + head * D + p8 * 8;
+  uint4 ka[2], kb2[2];
+  uint32_t vv[16];
+  auto ldk = [&](int t, int hh) __attribute__((always_inline)) {
+    const uint16_t* kp = kbase + (size_t)t * D + 64 * hh;
+    if (t != pk) return *reinterpret_cast<const uint4*>(kp);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(kp);
+    return make_uint4(ld_coh(w), ld_coh(w + 1), ld_coh(w + 2), ld_coh(w + 3));
+  };
+  auto load_step = [&](int t0) __attribute__((always_inline)) {
+    const int ta = t0 + g < hi ? t0 + g : hi - 1, tb = t0 + 8 + g < hi ? t0 + 8 + g : hi - 1;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      ka[hh] = ldk(ta, hh);
+      kb2[hh] = ldk(tb, hh);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int tj = t0 + j < hi ? t0 + j : hi - 1;
+      vv[j] = tj != pk ? vb[(size_t)tj * (D / 2)] : ld_coh(vb + (size_t)tj * (D / 2));
+    }
+  };
+  // this wave's first step, before the wait when all its rows are history
+  const int t0w = lo + wave * 16;
+  const int lastw = t0w + 15 < hi - 1 ? t0w + 15 : hi - 1;
+  const bool early = t0w < hi && (pk < 0 || lastw < pk);
+  if (early) load_step(t0w);
+
+  // wait for the q head's and the kv head's tickets; then count this consumer in (the group's
+  // last one returns the producer counters to zero)
+  if (tid == 0) {
+    const unsigned* cq = qa.cnt + (size_t)h * qa.cs;
+    const unsigned* ck = qa.cnt + (size_t)(fu.H + kvh) * qa.cs;
+    const unsigned* cv = qa.cnt + (size_t)(fu.H + fu.Hkv + kvh) * qa.cs;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int)ld_coh(cq) < qa.need || (int)ld_coh(ck) < qa.need || (int)ld_coh(cv) < qa.need) {
+      if (seam_timed_out(t0)) {
+        flag_decode_error(kDecodeErrSplitK);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (qa.fenced) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    unsigned* cons = qa.cnt + (size_t)(fu.H + 2 * fu.Hkv + kvh) * qa.cs;
+    const unsigned arrivals = (unsigned)(G * NS);
+    if (__hip_atomic_fetch_add(cons, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        arrivals - 1) {
+      for (int j = 0; j < G; ++j)
+        __hip_atomic_fetch_sub(qa.cnt + (size_t)(kvh * G + j) * qa.cs, (unsigned)qa.need,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_sub(qa.cnt + (size_t)(fu.H + kvh) * qa.cs, (unsigned)qa.need,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_sub(qa.cnt + (size_t)(fu.H + fu.Hkv + kvh) * qa.cs, (unsigned)qa.need,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_sub(cons, arrivals, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (t0w < hi && !early) load_step(t0w);
+  uint32_t qw[8];
+  {
+    const uint32_t* qp = reinterpret_cast<const uint32_t*>(qbuf + (size_t)h * D + p8 * 8);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qw[hh * 4 + e] = ld_coh(qp + 32 * hh + e);
+  }
+  float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
+  for (int t0 = t0w; t0 < hi; t0 += NW * 16) {
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const uint32_t wa[4] = {ka[hh].x, ka[hh].y, ka[hh].z, ka[hh].w};
+      const uint32_t wb[4] = {kb2[hh].x, kb2[hh].y, kb2[hh].z, kb2[hh].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sa = dot2_bf16(qw[hh * 4 + e], wa[e], sa);
+        sb = dot2_bf16(qw[hh * 4 + e], wb[e], sb);
+      }
+    }
+    float vf[32];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      vf[2 * j] = bf16lo_to_f32(vv[j]);
+      vf[2 * j + 1] = bf16hi_to_f32(vv[j]);
+    }
+    if (t0 + NW * 16 < hi) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
+    sa = wave_bfly<1, 8>(sa, lane_id(), [](float a, float b) { return a + b; });
+    sb = wave_bfly<1, 8>(sb, lane_id(), [](float a, float b) { return a + b; });
+    const bool va = t0 + g < hi, vbk = t0 + 8 + g < hi;
+    sa = va ? sa * qa.scale : -INFINITY;
+    sb = vbk ? sb * qa.scale : -INFINITY;
+    float mx = fmaxf(sa, sb);
+    mx = wave_bfly<8, 64>(mx, lane_id(), [](float a, float b) { return fmaxf(a, b); });
+    const float mn = fmaxf(m, mx);
+    const float corr = __expf(m - mn);
+    const float ea = va ? __expf(sa - mn) : 0.f, eb = vbk ? __expf(sb - mn) : 0.f;
+    float es = ea + eb;
+    es = wave_bfly<8, 64>(es, lane_id(), [](float a, float b) { return a + b; });
+    l = fmaf(l, corr, es);
+    o0 *= corr;
+    o1 *= corr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float pa =
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ea), 8 * j));
+      const float pb =
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, eb), 8 * j));
+      o0 = fmaf(pa, vf[2 * j], o0);
+      o1 = fmaf(pa, vf[2 * j + 1], o1);
+      o0 = fmaf(pb, vf[2 * (j + 8)], o0);
+      o1 = fmaf(pb, vf[2 * (j + 8) + 1], o1);
+    }
+    m = mn;
+  }
+  if (lane == 0) {
+    wm[wave] = m;
+    wl[wave] = l;
+  }
+  wo[wave * D + 2 * lane] = o0;
+  wo[wave * D + 2 * lane + 1] = o1;
+  __syncthreads();
+  float* rec = qa.part + ((size_t)h * NS + sp) * kQaRec;
+  if (wave == 0) {  // this split's partial over the NW waves (a wave without keys has m = -inf)
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w]);
+    float a0 = 0.f, a1 = 0.f, ls = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const float f = wm[w] == -INFINITY ? 0.f : __expf(wm[w] - M);
+      ls = fmaf(wl[w], f, ls);
+      a0 = fmaf(wo[w * D + 2 * lane], f, a0);
+      a1 = fmaf(wo[w * D + 2 * lane + 1], f, a1);
+    }
+    uint32_t* r32 = reinterpret_cast<uint32_t*>(rec);
+    st_coh(r32 + 2 * lane, __float_as_uint(a0));
+    st_coh(r32 + 2 * lane + 1, __float_as_uint(a1));
+    if (lane == 0) {
+      st_coh(r32 + D, __float_as_uint(M));
+      st_coh(r32 + D + 1, __float_as_uint(ls));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  unsigned* mc = qa.cnt + (size_t)(fu.H + 3 * fu.Hkv + h) * qa.cs;
+  if (!last_arriver(mc, (unsigned)NS, flag, qa.fenced)) return;
+  if (wave != 0) return;
+  float2 ml[NS];
+  float ov[NS][2];
+#pragma unroll
+  for (int s2 = 0; s2 < NS; ++s2) {
+    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(qa.part + ((size_t)h * NS + s2) * kQaRec);
+    ml[s2] = make_float2(__uint_as_float(ld_coh(r32 + D)), __uint_as_float(ld_coh(r32 + D + 1)));
+    ov[s2][0] = __uint_as_float(ld_coh(r32 + 2 * lane));
+    ov[s2][1] = __uint_as_float(ld_coh(r32 + 2 * lane + 1));
+  }
+  float wgt[NS], inv;
+  attn_merge_weights<NS>(ml, wgt, inv);
+  float r0 = 0.f, r1 = 0.f;
+#pragma unroll
+  for (int s2 = 0; s2 < NS; ++s2) {
+    r0 = fmaf(ov[s2][0], wgt[s2], r0);
+    r1 = fmaf(ov[s2][1], wgt[s2], r1);
+  }
+  reinterpret_cast<uint32_t*>(qa.out)[(size_t)h * (D / 2) + lane] =
+      (uint32_t)f32_to_bf16(r0 * inv) | ((uint32_t)f32_to_bf16(r1 * inv) << 16);
+}
+
+template <int NPT, bool PAIR, int NS>
+__global__ __launch_bounds__(256, 4) void int4wo_qkv_attn_kernel(
+    const uint16_t* __restrict__ x, const uint4* __restrict__ wq, const uint32_t* __restrict__ sz,
+    uint16_t* __restrict__ y, int N, int K, int gshift, int S, GemvFuse fu, QkvAttn qa) {
+  if ((int)blockIdx.x < qa.ngemv) {  // 4 waves x 2 rows, whole rows (Wk = 1)
+    gemv_body<1, 2, PAIR, NPT, kEpiRopeKV, 0, true>(x, wq, sz, nullptr, y, 1, N, K, gshift, 1, 4,
+                                                    S, fu, (int)blockIdx.x * 8);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's q / k / v stores landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (qa.fenced) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __hip_atomic_fetch_add(qa.cnt + (size_t)((int)blockIdx.x * 8 / fu.D) * qa.cs, 1u,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  qkv_attn_tail<4, NS>(fu, qa, y);
 }
 
 int gshift_of(int64_t g) {
@@ -917,4 +1166,114 @@ extern "C" int tao_tune_int4_lds(int bytes) {
   TAO_CHECK_ARG(bytes >= 0 && bytes <= 160 * 1024, "tune: int4_lds bytes must be 0..163840");
   tao::tuning().gemv_lds = bytes;
   return TAO_OK;
+}
+
+namespace tao {
+namespace {
+
+// the fused launch's GEMV shape is the RMSNorm-prologue shape of wqkv (pro_shape) when that is
+// 4 waves x 2 rows of whole rows; 0 if not (the caller then runs the two launches)
+int qkv_attn_npt(int64_t N, int64_t K, int64_t n_head, int64_t n_kv_head, int64_t head_dim) {
+  if (head_dim != 128 || n_head <= 0 || n_kv_head <= 0 || n_head % n_kv_head != 0 ||
+      N != (n_head + 2 * n_kv_head) * head_dim || K <= 0 || K % 256 != 0 || K > 8192)
+    return 0;
+  const M1Shape c = pro_shape((int)N, (int)K);
+  const int S = (int)((K / 32 + 63) / 64);
+  const int wk = c.sh.wk < S ? c.sh.wk : S;
+  if (c.rpw != 2 || wk != 1 || c.sh.g != 4) return 0;
+  return 256 * 8 * 2 >= K ? 2 : 4;
+}
+
+template <int NPT, bool PAIR, int NS>
+void launch_qkv_attn(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, uint16_t* y,
+                     int N, int K, int gs, int S, const GemvFuse& fu, const QkvAttn& qa,
+                     size_t lds, hipStream_t st) {
+  launch((int4wo_qkv_attn_kernel<NPT, PAIR, NS>), dim3((unsigned)(qa.ngemv + fu.H * NS)),
+         dim3(256), lds, st, x, reinterpret_cast<const uint4*>(packed),
+         reinterpret_cast<const uint32_t*>(sz), y, N, K, gs, S, fu, qa);
+}
+
+}  // namespace
+}  // namespace tao
+
+extern "C" int tao_int4wo_qkv_attn_supported(int64_t N, int64_t K, int64_t n_head,
+                                             int64_t n_kv_head, int64_t head_dim) {
+  return tao::qkv_attn_npt(N, K, n_head, n_kv_head, head_dim) > 0 ? 1 : 0;
+}
+
+extern "C" int tao_int4wo_qkv_attn_bf16(const uint16_t* x, const uint32_t* packed,
+                                        const uint16_t* scales_and_zeros, int64_t N, int64_t K,
+                                        int64_t group_size, const uint16_t* norm_weight,
+                                        float eps, uint16_t* q, uint16_t* out, const float* freqs,
+                                        const int64_t* pos, uint16_t* k_cache, uint16_t* v_cache,
+                                        int64_t n_head, int64_t n_kv_head, int64_t head_dim,
+                                        int64_t max_seq, float scale, int64_t splits,
+                                        void* stream) {
+  int rc = tao::int4_check_linear_args(x, packed, scales_and_zeros, q, 1, N, K, group_size);
+  if (rc != TAO_OK) return rc;
+  const int npt = tao::qkv_attn_npt(N, K, n_head, n_kv_head, head_dim);
+  TAO_CHECK_ARG(npt > 0,
+                "int4 qkv_attn: unsupported shape (N %lld, K %lld, heads %lld / %lld, head_dim "
+                "%lld; tao_int4wo_qkv_attn_supported)",
+                (long long)N, (long long)K, (long long)n_head, (long long)n_kv_head,
+                (long long)head_dim);
+  TAO_CHECK_ARG(splits == 2 || splits == 4, "int4 qkv_attn: splits must be 2 or 4 (got %lld)",
+                (long long)splits);
+  TAO_CHECK_ARG(norm_weight != nullptr && freqs != nullptr && pos != nullptr &&
+                    k_cache != nullptr && v_cache != nullptr && out != nullptr,
+                "int4 qkv_attn: norm_weight, freqs, pos, caches and out are required");
+  TAO_CHECK_ARG(max_seq > 0 && max_seq < (1LL << 24), "int4 qkv_attn: max_seq out of range");
+  TAO_CHECK_ALIGN(norm_weight, 16, "norm_weight");
+  TAO_CHECK_ALIGN(k_cache, 16, "k_cache");
+  TAO_CHECK_ALIGN(v_cache, 16, "v_cache");
+  TAO_CHECK_ALIGN(q, 16, "q");
+  TAO_CHECK_ALIGN(out, 4, "out");
+  hipStream_t st = tao::as_stream(stream);
+  const int H = (int)n_head, Hkv = (int)n_kv_head;
+  const int cs = tao::tuning().cnt_stride;
+  void* slab = nullptr;
+  unsigned* cnt = nullptr;
+  rc = tao::split_workspace(st, (size_t)H * splits * tao::kQaRec * sizeof(float),
+                            (size_t)(2 * H + 3 * Hkv) * cs, &slab, &cnt);
+  if (rc != TAO_OK) return rc;
+  tao::GemvFuse fu{};
+  fu.norm_w = norm_weight;
+  fu.eps = eps;
+  fu.norm_deferred = tao::tuning().norm;
+  fu.freqs = freqs;
+  fu.pos = pos;
+  fu.k_cache = k_cache;
+  fu.v_cache = v_cache;
+  fu.H = H;
+  fu.Hkv = Hkv;
+  fu.D = (int)head_dim;
+  fu.T = (int)max_seq;
+  tao::QkvAttn qa{};
+  qa.out = out;
+  qa.part = static_cast<float*>(slab);
+  qa.cnt = cnt;
+  qa.ngemv = (int)(N / 8);
+  qa.need = (int)(head_dim / 8);
+  qa.cs = cs;
+  qa.fenced = tao::tuning().splitk_fenced;
+  qa.scale = scale;
+  const int iN = (int)N, iK = (int)K, gs = tao::gshift_of(group_size);
+  const int S = (iK / 32 + 63) / 64;
+  // dynamic LDS: the GEMV prologue's ([4][1][2] partials + 8, x [K] bf16) or the attention's
+  const size_t lds_gemv = (((size_t)8 + 8 + 3) & ~(size_t)3) * sizeof(float) + (size_t)iK * 2;
+  const size_t lds_attn = (size_t)(2 * 4 + 4 * 128 + 1) * sizeof(float);
+  const size_t lds = lds_gemv > lds_attn ? lds_gemv : lds_attn;
+#define TAO_QA(NPT, PAIR, NS) \
+  tao::launch_qkv_attn<NPT, PAIR, NS>(x, packed, scales_and_zeros, q, iN, iK, gs, S, fu, qa, lds, st)
+  if (npt == 2) {
+    if (S > 1) {
+      if (splits == 2) TAO_QA(2, true, 2); else TAO_QA(2, true, 4);
+    } else {
+      if (splits == 2) TAO_QA(2, false, 2); else TAO_QA(2, false, 4);
+    }
+  } else {
+    if (splits == 2) TAO_QA(4, true, 2); else TAO_QA(4, true, 4);
+  }
+#undef TAO_QA
+  return tao::check_launch("int4wo_qkv_attn_kernel");
 }

@@ -301,6 +301,9 @@ def main(argv=None):
                          "(kernels.PREFILL_ADD_NORM; -1 = built-in)")
     ap.add_argument("--native_prefill_attn", action="store_true",
                     help="prefill attention on tao_attn_prefill_bf16 (kernels.PREFILL_ATTN = True)")
+    ap.add_argument("--qkv_attn", type=int, default=-1,
+                    help="1 / 0: decode wqkv + RoPE/KV + attention in one launch or two "
+                         "(kernels.DECODE_QKV_ATTN; -1 = built-in)")
     ap.add_argument("--head_prologue", action="store_true",
                     help="fuse the final RMSNorm into the output head GEMV (kernels.HEAD_PROLOGUE)")
     ap.add_argument("--steps_per_graph", type=int, default=32,
@@ -322,9 +325,12 @@ def main(argv=None):
     ap.add_argument("--write_result", type=Path, default=None)
     args = ap.parse_args(argv)
 
-    if (args.head_prologue or args.sdpa_prefill
+    if (args.head_prologue or args.sdpa_prefill or args.qkv_attn >= 0
             or args.native_prefill_attn or args.prefill_add_norm >= 0):
         from torchao._models.llama import kernels
+
+        if args.qkv_attn >= 0:
+            kernels.DECODE_QKV_ATTN = bool(args.qkv_attn)
 
         if args.prefill_add_norm >= 0:
             kernels.PREFILL_ADD_NORM = bool(args.prefill_add_norm)

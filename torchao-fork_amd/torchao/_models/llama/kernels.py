@@ -144,6 +144,54 @@ ATTN_SPLIT_MAX_T = 8192
 PART_STRIDE = 132  # fp32 per (head, split) record: o[128], m, l, 2 pad
 
 
+# Decode: RMSNorm -> wqkv -> RoPE + KV write and the decode attention in ONE launch
+# (tao_int4wo_qkv_attn_bf16): the attention workgroups sit at the tail of the wqkv GEMV's grid,
+# load their cache history while the GEMV streams, and start on the ticket of their q / kv heads
+# instead of a stream-ordered launch. For int4 wqkv at batch 1, head_dim 128, caches of at most
+# QKV_ATTN_MAX_T rows (each of the QKV_ATTN_SPLITS key ranges per head is walked by 4 waves).
+# Off: measured SLOWER than the two launches (profiles/r5k_qkv_attn_time.jsonl, us per layer in a
+# 32-layer graph, two launches vs one at 128 / 328 / 512 / 900 keys: 10.3 / 12.0 / 13.0 / 16.3 vs
+# 13.0 / 13.5 / 13.6 / 16.3; e2e 721-729 vs 677-681 tok/s, r5k_ab_qkv_attn.jsonl): the in-launch
+# chain of agent-scope hand-offs (q / k / v stores written through, ticket, poll, split partials,
+# merge ticket) costs more than the launch boundary it removes.
+DECODE_QKV_ATTN = False
+QKV_ATTN_SPLITS = 4
+QKV_ATTN_MAX_T = 2048
+
+
+def qkv_attn_supported(N: int, K: int, n_head: int, n_kv_head: int, head_dim: int) -> bool:
+    """Whether tao_int4wo_qkv_attn_bf16 serves this wqkv shape (its GEMV part runs the RMSNorm
+    prologue's 4 waves x 2 rows launch shape)."""
+    return bool(_lib.lib().tao_int4wo_qkv_attn_supported(N, K, n_head, n_kv_head, head_dim))
+
+
+def int4_qkv_attn(x: torch.Tensor, packed: torch.Tensor, scale_and_zero: torch.Tensor,
+                  group_size: int, norm_weight: torch.Tensor, eps: float, freqs: torch.Tensor,
+                  pos: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, n_head: int,
+                  scale: float, splits: int = 0) -> torch.Tensor:
+    """One token: RMSNorm(x) -> int4 wqkv -> RoPE, k / v into the caches at pos[0], and the
+    decode attention of the rotated q over keys 0..pos[0] -> [1, 1, n_head * D] bf16, in one
+    launch (tao_int4wo_qkv_attn_bf16). Same results as int4_decode(..., "rope_kv") followed by
+    attn_decode up to the attention's fp32 summation order."""
+    _check(x, torch.bfloat16, "int4_qkv_attn x")
+    _check(norm_weight, torch.bfloat16, "int4_qkv_attn norm_weight")
+    _check(pos, torch.int64, "int4_qkv_attn pos")
+    N, K = packed.shape[0], x.shape[-1]
+    if x.numel() != K:
+        raise RuntimeError(f"int4_qkv_attn takes one token, got x of shape {tuple(x.shape)}")
+    B, Hkv, T, D = k_cache.shape
+    if B != 1:
+        raise RuntimeError("int4_qkv_attn: batch 1 caches only")
+    q = torch.empty(1, n_head, 1, D, dtype=x.dtype, device=x.device)
+    out = torch.empty(1, 1, n_head * D, dtype=x.dtype, device=x.device)
+    _lib.call("tao_int4wo_qkv_attn_bf16", x.data_ptr(), packed.data_ptr(),
+              scale_and_zero.data_ptr(), N, K, int(group_size), norm_weight.data_ptr(),
+              float(eps), q.data_ptr(), out.data_ptr(), freqs.data_ptr(), pos.data_ptr(),
+              k_cache.data_ptr(), v_cache.data_ptr(), n_head, Hkv, D, T, float(scale),
+              int(splits or QKV_ATTN_SPLITS), _stream(x))
+    return out
+
+
 def attn_decode_split(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                       pos: torch.Tensor, scale: float, splits: int) -> torch.Tensor:
     """q [B, H, 1, D] against keys 0..pos[0], the keys split `splits` ways per head ->
@@ -412,3 +460,7 @@ def check_decode_status() -> None:
         raise RuntimeError("decode step at a position past the KV cache (max_seq_length): "
                            "no cache row was written; call setup_caches() with a larger "
                            "max_seq_length")
+    if bits.value & 2:
+        raise RuntimeError("a cross-workgroup hand-off (split-K reducer or fused decode "
+                           "attention) timed out waiting for its producers; those outputs are "
+                           "unspecified")

@@ -345,6 +345,17 @@ class Attention(nn.Module):
         from torchao._models.llama import kernels
 
         kv = self.kv_cache
+        scale = 1.0 / math.sqrt(self.head_dim)
+        # int4 at batch 1: RMSNorm -> wqkv -> RoPE + KV write -> attention in one launch
+        pq = None if (norm is None or not kernels.DECODE_QKV_ATTN) else _int4_parts(self.wqkv)
+        if (pq is not None and x.numel() == x.shape[-1] and kv.k_cache.shape[0] == 1
+                and kv.k_cache.shape[2] <= kernels.QKV_ATTN_MAX_T
+                and kernels.prologue_pays(pq[0].shape[0], x.shape[-1])
+                and kernels.qkv_attn_supported(pq[0].shape[0], x.shape[-1], self.n_head,
+                                               kv.k_cache.shape[1], self.head_dim)):
+            y = kernels.int4_qkv_attn(x, *pq, norm.weight, norm.eps, freqs_table, input_pos,
+                                      kv.k_cache, kv.v_cache, self.n_head, scale)
+            return _linear_plus(y, self.wo, residual)
         # RMSNorm -> wqkv -> RoPE + KV-cache write in one launch (int4 / int8 weight-only)
         q = None if norm is None else _fused_decode(
             x, self.wqkv, norm, "rope_kv", (freqs_table, input_pos, kv.k_cache, kv.v_cache,
@@ -354,7 +365,6 @@ class Attention(nn.Module):
                 x = kernels.rmsnorm(x, norm.weight, norm.eps)
             q = kernels.rope_kv(self.wqkv(x), freqs_table, input_pos, kv.k_cache, kv.v_cache,
                                 self.n_head)
-        scale = 1.0 / math.sqrt(self.head_dim)
         # int4 wo at batch 1: the attention split over key ranges (more workgroups than heads),
         # its merge folded into wo's x load (one launch each, as the unsplit pair)
         p4 = _int4_parts(self.wo)
