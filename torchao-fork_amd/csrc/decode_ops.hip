@@ -123,7 +123,9 @@ __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(
 // (tao_int4wo_linear_partials_f32): the linear's output is formed here as bf16(sum_z part[z]) in
 // slice order from 0 (the single-fetch reducer's order and rounding, so bit-identical to its bf16
 // output), then h = bf16(x + that), y = RMSNorm(h) as rmsnorm_rows_kernel<NP, true>.
-template <int NP>
+// SS > 0: S == SS known at compile time, so every slice's loads are issued before the first add
+// (one round trip; a runtime S loop waits once per slice). SS == 0: any S, one slice at a time.
+template <int NP, int SS>
 __global__ __launch_bounds__(256) void rmsnorm_part_kernel(
     const uint16_t* __restrict__ x, const float* __restrict__ part, int S, size_t plane,
     const uint16_t* __restrict__ w, uint16_t* __restrict__ h, uint16_t* __restrict__ y, int D,
@@ -143,15 +145,7 @@ __global__ __launch_bounds__(256) void rmsnorm_part_kernel(
 #pragma unroll
     for (int e = 0; e < 8; ++e) a[u][e] = 0.f;
   }
-  for (int z = 0; z < S; ++z) {  // every slice's loads of the row in flight before the adds
-    float4 p[NP][2];
-#pragma unroll
-    for (int u = 0; u < NP; ++u) {
-      const int i = threadIdx.x + 256 * u, ic = i < nv ? i : nv - 1;
-      const float4* pr = reinterpret_cast<const float4*>(part + (size_t)z * plane + row) + 2 * ic;
-      p[u][0] = pr[0];
-      p[u][1] = pr[1];
-    }
+  auto add_slice = [&](const float4 (&p)[NP][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < NP; ++u) {
       a[u][0] += p[u][0].x;
@@ -162,6 +156,28 @@ __global__ __launch_bounds__(256) void rmsnorm_part_kernel(
       a[u][5] += p[u][1].y;
       a[u][6] += p[u][1].z;
       a[u][7] += p[u][1].w;
+    }
+  };
+  auto load_slice = [&](int z, float4 (&p)[NP][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+      const int i = threadIdx.x + 256 * u, ic = i < nv ? i : nv - 1;
+      const float4* pr = reinterpret_cast<const float4*>(part + (size_t)z * plane + row) + 2 * ic;
+      p[u][0] = pr[0];
+      p[u][1] = pr[1];
+    }
+  };
+  if constexpr (SS > 0) {  // all SS slices in flight, then summed in slice order from 0
+    float4 p[SS][NP][2];
+#pragma unroll
+    for (int z = 0; z < SS; ++z) load_slice(z, p[z]);
+#pragma unroll
+    for (int z = 0; z < SS; ++z) add_slice(p[z]);
+  } else {
+    for (int z = 0; z < S; ++z) {
+      float4 p[NP][2];
+      load_slice(z, p);
+      add_slice(p);
     }
   }
 #pragma unroll
@@ -778,9 +794,16 @@ int tao_add_rmsnorm_partials_bf16(const uint16_t* x, const float* part, int64_t 
   const int D = (int)dim, nv = D / 8, S = (int)splits;
   const size_t plane = (size_t)rows * dim;
   hipStream_t st = as_stream(stream);
-  if (nv <= 256) launch(rmsnorm_part_kernel<1>, grid, blk, 0, st, x, part, S, plane, w, h, y, D, eps);
-  else if (nv <= 512) launch(rmsnorm_part_kernel<2>, grid, blk, 0, st, x, part, S, plane, w, h, y, D, eps);
-  else launch(rmsnorm_part_kernel<4>, grid, blk, 0, st, x, part, S, plane, w, h, y, D, eps);
+#define TAO_PART(NP)                                                                          \
+  switch (S) {                                                                                \
+    case 2: launch(rmsnorm_part_kernel<NP, 2>, grid, blk, 0, st, x, part, S, plane, w, h, y, D, eps); break; \
+    case 4: launch(rmsnorm_part_kernel<NP, 4>, grid, blk, 0, st, x, part, S, plane, w, h, y, D, eps); break; \
+    default: launch(rmsnorm_part_kernel<NP, 0>, grid, blk, 0, st, x, part, S, plane, w, h, y, D, eps); \
+  }
+  if (nv <= 256) TAO_PART(1)
+  else if (nv <= 512) TAO_PART(2)
+  else TAO_PART(4)
+#undef TAO_PART
   return check_launch("rmsnorm_part_kernel");
 }
 
