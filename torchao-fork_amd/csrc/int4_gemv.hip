@@ -35,7 +35,8 @@
 #ifndef TAO_GEMV_STAMPS
 #define TAO_GEMV_STAMPS 0
 #endif
-// TAO_NORM_DEBUG 1 (timing only): the RMSNorm prologue skips its cross-wave exchange.
+// TAO_NORM_DEBUG 1 (timing only): the RMSNorm prologue skips its cross-wave exchange; 2: it
+// keeps the exchange but stores x unnormalised.
 // 1 (variant builds for A/B): M = 1 slices load their x pieces with their weights, and a wave's
 // two paired slices are both issued before the first is consumed (see load_slice)
 #ifndef GEMV_XPRE
@@ -282,9 +283,16 @@ __device__ __forceinline__ void gemv_body(
       const int i = threadIdx.x + u * (int)blockDim.x;
       if (i < nx) {
         const int c = i >> 2;
+#if TAO_NORM_DEBUG == 2
+        // timing only: the sum, exchange and barriers kept, the per-element normalisation not
+        const uint32_t k = r > 1e30f ? 1u : 0u;
+        xs[c * 4 + (((i & 3) + (c >> 2)) & 3)] =
+            make_uint4(xv[u].x ^ k, xv[u].y ^ gv[u].y, xv[u].z, xv[u].w);
+#else
         xs[c * 4 + (((i & 3) + (c >> 2)) & 3)] =
             make_uint4(rmsnorm_pair(xv[u].x, gv[u].x, r), rmsnorm_pair(xv[u].y, gv[u].y, r),
                        rmsnorm_pair(xv[u].z, gv[u].z, r), rmsnorm_pair(xv[u].w, gv[u].w, r));
+#endif
       }
     }
     __syncthreads();
