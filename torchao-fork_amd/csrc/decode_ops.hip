@@ -26,6 +26,7 @@ int attn_prefill_mfma(const uint16_t* q, const uint16_t* k_cache, const uint16_t
                       const int64_t* pos, uint16_t* out, int64_t B, int64_t H, int64_t Hkv,
                       int64_t S, int64_t T, float scale, hipStream_t stream);
 }  // namespace tao
+#include "tao_attn.h"
 #include "tao_reduce.h"
 
 #ifndef TAO_ATTN_WAVES
@@ -533,53 +534,10 @@ __global__ __launch_bounds__(NW * 64) void attn_single_kernel(
     }
   }
   float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
-  for (int t0 = lo + wave * 16; t0 < hi; t0 += NW * 16) {
-    float sa = 0.f, sb = 0.f;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const uint32_t wa[4] = {ka[hh].x, ka[hh].y, ka[hh].z, ka[hh].w};
-      const uint32_t wb[4] = {kb2[hh].x, kb2[hh].y, kb2[hh].z, kb2[hh].w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        sa = dot2_bf16(qw[hh * 4 + e], wa[e], sa);
-        sb = dot2_bf16(qw[hh * 4 + e], wb[e], sb);
-      }
-    }
-    float vf[32];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      vf[2 * j] = bf16lo_to_f32(vv[j]);
-      vf[2 * j + 1] = bf16hi_to_f32(vv[j]);
-    }
-    if (t0 + NW * 16 < hi) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
-    sa = wave_bfly<1, 8>(sa, lane_id(), [](float a, float c) { return a + c; });
-    sb = wave_bfly<1, 8>(sb, lane_id(), [](float a, float c) { return a + c; });
-    const bool va = t0 + g < hi, vbk = t0 + 8 + g < hi;
-    sa = va ? sa * scale : -INFINITY;
-    sb = vbk ? sb * scale : -INFINITY;
-    float mx = fmaxf(sa, sb);
-    mx = wave_bfly<8, 64>(mx, lane_id(), [](float a, float c) { return fmaxf(a, c); });
-    const float mn = fmaxf(m, mx);  // finite: key t0 < L is valid
-    const float corr = __expf(m - mn);
-    const float ea = va ? __expf(sa - mn) : 0.f, eb = vbk ? __expf(sb - mn) : 0.f;
-    float es = ea + eb;  // each key sits in 8 lanes of one group: xor 8..32 counts it once
-    es = wave_bfly<8, 64>(es, lane_id(), [](float a, float c) { return a + c; });
-    l = fmaf(l, corr, es);
-    o0 *= corr;
-    o1 *= corr;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float pa =
-          __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ea), 8 * j));
-      const float pb =
-          __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, eb), 8 * j));
-      o0 = fmaf(pa, vf[2 * j], o0);
-      o1 = fmaf(pa, vf[2 * j + 1], o1);
-      o0 = fmaf(pb, vf[2 * (j + 8)], o0);
-      o1 = fmaf(pb, vf[2 * (j + 8) + 1], o1);
-    }
-    m = mn;
-  }
+  for (int t0 = lo + wave * 16; t0 < hi; t0 += NW * 16)
+    attn_decode_step(qw, ka, kb2, vv, t0, hi, g, scale, m, l, o0, o1, [&]() {
+      if (t0 + NW * 16 < hi) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
+    });
   if (lane == 0) {
     wm[wave] = m;
     wl[wave] = l;

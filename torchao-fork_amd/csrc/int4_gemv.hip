@@ -20,6 +20,7 @@
 #include <type_traits>
 
 #include "tao_common.h"
+#include "tao_attn.h"
 #include "tao_reduce.h"
 
 // Timing-only variant builds (experiments/gemv_debug.sh; never the shipped library):
@@ -570,7 +571,7 @@ __global__ __launch_bounds__(512, WPE) void int4wo_gemv_kernel(
 // the decode attention: one per (query head, key split), NW waves. A consumer loads its first
 // key step of cache history (rows < pos, written by earlier launches) before its wait, waits for
 // the q head's and the kv head's tickets, then reads q and the new row pos with agent-scope loads,
-// runs the one-pass attention of decode_ops.hip's attn_single_kernel over its key range, stores
+// runs the one-pass attention step (tao_attn.h, as attn_single_kernel) over its key range, stores
 // its split's unnormalised partial (sc1) and the split whose ticket comes last merges the head
 // (attn_merge_weights) into the bf16 output. No stream-ordered launch between wqkv and the
 // attention: the attention launch's fixed cost and its cold history loads overlap the GEMV.
@@ -678,53 +679,10 @@ __device__ __forceinline__ void qkv_attn_tail(const GemvFuse& fu, const QkvAttn&
       for (int e = 0; e < 4; ++e) qw[hh * 4 + e] = ld_coh(qp + 32 * hh + e);
   }
   float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
-  for (int t0 = t0w; t0 < hi; t0 += NW * 16) {
-    float sa = 0.f, sb = 0.f;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const uint32_t wa[4] = {ka[hh].x, ka[hh].y, ka[hh].z, ka[hh].w};
-      const uint32_t wb[4] = {kb2[hh].x, kb2[hh].y, kb2[hh].z, kb2[hh].w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        sa = dot2_bf16(qw[hh * 4 + e], wa[e], sa);
-        sb = dot2_bf16(qw[hh * 4 + e], wb[e], sb);
-      }
-    }
-    float vf[32];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      vf[2 * j] = bf16lo_to_f32(vv[j]);
-      vf[2 * j + 1] = bf16hi_to_f32(vv[j]);
-    }
-    if (t0 + NW * 16 < hi) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
-    sa = wave_bfly<1, 8>(sa, lane_id(), [](float a, float b) { return a + b; });
-    sb = wave_bfly<1, 8>(sb, lane_id(), [](float a, float b) { return a + b; });
-    const bool va = t0 + g < hi, vbk = t0 + 8 + g < hi;
-    sa = va ? sa * qa.scale : -INFINITY;
-    sb = vbk ? sb * qa.scale : -INFINITY;
-    float mx = fmaxf(sa, sb);
-    mx = wave_bfly<8, 64>(mx, lane_id(), [](float a, float b) { return fmaxf(a, b); });
-    const float mn = fmaxf(m, mx);
-    const float corr = __expf(m - mn);
-    const float ea = va ? __expf(sa - mn) : 0.f, eb = vbk ? __expf(sb - mn) : 0.f;
-    float es = ea + eb;
-    es = wave_bfly<8, 64>(es, lane_id(), [](float a, float b) { return a + b; });
-    l = fmaf(l, corr, es);
-    o0 *= corr;
-    o1 *= corr;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float pa =
-          __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ea), 8 * j));
-      const float pb =
-          __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, eb), 8 * j));
-      o0 = fmaf(pa, vf[2 * j], o0);
-      o1 = fmaf(pa, vf[2 * j + 1], o1);
-      o0 = fmaf(pb, vf[2 * (j + 8)], o0);
-      o1 = fmaf(pb, vf[2 * (j + 8) + 1], o1);
-    }
-    m = mn;
-  }
+  for (int t0 = t0w; t0 < hi; t0 += NW * 16)
+    attn_decode_step(qw, ka, kb2, vv, t0, hi, g, qa.scale, m, l, o0, o1, [&]() {
+      if (t0 + NW * 16 < hi) load_step(t0 + NW * 16);  // wave-uniform prefetch of the next step
+    });
   if (lane == 0) {
     wm[wave] = m;
     wl[wave] = l;
