@@ -192,6 +192,19 @@ int tao_int4wo_decode_bf16(const uint16_t* x, const uint32_t* packed,
                            uint16_t* k_cache, uint16_t* v_cache, int64_t n_head,
                            int64_t n_kv_head, int64_t head_dim, int64_t max_seq, void* stream);
 
+/* MoE decode: the A activated experts' int4 linears of one token in one launch. packed
+ * [E][N][K/8] and scales_and_zeros [E][N][K/g][2] are a 3-D Int4WeightOnlyConfig weight (the
+ * reference packs 3-D weights per expert, tensor_core_tiled_layout.py:283-294); expert_idx [A]
+ * int64 on the device; x [x_rows][K] bf16 with x_rows 1 (every expert reads the same token) or A
+ * (row a for expert a); y [A][N] bf16. Row a is bit-identical to tao_int4wo_linear_bf16 of expert
+ * expert_idx[a] alone. Replaces the per-expert F.linear(x, w[expert_indices][i]) loop of
+ * ConditionalFeedForwardAOQuantizable's one-token branch (_models/mixtral-moe/model.py:360-384).
+ * An index outside [0, E) is clamped and reported by tao_decode_status (bits & 4). */
+int tao_int4wo_grouped_gemv_bf16(const uint16_t* x, int64_t x_rows, const uint32_t* packed,
+                                 const uint16_t* scales_and_zeros, const int64_t* expert_idx,
+                                 int64_t A, int64_t E, int64_t N, int64_t K, int64_t group_size,
+                                 uint16_t* y, void* stream);
+
 /* Decode step, batch 1: RMSNorm -> int4 wqkv -> RoPE + KV-cache write (= tao_int4wo_decode_bf16
  * with norm_weight and epilogue 2, q into `q` [n_head * 128]) AND the decode attention of the
  * rotated q over cache keys 0..pos[0] (= tao_attn_decode_bf16) in ONE launch: out [n_head * 128]

@@ -758,6 +758,29 @@ __global__ __launch_bounds__(256, 4) void int4wo_qkv_attn_kernel(
   qkv_attn_tail<4, NS>(fu, qa, y);
 }
 
+// ---- grouped (MoE) decode GEMV: A experts' linears of one token in one launch ------------------
+// (tao_int4wo_grouped_gemv_bf16). blockIdx.y = activation a: expert e = idx[a] of the [E][N][K]
+// stack (packed [E][N][K/8], scales [E][N][K/g]); x row a (x_rows = A) or the shared x
+// (x_rows = 1); y [A][N]. Each activation runs the plain M = 1 GEMV body of its expert, so its
+// output is bit-identical to that expert's own linear. The expert index is read on the device,
+// so the launch is graph-capturable with the router's top-k on the GPU.
+template <int RPW, int WPE, bool PAIR>
+__global__ __launch_bounds__(512, WPE) void int4wo_grouped_gemv_kernel(
+    const uint16_t* __restrict__ x, int x_rows, const uint4* __restrict__ wq,
+    const uint32_t* __restrict__ sz, const int64_t* __restrict__ idx, int E,
+    uint16_t* __restrict__ y, int N, int K, int gshift, int Wk, int G, int S) {
+  const int a = (int)blockIdx.y;
+  int64_t e = idx[a];
+  if (e < 0 || e >= E) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) flag_decode_error(kDecodeErrExpert);
+    e = e < 0 ? 0 : E - 1;
+  }
+  const size_t nchunk = (size_t)K >> 5, ngroups = (size_t)K >> (5 + gshift);
+  gemv_body<1, RPW, PAIR>(x + (x_rows > 1 ? (size_t)a * K : 0), wq + (size_t)e * N * nchunk,
+                          sz + (size_t)e * N * ngroups, nullptr, y + (size_t)a * N, 1, N, K,
+                          gshift, Wk, G, S, GemvFuse{}, (int)blockIdx.x * G * RPW);
+}
+
 int gshift_of(int64_t g) {
   switch (g) {
     case 32: return 0;
@@ -1242,4 +1265,61 @@ extern "C" int tao_int4wo_qkv_attn_bf16(const uint16_t* x, const uint32_t* packe
   }
 #undef TAO_QA
   return tao::check_launch("int4wo_qkv_attn_kernel");
+}
+
+namespace tao {
+namespace {
+
+template <int RPW, int WPE>
+void launch_grouped(const uint16_t* x, int x_rows, const uint32_t* packed, const uint16_t* sz,
+                    const int64_t* idx, int A, int E, uint16_t* y, int N, int K, int gs,
+                    GemvShape sh, hipStream_t st) {
+  const int S = (K / 32 + 63) / 64;
+  const int wk = sh.wk < S ? sh.wk : S;
+  const int rows = sh.g * RPW;
+  const dim3 grid((unsigned)((N + rows - 1) / rows), (unsigned)A);
+  const size_t lds = (size_t)sh.g * wk * RPW * sizeof(float);
+  const uint4* w = reinterpret_cast<const uint4*>(packed);
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(sz);
+  if (S > wk)
+    launch((int4wo_grouped_gemv_kernel<RPW, WPE, true>), grid, dim3(64 * wk * sh.g), lds, st, x,
+           x_rows, w, s, idx, E, y, N, K, gs, wk, sh.g, S);
+  else
+    launch((int4wo_grouped_gemv_kernel<RPW, WPE, false>), grid, dim3(64 * wk * sh.g), lds, st,
+           x, x_rows, w, s, idx, E, y, N, K, gs, wk, sh.g, S);
+}
+
+}  // namespace
+}  // namespace tao
+
+extern "C" int tao_int4wo_grouped_gemv_bf16(const uint16_t* x, int64_t x_rows,
+                                            const uint32_t* packed,
+                                            const uint16_t* scales_and_zeros,
+                                            const int64_t* expert_idx, int64_t A, int64_t E,
+                                            int64_t N, int64_t K, int64_t group_size, uint16_t* y,
+                                            void* stream) {
+  int rc = tao::int4_check_linear_args(x, packed, scales_and_zeros, y, 1, N, K, group_size);
+  if (rc != TAO_OK) return rc;
+  TAO_CHECK_ARG(A >= 0 && A <= 65535 && E > 0 && E < (1LL << 20),
+                "int4 grouped: A (%lld) must be in [0, 65535] and E (%lld) positive",
+                (long long)A, (long long)E);
+  TAO_CHECK_ARG(x_rows == 1 || x_rows == A, "int4 grouped: x_rows (%lld) must be 1 or A (%lld)",
+                (long long)x_rows, (long long)A);
+  TAO_CHECK_ARG(expert_idx != nullptr, "int4 grouped: expert_idx is required");
+  TAO_CHECK_ARG(E * N * (K / 8) < (1LL << 40), "int4 grouped: weight stack too large");
+  if (A == 0 || N == 0) return TAO_OK;
+  const int gs = tao::gshift_of(group_size);
+  const int S = (int)((K / 32 + 63) / 64);
+  const tao::M1Shape c = tao::m1_shape((int)N, S);  // the plain M = 1 linear's launch shape
+  hipStream_t st = tao::as_stream(stream);
+  const int iN = (int)N, iK = (int)K, iA = (int)A, iE = (int)E, xr = (int)x_rows;
+#define TAO_GR(R, W) \
+  tao::launch_grouped<R, W>(x, xr, packed, scales_and_zeros, expert_idx, iA, iE, y, iN, iK, gs, c.sh, st)
+  if (c.rpw == 1) TAO_GR(1, 8);
+  else if (c.rpw == 2) TAO_GR(2, 8);
+  else if (c.rpw == 8) TAO_GR(8, 4);
+  else if (c.occ == 4) TAO_GR(4, 4);
+  else TAO_GR(4, 8);
+#undef TAO_GR
+  return tao::check_launch("int4wo_grouped_gemv_kernel");
 }

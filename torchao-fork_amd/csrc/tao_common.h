@@ -301,6 +301,8 @@ constexpr unsigned kDecodeErrKvPos = 1u;
 // tao_decode_status bits & 2: a single-fetch GEMM's split-K reducer timed out waiting for its
 // publishers (that tile was not written; never expected)
 constexpr unsigned kDecodeErrSplitK = 2u;
+// tao_decode_status bits & 4: a grouped (MoE) GEMV read an expert index outside [0, E) (clamped)
+constexpr unsigned kDecodeErrExpert = 4u;
 #define TAO_DECODE_ERROR_WORD(reader)                                                        \
   static __device__ unsigned g_decode_err = 0;                                                \
   __device__ __forceinline__ void flag_decode_error(unsigned bits) {                          \

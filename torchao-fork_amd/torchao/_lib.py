@@ -103,6 +103,7 @@ _SIGNATURES = {
     "tao_argmax_advance_bf16": [_p, _i64, _p, _p, _p, _i64, _p],
     "tao_int4_quantize_bf16": [_p, _p, _p, _i64, _i64, _i64, ctypes.c_float, _p],
     "tao_int8_quantize_rows_bf16": [_p, _p, _p, _i64, _i64, ctypes.c_float, _p],
+    "tao_int4wo_grouped_gemv_bf16": [_p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p, _p],
     "tao_int4wo_qkv_attn_supported": [_i64, _i64, _i64, _i64, _i64],
     "tao_int4wo_qkv_attn_bf16": [_p, _p, _p, _i64, _i64, _i64, _p, ctypes.c_float, _p, _p, _p,
                                  _p, _p, _p, _i64, _i64, _i64, _i64, ctypes.c_float, _i64, _p],

@@ -192,6 +192,45 @@ def int4_qkv_attn(x: torch.Tensor, packed: torch.Tensor, scale_and_zero: torch.T
     return out
 
 
+def int4_grouped_decode(x: torch.Tensor, packed: torch.Tensor, scale_and_zero: torch.Tensor,
+                        group_size: int, expert_idx: torch.Tensor) -> torch.Tensor:
+    """The A = expert_idx.numel() experts' int4 linears of one token in one launch
+    (tao_int4wo_grouped_gemv_bf16): packed [E, N, K/8] int32, scale_and_zero [E, N, K/g, 2] bf16
+    (a 3-D Int4WeightOnlyConfig weight's tensor_impl), x [K] / [1, K] (shared) or [A, K] (row a
+    for expert a) bf16 -> y [A, N] bf16, row a bit-identical to expert expert_idx[a]'s linear."""
+    _check(x, torch.bfloat16, "int4_grouped x")
+    _check(expert_idx, torch.int64, "int4_grouped expert_idx")
+    if packed.dim() != 3:
+        raise RuntimeError(f"int4_grouped: packed must be [E, N, K/8], got {tuple(packed.shape)}")
+    E, N, K8 = packed.shape
+    K, A = K8 * 8, expert_idx.numel()
+    rows = x.numel() // K
+    if x.shape[-1] != K or rows not in (1, A):
+        raise RuntimeError(f"int4_grouped: x {tuple(x.shape)} must be [K] or [A, K] with K = {K}")
+    y = torch.empty(A, N, dtype=x.dtype, device=x.device)
+    _lib.call("tao_int4wo_grouped_gemv_bf16", x.data_ptr(), rows, packed.data_ptr(),
+              scale_and_zero.data_ptr(), expert_idx.data_ptr(), A, E, N, K, int(group_size),
+              y.data_ptr(), _stream(x))
+    return y
+
+
+def int4_moe_ffn_decode(x: torch.Tensor, w1, w2, w3, expert_indices: torch.Tensor,
+                        expert_weights: torch.Tensor) -> torch.Tensor:
+    """The one-token branch of the reference's ConditionalFeedForwardAOQuantizable
+    (_models/mixtral-moe/model.py:360-384) on 3-D int4 weights (AffineQuantizedTensor [E, I, D] /
+    [E, D, I] / [E, I, D]): three grouped launches instead of 3 A per-expert linears, the same
+    bf16 ops in between (silu(w1 x) * w3 x, then w2, then the expert-weighted sum)."""
+    def parts(w):
+        impl = w.tensor_impl
+        return impl.packed_weight, impl.scale_and_zero, w.block_size[-1]
+
+    idx = expert_indices.reshape(-1)
+    y1 = torch.nn.functional.silu(int4_grouped_decode(x, *parts(w1), idx))
+    y3 = int4_grouped_decode(x, *parts(w3), idx)
+    y2 = int4_grouped_decode((y1 * y3).contiguous(), *parts(w2), idx)  # [A, D]
+    return (y2 * expert_weights.view(-1, 1)).sum(dim=0).unsqueeze(-1)
+
+
 def attn_decode_split(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                       pos: torch.Tensor, scale: float, splits: int) -> torch.Tensor:
     """q [B, H, 1, D] against keys 0..pos[0], the keys split `splits` ways per head ->
@@ -460,6 +499,9 @@ def check_decode_status() -> None:
         raise RuntimeError("decode step at a position past the KV cache (max_seq_length): "
                            "no cache row was written; call setup_caches() with a larger "
                            "max_seq_length")
+    if bits.value & 4:
+        raise RuntimeError("a grouped (MoE) linear read an expert index outside [0, num_experts) "
+                           "(clamped); those outputs are unspecified")
     if bits.value & 2:
         raise RuntimeError("a cross-workgroup hand-off (split-K reducer or fused decode "
                            "attention) timed out waiting for its producers; those outputs are "
