@@ -88,7 +88,7 @@ def main():
         pos.fill_(L - 1)
         ref = None
         for name, fn in (("two", two()), ("fused4", fused(4)), ("fused2", fused(2)),
-                         ("gemv_only", two(False))):
+                         ("fused1", fused(1)), ("gemv_only", two(False))):
             us = graph_us(fn, a.reps, NL, dev)
             rec = {"variant": name, "keys": L, "T": T, "us_per_layer_graph": round(us, 3)}
             if name != "gemv_only":

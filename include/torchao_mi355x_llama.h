@@ -210,7 +210,7 @@ int tao_int4wo_grouped_gemv_bf16(const uint16_t* x, int64_t x_rows, const uint32
  * rotated q over cache keys 0..pos[0] (= tao_attn_decode_bf16) in ONE launch: out [n_head * 128]
  * bf16. Replaces, at decode, the Attention.forward sequence wqkv -> apply_rotary_emb ->
  * KVCache.update -> F.scaled_dot_product_attention (model.py:547-562). The attention workgroups
- * (n_head x `splits` key ranges, splits 2 or 4) follow the GEMV's in the grid and start on
+ * (n_head x `splits` key ranges, splits 1, 2 or 4) follow the GEMV's in the grid and start on
  * per-head tickets; a ticket wait that times out sets tao_decode_status bit 2. head_dim 128,
  * caches [1][n_kv_head][max_seq][128]; shapes tao_int4wo_qkv_attn_supported() accepts (returns
  * 1 / 0, not a status). */

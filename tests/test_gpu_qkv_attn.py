@@ -49,7 +49,7 @@ def _attn_fp32(q, kc, vc, p, scale):
     return torch.einsum("hl,hld->hd", torch.softmax(s, -1), v).reshape(1, 1, -1)
 
 
-@pytest.mark.parametrize("splits", [2, 4])
+@pytest.mark.parametrize("splits", [1, 2, 4])
 @pytest.mark.parametrize("H,Hkv,K,T,g", [(32, 8, 4096, 328, 32), (8, 2, 1024, 200, 64),
                                          (4, 4, 512, 64, 32), (16, 2, 8192, 1100, 128)])
 def test_qkv_attn_matches_two_launches(H, Hkv, K, T, g, splits):

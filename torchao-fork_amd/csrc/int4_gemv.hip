@@ -703,6 +703,12 @@ __device__ __forceinline__ void qkv_attn_tail(const GemvFuse& fu, const QkvAttn&
       a0 = fmaf(wo[w * D + 2 * lane], f, a0);
       a1 = fmaf(wo[w * D + 2 * lane + 1], f, a1);
     }
+    if constexpr (NS == 1) {  // the whole head in this workgroup: no partial, no merge ticket
+      const float inv = 1.f / ls;
+      reinterpret_cast<uint32_t*>(qa.out)[(size_t)h * (D / 2) + lane] =
+          (uint32_t)f32_to_bf16(a0 * inv) | ((uint32_t)f32_to_bf16(a1 * inv) << 16);
+      return;
+    }
     uint32_t* r32 = reinterpret_cast<uint32_t*>(rec);
     st_coh(r32 + 2 * lane, __float_as_uint(a0));
     st_coh(r32 + 2 * lane + 1, __float_as_uint(a1));
@@ -712,6 +718,7 @@ __device__ __forceinline__ void qkv_attn_tail(const GemvFuse& fu, const QkvAttn&
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  if constexpr (NS == 1) return;
   unsigned* mc = qa.cnt + (size_t)(fu.H + 3 * fu.Hkv + h) * qa.cs;
   if (!last_arriver(mc, (unsigned)NS, flag, qa.fenced)) return;
   if (wave != 0) return;
@@ -1206,8 +1213,8 @@ extern "C" int tao_int4wo_qkv_attn_bf16(const uint16_t* x, const uint32_t* packe
                 "%lld; tao_int4wo_qkv_attn_supported)",
                 (long long)N, (long long)K, (long long)n_head, (long long)n_kv_head,
                 (long long)head_dim);
-  TAO_CHECK_ARG(splits == 2 || splits == 4, "int4 qkv_attn: splits must be 2 or 4 (got %lld)",
-                (long long)splits);
+  TAO_CHECK_ARG(splits == 1 || splits == 2 || splits == 4,
+                "int4 qkv_attn: splits must be 1, 2 or 4 (got %lld)", (long long)splits);
   TAO_CHECK_ARG(norm_weight != nullptr && freqs != nullptr && pos != nullptr &&
                     k_cache != nullptr && v_cache != nullptr && out != nullptr,
                 "int4 qkv_attn: norm_weight, freqs, pos, caches and out are required");
@@ -1256,12 +1263,12 @@ extern "C" int tao_int4wo_qkv_attn_bf16(const uint16_t* x, const uint32_t* packe
   tao::launch_qkv_attn<NPT, PAIR, NS>(x, packed, scales_and_zeros, q, iN, iK, gs, S, fu, qa, lds, st)
   if (npt == 2) {
     if (S > 1) {
-      if (splits == 2) TAO_QA(2, true, 2); else TAO_QA(2, true, 4);
+      if (splits == 1) TAO_QA(2, true, 1); else if (splits == 2) TAO_QA(2, true, 2); else TAO_QA(2, true, 4);
     } else {
-      if (splits == 2) TAO_QA(2, false, 2); else TAO_QA(2, false, 4);
+      if (splits == 1) TAO_QA(2, false, 1); else if (splits == 2) TAO_QA(2, false, 2); else TAO_QA(2, false, 4);
     }
   } else {
-    if (splits == 2) TAO_QA(4, true, 2); else TAO_QA(4, true, 4);
+    if (splits == 1) TAO_QA(4, true, 1); else if (splits == 2) TAO_QA(4, true, 2); else TAO_QA(4, true, 4);
   }
 #undef TAO_QA
   return tao::check_launch("int4wo_qkv_attn_kernel");
