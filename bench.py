@@ -74,7 +74,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E, spec (MI355X_MICROARCH.md chip table)
-PMC_FILE = os.path.join(ROOT, "profiles", "r5m_pmc_fetch_bench.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r5n_pmc_fetch_bench.json")
 
 LLAMA3_8B = dict(dim=4096, n_layer=32, n_head=32, n_kv_head=8, head_dim=128,
                  intermediate=14336, vocab=128256)
