@@ -834,7 +834,8 @@ int tao_attn_prefill_bf16(const uint16_t* q, const uint16_t* k_cache, const uint
   TAO_CHECK_ALIGN(out, 16, "out");
   TAO_CHECK_ARG(B * H <= 65535, "attn_prefill: B * H (%lld) exceeds the grid's y extent",
                 (long long)(B * H));
-  // MFMA flash-style kernel (attn_mfma.hip): a wave per 16 queries, K / V read once per block of
+  // MFMA flash-style kernel (attn_mfma.hip): 1-4 waves per 16 queries (key blocks split over
+  // them, merged in LDS), K / V read once per block of
   // 16 queries instead of once per query (the single-pass decode kernel generalised, which this
   // replaces, re-read the prefix per query: 24 us per layer at S = 128)
   return tao::attn_prefill_mfma(q, k_cache, v_cache, pos, out, B, H, Hkv, S, T, scale,
