@@ -28,9 +28,6 @@
 // Experiment switch (experiments/gemm_debug.sh builds variants; 0 in the product):
 // 1 = no x global loads, 2 = no weight global loads, 3 = no x LDS traffic, 4 = no step barrier,
 // 5 = no global loads at all.
-#ifndef TAO_GEMM_DEBUG
-#define TAO_GEMM_DEBUG 0
-#endif
 // Experiment switch: ring depth override (experiments/gemm_depth.sh; 0 = the policy below).
 #ifndef TAO_GEMM_DEPTH
 #define TAO_GEMM_DEPTH 0
@@ -93,11 +90,7 @@ __device__ __forceinline__ bf16x8_t as_bf16x8(uint32_t a, uint32_t b, uint32_t c
 // the previous row & 7 gave rows n and n + 8 the same bank group on every read pass
 // (SQ_LDS_BANK_CONFLICT 1.24-1.33 extra cycles per LDS cycle, profiles/r2_pmc_prefill.jsonl).
 __device__ __forceinline__ int stage_slot(int row, int slot) {
-#if TAO_STAGE_OLD
-  return row * 8 + (slot ^ (row & 7));  // timing A/B only
-#else
   return row * 8 + (slot ^ ((row >> 1) & 7));
-#endif
 }
 
 // Optional XCD-grouped workgroup order (tao_tune_gemm_order 1). Workgroups are dealt
@@ -440,16 +433,6 @@ __device__ __forceinline__ void static_for(F&& f) {
 //    sums them in slice order and runs the epilogue. Both sums have a fixed order, so results
 //    do not depend on arrival order. Protocol and its hardware assumption: last_arriver()
 //    (tao_common.h); `fenced` adds the agent release/acquire fences (tao_tune_splitk_fenced).
-// Experiment switch (timing only, experiments/gemm_stamps.py): per-workgroup wall-clock stamps
-// (s_memrealtime, 100 MHz) of gemm_mfma_kernel's phases: setup done, prologue done (first
-// barrier), k loop done, k-group reduction done, end; slot 5 = 1 for a split-K last arriver,
-// slot 6 = the kernel's first instruction. Never in the product library.
-#ifndef TAO_GEMM_STAMPS
-#define TAO_GEMM_STAMPS 0
-#endif
-#if TAO_GEMM_STAMPS
-__device__ unsigned long long g_gemm_stamps[16384 * 8];
-#endif
 // Experiment switch (timing A/B only): minimum waves per SIMD the register allocation must
 // allow (amdgpu_waves_per_eu); 0 = the compiler's choice (the product).
 #ifndef TAO_GEMM_WPE
@@ -465,9 +448,6 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int sps, typename P::Acc* __restrict__ slab,
     unsigned* __restrict__ cnt, int fenced, int order, int cs) {
-#if TAO_GEMM_STAMPS
-  const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();  // before any setup
-#endif
   typedef typename P::Acc Acc;
   constexpr int MT = BM / 16;
   constexpr int XSB = P::kABytes * P::kKStep;  // x bytes per row per step (256 or 512)
@@ -536,27 +516,14 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
       __attribute__((always_inline)) {
     const int st0 = abs_step(j);
     const int st = st0 < s1 ? st0 : s1 - 1;
-    if (TAO_GEMM_DEBUG != 1 && TAO_GEMM_DEBUG != 5) {
 #pragma unroll
-      for (int i = 0; i < XLOADS; ++i) xdst[i] = bload16(xrs, xv[i], st * XSB);
-    } else {
+    for (int i = 0; i < XLOADS; ++i) xdst[i] = bload16(xrs, xv[i], st * XSB);
 #pragma unroll
-      for (int i = 0; i < XLOADS; ++i) xdst[i] = make_uint4(st, i, 0x3c003c00u, 0);
-    }
-#pragma unroll
-    for (int c = 0; c < NW; ++c) {
-      if (TAO_GEMM_DEBUG != 2 && TAO_GEMM_DEBUG != 5) {
-        wdst[c] = pol.load(wl[c], st);
-      } else {
-        wdst[c] = typename P::Chunk{};
-        reinterpret_cast<uint32_t*>(&wdst[c])[0] = st * 0x01010101u;
-      }
-    }
+    for (int c = 0; c < NW; ++c) wdst[c] = pol.load(wl[c], st);
   };
   auto store_x = [&](const uint4 (&src)[XLOADS], int j) __attribute__((always_inline)) {
     const int st = abs_step(j);
     uint4* dst = xs + (j & 1) * TILE;
-    if (TAO_GEMM_DEBUG == 3) return;
     if (!ragged && st < s1) {
 #pragma unroll
       for (int i = 0; i < XLOADS; ++i) dst[xlds[i]] = src[i];
@@ -588,37 +555,16 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
         for (int t = 0; t < MT; ++t) {
           const int row = t * 16 + (lane & 15);
           // one A fragment read from LDS feeds the wave's NW column blocks
-          const uint4 a = TAO_GEMM_DEBUG == 3 ? xr[u][0] : xb[x_slot<SLOTS, P>(row, slot)];
+          const uint4 a = xb[x_slot<SLOTS, P>(row, slot)];
 #pragma unroll
           for (int c = 0; c < NW; ++c) acc[t * NW + c] = P::mfma(a, bfrag[c], acc[t * NW + c]);
         }
       }
     }
     if (j + 1 < J) store_x(xr[(u + 1) % D], j + 1);
-    if (TAO_GEMM_DEBUG != 4) __syncthreads();
+    __syncthreads();
   };
 
-#if TAO_GEMM_STAMPS
-  unsigned long long stamp[6] = {0, 0, 0, 0, 0, t_entry};
-  auto mark = [&](int i) __attribute__((always_inline)) {
-    if (tid == 0) stamp[i] = __builtin_amdgcn_s_memrealtime();
-  };
-  auto flush = [&](int last) __attribute__((always_inline)) {
-    if (tid < 64) {  // wave 0: lane i stores slot i (vector stores)
-      unsigned long long v = (unsigned long long)last;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const unsigned lo = __shfl((unsigned)stamp[i], 0), hi = __shfl((unsigned)(stamp[i] >> 32), 0);
-        if (lane == (i < 5 ? i : 6)) v = ((unsigned long long)hi << 32) | lo;
-      }
-      const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-      if (lane < 7 && b < 16384) g_gemm_stamps[b * 8 + lane] = v;
-    }
-  };
-#else
-  auto mark = [](int) {};
-  auto flush = [](int) {};
-#endif
   // Epilogue operands loaded now, ahead of the weights: loaded in the epilogue, their round
   // trip sat in every workgroup's tail (~1 µs of the int8-dyn M = 128 4096² kernel;
   // experiments/gemm_stamps.py). Per lane: the row factor of its 4 rows per M tile (rows
@@ -647,13 +593,11 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
     colf[c] = P::kColF ? bf16_to_f32(pol.col_factor()[nn]) : 1.f;
     biasf[c] = (kPre && bias != nullptr) ? bf16_to_f32(bias[nn]) : 0.f;
   }
-  mark(0);
   static_for<0, D - 1>([&](auto i) __attribute__((always_inline)) {
     load_step(decltype(i)::value, xr[decltype(i)::value], wr[decltype(i)::value]);
   });
   store_x(xr[0], 0);
   __syncthreads();
-  mark(1);
 
   int j = 0;
   for (; j + D <= J; j += D)
@@ -663,7 +607,6 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
   static_for<0, D - 1>([&](auto uc) __attribute__((always_inline)) {
     if (j + decltype(uc)::value < J) body(uc, j + decltype(uc)::value);
   });
-  mark(2);
 
   // k-groups 1..KG-1 hand their accumulators to k-group 0 through LDS (summed in order)
   if constexpr (KG > 1) {
@@ -681,7 +624,6 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
     }
     __syncthreads();  // LDS free again (the split-K flag below reuses it)
   }
-  mark(3);
 
   const int S = gridDim.z;
   if (S > 1) {
@@ -709,8 +651,6 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
     const bool last =
         last_arriver(&cnt[tile * cs], (unsigned)S, reinterpret_cast<unsigned*>(lds), fenced);
     if (!last || kg != 0) {
-      mark(4);
-      flush(0);
       return;
     }
 #pragma unroll
@@ -763,8 +703,6 @@ __global__ __launch_bounds__(256 * KG) TAO_GEMM_WPE_ATTR void gemm_mfma_kernel(
       }
     }
   }
-  mark(4);
-  flush(S > 1 ? 1 : 0);
 }
 
 // Launch shape: M tile, k-groups per workgroup and K slices. Per-workgroup time is set by its
@@ -1627,16 +1565,6 @@ extern "C" int tao_tune_gemm_table(int off) {
 
 // int4 MFMA GEMM kernel: 0 = built-in (gemm_mfma_kernel), 1 = gemm32_int4_kernel (32x32x16).
 // Calling thread only; for A/B measurement.
-#if TAO_GEMM_STAMPS
-// timing builds only: copy the per-workgroup stamps (8 u64 per workgroup) and clear them
-extern "C" int tao_debug_gemm_stamps(unsigned long long* out, int n) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tao::g_gemm_stamps), (size_t)n * 8 * 8) != hipSuccess)
-    return TAO_ERR_HIP;
-  static unsigned long long zero[16384 * 8];
-  return hipMemcpyToSymbol(HIP_SYMBOL(tao::g_gemm_stamps), zero, sizeof(zero)) == hipSuccess
-             ? TAO_OK : TAO_ERR_HIP;
-}
-#endif
 
 extern "C" int tao_tune_int4_mfma32(int on) {
   TAO_CHECK_ARG(on == 0 || on == 1, "tune: int4 mfma32 must be 0 or 1");

@@ -33,13 +33,6 @@
 #define TAO_SF_IL 0
 #endif
 
-// Experiment switch (timing only, experiments/sf_stamps.py): per-workgroup s_memrealtime stamps
-// (100 MHz): 0 entry, 1 prologue DMAs issued, 2 first stage landed, 3 k loop done, 4 publish or
-// poll done, 5 end; 6 = slice, 7 = 1 for the reducer. Never in the product library.
-#ifndef TAO_SF_STAMPS
-#define TAO_SF_STAMPS 0
-#endif
-
 namespace tao {
 
 TAO_DECODE_ERROR_WORD(sf_decode_status)
@@ -55,9 +48,6 @@ typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 constexpr int kBM = 128;   // rows per tile
 constexpr int kWaves = 8;  // 512 threads
 
-#if TAO_SF_STAMPS
-__device__ unsigned long long g_sf_stamps[8192 * 8];
-#endif
 // reducer poll timeouts (never expected: publishers never wait, and they precede the reducers in
 // every XCD's dispatch order); read and cleared by tao_gemm_sf_status()
 __device__ unsigned g_sf_err = 0;
@@ -238,16 +228,9 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
     uint16_t* __restrict__ y, int M, int N, int K, int a_steps, typename P::Acc* __restrict__ slab,
     unsigned* __restrict__ cnt, int fenced, int S, int ntn, int seam, int cs, SfEpi ep, int xmap) {
   const int epi = ep.kind;
-#if TAO_SF_STAMPS
-  const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
-  unsigned long long stamp[6] = {t_entry, 0, 0, 0, 0, 0};
-#define SF_MARK(i) \
-  if (threadIdx.x == 0) stamp[i] = __builtin_amdgcn_s_memrealtime()
-#else
 #define SF_MARK(i) \
   do {             \
   } while (0)
-#endif
   typedef typename P::Acc Acc;
   constexpr int WN = kWaves / WM;
   constexpr int RM = kBM / WM, CN = BN / WN;  // wave tile
@@ -496,18 +479,12 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
   for (; j < jiss; ++j) {
     wait_ahead<R>(NS - 2);  // this wave's DMAs of step j landed
     barrier_lgkm();         // ... and every wave's; step j - 1's fragment reads are done
-#if TAO_SF_STAMPS
-    if (j == 0) SF_MARK(2);
-#endif
     compute(j % NS, std::true_type{}, s0 + j + NS - 1, (j + NS - 1) % NS);
   }
   for (; j < J; ++j) {
     const int ahead = J - 1 - j < NS - 2 ? J - 1 - j : NS - 2;
     wait_ahead<R>(ahead);
     barrier_lgkm();
-#if TAO_SF_STAMPS
-    if (j == 0) SF_MARK(2);
-#endif
     compute(j % NS, std::false_type{}, 0, 0);
   }
   }  // LDW == 0
@@ -571,21 +548,6 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
       }
     }
     if (!seam && !reducer) {
-#if TAO_SF_STAMPS
-      SF_MARK(4);
-      SF_MARK(5);
-      if (tid < 64) {
-        unsigned long long v = 0;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          const unsigned l32 = __shfl((unsigned)stamp[i], 0), h32 = __shfl((unsigned)(stamp[i] >> 32), 0);
-          if (lane == i) v = ((unsigned long long)h32 << 32) | l32;
-        }
-        if (lane == 6) v = (unsigned long long)z;
-        if (lane == 7) v = 0;
-        if (lane < 8 && bid < 8192) g_sf_stamps[bid * 8 + lane] = v;
-      }
-#endif
       return;
     }
     // fixed reducer: wait for the S-1 publishers, then take their S-1 arrivals back off the
@@ -763,21 +725,6 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
         if (n_blk + 8 * cc + k < N) y[(size_t)m * N + n_blk + 8 * cc + k] = e[k];
     }
   }
-#if TAO_SF_STAMPS
-  SF_MARK(5);
-  if (tid < 64) {
-    const unsigned b = bid;
-    unsigned long long v = 0;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const unsigned l32 = __shfl((unsigned)stamp[i], 0), h32 = __shfl((unsigned)(stamp[i] >> 32), 0);
-      if (lane == i) v = ((unsigned long long)h32 << 32) | l32;
-    }
-    if (lane == 6) v = (unsigned long long)z;
-    if (lane == 7) v = seam ? 2 : 1;
-    if (lane < 8 && b < 8192) g_sf_stamps[b * 8 + lane] = v;
-  }
-#endif
 #undef SF_MARK
 }
 
@@ -1233,12 +1180,3 @@ extern "C" int tao_gemm_sf_status(unsigned* bits) {
   return tao::sf32_status(bits);
 }
 
-#if TAO_SF_STAMPS
-extern "C" int tao_debug_sf_stamps(unsigned long long* out, int n) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tao::g_sf_stamps), (size_t)n * 8 * 8) != hipSuccess)
-    return TAO_ERR_HIP;
-  static unsigned long long zero[8192 * 8];
-  return hipMemcpyToSymbol(HIP_SYMBOL(tao::g_sf_stamps), zero, sizeof(zero)) == hipSuccess
-             ? TAO_OK : TAO_ERR_HIP;
-}
-#endif

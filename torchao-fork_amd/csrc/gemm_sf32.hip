@@ -32,9 +32,6 @@
 // stages), 4 no A-fragment LDS reads (one read per step reused), 5 x read as if step-major
 // ([K / 128][M][128]: each step's x one contiguous block), 6 / 7 no (scale, zero) / W DMA after
 // the prologue (per-instruction vs per-byte cost of the DMA pieces).
-#ifndef TAO_SF32_DEBUG
-#define TAO_SF32_DEBUG 0
-#endif
 // 1: with 3+ stages, each step's DMA pieces are issued between its MFMA k sub-steps (0: all after
 // the step's barrier). 2-5% faster at 3 stages, slower at 2 (the stage is needed one step later):
 // profiles/r4_sf32_il.jsonl
@@ -51,9 +48,6 @@
 #ifndef TAO_SF32_ABUF
 #define TAO_SF32_ABUF 2
 #endif
-#ifndef TAO_SF32_STEPSTAMPS
-#define TAO_SF32_STEPSTAMPS 0
-#endif
 
 namespace tao {
 namespace {
@@ -67,10 +61,6 @@ constexpr int kBM = 128;
 constexpr int kXRow = 256, kWRow = 64, kZRow = 16;  // bytes per row per 128-k step
 
 __device__ unsigned g_sf32_err = 0;
-#if TAO_SF32_STEPSTAMPS
-// [wg 8][wave 8][step 64][4] + [wg 8][wave 8][4] (entry / exit memtime, memrealtime)
-__device__ unsigned long long g_sf32_ts[8 * 8 * 64 * 4 + 8 * 8 * 4];
-#endif
 
 template <int I, int N, class F>
 __device__ __forceinline__ void sfor(F&& f) {
@@ -125,7 +115,7 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
 // (profiles/r4_sf32_dmacost.jsonl), and Z16 takes a quarter of them for the (scale, zero) words.
 // LDW > 0 (KH = 1): LDW dedicated loader waves issue every LDS-DMA piece (they wait for their own
 // pieces, join the step barrier and refill the freed stage) and the WV compute waves only read
-// LDS, dequantise and issue MFMAs. The per-step stamps (TAO_SF32_STEPSTAMPS) put the one-wave
+// LDS, dequantise and issue MFMAs. Per-step stamps (a timing build, round 4) put the one-wave
 // kernel at ~2350 of ~2760 cycles per step in its compute phase (32 MFMAs = 1024 cycles), of
 // which the DMA pieces issued between the MFMA sub-steps are ~640 (the no-DMA timing build):
 // a loader wave on each SIMD takes that issue off the MFMA stream (VMEM and VALU / MFMA issue
@@ -148,9 +138,6 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
   static_assert(PX % DW == 0 && (!Z16 || ZB % 1024 == 0), "DMA pieces per wave");
   // piece i = r DW + dma wave: waves below RFULL issue R pieces per stage, the others R - 1
   constexpr int R = (T + DW - 1) / DW, RFULL = T - (R - 1) * DW;
-  // debug 6 / 7 skip each wave's 2 (scale, zero) / 2 W pieces after the prologue
-  constexpr bool DSK = (TAO_SF32_DEBUG == 6 || TAO_SF32_DEBUG == 7) && PW == 2 * NW && PZ == 2 * NW;
-  constexpr int RW = DSK ? R - 2 : R;
   static_assert(NS * STAGE <= 160 * 1024 && kBM * BN * 2 <= NS * STAGE, "LDS");
   __shared__ uint4 lds[NS * STAGE / 16];
 
@@ -179,8 +166,7 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
       const int i = r * DW + dwv;
       const int row = 4 * i + (lane >> 4), p = lane & 15;
       const int gm = m_blk + row < M ? m_blk + row : M - 1;
-      dv[r] = (TAO_SF32_DEBUG == 5 ? (uint32_t)gm * kXRow : (uint32_t)gm * row_bytes) +
-              16u * (uint32_t)xpos(row, p);
+      dv[r] = (uint32_t)gm * row_bytes + 16u * (uint32_t)xpos(row, p);
       dd[r] = i * 1024;
       dk[r] = 0;
     } else {
@@ -213,11 +199,8 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
     constexpr int r = decltype(rc)::value;
     uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * STAGE;
     if constexpr (r < PX / DW) {
-      dma_lds_ring<16>(xrs, dv[r], (uint32_t)st * (TAO_SF32_DEBUG == 5 ? (uint32_t)M * kXRow : kXRow),
-                  base + dd[r]);
+      dma_lds_ring<16>(xrs, dv[r], (uint32_t)st * kXRow, base + dd[r]);
     } else {
-      const bool skip = DSK && ((TAO_SF32_DEBUG == 6 && dk[r] == 2) || (TAO_SF32_DEBUG == 7 && dk[r] == 1));
-      if (skip && st >= s0 + NS - 1) return;
       if (dk[r] == 1) dma_lds_ring<16, kNT>(wrs, dv[r], (uint32_t)st * 64u, base + dd[r]);
       else if (dk[r] == 2) {
         if constexpr (Z16) dma_lds_ring<16, kNT>(zrs, dv[r], (uint32_t)st * 16u, base + dd[r]);
@@ -288,7 +271,7 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
             af[0][mt] = __builtin_bit_cast(bf16x8_t, img[m * 16 + xpos(m, 8 * h + ks0 + k)]);
           }
         }
-      } else if (k + 1 < KS && TAO_SF32_DEBUG != 4) {
+      } else if (k + 1 < KS) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
           const int m = 32 * mt + r32;
@@ -296,19 +279,10 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
               __builtin_bit_cast(bf16x8_t, img[m * 16 + xpos(m, 8 * h + ks0 + k + 1)]);
         }
       }
-#if TAO_SF32_DEBUG == 2
-      const bf16x8_t bf = __builtin_bit_cast(bf16x8_t, make_uint4(wd[k], wd[k] ^ 1u, wd[k] ^ 2u, wd[k] ^ 3u));
-#else
       const bf16x8_t bf = deq8s(wd[k], sf[k >> 2], cf[k >> 2]);
-#endif
-#if TAO_SF32_DEBUG == 1
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[mt][k] += (float)af[k & (AB - 1)][mt][0] + (float)bf[mt];
-#else
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
         acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[k & (AB - 1)][mt], bf, acc[mt], 0, 0, 0);
-#endif
       if constexpr (ISS && IL)  // DMA pieces r with r KS / R == k after sub-step k's MFMAs
         sfor<0, R>([&](auto rc) {
           constexpr int r = decltype(rc)::value;
@@ -319,29 +293,16 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
 
   // this wave's DMAs of the step landed (its own piece count)
   auto wait_own = [&](int ahead) __attribute__((always_inline)) {
-    if constexpr (RFULL == DW || DSK) {
-      wait_ahead<RW>(ahead);
+    if constexpr (RFULL == DW) {
+      wait_ahead<R>(ahead);
     } else {
       if (dwv < RFULL) wait_ahead<R>(ahead);
       else wait_ahead<R - 1>(ahead);
     }
   };
-#if TAO_SF32_STEPSTAMPS
-  const int flat_wg = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
-  const bool stamp = flat_wg < 8 && lane == 0;
-  unsigned long long* tsb = g_sf32_ts + ((size_t)flat_wg * 8 + wave) * 64 * 4;
-  unsigned long long* tse = g_sf32_ts + 8 * 8 * 64 * 4 + ((size_t)flat_wg * 8 + wave) * 4;
-  if (stamp) {
-    tse[0] = __builtin_amdgcn_s_memtime();
-    tse[1] = __builtin_amdgcn_s_memrealtime();
-  }
-#define SF32_TS(i) \
-  if (stamp && j < 64) tsb[j * 4 + (i)] = __builtin_amdgcn_s_memtime()
-#else
 #define SF32_TS(i) \
   do {             \
   } while (0)
-#endif
   if constexpr (LDW > 0) {
     if (loader) {
 #pragma unroll
@@ -372,7 +333,7 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < J) issue(s0 + p, p);
-  const int jiss = TAO_SF32_DEBUG == 3 ? 0 : J - (NS - 1);  // steps that issue a stage ahead
+  const int jiss = J - (NS - 1);  // steps that issue a stage ahead
   int j = 0;
   for (; j < jiss; ++j) {
     SF32_TS(0);
@@ -394,12 +355,6 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
     SF32_TS(3);
   }
   }  // LDW == 0
-#if TAO_SF32_STEPSTAMPS
-  if (stamp) {
-    tse[2] = __builtin_amdgcn_s_memtime();
-    tse[3] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
 #undef SF32_TS
   barrier_lgkm();
   if constexpr (KH == 2) {  // k half 1's accumulators into k half 0's, through LDS
@@ -659,15 +614,6 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
   return check_launch("gemm_sf32_int4_kernel");
 }
 
-#if TAO_SF32_STEPSTAMPS
-extern "C" int tao_debug_sf32_steps(unsigned long long* out) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sf32_ts), sizeof(g_sf32_ts)) != hipSuccess)
-    return TAO_ERR_HIP;
-  static unsigned long long zero[8 * 8 * 64 * 4 + 8 * 8 * 4];
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_sf32_ts), zero, sizeof(zero)) == hipSuccess ? TAO_OK
-                                                                                    : TAO_ERR_HIP;
-}
-#endif
 
 int sf32_status(unsigned* bits) {
   unsigned v = 0, zero = 0;

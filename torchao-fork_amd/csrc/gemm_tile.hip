@@ -32,19 +32,8 @@
 // (plain_layout.py:256-266) and int_scaled_matmul + scales (plain_layout.py:294-315).
 #include "tao_common.h"
 
-// Experiment switch (timing only; 0 in the product): 1 = no x loads, 2 = no weight loads,
-// 3 = no MFMAs, 4 = no B-image stores (conversion kept), 5 = no conversion, 6 = no fragment
-// reads (MFMAs on constant operands), 7 = DMA stream only (no reads, conversion or MFMAs).
-#ifndef TAO_TILE_DEBUG
-#define TAO_TILE_DEBUG 0
-#endif
-// Experiment switch (timing only, experiments/tile_stamps.py): per-workgroup s_memrealtime stamps
-// (100 MHz) at: 0 entry, 1 prologue done, 2 k loop done, 3 slab stored + barrier, 4 arrival /
-// poll / claim done, 5 own part reduced (or epilogue), 6 end of the last arriver's extra parts;
-// 7 = flags (bit 0 last arriver, bit 1 claimed own part). Never in the product library.
-#ifndef TAO_TILE_STAMPS
-#define TAO_TILE_STAMPS 0
-#endif
+// The timing-only variant builds (TAO_TILE_DEBUG / TAO_TILE_STAMPS) were removed in round 6;
+// their code is in git history (commit 1bac331), their measurements in profiles/r3_*.
 
 namespace tao {
 namespace {
@@ -177,8 +166,8 @@ struct TInt4 {
     const uint32_t d4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-      const uint4 v = TAO_TILE_DEBUG == 5 ? make_uint4(d4[d], d4[d], d4[d], d4[d]) : dq8(d4[d], s, zc);
-      if (TAO_TILE_DEBUG != 4) img[(kb * 4 + wave) * 64 + 16 * d + (r ^ (2 * kb))] = v;
+      const uint4 v = dq8(d4[d], s, zc);
+      img[(kb * 4 + wave) * 64 + 16 * d + (r ^ (2 * kb))] = v;
     }
   }
   static __device__ __forceinline__ int rslot(int lane, int kb) {
@@ -240,15 +229,9 @@ struct TInt8WO {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int d = 2 * (c & 1) + h;
-        uint4 o;
-        if (TAO_TILE_DEBUG == 5) {
-          o = make_uint4(d4[2 * h], d4[2 * h + 1], d4[2 * h], d4[2 * h + 1]);
-        } else {
-          const uint2 a = cv4(d4[2 * h]), b = cv4(d4[2 * h + 1]);
-          o = make_uint4(a.x, a.y, b.x, b.y);
-        }
-        if (TAO_TILE_DEBUG != 4)
-          img[(kb * 4 + wave) * 64 + 16 * d + (r ^ ((2 * kb + (c & 1)) & 7))] = o;
+        const uint2 a = cv4(d4[2 * h]), b = cv4(d4[2 * h + 1]);
+        const uint4 o = make_uint4(a.x, a.y, b.x, b.y);
+        img[(kb * 4 + wave) * 64 + 16 * d + (r ^ ((2 * kb + (c & 1)) & 7))] = o;
       }
     }
   }
@@ -323,9 +306,6 @@ struct TInt8Dyn {
 };
 
 // ---- the kernel ---------------------------------------------------------------------------------
-#if TAO_TILE_STAMPS
-__device__ unsigned long long g_tile_stamps[16384 * 8];
-#endif
 
 // LDS: an x ring of R stages, a deeper weight ring (the weights come from HBM: their round trip
 // is the long one, and their stages are small) of RW stages, and two B images when the weights are
@@ -352,27 +332,6 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(
     const uint8_t* __restrict__ x, P pol, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int M, int N, int K, int sps, typename P::Acc* __restrict__ slab,
     unsigned long long* __restrict__ sync, int fenced) {
-#if TAO_TILE_STAMPS
-  unsigned long long stamp[8] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0, 0};
-  auto mark = [&](int i) __attribute__((always_inline)) {
-    if (threadIdx.x == 0) stamp[i] = __builtin_amdgcn_s_memrealtime();
-  };
-  auto flush = [&]() __attribute__((always_inline)) {
-    if (threadIdx.x < 64) {
-      unsigned long long v = 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const unsigned lo = __shfl((unsigned)stamp[i], 0), hi = __shfl((unsigned)(stamp[i] >> 32), 0);
-        if ((int)threadIdx.x == i) v = ((unsigned long long)hi << 32) | lo;
-      }
-      const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-      if (threadIdx.x < 8 && b < 16384) g_tile_stamps[b * 8 + threadIdx.x] = v;
-    }
-  };
-#else
-  auto mark = [](int) {};
-  auto flush = []() {};
-#endif
   typedef typename P::Acc Acc;
   typedef TileLds<BM, R, P> L;
   constexpr int NW = 8;
@@ -465,9 +424,9 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(
     if constexpr (P::kImageW) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        if (TAO_TILE_DEBUG != 2) glds<16, kNT>(wrs, wv[i], so, wsg + (2 * wave + i) * 64);
+        glds<16, kNT>(wrs, wv[i], so, wsg + (2 * wave + i) * 64);
     } else {
-      if (wconv && TAO_TILE_DEBUG != 2) pol.issue(wl, st, wm, wsg);
+      if (wconv) pol.issue(wl, st, wm, wsg);
     }
   };
   auto issue_x = [&](int j) __attribute__((always_inline)) {
@@ -477,20 +436,16 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(
     if (P::kImageW || !wconv) {
 #pragma unroll
       for (int i = 0; i < XI; ++i)
-        if (TAO_TILE_DEBUG != 1) glds<16>(xrs, xv[i], so, xs + (x0 + i) * 64);
+        glds<16>(xrs, xv[i], so, xs + (x0 + i) * 64);
     } else {
 #pragma unroll
       for (int i = 0; i < XC; ++i)
-        if (TAO_TILE_DEBUG != 1) glds<16>(xrs, xv[i], so, xs + (x0 + i) * 64);
+        glds<16>(xrs, xv[i], so, xs + (x0 + i) * 64);
     }
   };
   // this wave's DMAs of the next step have landed (the wave's DMA count per step is fixed)
   auto wait_next = [&]() __attribute__((always_inline)) {
-    if constexpr (TAO_TILE_DEBUG == 1 || TAO_TILE_DEBUG == 2) {
-      wait_vm<0>();
-    } else {
-      wait_vm<(R - 2) * NG>();
-    }
+    wait_vm<(R - 2) * NG>();
   };
 
   Acc acc[MT][4];
@@ -506,15 +461,6 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(
     const uint4* wsg = ws0 + (j % RW) * L::kW;
     const uint4* img = img0 + (j & 1) * L::kImg;
     uint4 b[2][4], a[2][MT];
-    if (TAO_TILE_DEBUG == 6 || TAO_TILE_DEBUG == 7) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb) b[u][nb] = make_uint4(j, u, nb, lane);
-#pragma unroll
-        for (int t = 0; t < MT; ++t) a[u][t] = make_uint4(u, t, j, lane);
-      }
-    } else
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int kb = 2 * grp + u, c = 4 * u + (lane >> 4);
@@ -534,10 +480,7 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(
       for (int t = 0; t < MT; ++t)
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb) {
-          if (TAO_TILE_DEBUG == 3 || TAO_TILE_DEBUG == 7)
-            acc[t][nb][0] += (int)(a[u][t].x ^ b[u][nb].y);
-          else
-            acc[t][nb] = P::mfma(a[u][t], b[u][nb], acc[t][nb]);
+          acc[t][nb] = P::mfma(a[u][t], b[u][nb], acc[t][nb]);
         }
   };
 
@@ -546,32 +489,28 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(
   for (int j = 0; j < RW - 1; ++j) issue_w(j);
   for (int j = 0; j < R - 1; ++j) issue_x(j);
   // step 0's x landed: only x of steps 1 .. R - 2 may be younger (the weights were issued first)
-  if constexpr (TAO_TILE_DEBUG == 1 || TAO_TILE_DEBUG == 2) {
-    wait_vm<0>();
-  } else if (P::kImageW || !wconv) {
+  if (P::kImageW || !wconv) {
     wait_vm<(R - 2) * XI>();
   } else {
     wait_vm<(R - 2) * XC>();
   }
   if constexpr (!P::kImageW) {
-    if (wconv && TAO_TILE_DEBUG != 7) pol.convert(ws0, img0, wm, lane);
+    if (wconv) pol.convert(ws0, img0, wm, lane);
   }
   raw_barrier();
-  mark(1);
   for (int j = 0; j < J; ++j) {
     issue_w(j + RW - 1);
     issue_x(j + R - 1);
     compute(j);
     wait_next();  // this wave's DMAs of step j + 1 landed (its weights were issued earlier still)
     if constexpr (!P::kImageW) {
-      if (wconv && j + 1 < J && TAO_TILE_DEBUG != 7)
+      if (wconv && j + 1 < J)
         pol.convert(ws0 + ((j + 1) % RW) * L::kW, img0 + ((j + 1) & 1) * L::kImg, wm, lane);
     }
     raw_barrier();
   }
   wait_vm<0>();  // the clamped re-reads past the slice
   __syncthreads();
-  mark(2);
   // group 1 hands its sums to group 0 (added in group order); the epilogue operand table -> LDS
   {
     Acc* red = reinterpret_cast<Acc*>(lds + 256);
@@ -617,8 +556,6 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb) emit(acc[t][nb], wm * (BM / 4) + 16 * t, 16 * nb);
     }
-    mark(5);
-    flush();
     return;
   }
 
@@ -643,7 +580,6 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  mark(3);
   unsigned long long* tsync = sync + (size_t)tile * kSyncWords;
   // flag words after the epilogue table: [0] last, [1..2] epoch, [3] go, [4 + p] last's claims
   unsigned* word = reinterpret_cast<unsigned*>(lds) + 512;
@@ -694,7 +630,6 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(
     word[3] = go;
   }
   __syncthreads();
-  mark(4);
   const bool last = word[0] != 0;
   const unsigned long long epoch = ((unsigned long long)word[2] << 32) | word[1];
   const int per = NT / S;  // accumulator tiles per part
@@ -723,15 +658,8 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(
       default: run(std::integral_constant<int, 16>{}); break;
     }
   };
-#if TAO_TILE_STAMPS
-  stamp[7] = (word[0] ? 1u : 0u) | (word[3] ? 2u : 0u);
-#endif
   if (word[3]) reduce_part(z);
-  mark(5);
-  if (!last) {
-    flush();
-    return;
-  }
+  if (!last) return;
   // the last arriver: claim, in one round trip, every part whose owner has not claimed it
   if (tid < S && tid != z)
     word[4 + tid] = __hip_atomic_fetch_max(&tsync[1 + tid], epoch, __ATOMIC_RELAXED,
@@ -739,8 +667,6 @@ __global__ __launch_bounds__(512) void gemm_tile_kernel(
   __syncthreads();
   for (int p = 0; p < S; ++p)
     if (p != z && word[4 + p]) reduce_part(p);
-  mark(6);
-  flush();
 }
 
 }  // namespace
@@ -830,15 +756,6 @@ int tile_int8dyn(const int8_t* xq, const uint16_t* xs, const int8_t* wq, const u
 
 }  // namespace tao
 
-#if TAO_TILE_STAMPS
-extern "C" int tao_debug_tile_stamps(unsigned long long* out, int n) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tao::g_tile_stamps), (size_t)n * 8 * 8) != hipSuccess)
-    return TAO_ERR_HIP;
-  static unsigned long long zero[16384 * 8];
-  return hipMemcpyToSymbol(HIP_SYMBOL(tao::g_tile_stamps), zero, sizeof(zero)) == hipSuccess
-             ? TAO_OK : TAO_ERR_HIP;
-}
-#endif
 
 extern "C" int tao_tune_gemm_tile(int mode, int splits) {
   TAO_CHECK_ARG(mode >= 0 && mode <= 2, "tune: gemm tile mode must be 0 (auto), 1 (off) or 2 (on)");

@@ -23,36 +23,15 @@
 #include "tao_attn.h"
 #include "tao_reduce.h"
 
-// Timing-only variant builds (experiments/gemv_debug.sh; never the shipped library):
-// 1 x not loaded (a lane-dependent constant), 2 no dequant/dot arithmetic (the weight words
-// are folded in with one integer add), 3 no (scale, zero) loads, 4 no cross-lane / cross-wave
-// reduction (each wave's lane 0 writes its own partial), 5 = 2 + 4, 6 = 1 + 2 + 3 + 4 (only the
-// weight loads in the GEMV's pattern). Results are wrong in every variant.
-#ifndef TAO_GEMV_DEBUG
-#define TAO_GEMV_DEBUG 0
-#endif
-// TAO_GEMV_STAMPS 1 (timing only, experiments/gemv_stamps.py): per-workgroup s_memrealtime
-// stamps of the plain M = 1 path: first instruction, slices done, end (wave 0 of each group).
-#ifndef TAO_GEMV_STAMPS
-#define TAO_GEMV_STAMPS 0
-#endif
-// TAO_NORM_DEBUG 1 (timing only): the RMSNorm prologue skips its cross-wave exchange; 2: it
-// keeps the exchange but stores x unnormalised.
-// 1 (variant builds for A/B): M = 1 slices load their x pieces with their weights, and a wave's
-// two paired slices are both issued before the first is consumed (see load_slice)
-#ifndef GEMV_XPRE
-#define GEMV_XPRE 0
-#endif
-#ifndef TAO_NORM_DEBUG
-#define TAO_NORM_DEBUG 0
-#endif
+// The timing-only variant builds of rounds 1-5 (no x loads, no arithmetic, no (scale, zero)
+// loads, no reduction, per-workgroup s_memrealtime stamps, the RMSNorm-prologue variants and the
+// both-slices-issued XPRE order) lived in this file behind TAO_GEMV_DEBUG /
+// TAO_GEMV_STAMPS / TAO_NORM_DEBUG / GEMV_XPRE up to commit 1bac331; their measurements are in
+// profiles/ (r1_gemv_debug*.log, r2/r5g_gemv_stamps.jsonl, r5g_ab_gemv_*.jsonl).
 
 namespace tao {
 
 TAO_DECODE_ERROR_WORD(int4gemv_decode_status)
-#if TAO_GEMV_STAMPS
-__device__ unsigned long long g_gemv_stamps[65536 * 4];
-#endif
 
 namespace {
 
@@ -118,9 +97,6 @@ __device__ __forceinline__ void gemv_body(
   static_assert(!(PRO || EPI) || (MT == 1 && RPW % 2 == 0), "fusions are M == 1, row pairs");
   constexpr int V = RPW * MT;
   extern __shared__ float red[];  // [G][Wk][V] (PRO: + [8] partial sums, + normalised x [K])
-#if TAO_GEMV_STAMPS
-  const unsigned long long st_entry = __builtin_amdgcn_s_memrealtime();
-#endif
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int wk = wave % Wk;
@@ -237,24 +213,6 @@ __device__ __forceinline__ void gemv_body(
       }
     }
     ss = wave_sum(ss);
-#if TAO_NORM_DEBUG == 1
-    // timing only: this wave's own sum stands in for the workgroup's (no exchange, no barrier)
-    {
-      const float r = rsqrtf(ss * (float)(G * Wk) / (float)K + fu.eps);
-#pragma unroll
-      for (int u = 0; u < NPT; ++u) {
-        const int i = threadIdx.x + u * (int)blockDim.x;
-        if (i < nx) {
-          const int c = i >> 2;
-          xs[c * 4 + (((i & 3) + (c >> 2)) & 3)] =
-              make_uint4(rmsnorm_pair(xv[u].x, gv[u].x, r), rmsnorm_pair(xv[u].y, gv[u].y, r),
-                         rmsnorm_pair(xv[u].z, gv[u].z, r), rmsnorm_pair(xv[u].w, gv[u].w, r));
-        }
-      }
-      __syncthreads();
-      return;
-    }
-#endif
     float* ssr = red + G * Wk * V;
     if (lane == 0) ssr[wave] = ss;
     if (fu.norm_deferred) {
@@ -284,16 +242,9 @@ __device__ __forceinline__ void gemv_body(
       const int i = threadIdx.x + u * (int)blockDim.x;
       if (i < nx) {
         const int c = i >> 2;
-#if TAO_NORM_DEBUG == 2
-        // timing only: the sum, exchange and barriers kept, the per-element normalisation not
-        const uint32_t k = r > 1e30f ? 1u : 0u;
-        xs[c * 4 + (((i & 3) + (c >> 2)) & 3)] =
-            make_uint4(xv[u].x ^ k, xv[u].y ^ gv[u].y, xv[u].z, xv[u].w);
-#else
         xs[c * 4 + (((i & 3) + (c >> 2)) & 3)] =
             make_uint4(rmsnorm_pair(xv[u].x, gv[u].x, r), rmsnorm_pair(xv[u].y, gv[u].y, r),
                        rmsnorm_pair(xv[u].z, gv[u].z, r), rmsnorm_pair(xv[u].w, gv[u].w, r));
-#endif
       }
     }
     __syncthreads();
@@ -302,40 +253,20 @@ __device__ __forceinline__ void gemv_body(
   // PAIR (waves owning >= 2 slices): slices are processed two at a time, both slices' weight
   // and (scale, zero) loads issued before either is consumed, so a wave walking two slices pays
   // one memory round trip, not two.
-  // XPRE (M == 1 without the LDS prologue, tao_tune_int4_xpre): a slice's x pieces are loaded
-  // with its weights, so a wave holding two slices in flight can consume the first while the
-  // second's loads are still out (in-order vmcnt: the first slice's loads are all older)
-  constexpr bool kXPre = GEMV_XPRE && MT == 1 && !PRO;
-  auto load_slice = [&](int s, uint4 (&wv)[RPW], uint32_t (&szv)[RPW], uint4 (&xv)[4], int& cc,
+  auto load_slice = [&](int s, uint4 (&wv)[RPW], uint32_t (&szv)[RPW], int& cc,
                         bool& cval) __attribute__((always_inline)) {
     const int c = s * 64 + lane;
     cval = s < S && c < nchunk;
     cc = c < nchunk ? c : nchunk - 1;  // clamped: every load stays in bounds, no branches
-    if constexpr (kXPre) {
-      const uint4* xp = reinterpret_cast<const uint4*>(x + (size_t)cc * 32);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-#if TAO_GEMV_DEBUG == 1 || TAO_GEMV_DEBUG == 6
-        xv[j] = make_uint4(0x3F803F80u + cc + j, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
-        (void)xp;
-#else
-        xv[j] = xp[j];
-#endif
-      }
-    }
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
       const int n = row0 + r;
       const int nn = n < N ? n : N - 1;
       wv[r] = ld_nt_u4(wq + (size_t)nn * nchunk + cc);
-#if TAO_GEMV_DEBUG == 3 || TAO_GEMV_DEBUG == 6
-      szv[r] = 0x3F803F80u ^ (uint32_t)cc;
-#else
       szv[r] = ld_nt(sz + (size_t)nn * ngroups + (cc >> gshift));
-#endif
     }
   };
-  auto do_slice = [&](const uint4 (&wv)[RPW], const uint32_t (&szv)[RPW], const uint4 (&xv)[4],
+  auto do_slice = [&](const uint4 (&wv)[RPW], const uint32_t (&szv)[RPW],
                       int cc, bool cval) __attribute__((always_inline)) {
     // Lanes past K contribute nothing: zero their (s, z) so the chunk term vanishes.
     float sc[RPW], zp[RPW];
@@ -355,13 +286,7 @@ __device__ __forceinline__ void gemv_body(
       uint32_t xd[4][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-#if TAO_GEMV_DEBUG == 1 || TAO_GEMV_DEBUG == 6
-        const uint4 t4 = make_uint4(0x3F803F80u + cc + j, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
-        (void)xp;
-        (void)xv;
-#else
-        const uint4 t4 = kXPre ? xv[j] : PRO ? xs[cc * 4 + ((j + (cc >> 2)) & 3)] : xp[j];
-#endif
+        const uint4 t4 = PRO ? xs[cc * 4 + ((j + (cc >> 2)) & 3)] : xp[j];
         xd[j][0] = t4.x;
         xd[j][1] = t4.y;
         xd[j][2] = t4.z;
@@ -376,10 +301,6 @@ __device__ __forceinline__ void gemv_body(
 #pragma unroll
       for (int r = 0; r < RPW; ++r) {
         const uint32_t wd[4] = {wv[r].x, wv[r].y, wv[r].z, wv[r].w};
-#if TAO_GEMV_DEBUG == 2 || TAO_GEMV_DEBUG >= 5
-        acc[r][m] += __uint_as_float((wd[0] + wd[1] + wd[2] + wd[3] + xd[0][0] + xd[3][3]) & 0x3FFFFFFFu) + sc[r] + zp[r];
-        continue;
-#endif
         float d = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -393,76 +314,60 @@ __device__ __forceinline__ void gemv_body(
   // With PRO the first slice (every wave has one: Wk <= S) is peeled so the RMSNorm prologue
   // can sit around its loads.
   auto pair_step = [&](int s, auto first) __attribute__((always_inline)) {
-    uint4 wv0[RPW], wv1[RPW], xv0[4], xv1[4];
+    uint4 wv0[RPW], wv1[RPW];
     uint32_t szv0[RPW], szv1[RPW];
     int cc0, cc1;
     bool cv0, cv1;
     if constexpr (PRO && decltype(first)::value) norm_load();
-    load_slice(s, wv0, szv0, xv0, cc0, cv0);
-    load_slice(s + Wk, wv1, szv1, xv1, cc1, cv1);
+    load_slice(s, wv0, szv0, cc0, cv0);
+    load_slice(s + Wk, wv1, szv1, cc1, cv1);
     if constexpr (PRO && decltype(first)::value) norm_finish();
-    do_slice(wv0, szv0, xv0, cc0, cv0);
-    if (s + Wk < S) do_slice(wv1, szv1, xv1, cc1, cv1);  // wave-uniform
+    do_slice(wv0, szv0, cc0, cv0);
+    if (s + Wk < S) do_slice(wv1, szv1, cc1, cv1);  // wave-uniform
   };
   auto single_step = [&](int s, auto first) __attribute__((always_inline)) {
-    uint4 wv0[RPW], xv0[4];
+    uint4 wv0[RPW];
     uint32_t szv0[RPW];
     int cc0;
     bool cv0;
     if constexpr (PRO && decltype(first)::value) norm_load();
-    load_slice(s, wv0, szv0, xv0, cc0, cv0);
+    load_slice(s, wv0, szv0, cc0, cv0);
     if constexpr (PRO && decltype(first)::value) norm_finish();
-    do_slice(wv0, szv0, xv0, cc0, cv0);
+    do_slice(wv0, szv0, cc0, cv0);
   };
   if constexpr (PAIR && PRO) {
     pair_step(wk, std::true_type{});
     for (int s = wk + 2 * Wk; s < S; s += 2 * Wk) pair_step(s, std::false_type{});
   } else if constexpr (PAIR) {
     for (int s = wk; s < S; s += 2 * Wk) {
-      uint4 wv0[RPW], wv1[RPW], xv0[4], xv1[4];
+      uint4 wv0[RPW], wv1[RPW];
       uint32_t szv0[RPW], szv1[RPW];
       int cc0, cc1;
       bool cv0, cv1;
-      load_slice(s, wv0, szv0, xv0, cc0, cv0);
-      load_slice(s + Wk, wv1, szv1, xv1, cc1, cv1);
-      if constexpr (kXPre) __builtin_amdgcn_sched_barrier(0);  // both slices' loads issued first
-      do_slice(wv0, szv0, xv0, cc0, cv0);
+      load_slice(s, wv0, szv0, cc0, cv0);
+      load_slice(s + Wk, wv1, szv1, cc1, cv1);
+      do_slice(wv0, szv0, cc0, cv0);
       // wave-uniform. hipcc sinks slice s + Wk's loads into this branch, behind slice s's
       // arithmetic; issuing both slices' loads first (the second do_slice unconditional) measured
       // SLOWER: 28672x4096 14.6-15.0 -> 16.0 us, 4096x14336 9.3 -> 11.4 (every grid is resident
       // at once, and a wave holding less in flight computes while the others' loads stream;
       // profiles/r5g_ab_gemv_pair.jsonl)
-      if (GEMV_XPRE) do_slice(wv1, szv1, xv1, cc1, cv1);  // (past S: cv1 false, zero terms)
-      else if (s + Wk < S) do_slice(wv1, szv1, xv1, cc1, cv1);
+      if (s + Wk < S) do_slice(wv1, szv1, cc1, cv1);
     }
   } else if constexpr (PRO) {
     single_step(wk, std::true_type{});
     for (int s = wk + Wk; s < S; s += Wk) single_step(s, std::false_type{});
   } else {
     for (int s = wk; s < S; s += Wk) {
-      uint4 wv0[RPW], xv0[4];
+      uint4 wv0[RPW];
       uint32_t szv0[RPW];
       int cc0;
       bool cv0;
-      load_slice(s, wv0, szv0, xv0, cc0, cv0);
-      do_slice(wv0, szv0, xv0, cc0, cv0);
+      load_slice(s, wv0, szv0, cc0, cv0);
+      do_slice(wv0, szv0, cc0, cv0);
     }
   }
 
-#if TAO_GEMV_STAMPS
-  const unsigned long long st_loop = __builtin_amdgcn_s_memrealtime();
-#endif
-#if TAO_GEMV_DEBUG == 4 || TAO_GEMV_DEBUG >= 5
-  if constexpr (EPI == kEpiNone && !PRO) {
-    float t = 0.f;
-#pragma unroll
-    for (int r = 0; r < RPW; ++r)
-#pragma unroll
-      for (int m = 0; m < MT; ++m) t += acc[r][m];
-    if (lane == 0 && row0 < N) y[row0] = f32_to_bf16(t);
-    return;
-  }
-#endif
   float v[V];
 #pragma unroll
   for (int r = 0; r < RPW; ++r)
@@ -507,13 +412,6 @@ __device__ __forceinline__ void gemv_body(
         y[(size_t)m * N + n] = out;
       }
     }
-#if TAO_GEMV_STAMPS
-    if (threadIdx.x < 64 && blockIdx.x < 65536) {  // wave 0: lane i stores stamp i
-      const unsigned long long st_end = __builtin_amdgcn_s_memrealtime();
-      const unsigned long long v = lane == 0 ? st_entry : lane == 1 ? st_loop : st_end;
-      if (lane < 3) g_gemv_stamps[blockIdx.x * 4 + lane] = v;
-    }
-#endif
   } else {
     // Row pair (2p, 2p+1) meets in lane p of the writing wave. Row r's total sits in lane r
     // (Wk > 1) or in owner lane r << (6 - T) (Wk == 1); every lane takes part in the shuffles.
@@ -1030,16 +928,6 @@ int int4_check_linear_args(const uint16_t* x, const uint32_t* packed, const uint
 }
 
 }  // namespace tao
-
-#if TAO_GEMV_STAMPS
-extern "C" int tao_debug_gemv_stamps(unsigned long long* out, int n) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tao::g_gemv_stamps), (size_t)n * 4 * 8) != hipSuccess)
-    return TAO_ERR_HIP;
-  static unsigned long long zero[65536 * 4];
-  return hipMemcpyToSymbol(HIP_SYMBOL(tao::g_gemv_stamps), zero, sizeof(zero)) == hipSuccess
-             ? TAO_OK : TAO_ERR_HIP;
-}
-#endif
 
 extern "C" int tao_tune_int4_norm(int mode) {
   TAO_CHECK_ARG(mode == 0 || mode == 1, "tune: norm mode must be 0 (exact) or 1 (deferred)");
