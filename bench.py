@@ -74,7 +74,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E, spec (MI355X_MICROARCH.md chip table)
-PMC_FILE = os.path.join(ROOT, "profiles", "r5n_pmc_fetch_bench.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r5n_pmc_fetch_bench.json")  # --pmc-file overrides
 
 LLAMA3_8B = dict(dim=4096, n_layer=32, n_head=32, n_kv_head=8, head_dim=128,
                  intermediate=14336, vocab=128256)
@@ -445,6 +445,75 @@ def config2_shapes(device, g=32, copies=32, reps=20):
     return out
 
 
+INT8WO_SHAPES = ((4096, 4096), (6144, 4096), (14336, 4096), (4096, 14336))
+PMC_INT8WO_FILE = os.path.join(ROOT, "profiles", "r6_pmc_fetch_int8wo.json")
+
+
+def int8wo_alg_bytes(N, K, M=1):
+    """SURVEY §8(d) for int8 weight-only: N*K + 2N (bf16 scales) + 2MK + 2MN."""
+    return N * K + 2 * N + 2 * M * K + 2 * M * N
+
+
+def int8wo_m1(device, copies_bytes=512 << 20, reps=20, pmc_file=PMC_INT8WO_FILE):
+    """The int8 weight-only linear at M = 1 (the int8 GEMV, Int8WeightOnlyConfig's decode path,
+    plain_layout.py:250-266) on the Llama-3-8B shapes: us per launch inside a HIP graph over
+    distinct weight copies (> 256 MiB MALL), HIP events on the replay stream; GB/s and fraction
+    of 8 TB/s over the algorithmic bytes; a pure 16-B read of the same bytes replayed the same way
+    beside it (tao_hbm_read_probe); FETCH_SIZE x2 per launch from the committed counter pass of
+    this block (--only-int8wo under rocprofv3 --pmc) when present."""
+    from torchao import _lib
+
+    lib = _lib.lib()
+    pmc = None
+    if pmc_file and os.path.exists(pmc_file):
+        with open(pmc_file) as f:
+            pmc = json.load(f)
+    out = {}
+    gen = torch.Generator(device=device).manual_seed(11)
+    sink = torch.zeros(1024, dtype=torch.int32, device=device)
+    for (N, K) in INT8WO_SHAPES:
+        b = int8wo_alg_bytes(N, K)
+        copies = max(4, min(32, copies_bytes // b))
+        ws = [torch.randint(-127, 128, (N, K), dtype=torch.int8, device=device, generator=gen)
+              for _ in range(copies)]
+        sc = [(torch.rand(N, device=device, generator=gen) * 0.01 + 1e-3).to(torch.bfloat16)
+              for _ in range(copies)]
+        x = torch.randn(1, K, device=device, dtype=torch.bfloat16, generator=gen)
+        y = torch.empty(1, N, device=device, dtype=torch.bfloat16)
+        rbufs = [torch.full(((b + 8191) // 8192 * 8192,), 7, dtype=torch.uint8, device=device)
+                 for _ in range(copies)]
+
+        def gemv(c):
+            sp = torch.cuda.current_stream(device).cuda_stream
+            rc = lib.tao_int8wo_linear_bf16(x.data_ptr(), ws[c].data_ptr(), sc[c].data_ptr(), None,
+                                            y.data_ptr(), 1, N, K, sp)
+            if rc:
+                raise RuntimeError(lib.tao_last_error().decode())
+
+        def read(c):
+            sp = torch.cuda.current_stream(device).cuda_stream
+            rc = lib.tao_hbm_read_probe(rbufs[c].data_ptr(), rbufs[c].numel(), sink.data_ptr(), sp)
+            if rc:
+                raise RuntimeError(lib.tao_last_error().decode())
+
+        us = graph_us_per_call(gemv, copies, device, reps=reps)
+        kern = lib.tao_last_kernel().decode()
+        rus = graph_us_per_call(read, copies, device, reps=reps)
+        key = f"{N}x{K}"
+        rec = {"us": round(us, 3), "GBps": round(b / (us * 1e-6) / 1e9, 1),
+               "frac": round(b / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4), "alg_bytes": b,
+               "pure_read_us": round(rus, 3), "gemv_over_pure_read": round(us / rus, 3),
+               "kernel": kern, "copies": copies}
+        if pmc and key in pmc.get("hbm_bytes_per_launch", {}):
+            rec["traffic"] = pmc["hbm_bytes_per_launch"][key]
+            rec["traffic_over_alg"] = round(rec["traffic"] / b, 3)
+        out[key] = rec
+        del ws, sc, rbufs
+        torch.cuda.empty_cache()
+    out["traffic_source"] = os.path.relpath(pmc_file, ROOT) if pmc else None
+    return out
+
+
 def graph_us_per_call(fn, copies, device, reps=3):
     """us per call of fn(c), c over `copies` weight copies, captured once in a HIP graph and
     replayed: events on the replay stream (launch gaps inside the graph included)."""
@@ -693,17 +762,24 @@ def cpu_baseline(cfg, g, budget_s=12.0):
             break
     dt = time.perf_counter() - t0
     # PyTorch's own CPU int4 GEMM (what the reference's Int4CPULayout dispatches to), same sample
-    tg = None
+    # rotated over distinct copies of the packed weights (> 512 MB in all, past the host's L3:
+    # a same-weights loop would time a cache-resident working set)
+    tg, tg_footprint = None, None
     try:
         packs = [oracle.int4_tinygemm_cpu_pack(q, s, z) + (x,) for (x, q, s, z, _, _) in mats]
-        for p, sz, x in packs:
+        ncopy = max(1, -(-(600 << 20) // sample_bytes))
+        rot = [(p.clone(), sz.clone(), x) for _ in range(ncopy) for (p, sz, x) in packs]
+        tg_footprint = sum(p.numel() * p.element_size() + sz.numel() * sz.element_size()
+                           for (p, sz, _) in rot)
+        for p, sz, x in rot:
             oracle.int4_tinygemm_cpu(x, p, sz, g)
         r2, t1 = 0, time.perf_counter()
-        while time.perf_counter() - t1 < 2.0:
-            for p, sz, x in packs:
+        while time.perf_counter() - t1 < 3.0:
+            for p, sz, x in rot:
                 oracle.int4_tinygemm_cpu(x, p, sz, g)
             r2 += 1
-        tg = sample_bytes * r2 / (time.perf_counter() - t1) / 1e9
+        tg = sample_bytes * ncopy * r2 / (time.perf_counter() - t1) / 1e9
+        del rot, packs
     except Exception as e:  # pragma: no cover - depends on the host's torch build
         tg = f"unavailable: {type(e).__name__}"
     # BASELINE config 1: a single nn.Linear 4096x4096, int4 g32, the same CPU dequant path
@@ -734,6 +810,10 @@ def cpu_baseline(cfg, g, budget_s=12.0):
                    f"layer 0's 5 int4 g{g} linears at M=1, {reps} reps in {dt:.1f}s"),
         "ms_per_token_extrapolated": round(dt / reps * 1e3 * cfg["n_layer"], 1),
         "aten_weight_int4pack_mm_for_cpu_GBps": round(tg, 3) if isinstance(tg, float) else tg,
+        "aten_weight_int4pack_mm_for_cpu_footprint_bytes": tg_footprint,
+        "aten_weight_int4pack_mm_for_cpu_note": (
+            f"PyTorch's CPU int4 GEMM (Int4CPULayout's kernel) on {cores} threads over distinct "
+            "copies of layer 0's packed weights rotated per pass (footprint above, beyond L3)"),
     }
 
 
@@ -1046,6 +1126,54 @@ def unfused_record(cfg, g, device, steps):
     return rec
 
 
+def n_launches_expected(args):
+    return 161 if args.no_fuse_w13 else 129
+
+
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, script=None, timeout_s=None):
+    """`bench.py --gpus N` without torchrun: run `torch.distributed.run --nproc-per-node N
+    bench.py ...` as a CHILD process (one rank per GPU, rendezvous on 127.0.0.1) and return its
+    exit code. The caller has not initialised the GPU (nothing before this touches HIP) and does
+    not exec: the child's stdout (rank 0's JSON line) and stderr stream through unchanged."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           script or os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    proc = subprocess.run(cmd, env=env, timeout=timeout_s)
+    return proc.returncode
+
+
+def rank_census(P, device, rehearsal):
+    """Proof of the ranks the line was measured on: the process group's size and, all-gathered
+    from every rank, the PCI location of the GPU it drove. Under RCCL the N ranks must sit on N
+    distinct devices (asserted); a gloo rehearsal puts every rank on device 0 (recorded as is)."""
+    props = torch.cuda.get_device_properties(device)
+    mine = f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}"
+    seen = dist.get_world_size() if P > 1 else 1
+    ids = [mine]
+    if P > 1:
+        ids = [None] * P
+        dist.all_gather_object(ids, mine)
+    distinct = sorted(set(ids))
+    if P > 1 and not rehearsal and len(distinct) != P:
+        raise SystemExit(f"rank census: {P} RCCL ranks on {len(distinct)} distinct GPUs: {ids}")
+    return {"ranks_seen": seen, "pci_bus_ids": ids, "distinct_gpus": len(distinct),
+            "backend": "single" if P == 1 else ("gloo (rehearsal, shared device)" if rehearsal
+                                                 else "nccl (RCCL)")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1080,10 +1208,18 @@ def main():
                          "shapes (43 GB of int4 weights per step)")
     ap.add_argument("--no-config5", action="store_true",
                     help="P > 1: skip the Llama-3-70B (BASELINE config 5) sub-record")
+    ap.add_argument("--pmc-file", default=PMC_FILE,
+                    help="FETCH_SIZE summary (experiments/pmc_summary.py) for roofline.traffic")
+    ap.add_argument("--pmc-int8wo-file", default=PMC_INT8WO_FILE,
+                    help="FETCH_SIZE summary (experiments/int8wo_pmc.py) for int8wo_m1")
     ap.add_argument("--no-fuse-w13", action="store_true",
                     help="w1 and w3 as two linears (the reference's module layout, 161 launches)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no outer launcher: start one rank per GPU ourselves (a child process; this process has
+        # not touched the GPU and never will) and pass rank 0's line through
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -1107,6 +1243,7 @@ def main():
     from torchao import _lib
 
     _lib.lib()  # fail loudly if the native library is missing
+    census = rank_census(world, device, rehearsal)
     model_name, cfg = MODELS[args.model]
     g, P = args.group_size, world
     lins = llama_linears(cfg, fuse_w13=not args.no_fuse_w13)
@@ -1183,10 +1320,12 @@ def main():
     # HBM traffic from the committed counter pass (rocprofv3 --pmc FETCH_SIZE of this bench,
     # P = 1 shapes): bytes per step, to set against the algorithmic bytes
     traffic = None
-    if P == 1 and args.model == "8b" and os.path.exists(PMC_FILE):
-        with open(PMC_FILE) as f:
+    pmc_file = args.pmc_file
+    if P == 1 and args.model == "8b" and pmc_file and os.path.exists(pmc_file):
+        with open(pmc_file) as f:
             pmc = json.load(f)
-        traffic = pmc.get("hbm_bytes_per_step")
+        if pmc.get("launches_per_step", n_launches_expected(args)) == len(plan):
+            traffic = pmc.get("hbm_bytes_per_step")
 
     comm_ms = None
     if P > 1:
@@ -1216,6 +1355,8 @@ def main():
     if P == 1 and args.model == "8b" and not args.no_prefill:
         prefill = prefill_mfma(device)
     extras = P == 1 and not args.no_extras
+    int8wo = (int8wo_m1(device, pmc_file=args.pmc_int8wo_file)
+              if extras and args.model == "8b" else None)
     config2 = config2_shapes(device) if extras and args.model == "8b" else None
     ceil = hbm_ceilings(device) if extras else None
 
@@ -1271,6 +1412,7 @@ def main():
                 "parallelism": par_desc,
                 "hip_graph": has_graph,
             },
+            "ranks": census,
             "roofline": {
                 "bound": "hbm",
                 "kernel": "int4wo_gemv_kernel",
@@ -1290,7 +1432,7 @@ def main():
                 "traffic": traffic,
                 "traffic_unit": f"HBM bytes per step ({n_launches} launches)",
                 "alg_bytes_per_step": bytes_per_step,
-                "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic else None,
+                "traffic_source": os.path.relpath(pmc_file, ROOT) if traffic else None,
                 "launches": len(durs),
                 "kernel_ms_per_step": round(kernel_ms, 4),
                 # the same launches as pure 16-B streaming reads of the same bytes, one graph
@@ -1335,6 +1477,8 @@ def main():
             rec["prefill_mfma"] = prefill
         if config2 is not None:
             rec["config2_shapes"] = config2
+        if int8wo is not None:
+            rec["int8wo_m1"] = int8wo
         if P == 1 and args.model == "8b" and not args.no_e2e:
             rec["e2e_decode"] = e2e_decode()
         if comm_ms is not None:

@@ -34,6 +34,7 @@ def main():
     summary["launches"] = launches
     summary["hbm_bytes_per_launch_avg"] = round(total / max(launches, 1))
     summary["hbm_bytes_total"] = round(total)
+    summary["launches_per_step"] = per_step
     summary["steps"] = launches / per_step
     summary["hbm_bytes_per_step"] = round(total / (launches / per_step))
     json.dump(summary, open(out, "w"), indent=1)

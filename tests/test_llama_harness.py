@@ -469,6 +469,52 @@ def test_prefill_last_row_gpu(quant, fuse):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("quant", ["int4wo-32", "int8wo"])
+def test_prefill_last_row_first_token_over_prompts_gpu(quant):
+    """PREFILL_LAST_ROW (on by default) computes the greedy first token from the
+    one-token kernels, which sum K in another order than the all-rows M = S GEMMs of the
+    reference's model(idx)[:, -1].argmax. Over 12 seeded prompts the first token with the flag
+    on equals the flag-off (all-rows) token wherever the all-rows top-2 margin decides it
+    (> 1% of the top logit); near-ties may differ and are counted, not asserted. The switch
+    restores the all-rows path (generate.py --prefill_last_row 0)."""
+    from torchao._models.llama import kernels
+    from torchao._models.llama.generate import apply_quantization
+
+    dev = torch.device("cuda")
+    model = _tiny(dev)
+    model.fuse_w13()
+    apply_quantization(model, quant)
+    model.setup_caches(1, 96)
+    model.enable_fused_kernels()
+    decided = agree = 0
+    old = kernels.PREFILL_LAST_ROW
+    try:
+        for seed in range(12):
+            S = 24 + 5 * seed
+            pos = torch.arange(S, device=dev)
+            prompt = torch.randint(0, model.config.vocab_size, (1, S), device=dev,
+                                   generator=torch.Generator(device=dev).manual_seed(100 + seed))
+            with torch.no_grad():
+                kernels.PREFILL_LAST_ROW = False
+                full = model._layers_prefill(prompt, pos)[:, -1:]
+                logits = model.output(kernels.rmsnorm(full, model.norm.weight,
+                                                      model.norm.eps)).float()[0, -1]
+                tok_off = int(model.prefill_next(prompt, pos).item())
+                kernels.PREFILL_LAST_ROW = True
+                tok_on = int(model.prefill_next(prompt, pos).item())
+            top2 = logits.topk(2)
+            assert tok_off == int(top2.indices[0].item()) or \
+                (top2.values[0] - top2.values[1]).item() <= 1e-2 * top2.values[0].abs().item()
+            if (top2.values[0] - top2.values[1]).item() > 1e-2 * top2.values[0].abs().item():
+                decided += 1
+                agree += tok_on == tok_off
+                assert tok_on == tok_off, (seed, tok_on, tok_off)
+    finally:
+        kernels.PREFILL_LAST_ROW = old
+    assert decided >= 6, decided
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("fuse", [True, False])
 def test_prefill_partials_bit_identical_gpu(fuse):
     """The prefill with wo / w2's K slices summed by the following add + RMSNorm

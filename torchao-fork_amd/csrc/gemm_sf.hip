@@ -560,10 +560,10 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
     if (tid == 0) {
       const unsigned need = seam ? (unsigned)S : (unsigned)(S - 1);
       unsigned ok = 1;
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      SeamWait sw;
       while (__hip_atomic_load(&cnt[tile * cs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
         __builtin_amdgcn_s_sleep(1);
-        if (seam_timed_out(t0)) {  // give up, report (outputs of this tile are invalid)
+        if (sw.timed_out()) {  // give up, report (outputs of this tile are invalid)
           ok = 0;
           (void)__hip_atomic_fetch_or(&g_sf_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;

@@ -415,11 +415,11 @@ __global__ __launch_bounds__((WV * KH + LDW) * 64) void gemm_sf32_int4_kernel(
     }
     if (tid == 0) {
       unsigned ok = 1;
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      SeamWait sw;
       while (__hip_atomic_load(&cnt[tile * cs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
              (unsigned)(S - 1)) {
         __builtin_amdgcn_s_sleep(1);
-        if (seam_timed_out(t0)) {
+        if (sw.timed_out()) {
           ok = 0;
           (void)__hip_atomic_fetch_or(&g_sf32_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
@@ -583,6 +583,10 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
                                     (ldm == 0 && bn == 128 && stages == 3))) ||
                        (kh == 2 && bn == 128 && (ldm == 2 || (ldm == 0 && stages == 3)));
   if (loaders) {
+    // the loader-wave kernels are instantiated at 3 stages only: a forced loader run at another
+    // stage count is refused rather than silently measured at 3
+    if (stages != 3)
+      return set_error(TAO_ERR_UNSUPPORTED, "gemm_sf32: loader waves need 3 stages, got %d", stages);
     if (kh == 2) {  // two compute waves per column group (k halves) + 4 loader waves
       if (z16) go1(gemm_sf32_int4_kernel<4, 3, 2, true, 4>, 12 * 64);
       else go1(gemm_sf32_int4_kernel<4, 3, 2, false, 4>, 12 * 64);

@@ -543,9 +543,9 @@ __device__ __forceinline__ void qkv_attn_tail(const GemvFuse& fu, const QkvAttn&
     const unsigned* cq = qa.cnt + (size_t)h * qa.cs;
     const unsigned* ck = qa.cnt + (size_t)(fu.H + kvh) * qa.cs;
     const unsigned* cv = qa.cnt + (size_t)(fu.H + fu.Hkv + kvh) * qa.cs;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    SeamWait sw;
     while ((int)ld_coh(cq) < qa.need || (int)ld_coh(ck) < qa.need || (int)ld_coh(cv) < qa.need) {
-      if (seam_timed_out(t0)) {
+      if (sw.timed_out()) {
         flag_decode_error(kDecodeErrSplitK);
         break;
       }

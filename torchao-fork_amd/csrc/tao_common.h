@@ -145,13 +145,22 @@ __device__ __forceinline__ void st_nt_u4(uint4* p, uint4 v) {  // 16-B non-tempo
 }
 
 // ---- split-K seam waits ------------------------------------------------------------------------
-// A reducer gives up on its tile's publishers after kSeamTimeoutTicks of the 100 MHz
-// s_memrealtime clock (0.25 s), reports, and writes nothing for that tile.
+// A reducer gives up on its tile's publishers once BOTH kSeamTimeoutTicks of the 100 MHz
+// s_memrealtime clock (0.25 s) have passed AND it has polled kSeamMinPolls times itself, reports,
+// and writes nothing for that tile. The poll count only advances while the waiting wave runs, so
+// time the GPU spends on other work (a shared or preempted card, e.g. every rank of a gloo
+// rehearsal on one device) does not count toward a timeout.
 constexpr unsigned long long kSeamTimeoutTicks = 25000000ull;
+constexpr unsigned kSeamMinPolls = 200000u;
 
-__device__ __forceinline__ bool seam_timed_out(unsigned long long t0) {
-  return __builtin_amdgcn_s_memrealtime() - t0 > kSeamTimeoutTicks;
-}
+struct SeamWait {
+  unsigned long long t0;
+  unsigned polls;
+  __device__ __forceinline__ SeamWait() : t0(__builtin_amdgcn_s_memrealtime()), polls(0u) {}
+  __device__ __forceinline__ bool timed_out() {
+    return ++polls > kSeamMinPolls && __builtin_amdgcn_s_memrealtime() - t0 > kSeamTimeoutTicks;
+  }
+};
 
 // Test hook (tao_debug_sf_late_publisher): a slice-0 publisher holds its ticket add until some
 // reducer has timed out (its error word set) or 2 s passed, so a test can check that the

@@ -217,6 +217,7 @@ def generate(model: Transformer, prompt: torch.Tensor, max_new_tokens: int,
         tok = prefill(model, prompt, torch.arange(P, device=device))
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    _check_status(model)  # a timed-out split-K hand-off in the prefill raises here, not later
     if decoder is not None:
         decoder.reset(prompt, tok)
         decoder.run(max_new_tokens - 1)
@@ -299,6 +300,11 @@ def main(argv=None):
     ap.add_argument("--prefill_add_norm", type=int, default=-1,
                     help="1 / 0: fuse the prefill residual adds with the next RMSNorm or not "
                          "(kernels.PREFILL_ADD_NORM; -1 = built-in)")
+    ap.add_argument("--prefill_last_row", type=int, default=-1,
+                    help="1 / 0: the greedy first token from the last block's last row on the "
+                         "one-token kernels (a different K summation order than the reference's "
+                         "all-rows model(idx)[:, -1].argmax; 0 restores the all-rows path; "
+                         "kernels.PREFILL_LAST_ROW; -1 = built-in, on)")
     ap.add_argument("--native_prefill_attn", action="store_true",
                     help="prefill attention on tao_attn_prefill_bf16 (kernels.PREFILL_ATTN = True)")
     ap.add_argument("--qkv_attn", type=int, default=-1,
@@ -326,9 +332,12 @@ def main(argv=None):
     args = ap.parse_args(argv)
 
     if (args.head_prologue or args.sdpa_prefill or args.qkv_attn >= 0
-            or args.native_prefill_attn or args.prefill_add_norm >= 0):
+            or args.native_prefill_attn or args.prefill_add_norm >= 0
+            or args.prefill_last_row >= 0):
         from torchao._models.llama import kernels
 
+        if args.prefill_last_row >= 0:
+            kernels.PREFILL_LAST_ROW = bool(args.prefill_last_row)
         if args.qkv_attn >= 0:
             kernels.DECODE_QKV_ATTN = bool(args.qkv_attn)
 

@@ -137,9 +137,12 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
 # all heads' partials), so the pair pays only past ~600 keys: 328 keys one-pass 9.98 us vs
 # 10.33 / 11.16 split 2 / 4; 512 keys 10.98 vs 10.83 / 11.38; 900 keys 14.29 vs 12.69 / 12.30;
 # past 1024 rows against the two-launch chunk split: 1500 keys 23.3 vs 14.5, 3000 keys 35.1 vs
-# 18.5 (split 4; profiles/r5b_attn_pair_long.jsonl).
+# 18.5 (split 4; profiles/r5b_attn_pair_long.jsonl). The route is chosen by the cache's
+# capacity T (a graph is captured once per capacity, not per position), so it is taken only
+# where every position gains: T > 1024, where the one-pass kernel's alternative is the two-launch
+# chunk split; a 768-1024-row cache would run its early (short-history) steps slower on the pair.
 ATTN_SPLITS = 4
-ATTN_SPLIT_MIN_T = 768
+ATTN_SPLIT_MIN_T = 1025
 ATTN_SPLIT_MAX_T = 8192
 PART_STRIDE = 132  # fp32 per (head, split) record: o[128], m, l, 2 pad
 
@@ -363,7 +366,11 @@ PREFILL_ADD_NORM = True
 # Greedy prefill (Transformer.prefill_next) reads only the last position's hidden state: the last
 # block runs wqkv + RoPE + KV write over every row (the caches need them) and everything after it
 # for the last row only, on the one-token kernels (attention, wo + residual, RMSNorm + w1||w3 +
-# SwiGLU, w2 + residual).
+# SwiGLU, w2 + residual). Parity note: those kernels sum K in another order than the M = S GEMMs,
+# so the first token is not bit-tied to the reference's model(idx)[:, -1].argmax; it agrees
+# wherever the top-2 margin decides it (tests/test_llama_harness.py
+# test_prefill_last_row_first_token_over_prompts_gpu); False (generate.py --prefill_last_row 0)
+# restores the all-rows path.
 PREFILL_LAST_ROW = True
 # Prefill wo / w2 (int4, where the 16x16 single-fetch GEMM serves them): the K slices' fp32
 # partial tiles are summed by the residual add + RMSNorm launch that follows instead of at an
