@@ -1,0 +1,99 @@
+"""Time the decode FFN engine (tao_int4wo_ffn_engine_bf16) against the launch path it replaces,
+on Llama-3-8B's feed-forward: L layers with distinct int4 g32 weights (110 MB each, past the
+MALL), each layer's output the next layer's input (the real dependency), captured in one HIP
+graph and replayed; us per layer from HIP events on the replay stream.
+
+python3 experiments/engine_time.py [--layers 32] [--reps 20]
+prints one JSON line: launch_us_per_layer, engine_us_per_layer, ratio, GB/s of each, and the
+output agreement of the two chains (rel L2 of the last layer's output)."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "torchao-fork_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from torchao import _lib  # noqa: E402
+from torchao._models.llama import kernels  # noqa: E402
+
+DIM, INTER, G = 4096, 14336, 32
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    L = args.layers
+    layers = []
+    for i in range(L):
+        p13 = bench.make_int4_weight(2 * INTER, DIM, G, seed=10 * i + 1, device=dev)
+        p2 = bench.make_int4_weight(DIM, INTER, G, seed=10 * i + 2, device=dev)
+        nw = (torch.rand(DIM, device=dev) + 0.5).to(torch.bfloat16)
+        layers.append((p13 + (G,), p2 + (G,), nw))
+    nbytes = bench.int4_alg_bytes(2 * INTER, DIM, G) + bench.int4_alg_bytes(DIM, INTER, G)
+    x0 = torch.randn(1, 1, DIM, device=dev, dtype=torch.bfloat16)
+    lib = _lib.lib()
+
+    def launch_chain(x):
+        for (p13, p2, nw) in layers:
+            g = kernels.int4_decode(x, *p13, norm_weight=nw, eps=1e-5, epilogue="swiglu")
+            y = torch.empty_like(x)
+            rc = lib.tao_int4wo_linear_bf16(g.data_ptr(), p2[0].data_ptr(), p2[1].data_ptr(),
+                                            x.data_ptr(), y.data_ptr(), 1, DIM, INTER, G,
+                                            torch.cuda.current_stream().cuda_stream)
+            assert rc == 0
+            x = y
+        return x
+
+    def engine_chain(x):
+        for (p13, p2, nw) in layers:
+            x = kernels.int4_ffn_engine(x, nw, 1e-5, p13, p2)
+        return x
+
+    def timed(fn):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            fn(x0)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=s):
+                out = fn(x0)
+            graph.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(args.reps):
+                graph.replay()
+            e1.record(s)
+        e1.synchronize()
+        torch.cuda.current_stream().wait_stream(s)
+        us = e0.elapsed_time(e1) * 1e3 / args.reps / L
+        return us, out.clone(), graph
+
+    res = {"layers": L, "bytes_per_layer": nbytes}
+    for rnd in range(2):  # alternate twice (box drift)
+        lu, lout, gl = timed(launch_chain)
+        eu, eout, ge = timed(engine_chain)
+        del gl, ge
+        res[f"launch_us_per_layer_{rnd}"] = round(lu, 3)
+        res[f"engine_us_per_layer_{rnd}"] = round(eu, 3)
+    lu = min(res["launch_us_per_layer_0"], res["launch_us_per_layer_1"])
+    eu = min(res["engine_us_per_layer_0"], res["engine_us_per_layer_1"])
+    res.update({"launch_us_per_layer": lu, "engine_us_per_layer": eu,
+                "engine_over_launch": round(eu / lu, 4),
+                "launch_GBps": round(nbytes / (lu * 1e-6) / 1e9, 1),
+                "engine_GBps": round(nbytes / (eu * 1e-6) / 1e9, 1),
+                "last_output_rel_l2": round(float((eout.float() - lout.float()).norm()
+                                                  / lout.float().norm()), 5)})
+    kernels.check_decode_status()
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -192,6 +192,26 @@ int tao_int4wo_decode_bf16(const uint16_t* x, const uint32_t* packed,
                            uint16_t* k_cache, uint16_t* v_cache, int64_t n_head,
                            int64_t n_kv_head, int64_t head_dim, int64_t max_seq, void* stream);
 
+/* Decode step, batch 1: one Llama block's feed-forward in ONE persistent launch (the LDS-DMA
+ * engine, csrc/decode_engine.hip): out [dim] = h + w2(swiglu(w13(rmsnorm(h)))) with the roundings
+ * of tao_int4wo_decode_bf16 (norm_weight, epilogue 1) followed by tao_int4wo_linear_bf16 with h as
+ * its bias. w13 / sz13: the fused (w1_i, w3_i)-interleaved int4 linear [2 inter][dim/8] /
+ * [2 inter][dim/32][2]; w2 / sz2: [dim][inter/8] / [dim][inter/32][2]; group size 32. The
+ * summation order differs from the two launches (not bit-identical; within the oracle bars).
+ * `ctl` / `granules`: a device workspace of tao_int4wo_ffn_engine_workspace_bytes(inter) bytes,
+ * zeroed, then ctl[0] = 1 (an epoch the kernel advances per launch; one workspace per stream,
+ * shared by every layer). One workgroup per CU, all co-resident: shapes and devices
+ * tao_int4wo_ffn_engine_supported() accepts (1 / 0, not a status); a timed-out in-launch wait
+ * sets tao_decode_status bit 2. Replaces FeedForward.forward's w1 / w3 / silu / w2 around the
+ * reference's int4 linears at decode (torchao/_models/llama/model.py:481-492). */
+int tao_int4wo_ffn_engine_supported(int64_t dim, int64_t inter, int64_t group_size);
+int64_t tao_int4wo_ffn_engine_workspace_bytes(int64_t inter);
+int tao_int4wo_ffn_engine_bf16(const uint16_t* h, const uint16_t* norm_weight, float eps,
+                               const uint32_t* w13, const uint16_t* sz13, const uint32_t* w2,
+                               const uint16_t* sz2, uint16_t* out, int64_t dim, int64_t inter,
+                               int64_t group_size, unsigned* ctl, uint64_t* granules,
+                               void* stream);
+
 /* MoE decode: the A activated experts' int4 linears of one token in one launch. packed
  * [E][N][K/8] and scales_and_zeros [E][N][K/g][2] are a 3-D Int4WeightOnlyConfig weight (the
  * reference packs 3-D weights per expert, tensor_core_tiled_layout.py:283-294); expert_idx [A]

@@ -1,0 +1,401 @@
+// Persistent LDS-DMA decode engine (MI355X_MICROARCH.md rows ldsdma-fill,
+// prefetch-credit, gather-pass, engine-vs-launches): one Llama decode block's feed-forward at
+// batch 1 — RMSNorm -> int4 w1||w3 -> SwiGLU -> int4 w2 -> + residual — in ONE launch, with the
+// real data dependency (w2 reads every SwiGLU output) kept inside it.
+//
+// Replaces, at decode, FeedForward.forward's w1 / w3 / silu / w2 sequence around the reference's
+// int4 linears (torchao/_models/llama/model.py:481-492, tensor_core_tiled_layout.py:104 for each
+// linear), which the launch path runs as two launches (tao_int4wo_decode_bf16 with the RMSNorm
+// prologue and SwiGLU epilogue, then the w2 GEMV with the residual on its bias).
+//
+// Geometry: kNWG = 256 workgroups, one per CU (160 KiB LDS each: all resident), 4 waves:
+//   wave 0 (loader)    streams this CU's weight rows of BOTH linears, in order, into a ring of
+//                      kRing LDS slots with non-temporal LDS-DMA (buffer_load ... lds), kAhead
+//                      slots in flight; it never waits for an activation, so w2's rows stream in
+//                      while w1||w3's outputs are still being gathered (prefetch credit);
+//   waves 1..3         consume slots round-robin (slot g -> consumer g % 3):
+//     phase 1  x = RMSNorm(h) held in registers (each consumer wave normalises the whole h,
+//              so no cross-wave exchange); a slot is 8 rows (4 (w1_i, w3_i) pairs) x 4096 k;
+//              per row the GEMV's lane math (v_dot2c_f32_bf16 on magic-number nibble pairs),
+//              a reduce-scatter, then SwiGLU -> 4 outputs = two 8-byte {tag, 2 x bf16}
+//              granules stored sc1 (MI355X_MICROARCH.md hand-off R2: the data is the flag);
+//     phase 2  a slot is 16 rows x one 2048-k unit of w2; a consumer gathers the SwiGLU outputs
+//              of ITS units straight into registers (16-B sc1 loads of granules, re-polled until
+//              every tag is this launch's epoch), accumulates its units' partial dot products,
+//              and the three consumers' partials meet in LDS (fixed order) -> + h -> out.
+// In-CU hand-offs are LDS words: FULL[slot] (loader, after a counted vmcnt wait) and FREE[slot]
+// (consumer, after its reads of the slot). The granule tag is a per-launch epoch kept on the
+// device (ctl[0]); the last workgroup out advances it, so HIP-graph replays need no reset.
+// Every wait is bounded (SeamWait): a timeout sets tao_decode_status bit 2 and the grid drains.
+#include "tao_common.h"
+#include "tao_reduce.h"
+
+namespace tao {
+
+TAO_DECODE_ERROR_WORD(engine_decode_status)
+
+namespace {
+
+constexpr int kNWG = 256;            // one workgroup per CU
+constexpr int kSlotB = 20 * 1024;    // slot: 16 KiB of nibbles + 4 KiB of (scale, zero) words
+constexpr int kScaleOff = 16 * 1024;
+constexpr int kRing = 6;             // 120 KiB of ring
+constexpr int kPieces = 20;          // DMA wave-instructions per slot (1 KiB each)
+constexpr int kAhead = 2;            // slots in flight beyond the last published one
+constexpr int kCons = 3;             // consumer waves
+
+struct FfnArgs {
+  const uint16_t* h;       // [4096] residual stream (the FFN's input and residual)
+  const uint16_t* norm_w;  // [4096] ffn_norm weight
+  float eps;
+  const uint32_t* w13;     // [2I][512] nibbles (row-stream layout), rows (w1_i, w3_i) interleaved
+  const uint32_t* sz13;    // [2I][128] (scale, zero) bf16 pairs, group size 32
+  const uint32_t* w2;      // [4096][I/8]
+  const uint32_t* sz2;     // [4096][I/32]
+  uint16_t* out;           // [4096] h + w2(swiglu(w13(rmsnorm(h))))
+  unsigned* ctl;           // [0] epoch (>= 1), [32] workgroups done (own cache line)
+  uint64_t* gran;          // [I/2] granules of the SwiGLU output
+  int inter;               // I (multiple of 2048)
+};
+
+__device__ __forceinline__ unsigned lds_ld(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// one 2048-k unit of one row for this lane: 16 B of nibbles (32 k), its (scale, zero) word and
+// the lane's 32 x values (16 bf16 pairs) with their sum sx: s (D - 136 sx) + z sx, D = sum x (128 + q)
+__device__ __forceinline__ float unit_dot(const uint4 w, uint32_t szw, const uint32_t (&x)[16],
+                                          float sx) {
+  const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+  float d = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d = dot2_bf16(x[4 * j + i], nib_pair_bf16(wd[j], i), d);
+  return fmaf(bf16lo_to_f32(szw), d - 136.f * sx, bf16hi_to_f32(szw) * sx);
+}
+
+__device__ __forceinline__ float pair_sum(const uint32_t (&x)[16]) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s = dot2_bf16(x[i], 0x3F803F80u, s);
+  return s;
+}
+
+template <int NS1, int NS2>
+__global__ __launch_bounds__(256, 1) void ffn_engine_kernel(FfnArgs a) {
+  __shared__ __attribute__((aligned(16))) uint4 ring[kRing * kSlotB / 16];
+  __shared__ unsigned full[kRing], freew[kRing], done_lds;
+  __shared__ float red[kCons][16];
+  constexpr int NSL = NS1 + NS2;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wg = blockIdx.x;
+  constexpr int kRows13 = NS1 * 8;   // w1||w3 rows of this workgroup
+  constexpr int kRows2 = 16;         // w2 rows of this workgroup
+  constexpr int kK2B = NS2 * 1024;   // bytes of one w2 row's nibbles (NS2 units of 2048 k)
+  constexpr int kS2B = NS2 * 256;    // bytes of one w2 row's (scale, zero) words
+
+  if (threadIdx.x < kRing) {
+    full[threadIdx.x] = 0u;
+    freew[threadIdx.x] = 0u;
+  }
+  if (threadIdx.x == 0) done_lds = 0u;
+  __syncthreads();  // the only workgroup barrier: the roles below never meet again
+
+  if (wave == 0) {
+    // ---------------------------------- loader ----------------------------------------------
+    const Rsrc r13 = make_rsrc(a.w13, (uint32_t)((size_t)kNWG * kRows13 * 2048));
+    const Rsrc rz13 = make_rsrc(a.sz13, (uint32_t)((size_t)kNWG * kRows13 * 512));
+    const Rsrc r2 = make_rsrc(a.w2, (uint32_t)((size_t)kNWG * kRows2 * kK2B));
+    const Rsrc rz2 = make_rsrc(a.sz2, (uint32_t)((size_t)kNWG * kRows2 * kS2B));
+    const uint32_t v16 = 16u * lane;
+    // phase-2 (scale, zero) pieces: 4 rows x 256 B per wave-instruction
+    const uint32_t vz2 = (uint32_t)(lane >> 4) * kS2B + 16u * (lane & 15);
+    const uint32_t base13 = (uint32_t)wg * kRows13;
+    const uint32_t base2 = (uint32_t)wg * kRows2;
+    auto issue = [&](int g) __attribute__((always_inline)) {
+      uint8_t* dst = reinterpret_cast<uint8_t*>(ring) + (g % kRing) * kSlotB;
+      if (g < NS1) {  // 8 rows x 2048 B contiguous, then their 8 x 512 B of words
+        const uint32_t r0 = base13 + 8u * g;
+#pragma unroll
+        for (int p = 0; p < 16; ++p)
+          dma_lds_ring<16, kNT>(r13, v16, r0 * 2048u + 1024u * p, dst + 1024 * p);
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+          dma_lds_ring<16, kNT>(rz13, v16, r0 * 512u + 1024u * p, dst + kScaleOff + 1024 * p);
+      } else {  // unit u of 16 rows: one 1 KiB piece per row, words 4 rows per piece
+        const uint32_t u = (uint32_t)(g - NS1);
+#pragma unroll
+        for (int p = 0; p < 16; ++p)
+          dma_lds_ring<16, kNT>(r2, v16, (base2 + p) * (uint32_t)kK2B + 1024u * u, dst + 1024 * p);
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+          dma_lds_ring<16, kNT>(rz2, vz2, (base2 + 4u * p) * (uint32_t)kS2B + 256u * u,
+                                dst + kScaleOff + 1024 * p);
+      }
+    };
+    for (int g = 0; g < NSL; ++g) {
+      if (g >= kRing) {  // slot g % kRing free again (consumer of slot g - kRing done reading)
+        SeamWait sw;
+        while (lds_ld(&freew[g % kRing]) != (unsigned)(g - kRing + 1)) {
+          if (sw.timed_out()) {
+            flag_decode_error(kDecodeErrSplitK);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      issue(g);
+      if (g >= kAhead) {  // slot g - kAhead has landed: kAhead slots' pieces may still be out
+        wait_vmcnt<kAhead * kPieces>();
+        lds_st(&full[(g - kAhead) % kRing], (unsigned)(g - kAhead + 1));
+      }
+    }
+    wait_vmcnt<kPieces>();
+    lds_st(&full[(NSL - 2) % kRing], (unsigned)(NSL - 1));
+    wait_vmcnt<0>();
+    lds_st(&full[(NSL - 1) % kRing], (unsigned)NSL);
+    return;
+  }
+
+  // ------------------------------------ consumers -------------------------------------------
+  const int c = wave - 1;
+  const unsigned epoch = a.ctl[0];
+  const uint8_t* ringb = reinterpret_cast<const uint8_t*>(ring);
+  auto wait_full = [&](int g) __attribute__((always_inline)) {
+    SeamWait sw;
+    while (lds_ld(&full[g % kRing]) != (unsigned)(g + 1)) {
+      if (sw.timed_out()) {
+        flag_decode_error(kDecodeErrSplitK);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+  };
+  auto release = [&](int g) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are back
+    if (lane == 0) lds_st(&freew[g % kRing], (unsigned)(g + 1));
+  };
+
+  // phase-1 input: x = bf16(bf16(h * r) * w), r = rsqrt(mean(h^2) + eps); lane l holds
+  // k = 32 l .. 32 l + 31 (unit 0) and 2048 + 32 l .. (unit 1)
+  uint32_t x1[2][16];
+  float sx1[2];
+  {
+    const uint4* hp = reinterpret_cast<const uint4*>(a.h);
+    const uint4* wp = reinterpret_cast<const uint4*>(a.norm_w);
+    uint4 hv[2][4], gv[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        hv[u][j] = hp[u * 256 + lane * 4 + j];
+        gv[u][j] = wp[u * 256 + lane * 4 + j];
+      }
+    float ss = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t d[4] = {hv[u][j].x, hv[u][j].y, hv[u][j].z, hv[u][j].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float lo = bf16lo_to_f32(d[i]), hi = bf16hi_to_f32(d[i]);
+          ss = fmaf(lo, lo, fmaf(hi, hi, ss));
+        }
+      }
+    ss = wave_sum(ss);
+    const float r = rsqrtf(ss / 4096.f + a.eps);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t d[4] = {hv[u][j].x, hv[u][j].y, hv[u][j].z, hv[u][j].w};
+        const uint32_t w[4] = {gv[u][j].x, gv[u][j].y, gv[u][j].z, gv[u][j].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float lo = round_bf16(bf16lo_to_f32(d[i]) * r) * bf16lo_to_f32(w[i]);
+          const float hi = round_bf16(bf16hi_to_f32(d[i]) * r) * bf16hi_to_f32(w[i]);
+          x1[u][4 * j + i] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+        }
+      }
+      sx1[u] = pair_sum(x1[u]);
+    }
+  }
+
+  // ---- phase 1: w1||w3 rows -> SwiGLU granules ----
+  for (int g = c; g < NS1; g += kCons) {
+    wait_full(g);
+    const uint8_t* sl = ringb + (g % kRing) * kSlotB;
+    float v[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      float acc = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint4 w = *reinterpret_cast<const uint4*>(sl + r * 2048 + u * 1024 + 16 * lane);
+        const uint32_t szw =
+            *reinterpret_cast<const uint32_t*>(sl + kScaleOff + r * 512 + u * 256 + 4 * lane);
+        acc += unit_dot(w, szw, x1[u], sx1[u]);
+      }
+      v[r] = acc;
+    }
+    release(g);
+    wave_reduce_scatter<8>(v, lane);  // v[0] = total of row lane >> 3
+    const float o = round_bf16(v[0]);
+    const int b = (lane & 1) * 32;    // lane 0: rows 0..3, lane 1: rows 4..7
+    const float a0 = __shfl(o, b), b0 = __shfl(o, b + 8), a1 = __shfl(o, b + 16),
+                b1 = __shfl(o, b + 24);
+    if (lane < 2) {
+      const uint32_t s0 = f32_to_bf16(round_bf16(a0 / (1.f + __expf(-a0))) * b0);
+      const uint32_t s1 = f32_to_bf16(round_bf16(a1 / (1.f + __expf(-a1))) * b1);
+      const size_t gi = (size_t)wg * (kRows13 / 4) + 2 * g + lane;
+      __hip_atomic_store(a.gran + gi, ((uint64_t)epoch << 32) | s0 | (s1 << 16),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+
+  // ---- phase 2: gather this consumer's units of the SwiGLU output, then w2 ----
+  // phase-2 slots g = NS1 + u; consumer c owns the units u with (NS1 + u) % 3 == c (<= 3 of 7)
+  constexpr int kMaxU = (NS2 + kCons - 1) / kCons;
+  const int u0 = ((c - NS1) % kCons + kCons) % kCons;  // first unit of this consumer
+  const int nu = u0 < NS2 ? (NS2 - u0 + kCons - 1) / kCons : 0;
+  uint32_t x2[kMaxU][16];
+  float sx2[kMaxU];
+  {
+    const Rsrc rg = make_rsrc(a.gran, (uint32_t)((size_t)a.inter * 4));
+    uint4 gv[kMaxU][8];
+    uint32_t pend = 0;
+#pragma unroll
+    for (int ui = 0; ui < kMaxU; ++ui)
+      if (ui < nu) pend |= 0xFFu << (8 * ui);
+    SeamWait sw;
+    while (true) {
+#pragma unroll
+      for (int ui = 0; ui < kMaxU; ++ui)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (pend & (1u << (8 * ui + i))) {
+            const int u = u0 + kCons * ui;
+            gv[ui][i] = bload16<kSC1>(rg, (uint32_t)(128 * lane + 16 * i), (uint32_t)(8192 * u));
+          }
+#pragma unroll
+      for (int ui = 0; ui < kMaxU; ++ui)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if ((pend & (1u << (8 * ui + i))) && gv[ui][i].y == epoch && gv[ui][i].w == epoch)
+            pend &= ~(1u << (8 * ui + i));
+      if (!__any(pend != 0u)) break;
+      if (sw.timed_out()) {
+        flag_decode_error(kDecodeErrSplitK);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+#pragma unroll
+    for (int ui = 0; ui < kMaxU; ++ui) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        x2[ui][2 * i] = gv[ui][i].x;
+        x2[ui][2 * i + 1] = gv[ui][i].z;
+      }
+      sx2[ui] = pair_sum(x2[ui]);
+    }
+  }
+  float acc2[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
+#pragma unroll
+  for (int ui = 0; ui < kMaxU; ++ui) {
+    if (ui < nu) {
+      const int g = NS1 + u0 + kCons * ui;
+      wait_full(g);
+      const uint8_t* sl = ringb + (g % kRing) * kSlotB;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint4 w = *reinterpret_cast<const uint4*>(sl + r * 1024 + 16 * lane);
+        const uint32_t szw =
+            *reinterpret_cast<const uint32_t*>(sl + kScaleOff + r * 256 + 4 * lane);
+        acc2[r] += unit_dot(w, szw, x2[ui], sx2[ui]);
+      }
+      release(g);
+    }
+  }
+  wave_reduce_scatter<16>(acc2, lane);  // acc2[0] = this wave's total of row lane >> 2
+  if ((lane & 3) == 0) red[c][lane >> 2] = acc2[0];
+  unsigned last = 0;
+  if (lane == 0) last = __hip_atomic_fetch_add(&done_lds, 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP) == kCons - 1;
+  last = __shfl(last, 0);
+  if (!last) return;
+  asm volatile("" ::: "memory");
+  if (lane < 16) {
+    const float t = (red[0][lane] + red[1][lane]) + red[2][lane];
+    const int n = wg * kRows2 + lane;
+    a.out[n] = f32_to_bf16(round_bf16(t) + bf16_to_f32(a.h[n]));
+  }
+  if (lane == 0) {  // epoch hand-over: the last workgroup out advances it for the next launch
+    const unsigned prev =
+        __hip_atomic_fetch_add(a.ctl + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == kNWG - 1) {
+      __hip_atomic_store(a.ctl + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.ctl, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace
+
+int ffn_engine_cus() {
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 0;
+    cus = n;
+  }
+  return cus;
+}
+
+}  // namespace tao
+
+extern "C" int tao_int4wo_ffn_engine_supported(int64_t dim, int64_t inter, int64_t group_size) {
+  return dim == 4096 && inter == 14336 && group_size == 32 && tao::ffn_engine_cus() >= tao::kNWG;
+}
+
+extern "C" int tao_int4wo_ffn_engine_bf16(const uint16_t* h, const uint16_t* norm_weight,
+                                          float eps, const uint32_t* w13, const uint16_t* sz13,
+                                          const uint32_t* w2, const uint16_t* sz2, uint16_t* out,
+                                          int64_t dim, int64_t inter, int64_t group_size,
+                                          unsigned* ctl, uint64_t* granules, void* stream) {
+  using namespace tao;
+  TAO_CHECK_ARG(h && norm_weight && w13 && sz13 && w2 && sz2 && out && ctl && granules,
+                "ffn engine: null operand");
+  TAO_CHECK_ARG(tao_int4wo_ffn_engine_supported(dim, inter, group_size),
+                "ffn engine: shape (dim %lld, inter %lld, g %lld) or device (%d CUs) unsupported",
+                (long long)dim, (long long)inter, (long long)group_size, ffn_engine_cus());
+  TAO_CHECK_ARG(out != h, "ffn engine: out must not alias h");
+  TAO_CHECK_ALIGN(h, 16, "h");
+  TAO_CHECK_ALIGN(norm_weight, 16, "norm_weight");
+  TAO_CHECK_ALIGN(w13, 16, "w13");
+  TAO_CHECK_ALIGN(sz13, 16, "sz13");
+  TAO_CHECK_ALIGN(w2, 16, "w2");
+  TAO_CHECK_ALIGN(sz2, 16, "sz2");
+  TAO_CHECK_ALIGN(granules, 16, "granules");
+  FfnArgs a{h, norm_weight, eps, w13, reinterpret_cast<const uint32_t*>(sz13), w2,
+            reinterpret_cast<const uint32_t*>(sz2), out, ctl, granules, (int)inter};
+  hipLaunchKernelGGL((ffn_engine_kernel<14, 7>), dim3(kNWG), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  return check_launch("ffn_engine_kernel");
+}
+
+// workspace: ctl (64 unsigned: epoch at [0] = 1, done counter at [32] = 0) + granules [inter/2]
+extern "C" int64_t tao_int4wo_ffn_engine_workspace_bytes(int64_t inter) {
+  return 256 + inter / 2 * 8;
+}

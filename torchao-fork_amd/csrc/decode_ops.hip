@@ -40,6 +40,7 @@ int int4gemv_decode_status(unsigned* bits);
 int sf_decode_status(unsigned* bits);
 int int8gemv_decode_status(unsigned* bits);
 int int8dyn_decode_status(unsigned* bits);
+int engine_decode_status(unsigned* bits);
 
 namespace {
 
@@ -935,6 +936,7 @@ extern "C" int tao_decode_status(int* bits) {
   if (rc == TAO_OK) rc = tao::int8gemv_decode_status(&v);
   if (rc == TAO_OK) rc = tao::int8dyn_decode_status(&v);
   if (rc == TAO_OK) rc = tao::sf_decode_status(&v);
+  if (rc == TAO_OK) rc = tao::engine_decode_status(&v);
   unsigned to = 0;  // split-K reducer timeouts of the single-fetch GEMMs (prefill)
   if (rc == TAO_OK) rc = tao_gemm_sf_status(&to);
   if (to != 0) v |= tao::kDecodeErrSplitK;

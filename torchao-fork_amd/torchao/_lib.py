@@ -107,6 +107,10 @@ _SIGNATURES = {
     "tao_int4wo_qkv_attn_supported": [_i64, _i64, _i64, _i64, _i64],
     "tao_int4wo_qkv_attn_bf16": [_p, _p, _p, _i64, _i64, _i64, _p, ctypes.c_float, _p, _p, _p,
                                  _p, _p, _p, _i64, _i64, _i64, _i64, ctypes.c_float, _i64, _p],
+    "tao_int4wo_ffn_engine_supported": [_i64, _i64, _i64],
+    "tao_int4wo_ffn_engine_workspace_bytes": [_i64],
+    "tao_int4wo_ffn_engine_bf16": [_p, _p, ctypes.c_float, _p, _p, _p, _p, _p, _i64, _i64, _i64,
+                                   _p, _p, _p],
     "tao_int4wo_decode_bf16": [_p, _p, _p, _i64, _i64, _i64, _p, ctypes.c_float, _int, _p, _p,
                                _p, _p, _p, _i64, _i64, _i64, _i64, _p],
     "tao_int8wo_decode_bf16": [_p, _p, _p, _i64, _i64, _p, ctypes.c_float, _int, _p, _p, _p, _p, _p,
@@ -115,7 +119,8 @@ _SIGNATURES = {
                                _i64, _i64, _i64, _i64, _p],
 }
 _RESTYPES = {"tao_version": ctypes.c_char_p, "tao_last_error": ctypes.c_char_p,
-             "tao_last_kernel": ctypes.c_char_p}
+             "tao_last_kernel": ctypes.c_char_p,
+             "tao_int4wo_ffn_engine_workspace_bytes": ctypes.c_int64}
 
 
 def library_path() -> str:

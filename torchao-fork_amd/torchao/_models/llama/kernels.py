@@ -394,6 +394,56 @@ def prologue_pays(N: int, K: int) -> bool:
     return K <= 4096 or N < 16384
 
 
+# Decode feed-forward (RMSNorm -> w1||w3 -> SwiGLU -> w2 -> + residual) in ONE persistent launch
+# on the LDS-DMA engine (tao_int4wo_ffn_engine_bf16, csrc/decode_engine.hip) instead of the two
+# fused GEMV launches, for int4 g32 at the shapes the engine serves (Llama-3-8B).
+DECODE_FFN_ENGINE = False
+_ENGINE_WS = {}
+
+
+def ffn_engine_supported(dim: int, inter: int, group_size: int) -> bool:
+    return bool(_lib.lib().tao_int4wo_ffn_engine_supported(dim, inter, group_size))
+
+
+def ffn_engine_workspace(device: torch.device) -> torch.Tensor:
+    """The engine's per-device workspace (epoch word + SwiGLU granules), created and initialised
+    once, eagerly: its epoch advances on the device with every launch (graph replays included),
+    so it must never be re-initialised by a captured op. Engine launches of one device must run
+    on one stream at a time."""
+    dev = torch.device(device)
+    ws = _ENGINE_WS.get(dev)
+    if ws is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("ffn engine: run once eagerly before graph capture (workspace)")
+        nbytes = int(_lib.lib().tao_int4wo_ffn_engine_workspace_bytes(65536))
+        ws = torch.zeros(nbytes // 4, dtype=torch.int32, device=dev)
+        ws[0] = 1
+        torch.cuda.synchronize(dev)
+        _ENGINE_WS[dev] = ws
+    return ws
+
+
+def int4_ffn_engine(h: torch.Tensor, norm_weight: torch.Tensor, eps: float, w13: tuple,
+                    w2: tuple) -> torch.Tensor:
+    """One token through a Llama FFN with its residual, out = h + w2(swiglu(w13(rmsnorm(h)))),
+    in one launch (tao_int4wo_ffn_engine_bf16). w13 / w2 = (packed, scale_and_zero, group_size)
+    of the fused (w1_i, w3_i) int4 linear and of w2."""
+    _check(h, torch.bfloat16, "ffn_engine h")
+    _check(norm_weight, torch.bfloat16, "ffn_engine norm_weight")
+    (p13, z13, g13), (p2, z2, g2) = w13, w2
+    dim = h.shape[-1]
+    inter = p13.shape[0] // 2
+    if h.numel() != dim or g13 != g2 or p2.shape[0] != dim:
+        raise RuntimeError("ffn_engine: one token, matching group sizes and shapes")
+    ws = ffn_engine_workspace(h.device)
+    out = torch.empty_like(h)
+    base = ws.data_ptr()
+    _lib.call("tao_int4wo_ffn_engine_bf16", h.data_ptr(), norm_weight.data_ptr(), float(eps),
+              p13.data_ptr(), z13.data_ptr(), p2.data_ptr(), z2.data_ptr(), out.data_ptr(), dim,
+              inter, int(g13), base, base + 256, _stream(h))
+    return out
+
+
 def int4_decode(x: torch.Tensor, packed: torch.Tensor, scale_and_zero: torch.Tensor,
                 group_size: int, norm_weight=None, eps: float = 0.0, epilogue: str = "none",
                 rope=None) -> torch.Tensor:

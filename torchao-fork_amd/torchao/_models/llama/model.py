@@ -427,6 +427,12 @@ class FeedForward(nn.Module):
     def forward_fused(self, x, residual, norm=None):
         from torchao._models.llama import kernels
 
+        if (kernels.DECODE_FFN_ENGINE and norm is not None and self.w13 is not None
+                and x.numel() == x.shape[-1] and residual is x):
+            p13, p2 = _int4_parts(self.w13), _int4_parts(self.w2)
+            if (p13 is not None and p2 is not None and p13[2] == p2[2]
+                    and kernels.ffn_engine_supported(x.shape[-1], p13[0].shape[0] // 2, p13[2])):
+                return kernels.int4_ffn_engine(x, norm.weight, norm.eps, p13, p2)
         if norm is not None:
             # RMSNorm -> w13 -> SwiGLU in one launch (int4 / int8 weight-only)
             g = None if self.w13 is None else _fused_decode(x, self.w13, norm, "swiglu")
