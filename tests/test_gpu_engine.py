@@ -99,7 +99,14 @@ def test_engine_matches_launch_path_and_oracle(ffn, scale):
     ab = (wd13 @ xn).reshape(-1, 2)
     sg = torch.nn.functional.silu(ab[:, 0]) * ab[:, 1]
     ref = hf + wd2 @ sg
-    assert _rel(out.float().reshape(-1) - hf, ref - hf) < 1e-2
+    # the block output against fp32 (bf16 output rounding included), and no worse than the
+    # launch path's own distance from it
+    e_eng, e_lp = _rel(out.float().reshape(-1), ref), _rel(out_ref.float().reshape(-1), ref)
+    assert e_eng < 1e-2 and e_eng <= 1.25 * e_lp + 1e-3, (e_eng, e_lp)
+    # the FFN branch alone (before the residual's rounding): same bar for both paths
+    ffn = wd2 @ sg
+    assert _rel(out.float().reshape(-1) - hf, ffn) <= 1.25 * _rel(out_ref.float().reshape(-1) - hf,
+                                                                  ffn) + 1e-3
     kernels.check_decode_status()
 
 
