@@ -198,9 +198,9 @@ int tao_int4wo_decode_bf16(const uint16_t* x, const uint32_t* packed,
  * its bias. w13 / sz13: the fused (w1_i, w3_i)-interleaved int4 linear [2 inter][dim/8] /
  * [2 inter][dim/32][2]; w2 / sz2: [dim][inter/8] / [dim][inter/32][2]; group size 32. The
  * summation order differs from the two launches (not bit-identical; within the oracle bars).
- * `ctl` / `granules`: a device workspace of tao_int4wo_ffn_engine_workspace_bytes(inter) bytes,
+ * `ctl` / `payload`: a device workspace of tao_int4wo_ffn_engine_workspace_bytes(inter) bytes,
  * zeroed, then ctl[0] = 1 (an epoch the kernel advances per launch; one workspace per stream,
- * shared by every layer). One workgroup per CU, all co-resident: shapes and devices
+ * shared by every layer); ctl is its first 2 KiB (128-B aligned), payload the rest. One workgroup per CU, all co-resident: shapes and devices
  * tao_int4wo_ffn_engine_supported() accepts (1 / 0, not a status); a timed-out in-launch wait
  * sets tao_decode_status bit 2. Replaces FeedForward.forward's w1 / w3 / silu / w2 around the
  * reference's int4 linears at decode (torchao/_models/llama/model.py:481-492). */
@@ -209,7 +209,7 @@ int64_t tao_int4wo_ffn_engine_workspace_bytes(int64_t inter);
 int tao_int4wo_ffn_engine_bf16(const uint16_t* h, const uint16_t* norm_weight, float eps,
                                const uint32_t* w13, const uint16_t* sz13, const uint32_t* w2,
                                const uint16_t* sz2, uint16_t* out, int64_t dim, int64_t inter,
-                               int64_t group_size, unsigned* ctl, uint64_t* granules,
+                               int64_t group_size, unsigned* ctl, uint32_t* payload,
                                void* stream);
 
 /* MoE decode: the A activated experts' int4 linears of one token in one launch. packed

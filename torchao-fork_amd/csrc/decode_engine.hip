@@ -8,24 +8,28 @@
 // linear), which the launch path runs as two launches (tao_int4wo_decode_bf16 with the RMSNorm
 // prologue and SwiGLU epilogue, then the w2 GEMV with the residual on its bias).
 //
-// Geometry: kNWG = 256 workgroups, one per CU (160 KiB LDS each: all resident), 4 waves:
+// Geometry: kNWG = 256 workgroups, one per CU (123 KiB LDS each: all resident), C + 1 waves:
 //   wave 0 (loader)    streams this CU's weight rows of BOTH linears, in order, into a ring of
 //                      kRing LDS slots with non-temporal LDS-DMA (buffer_load ... lds), kAhead
 //                      slots in flight; it never waits for an activation, so w2's rows stream in
 //                      while w1||w3's outputs are still being gathered (prefetch credit);
-//   waves 1..3         consume slots round-robin (slot g -> consumer g % 3):
+//   waves 1..C         consume slots round-robin (slot g -> consumer g % C; C = 7 consumer waves,
+//                      two per SIMD, or 3 with tao_tune_ffn_engine):
 //     phase 1  x = RMSNorm(h) held in registers (each consumer wave normalises the whole h,
 //              so no cross-wave exchange); a slot is 8 rows (4 (w1_i, w3_i) pairs) x 4096 k;
 //              per row the GEMV's lane math (v_dot2c_f32_bf16 on magic-number nibble pairs),
-//              a reduce-scatter, then SwiGLU -> 4 outputs = two 8-byte {tag, 2 x bf16}
-//              granules stored sc1 (MI355X_MICROARCH.md hand-off R2: the data is the flag);
-//     phase 2  a slot is 16 rows x one 2048-k unit of w2; a consumer gathers the SwiGLU outputs
-//              of ITS units straight into registers (16-B sc1 loads of granules, re-polled until
-//              every tag is this launch's epoch), accumulates its units' partial dot products,
-//              and the three consumers' partials meet in LDS (fixed order) -> + h -> out.
+//              a reduce-scatter, then SwiGLU -> 4 outputs stored sc1 (write-through);
+//     edge     every storing wave drains (vmcnt(0)) and counts itself in LDS; the last one adds
+//              the workgroup's arrival to one of 8 shard counters (agent-scope atomic). The
+//              counters only grow (32 arrivals per launch each), so a launch with epoch E waits
+//              for 32 E on all 8 (MI355X_MICROARCH.md hand-offs with sc1 loads, first row);
+//     phase 2  a slot is 16 rows x one 2048-k unit of w2; after the counters match, a consumer
+//              loads the SwiGLU outputs of ITS units with 16-B sc1 loads straight into registers,
+//              accumulates its units' partial dot products, and the consumers' partials meet in
+//              LDS (fixed order) -> + h -> out.
 // In-CU hand-offs are LDS words: FULL[slot] (loader, after a counted vmcnt wait) and FREE[slot]
-// (consumer, after its reads of the slot). The granule tag is a per-launch epoch kept on the
-// device (ctl[0]); the last workgroup out advances it, so HIP-graph replays need no reset.
+// (consumer, after its reads of the slot). The epoch lives on the device (ctl[0]); the last
+// workgroup out advances it, so HIP-graph replays need no reset.
 // Every wait is bounded (SeamWait): a timeout sets tao_decode_status bit 2 and the grid drains.
 #include "tao_common.h"
 #include "tao_reduce.h"
@@ -42,7 +46,8 @@ constexpr int kScaleOff = 16 * 1024;
 constexpr int kRing = 6;             // 120 KiB of ring
 constexpr int kPieces = 20;          // DMA wave-instructions per slot (1 KiB each)
 constexpr int kAhead = 2;            // slots in flight beyond the last published one
-constexpr int kCons = 3;             // consumer waves
+constexpr int kShards = 8;           // phase-1 arrival counters (workgroup wg -> shard wg % 8)
+constexpr int kShard0 = 64;          // word offset of shard 0 in ctl
 
 struct FfnArgs {
   const uint16_t* h;       // [4096] residual stream (the FFN's input and residual)
@@ -53,10 +58,21 @@ struct FfnArgs {
   const uint32_t* w2;      // [4096][I/8]
   const uint32_t* sz2;     // [4096][I/32]
   uint16_t* out;           // [4096] h + w2(swiglu(w13(rmsnorm(h))))
-  unsigned* ctl;           // [0] epoch (>= 1), [32] workgroups done (own cache line)
-  uint64_t* gran;          // [I/2] granules of the SwiGLU output
+  unsigned* ctl;           // [0] epoch (>= 1), [32] workgroups done, [kShard0 + 32 s] shard s
+                           // arrival counters (each on its own 128-B line)
+  uint32_t* pay;           // [I/2] the SwiGLU output, bf16 pairs
   int inter;               // I (multiple of 2048)
+  unsigned long long* stamps;  // measurement hook (tao_debug_ffn_engine_stamps), else null
 };
+
+__device__ __forceinline__ unsigned long long now() { return __builtin_amdgcn_s_memrealtime(); }
+// per workgroup 32 x u64 (lane 0 of the stamping wave): [0] loader entry, [1] last phase-1 slot
+// issued, [2] every slot issued, [3] last FULL, [4] loader time waiting on FREE; consumer c at
+// 8 + 6 c: [0] x normalised, [1] phase 1 done, [2] gather done, [3] phase 2 done, [4] end,
+// [5] time waiting on FULL
+__device__ __forceinline__ void stamp(const FfnArgs& a, int slot, unsigned long long v) {
+  if (a.stamps != nullptr && slot < 32 && (threadIdx.x & 63) == 0) a.stamps[blockIdx.x * 32 + slot] = v;
+}
 
 __device__ __forceinline__ unsigned lds_ld(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -85,10 +101,10 @@ __device__ __forceinline__ float pair_sum(const uint32_t (&x)[16]) {
   return s;
 }
 
-template <int NS1, int NS2>
-__global__ __launch_bounds__(256, 1) void ffn_engine_kernel(FfnArgs a) {
+template <int NS1, int NS2, int kCons>
+__global__ __launch_bounds__(64 * (kCons + 1), 1) void ffn_engine_kernel(FfnArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 ring[kRing * kSlotB / 16];
-  __shared__ unsigned full[kRing], freew[kRing], done_lds;
+  __shared__ unsigned full[kRing], freew[kRing], done_lds, p1_lds;
   __shared__ float red[kCons][16];
   constexpr int NSL = NS1 + NS2;
   const int lane = threadIdx.x & 63;
@@ -103,11 +119,16 @@ __global__ __launch_bounds__(256, 1) void ffn_engine_kernel(FfnArgs a) {
     full[threadIdx.x] = 0u;
     freew[threadIdx.x] = 0u;
   }
-  if (threadIdx.x == 0) done_lds = 0u;
+  if (threadIdx.x == 0) {
+    done_lds = 0u;
+    p1_lds = 0u;
+  }
   __syncthreads();  // the only workgroup barrier: the roles below never meet again
 
   if (wave == 0) {
     // ---------------------------------- loader ----------------------------------------------
+    stamp(a, 0, now());
+    unsigned long long t_free = 0;
     const Rsrc r13 = make_rsrc(a.w13, (uint32_t)((size_t)kNWG * kRows13 * 2048));
     const Rsrc rz13 = make_rsrc(a.sz13, (uint32_t)((size_t)kNWG * kRows13 * 512));
     const Rsrc r2 = make_rsrc(a.w2, (uint32_t)((size_t)kNWG * kRows2 * kK2B));
@@ -140,6 +161,7 @@ __global__ __launch_bounds__(256, 1) void ffn_engine_kernel(FfnArgs a) {
     };
     for (int g = 0; g < NSL; ++g) {
       if (g >= kRing) {  // slot g % kRing free again (consumer of slot g - kRing done reading)
+        const unsigned long long tw = a.stamps ? now() : 0;
         SeamWait sw;
         while (lds_ld(&freew[g % kRing]) != (unsigned)(g - kRing + 1)) {
           if (sw.timed_out()) {
@@ -148,17 +170,22 @@ __global__ __launch_bounds__(256, 1) void ffn_engine_kernel(FfnArgs a) {
           }
           __builtin_amdgcn_s_sleep(1);
         }
+        if (a.stamps) t_free += now() - tw;
       }
       issue(g);
+      if (g == NS1 - 1) stamp(a, 1, now());
       if (g >= kAhead) {  // slot g - kAhead has landed: kAhead slots' pieces may still be out
         wait_vmcnt<kAhead * kPieces>();
         lds_st(&full[(g - kAhead) % kRing], (unsigned)(g - kAhead + 1));
       }
     }
+    stamp(a, 2, now());
     wait_vmcnt<kPieces>();
     lds_st(&full[(NSL - 2) % kRing], (unsigned)(NSL - 1));
     wait_vmcnt<0>();
     lds_st(&full[(NSL - 1) % kRing], (unsigned)NSL);
+    stamp(a, 3, now());
+    stamp(a, 4, t_free);
     return;
   }
 
@@ -166,7 +193,9 @@ __global__ __launch_bounds__(256, 1) void ffn_engine_kernel(FfnArgs a) {
   const int c = wave - 1;
   const unsigned epoch = a.ctl[0];
   const uint8_t* ringb = reinterpret_cast<const uint8_t*>(ring);
+  unsigned long long t_full = 0;
   auto wait_full = [&](int g) __attribute__((always_inline)) {
+    const unsigned long long tw = a.stamps ? now() : 0;
     SeamWait sw;
     while (lds_ld(&full[g % kRing]) != (unsigned)(g + 1)) {
       if (sw.timed_out()) {
@@ -175,6 +204,7 @@ __global__ __launch_bounds__(256, 1) void ffn_engine_kernel(FfnArgs a) {
       }
       __builtin_amdgcn_s_sleep(1);
     }
+    if (a.stamps) t_full += now() - tw;
     asm volatile("" ::: "memory");
   };
   auto release = [&](int g) __attribute__((always_inline)) {
@@ -228,6 +258,7 @@ __global__ __launch_bounds__(256, 1) void ffn_engine_kernel(FfnArgs a) {
     }
   }
 
+  stamp(a, 8 + 6 * c, now());
   // ---- phase 1: w1||w3 rows -> SwiGLU granules ----
   for (int g = c; g < NS1; g += kCons) {
     wait_full(g);
@@ -255,58 +286,66 @@ __global__ __launch_bounds__(256, 1) void ffn_engine_kernel(FfnArgs a) {
       const uint32_t s0 = f32_to_bf16(round_bf16(a0 / (1.f + __expf(-a0))) * b0);
       const uint32_t s1 = f32_to_bf16(round_bf16(a1 / (1.f + __expf(-a1))) * b1);
       const size_t gi = (size_t)wg * (kRows13 / 4) + 2 * g + lane;
-      __hip_atomic_store(a.gran + gi, ((uint64_t)epoch << 32) | s0 | (s1 << 16),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.pay + gi, s0 | (s1 << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 
-  // ---- phase 2: gather this consumer's units of the SwiGLU output, then w2 ----
-  // phase-2 slots g = NS1 + u; consumer c owns the units u with (NS1 + u) % 3 == c (<= 3 of 7)
+  // publish: every storing wave drains its sc1 stores, counts itself in LDS, and the last of
+  // the workgroup's consumer waves adds the workgroup's arrival to its shard counter
+  // (MI355X_MICROARCH.md hand-offs with sc1 loads, first row: one signal per storing workgroup,
+  // sc1 payload stores and loads, the polling wave loads only after its poll matched)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  {
+    unsigned arrived = 0;
+    if (lane == 0)
+      arrived = __hip_atomic_fetch_add(&p1_lds, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    arrived = __shfl(arrived, 0);
+    if (arrived == kCons - 1 && lane == 0)
+      (void)__hip_atomic_fetch_add(a.ctl + kShard0 + 32 * (wg % kShards), 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  }
+  stamp(a, 9 + 6 * c, now());
+  // ---- phase 2: wait for every workgroup's SwiGLU outputs, load this consumer's units, w2 ----
+  // phase-2 slots g = NS1 + u; consumer c owns the units u with (NS1 + u) % kCons == c
   constexpr int kMaxU = (NS2 + kCons - 1) / kCons;
   const int u0 = ((c - NS1) % kCons + kCons) % kCons;  // first unit of this consumer
   const int nu = u0 < NS2 ? (NS2 - u0 + kCons - 1) / kCons : 0;
   uint32_t x2[kMaxU][16];
   float sx2[kMaxU];
   {
-    const Rsrc rg = make_rsrc(a.gran, (uint32_t)((size_t)a.inter * 4));
-    uint4 gv[kMaxU][8];
-    uint32_t pend = 0;
-#pragma unroll
-    for (int ui = 0; ui < kMaxU; ++ui)
-      if (ui < nu) pend |= 0xFFu << (8 * ui);
+    // the shard counters only grow: kNWG / kShards arrivals per launch, so this launch's are
+    // complete at (kNWG / kShards) x epoch
+    const unsigned need = (unsigned)(kNWG / kShards) * epoch;
     SeamWait sw;
     while (true) {
-#pragma unroll
-      for (int ui = 0; ui < kMaxU; ++ui)
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (pend & (1u << (8 * ui + i))) {
-            const int u = u0 + kCons * ui;
-            gv[ui][i] = bload16<kSC1>(rg, (uint32_t)(128 * lane + 16 * i), (uint32_t)(8192 * u));
-          }
-#pragma unroll
-      for (int ui = 0; ui < kMaxU; ++ui)
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if ((pend & (1u << (8 * ui + i))) && gv[ui][i].y == epoch && gv[ui][i].w == epoch)
-            pend &= ~(1u << (8 * ui + i));
-      if (!__any(pend != 0u)) break;
+      bool ok = true;
+      if (lane < kShards)
+        ok = __hip_atomic_load(a.ctl + kShard0 + 32 * lane, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT) >= need;
+      if (__all(ok)) break;
       if (sw.timed_out()) {
         flag_decode_error(kDecodeErrSplitK);
         break;
       }
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(1);
     }
+    asm volatile("" ::: "memory");
+    const Rsrc rp = make_rsrc(a.pay, (uint32_t)((size_t)a.inter * 2));
 #pragma unroll
     for (int ui = 0; ui < kMaxU; ++ui) {
+      const int u = ui < nu ? u0 + kCons * ui : u0;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        x2[ui][2 * i] = gv[ui][i].x;
-        x2[ui][2 * i + 1] = gv[ui][i].z;
+      for (int i = 0; i < 4; ++i) {
+        const uint4 v = bload16<kSC1>(rp, (uint32_t)(64 * lane + 16 * i), (uint32_t)(4096 * u));
+        x2[ui][4 * i] = v.x;
+        x2[ui][4 * i + 1] = v.y;
+        x2[ui][4 * i + 2] = v.z;
+        x2[ui][4 * i + 3] = v.w;
       }
       sx2[ui] = pair_sum(x2[ui]);
     }
   }
+  stamp(a, 10 + 6 * c, now());
   float acc2[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
@@ -326,16 +365,23 @@ __global__ __launch_bounds__(256, 1) void ffn_engine_kernel(FfnArgs a) {
       release(g);
     }
   }
+  stamp(a, 11 + 6 * c, now());
+  stamp(a, 13 + 6 * c, t_full);
   wave_reduce_scatter<16>(acc2, lane);  // acc2[0] = this wave's total of row lane >> 2
   if ((lane & 3) == 0) red[c][lane >> 2] = acc2[0];
   unsigned last = 0;
   if (lane == 0) last = __hip_atomic_fetch_add(&done_lds, 1u, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP) == kCons - 1;
   last = __shfl(last, 0);
-  if (!last) return;
+  if (!last) {
+    stamp(a, 12 + 6 * c, now());
+    return;
+  }
   asm volatile("" ::: "memory");
   if (lane < 16) {
-    const float t = (red[0][lane] + red[1][lane]) + red[2][lane];
+    float t = red[0][lane];
+#pragma unroll
+    for (int k = 1; k < kCons; ++k) t += red[k][lane];
     const int n = wg * kRows2 + lane;
     a.out[n] = f32_to_bf16(round_bf16(t) + bf16_to_f32(a.h[n]));
   }
@@ -347,6 +393,7 @@ __global__ __launch_bounds__(256, 1) void ffn_engine_kernel(FfnArgs a) {
       __hip_atomic_store(a.ctl, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  stamp(a, 12 + 6 * c, now());
 }
 
 }  // namespace
@@ -365,6 +412,24 @@ int ffn_engine_cus() {
 
 }  // namespace tao
 
+static unsigned long long* g_engine_stamps = nullptr;
+static int g_engine_consumers = 7;
+
+// A/B knob: consumer waves per workgroup (3: 256-thread workgroups, one consumer per SIMD
+// beside the loader's; 7: 512 threads, two per SIMD)
+extern "C" int tao_tune_ffn_engine(int consumers) {
+  TAO_CHECK_ARG(consumers == 3 || consumers == 7, "tune: ffn engine consumers must be 3 or 7");
+  g_engine_consumers = consumers;
+  return TAO_OK;
+}
+
+// measurement hook: per-workgroup phase stamps of the following engine launches into `buf`
+// (256 x 32 u64 device memory; NULL turns it off)
+extern "C" int tao_debug_ffn_engine_stamps(void* buf) {
+  g_engine_stamps = reinterpret_cast<unsigned long long*>(buf);
+  return TAO_OK;
+}
+
 extern "C" int tao_int4wo_ffn_engine_supported(int64_t dim, int64_t inter, int64_t group_size) {
   return dim == 4096 && inter == 14336 && group_size == 32 && tao::ffn_engine_cus() >= tao::kNWG;
 }
@@ -373,9 +438,9 @@ extern "C" int tao_int4wo_ffn_engine_bf16(const uint16_t* h, const uint16_t* nor
                                           float eps, const uint32_t* w13, const uint16_t* sz13,
                                           const uint32_t* w2, const uint16_t* sz2, uint16_t* out,
                                           int64_t dim, int64_t inter, int64_t group_size,
-                                          unsigned* ctl, uint64_t* granules, void* stream) {
+                                          unsigned* ctl, uint32_t* payload, void* stream) {
   using namespace tao;
-  TAO_CHECK_ARG(h && norm_weight && w13 && sz13 && w2 && sz2 && out && ctl && granules,
+  TAO_CHECK_ARG(h && norm_weight && w13 && sz13 && w2 && sz2 && out && ctl && payload,
                 "ffn engine: null operand");
   TAO_CHECK_ARG(tao_int4wo_ffn_engine_supported(dim, inter, group_size),
                 "ffn engine: shape (dim %lld, inter %lld, g %lld) or device (%d CUs) unsupported",
@@ -387,15 +452,22 @@ extern "C" int tao_int4wo_ffn_engine_bf16(const uint16_t* h, const uint16_t* nor
   TAO_CHECK_ALIGN(sz13, 16, "sz13");
   TAO_CHECK_ALIGN(w2, 16, "w2");
   TAO_CHECK_ALIGN(sz2, 16, "sz2");
-  TAO_CHECK_ALIGN(granules, 16, "granules");
+  TAO_CHECK_ALIGN(payload, 16, "payload");
+  TAO_CHECK_ALIGN(ctl, 128, "ctl");
   FfnArgs a{h, norm_weight, eps, w13, reinterpret_cast<const uint32_t*>(sz13), w2,
-            reinterpret_cast<const uint32_t*>(sz2), out, ctl, granules, (int)inter};
-  hipLaunchKernelGGL((ffn_engine_kernel<14, 7>), dim3(kNWG), dim3(256), 0,
-                     (hipStream_t)stream, a);
+            reinterpret_cast<const uint32_t*>(sz2), out, ctl, payload, (int)inter,
+            g_engine_stamps};
+  if (g_engine_consumers == 3)
+    hipLaunchKernelGGL((ffn_engine_kernel<14, 7, 3>), dim3(kNWG), dim3(256), 0,
+                       (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL((ffn_engine_kernel<14, 7, 7>), dim3(kNWG), dim3(512), 0,
+                       (hipStream_t)stream, a);
   return check_launch("ffn_engine_kernel");
 }
 
-// workspace: ctl (64 unsigned: epoch at [0] = 1, done counter at [32] = 0) + granules [inter/2]
+// workspace: ctl (2 KiB: epoch at word 0 = 1, done counter at 32, shard counters at 64 + 32 s,
+// all zero otherwise) + the SwiGLU payload [inter / 2] u32
 extern "C" int64_t tao_int4wo_ffn_engine_workspace_bytes(int64_t inter) {
-  return 256 + inter / 2 * 8;
+  return 2048 + inter / 2 * 4;
 }

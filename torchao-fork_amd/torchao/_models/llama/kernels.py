@@ -406,7 +406,7 @@ def ffn_engine_supported(dim: int, inter: int, group_size: int) -> bool:
 
 
 def ffn_engine_workspace(device: torch.device) -> torch.Tensor:
-    """The engine's per-device workspace (epoch word + SwiGLU granules), created and initialised
+    """The engine's per-device workspace (epoch word, arrival counters, SwiGLU payload), created and initialised
     once, eagerly: its epoch advances on the device with every launch (graph replays included),
     so it must never be re-initialised by a captured op. Engine launches of one device must run
     on one stream at a time."""
@@ -440,7 +440,7 @@ def int4_ffn_engine(h: torch.Tensor, norm_weight: torch.Tensor, eps: float, w13:
     base = ws.data_ptr()
     _lib.call("tao_int4wo_ffn_engine_bf16", h.data_ptr(), norm_weight.data_ptr(), float(eps),
               p13.data_ptr(), z13.data_ptr(), p2.data_ptr(), z2.data_ptr(), out.data_ptr(), dim,
-              inter, int(g13), base, base + 256, _stream(h))
+              inter, int(g13), base, base + 2048, _stream(h))
     return out
 
 
