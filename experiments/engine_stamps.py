@@ -29,6 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--consumers", type=int, default=7)
+    ap.add_argument("--dq", type=int, default=1)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     layers = []
@@ -37,9 +38,9 @@ def main():
         p2 = bench.make_int4_weight(DIM, INTER, G, seed=10 * i + 2, device=dev)
         layers.append((p13 + (G,), p2 + (G,), (torch.rand(DIM, device=dev) + 0.5).to(torch.bfloat16)))
     x0 = torch.randn(1, 1, DIM, device=dev, dtype=torch.bfloat16)
-    st = torch.zeros(256 * 32, dtype=torch.int64, device=dev)
+    st = torch.zeros(256 * 64, dtype=torch.int64, device=dev)
     lib = _lib.lib()
-    assert lib.tao_tune_ffn_engine(args.consumers) == 0
+    assert lib.tao_tune_ffn_engine(args.consumers, args.dq) == 0
 
     def chain(x):
         for (p13, p2, nw) in layers:
@@ -62,17 +63,17 @@ def main():
         st.zero_()
         graph.replay()
         torch.cuda.synchronize()
-        t = st.view(256, 32).cpu().double()
+        t = st.view(256, 64).cpu().double()
         t0 = t[:, 0].min()
         us = lambda col: [(float(v) - float(t0)) / 100.0 for v in t[:, col]]  # noqa: E731
         dur = lambda col: [float(v) / 100.0 for v in t[:, col]]  # noqa: E731
         rec = {"loader_entry": q(us(0)), "loader_p1_issued": q(us(1)), "loader_all_issued": q(us(2)),
                "loader_last_full": q(us(3)), "loader_free_wait": q(dur(4))}
-        for c in range(3):
+        for c in range(args.consumers):
             b = 8 + 6 * c
             rec[f"c{c}"] = {"norm": q(us(b)), "p1_done": q(us(b + 1)), "gather_done": q(us(b + 2)),
                             "p2_done": q(us(b + 3)), "end": q(us(b + 4)), "full_wait": q(dur(b + 5))}
-        rec["end_max"] = round(max(max(us(8 + 6 * c + 4)) for c in range(3)), 3)
+        rec["end_max"] = round(max(max(us(8 + 6 * c + 4)) for c in range(args.consumers)), 3)
         out[f"rep{rep}"] = rec
     print(json.dumps(out), flush=True)
     kernels.check_decode_status()

@@ -28,7 +28,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--consumers", type=int, nargs="*", default=[7, 3])
+    ap.add_argument("--configs", nargs="*", default=["7:1", "7:0", "3:1"],
+                    help="consumers:decode pairs (tao_tune_ffn_engine)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     L = args.layers
@@ -84,18 +85,20 @@ def main():
         del gl
         res[f"launch_us_per_layer_{rnd}"] = round(lu, 3)
         best["launch"] = min(best.get("launch", 1e9), lu)
-        for nc in args.consumers:
-            assert lib.tao_tune_ffn_engine(nc) == 0
+        for cfg in args.configs:
+            nc, dq = (int(v) for v in cfg.split(":"))
+            assert lib.tao_tune_ffn_engine(nc, dq) == 0
             eu, eout, ge = timed(engine_chain)
             del ge
-            res[f"engine{nc}_us_per_layer_{rnd}"] = round(eu, 3)
-            best[nc] = min(best.get(nc, 1e9), eu)
-    assert lib.tao_tune_ffn_engine(args.consumers[0]) == 0
+            res[f"engine{nc}_{dq}_us_per_layer_{rnd}"] = round(eu, 3)
+            best[cfg] = min(best.get(cfg, 1e9), eu)
+    nc, dq = (int(v) for v in args.configs[0].split(":"))
+    assert lib.tao_tune_ffn_engine(nc, dq) == 0
     eout = engine_chain(x0)
-    for nc in args.consumers:
-        res[f"engine{nc}_us_per_layer"] = round(best[nc], 3)
+    for cfg in args.configs:
+        res[f"engine{cfg}_us_per_layer"] = round(best[cfg], 3)
     lu = best["launch"]
-    eu = min(best[nc] for nc in args.consumers)
+    eu = min(best[cfg] for cfg in args.configs)
     res.update({"launch_us_per_layer": lu, "engine_us_per_layer": eu,
                 "engine_over_launch": round(eu / lu, 4),
                 "launch_GBps": round(nbytes / (lu * 1e-6) / 1e9, 1),

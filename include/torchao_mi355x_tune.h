@@ -142,12 +142,13 @@ int tao_debug_sf_late_publisher(int on);
 int tao_gemm_sf_status(unsigned* bits);
 
 /* Measurement hook (experiments/engine_stamps.py): the following tao_int4wo_ffn_engine_bf16
- * launches of this process write per-workgroup phase stamps (s_memrealtime, 100 MHz; 32 u64 per
- * workgroup, layout in csrc/decode_engine.hip) into `buf` (>= 256 x 32 x 8 bytes of device
+ * launches of this process write per-workgroup phase stamps (s_memrealtime, 100 MHz; 64 u64 per
+ * workgroup, layout in csrc/decode_engine.hip) into `buf` (>= 256 x 64 x 8 bytes of device
  * memory); NULL turns it off. */
 int tao_debug_ffn_engine_stamps(void* buf);
-/* A/B knob: consumer waves per workgroup of the decode FFN engine, 3 or 7 (built-in). */
-int tao_tune_ffn_engine(int consumers);
+/* A/B knobs of the decode FFN engine: consumer waves per workgroup (3 or 7, built-in 7) and the
+ * nibble decode (0 shift + and + or, 1 byte permutes, built-in 1). */
+int tao_tune_ffn_engine(int consumers, int dq);
 /* Measurement kernel (bench.py, not the product path): a pure streaming read of `bytes` (a
  * positive multiple of 8192) from `buf` (16-B aligned) with 16-B non-temporal loads; `sink` is
  * >= 4 KiB of device memory the kernel may write (it never does in practice). Graph-capturable. */

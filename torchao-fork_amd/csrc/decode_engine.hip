@@ -43,7 +43,7 @@ namespace {
 constexpr int kNWG = 256;            // one workgroup per CU
 constexpr int kSlotB = 20 * 1024;    // slot: 16 KiB of nibbles + 4 KiB of (scale, zero) words
 constexpr int kScaleOff = 16 * 1024;
-constexpr int kRing = 6;             // 120 KiB of ring
+constexpr int kRing = 7;             // 140 KiB of ring: w2's 7 slots all fit behind w1||w3's
 constexpr int kPieces = 20;          // DMA wave-instructions per slot (1 KiB each)
 constexpr int kAhead = 2;            // slots in flight beyond the last published one
 constexpr int kShards = 8;           // phase-1 arrival counters (workgroup wg -> shard wg % 8)
@@ -63,15 +63,16 @@ struct FfnArgs {
   uint32_t* pay;           // [I/2] the SwiGLU output, bf16 pairs
   int inter;               // I (multiple of 2048)
   unsigned long long* stamps;  // measurement hook (tao_debug_ffn_engine_stamps), else null
+  uint32_t nib_mask, nib_magic;  // 0x000F000F, 0x43004300 (see NibConst)
 };
 
 __device__ __forceinline__ unsigned long long now() { return __builtin_amdgcn_s_memrealtime(); }
-// per workgroup 32 x u64 (lane 0 of the stamping wave): [0] loader entry, [1] last phase-1 slot
+// per workgroup 64 x u64 (lane 0 of the stamping wave): [0] loader entry, [1] last phase-1 slot
 // issued, [2] every slot issued, [3] last FULL, [4] loader time waiting on FREE; consumer c at
 // 8 + 6 c: [0] x normalised, [1] phase 1 done, [2] gather done, [3] phase 2 done, [4] end,
 // [5] time waiting on FULL
 __device__ __forceinline__ void stamp(const FfnArgs& a, int slot, unsigned long long v) {
-  if (a.stamps != nullptr && slot < 32 && (threadIdx.x & 63) == 0) a.stamps[blockIdx.x * 32 + slot] = v;
+  if (a.stamps != nullptr && slot < 64 && (threadIdx.x & 63) == 0) a.stamps[blockIdx.x * 64 + slot] = v;
 }
 
 __device__ __forceinline__ unsigned lds_ld(const unsigned* p) {
@@ -83,14 +84,51 @@ __device__ __forceinline__ void lds_st(unsigned* p, unsigned v) {
 
 // one 2048-k unit of one row for this lane: 16 B of nibbles (32 k), its (scale, zero) word and
 // the lane's 32 x values (16 bf16 pairs) with their sum sx: s (D - 136 sx) + z sx, D = sum x (128 + q)
-__device__ __forceinline__ float unit_dot(const uint4 w, uint32_t szw, const uint32_t (&x)[16],
-                                          float sx) {
+// The magic-number pair of nibble pair i of a word, ((w >> 4 i) & 0x000F000F) | 0x43004300, is one
+// v_and_or_b32 (mask in an SGPR, magic in a VGPR: a VOP3 takes no literal here) after the shift:
+// 7 VALU per 8 weights before the 4 dot2s instead of 11 (the engine's consumers are VALU-bound;
+// same bits as nib_pair_bf16, so the same results)
+struct NibConst {
+  uint32_t mask, magic;
+  // the constants come in as kernel arguments (0x000F000F, 0x43004300), opaque to the compiler,
+  // so it cannot fold them into literals (it still splits the and-or into two VOP2s)
+  __device__ __forceinline__ NibConst(uint32_t m, uint32_t g) : mask(m), magic(g) {}
+  __device__ __forceinline__ uint32_t pair(uint32_t t) const { return (t & mask) | magic; }
+};
+
+// DQ 0: the four magic-number pairs of a word by shift + and + or (11 VALU per 8 weights before
+// the dot2s). DQ 1: byte permutes: lo = w & 0x0F0F0F0F holds q0, q4, q1, q5 in its bytes and
+// hi = (w >> 4) & 0x0F0F0F0F holds q2, q6, q3, q7; v_perm_b32 puts two of them under 0x43 bytes,
+// [q_a, 0x43, q_b, 0x43] = the bf16 pair (128 + q_a, 128 + q_b): 7 VALU per 8 weights, the same
+// bits as DQ 0.
+template <int DQ>
+__device__ __forceinline__ void nib_pairs(const NibConst& nc, uint32_t w, uint32_t (&p)[4]) {
+  if constexpr (DQ == 0) {
+    p[0] = nc.pair(w);
+    p[1] = nc.pair(w >> 4);
+    p[2] = nc.pair(w >> 8);
+    p[3] = nc.pair(w >> 12);
+  } else {
+    const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
+    p[0] = __builtin_amdgcn_perm(0x43434343u, lo, 0x04020400u);
+    p[1] = __builtin_amdgcn_perm(0x43434343u, hi, 0x04020400u);
+    p[2] = __builtin_amdgcn_perm(0x43434343u, lo, 0x04030401u);
+    p[3] = __builtin_amdgcn_perm(0x43434343u, hi, 0x04030401u);
+  }
+}
+
+template <int DQ>
+__device__ __forceinline__ float unit_dot(const NibConst& nc, const uint4 w, uint32_t szw,
+                                          const uint32_t (&x)[16], float sx) {
   const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
   float d = 0.f;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < 4; ++j) {
+    uint32_t p[4];
+    nib_pairs<DQ>(nc, wd[j], p);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) d = dot2_bf16(x[4 * j + i], nib_pair_bf16(wd[j], i), d);
+    for (int i = 0; i < 4; ++i) d = dot2_bf16(x[4 * j + i], p[i], d);
+  }
   return fmaf(bf16lo_to_f32(szw), d - 136.f * sx, bf16hi_to_f32(szw) * sx);
 }
 
@@ -101,10 +139,11 @@ __device__ __forceinline__ float pair_sum(const uint32_t (&x)[16]) {
   return s;
 }
 
-template <int NS1, int NS2, int kCons>
-__global__ __launch_bounds__(64 * (kCons + 1), 1) void ffn_engine_kernel(FfnArgs a) {
+template <int NS1, int NS2, int kCons, int DQ>
+__global__ __launch_bounds__(64 * (kCons + 1), 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void
+ffn_engine_kernel(FfnArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 ring[kRing * kSlotB / 16];
-  __shared__ unsigned full[kRing], freew[kRing], done_lds, p1_lds;
+  __shared__ unsigned full[kRing], freew[kRing], done_lds, p1_lds, p2go;
   __shared__ float red[kCons][16];
   constexpr int NSL = NS1 + NS2;
   const int lane = threadIdx.x & 63;
@@ -122,6 +161,7 @@ __global__ __launch_bounds__(64 * (kCons + 1), 1) void ffn_engine_kernel(FfnArgs
   if (threadIdx.x == 0) {
     done_lds = 0u;
     p1_lds = 0u;
+    p2go = 0u;
   }
   __syncthreads();  // the only workgroup barrier: the roles below never meet again
 
@@ -191,6 +231,7 @@ __global__ __launch_bounds__(64 * (kCons + 1), 1) void ffn_engine_kernel(FfnArgs
 
   // ------------------------------------ consumers -------------------------------------------
   const int c = wave - 1;
+  const NibConst nc(a.nib_mask, a.nib_magic);
   const unsigned epoch = a.ctl[0];
   const uint8_t* ringb = reinterpret_cast<const uint8_t*>(ring);
   unsigned long long t_full = 0;
@@ -260,23 +301,29 @@ __global__ __launch_bounds__(64 * (kCons + 1), 1) void ffn_engine_kernel(FfnArgs
 
   stamp(a, 8 + 6 * c, now());
   // ---- phase 1: w1||w3 rows -> SwiGLU granules ----
+#pragma unroll 1
   for (int g = c; g < NS1; g += kCons) {
     wait_full(g);
     const uint8_t* sl = ringb + (g % kRing) * kSlotB;
+    // the slot's 8 rows x 2 units into registers, then the slot is released before the
+    // arithmetic: a slot is held for its landing plus one LDS pass, not for the dot products
+    uint4 w[8][2];
+    uint32_t szw[8][2];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        w[r][u] = *reinterpret_cast<const uint4*>(sl + r * 2048 + u * 1024 + 16 * lane);
+        szw[r][u] =
+            *reinterpret_cast<const uint32_t*>(sl + kScaleOff + r * 512 + u * 256 + 4 * lane);
+      }
+    release(g);
     float v[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      float acc = 0.f;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const uint4 w = *reinterpret_cast<const uint4*>(sl + r * 2048 + u * 1024 + 16 * lane);
-        const uint32_t szw =
-            *reinterpret_cast<const uint32_t*>(sl + kScaleOff + r * 512 + u * 256 + 4 * lane);
-        acc += unit_dot(w, szw, x1[u], sx1[u]);
-      }
-      v[r] = acc;
+      v[r] = unit_dot<DQ>(nc, w[r][0], szw[r][0], x1[0], sx1[0]) +
+             unit_dot<DQ>(nc, w[r][1], szw[r][1], x1[1], sx1[1]);
     }
-    release(g);
     wave_reduce_scatter<8>(v, lane);  // v[0] = total of row lane >> 3
     const float o = round_bf16(v[0]);
     const int b = (lane & 1) * 32;    // lane 0: rows 0..3, lane 1: rows 4..7
@@ -295,12 +342,13 @@ __global__ __launch_bounds__(64 * (kCons + 1), 1) void ffn_engine_kernel(FfnArgs
   // (MI355X_MICROARCH.md hand-offs with sc1 loads, first row: one signal per storing workgroup,
   // sc1 payload stores and loads, the polling wave loads only after its poll matched)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bool signaller;
   {
     unsigned arrived = 0;
     if (lane == 0)
       arrived = __hip_atomic_fetch_add(&p1_lds, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    arrived = __shfl(arrived, 0);
-    if (arrived == kCons - 1 && lane == 0)
+    signaller = __shfl(arrived, 0) == kCons - 1;
+    if (signaller && lane == 0)
       (void)__hip_atomic_fetch_add(a.ctl + kShard0 + 32 * (wg % kShards), 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -313,21 +361,34 @@ __global__ __launch_bounds__(64 * (kCons + 1), 1) void ffn_engine_kernel(FfnArgs
   uint32_t x2[kMaxU][16];
   float sx2[kMaxU];
   {
-    // the shard counters only grow: kNWG / kShards arrivals per launch, so this launch's are
-    // complete at (kNWG / kShards) x epoch
-    const unsigned need = (unsigned)(kNWG / kShards) * epoch;
+    // ONE poller per workgroup (the wave that signalled it) reads the 8 shard counters, sleeping
+    // ~0.2 us between polls; the counters only grow (kNWG / kShards arrivals per launch), so this
+    // launch's are complete at (kNWG / kShards) x epoch. It then sets an LDS word the other
+    // consumer waves poll (the table row's "after an LDS word it then sets").
     SeamWait sw;
-    while (true) {
-      bool ok = true;
-      if (lane < kShards)
-        ok = __hip_atomic_load(a.ctl + kShard0 + 32 * lane, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT) >= need;
-      if (__all(ok)) break;
-      if (sw.timed_out()) {
-        flag_decode_error(kDecodeErrSplitK);
-        break;
+    if (signaller) {
+      const unsigned need = (unsigned)(kNWG / kShards) * epoch;
+      while (true) {
+        bool ok = true;
+        if (lane < kShards)
+          ok = __hip_atomic_load(a.ctl + kShard0 + 32 * lane, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT) >= need;
+        if (__all(ok)) break;
+        if (sw.timed_out()) {
+          flag_decode_error(kDecodeErrSplitK);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
       }
-      __builtin_amdgcn_s_sleep(1);
+      if (lane == 0) lds_st(&p2go, 1u);
+    } else {
+      while (lds_ld(&p2go) == 0u) {
+        if (sw.timed_out()) {
+          flag_decode_error(kDecodeErrSplitK);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
     }
     asm volatile("" ::: "memory");
     const Rsrc rp = make_rsrc(a.pay, (uint32_t)((size_t)a.inter * 2));
@@ -355,12 +416,13 @@ __global__ __launch_bounds__(64 * (kCons + 1), 1) void ffn_engine_kernel(FfnArgs
       const int g = NS1 + u0 + kCons * ui;
       wait_full(g);
       const uint8_t* sl = ringb + (g % kRing) * kSlotB;
+      // computed straight from LDS: with kRing = 7 the phase-2 slots never wait for one another,
+      // so holding the slot through the arithmetic delays nothing
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const uint4 w = *reinterpret_cast<const uint4*>(sl + r * 1024 + 16 * lane);
-        const uint32_t szw =
-            *reinterpret_cast<const uint32_t*>(sl + kScaleOff + r * 256 + 4 * lane);
-        acc2[r] += unit_dot(w, szw, x2[ui], sx2[ui]);
+        const uint32_t szw = *reinterpret_cast<const uint32_t*>(sl + kScaleOff + r * 256 + 4 * lane);
+        acc2[r] += unit_dot<DQ>(nc, w, szw, x2[ui], sx2[ui]);
       }
       release(g);
     }
@@ -414,12 +476,16 @@ int ffn_engine_cus() {
 
 static unsigned long long* g_engine_stamps = nullptr;
 static int g_engine_consumers = 7;
+static int g_engine_dq = 1;
 
-// A/B knob: consumer waves per workgroup (3: 256-thread workgroups, one consumer per SIMD
-// beside the loader's; 7: 512 threads, two per SIMD)
-extern "C" int tao_tune_ffn_engine(int consumers) {
+// A/B knobs: consumer waves per workgroup (3: 256-thread workgroups, one consumer per SIMD
+// beside the loader's; 7: 512 threads, two per SIMD) and the nibble decode (0: shift, and, or;
+// 1: byte permutes)
+extern "C" int tao_tune_ffn_engine(int consumers, int dq) {
   TAO_CHECK_ARG(consumers == 3 || consumers == 7, "tune: ffn engine consumers must be 3 or 7");
+  TAO_CHECK_ARG(dq == 0 || dq == 1, "tune: ffn engine decode must be 0 or 1");
   g_engine_consumers = consumers;
+  g_engine_dq = dq;
   return TAO_OK;
 }
 
@@ -456,12 +522,19 @@ extern "C" int tao_int4wo_ffn_engine_bf16(const uint16_t* h, const uint16_t* nor
   TAO_CHECK_ALIGN(ctl, 128, "ctl");
   FfnArgs a{h, norm_weight, eps, w13, reinterpret_cast<const uint32_t*>(sz13), w2,
             reinterpret_cast<const uint32_t*>(sz2), out, ctl, payload, (int)inter,
-            g_engine_stamps};
-  if (g_engine_consumers == 3)
-    hipLaunchKernelGGL((ffn_engine_kernel<14, 7, 3>), dim3(kNWG), dim3(256), 0,
+            g_engine_stamps, 0x000F000Fu, 0x43004300u};
+  const int nc = g_engine_consumers, dq = g_engine_dq;
+  if (nc == 3 && dq == 0)
+    hipLaunchKernelGGL((ffn_engine_kernel<14, 7, 3, 0>), dim3(kNWG), dim3(256), 0,
+                       (hipStream_t)stream, a);
+  else if (nc == 3)
+    hipLaunchKernelGGL((ffn_engine_kernel<14, 7, 3, 1>), dim3(kNWG), dim3(256), 0,
+                       (hipStream_t)stream, a);
+  else if (dq == 0)
+    hipLaunchKernelGGL((ffn_engine_kernel<14, 7, 7, 0>), dim3(kNWG), dim3(512), 0,
                        (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL((ffn_engine_kernel<14, 7, 7>), dim3(kNWG), dim3(512), 0,
+    hipLaunchKernelGGL((ffn_engine_kernel<14, 7, 7, 1>), dim3(kNWG), dim3(512), 0,
                        (hipStream_t)stream, a);
   return check_launch("ffn_engine_kernel");
 }
