@@ -1443,6 +1443,11 @@ def main():
                 "eager_kernel_ms_per_step": round(sum(durs), 4),
                 "per_shape_eager": per_shape,
                 "per_shape_graph": per_shape_graph or None,
+                # the step rebuilt from the per-shape graph times (launches x us), this run: sits
+                # beside kernel_ms_per_step as the in-run check of the step's kernel time
+                "per_shape_graph_step_ms": (round(sum(v["launches"] * v["us"]
+                                                      for v in per_shape_graph.values()) * 1e-3, 4)
+                                            if per_shape_graph else None),
                 "per_shape_frac": ({k: v["frac"] for k, v in per_shape_graph.items()}
                                    if per_shape_graph else None),
             },

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--consumers", type=int, default=7)
     ap.add_argument("--dq", type=int, default=1)
+    ap.add_argument("--ahead", type=int, default=2)
+    ap.add_argument("--dyn", type=int, default=1)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     layers = []
@@ -40,7 +42,7 @@ def main():
     x0 = torch.randn(1, 1, DIM, device=dev, dtype=torch.bfloat16)
     st = torch.zeros(256 * 64, dtype=torch.int64, device=dev)
     lib = _lib.lib()
-    assert lib.tao_tune_ffn_engine(args.consumers, args.dq) == 0
+    assert lib.tao_tune_ffn_engine(args.consumers, args.dq, args.ahead, args.dyn) == 0
 
     def chain(x):
         for (p13, p2, nw) in layers:
@@ -74,6 +76,13 @@ def main():
             rec[f"c{c}"] = {"norm": q(us(b)), "p1_done": q(us(b + 1)), "gather_done": q(us(b + 2)),
                             "p2_done": q(us(b + 3)), "end": q(us(b + 4)), "full_wait": q(dur(b + 5))}
         rec["end_max"] = round(max(max(us(8 + 6 * c + 4)) for c in range(args.consumers)), 3)
+        # phase-1 completion of each workgroup (its last consumer) and its loader's phase-1 issue,
+        # grouped by blockIdx % 8 (the XCD under round-robin placement)
+        p1 = [max(us(8 + 6 * c + 1)[w] for c in range(args.consumers)) for w in range(256)]
+        li = us(1)
+        rec["by_wg_mod8"] = {str(x): {"p1_done": q([p1[w] for w in range(x, 256, 8)]),
+                                      "loader_p1_issued": q([li[w] for w in range(x, 256, 8)])}
+                             for x in range(8)}
         out[f"rep{rep}"] = rec
     print(json.dumps(out), flush=True)
     kernels.check_decode_status()

@@ -28,7 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--configs", nargs="*", default=["7:1", "7:0", "3:1"],
+    ap.add_argument("--configs", nargs="*", default=["7:1:2:1", "7:1:2:0", "7:1:3:0"],
                     help="consumers:decode pairs (tao_tune_ffn_engine)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -86,14 +86,14 @@ def main():
         res[f"launch_us_per_layer_{rnd}"] = round(lu, 3)
         best["launch"] = min(best.get("launch", 1e9), lu)
         for cfg in args.configs:
-            nc, dq = (int(v) for v in cfg.split(":"))
-            assert lib.tao_tune_ffn_engine(nc, dq) == 0
+            nc, dq, ah, dy = (int(v) for v in cfg.split(":"))
+            assert lib.tao_tune_ffn_engine(nc, dq, ah, dy) == 0
             eu, eout, ge = timed(engine_chain)
             del ge
-            res[f"engine{nc}_{dq}_us_per_layer_{rnd}"] = round(eu, 3)
+            res[f"engine{nc}_{dq}_{ah}_{dy}_us_per_layer_{rnd}"] = round(eu, 3)
             best[cfg] = min(best.get(cfg, 1e9), eu)
-    nc, dq = (int(v) for v in args.configs[0].split(":"))
-    assert lib.tao_tune_ffn_engine(nc, dq) == 0
+    nc, dq, ah, dy = (int(v) for v in args.configs[0].split(":"))
+    assert lib.tao_tune_ffn_engine(nc, dq, ah, dy) == 0
     eout = engine_chain(x0)
     for cfg in args.configs:
         res[f"engine{cfg}_us_per_layer"] = round(best[cfg], 3)

@@ -68,7 +68,7 @@ def _payload(h):
     from torchao._models.llama import kernels
 
     ws = kernels.ffn_engine_workspace(h.device)
-    return ws[512:512 + INTER // 2].view(torch.bfloat16).reshape(-1)  # 2 KiB in: [I/2] u32
+    return ws[1024:1024 + INTER // 2].view(torch.bfloat16).reshape(-1)  # 4 KiB in: [I/2] u32
 
 
 def _shards(h):

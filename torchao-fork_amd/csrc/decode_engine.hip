@@ -31,6 +31,8 @@
 // (consumer, after its reads of the slot). The epoch lives on the device (ctl[0]); the last
 // workgroup out advances it, so HIP-graph replays need no reset.
 // Every wait is bounded (SeamWait): a timeout sets tao_decode_status bit 2 and the grid drains.
+#include <type_traits>
+
 #include "tao_common.h"
 #include "tao_reduce.h"
 
@@ -45,9 +47,13 @@ constexpr int kSlotB = 20 * 1024;    // slot: 16 KiB of nibbles + 4 KiB of (scal
 constexpr int kScaleOff = 16 * 1024;
 constexpr int kRing = 7;             // 140 KiB of ring: w2's 7 slots all fit behind w1||w3's
 constexpr int kPieces = 20;          // DMA wave-instructions per slot (1 KiB each)
-constexpr int kAhead = 2;            // slots in flight beyond the last published one
 constexpr int kShards = 8;           // phase-1 arrival counters (workgroup wg -> shard wg % 8)
 constexpr int kShard0 = 64;          // word offset of shard 0 in ctl
+constexpr int kHeads = 8;            // DYN: w1||w3 block queues (workgroup wg -> queue wg % 8)
+constexpr int kHead0 = 320;          // word offset of queue 0's head in ctl
+constexpr int kCtlBytes = 4096;      // ctl words; the SwiGLU payload follows
+constexpr int kTq = 8;               // DYN: LDS ticket ring
+constexpr int kTqAhead = 2;          // DYN: tickets the dispatcher holds beyond the loader's
 
 struct FfnArgs {
   const uint16_t* h;       // [4096] residual stream (the FFN's input and residual)
@@ -73,6 +79,14 @@ __device__ __forceinline__ unsigned long long now() { return __builtin_amdgcn_s_
 // [5] time waiting on FULL
 __device__ __forceinline__ void stamp(const FfnArgs& a, int slot, unsigned long long v) {
   if (a.stamps != nullptr && slot < 64 && (threadIdx.x & 63) == 0) a.stamps[blockIdx.x * 64 + slot] = v;
+}
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
 }
 
 __device__ __forceinline__ unsigned lds_ld(const unsigned* p) {
@@ -139,11 +153,11 @@ __device__ __forceinline__ float pair_sum(const uint32_t (&x)[16]) {
   return s;
 }
 
-template <int NS1, int NS2, int kCons, int DQ>
-__global__ __launch_bounds__(64 * (kCons + 1), 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void
-ffn_engine_kernel(FfnArgs a) {
+template <int NS1, int NS2, int kCons, int DQ, int kAhead, bool DYN>
+__global__ __launch_bounds__(64 * (kCons + 1 + DYN), 1) void ffn_engine_kernel(FfnArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 ring[kRing * kSlotB / 16];
-  __shared__ unsigned full[kRing], freew[kRing], done_lds, p1_lds, p2go;
+  __shared__ unsigned full[kRing], freew[kRing], blk[kRing], tq[kTq], done_lds, p1_lds, p2go, n1w,
+      tqn, ldr_g;
   __shared__ float red[kCons][16];
   constexpr int NSL = NS1 + NS2;
   const int lane = threadIdx.x & 63;
@@ -162,6 +176,9 @@ ffn_engine_kernel(FfnArgs a) {
     done_lds = 0u;
     p1_lds = 0u;
     p2go = 0u;
+    n1w = DYN ? ~0u : (unsigned)NS1;
+    tqn = 0u;
+    ldr_g = 0u;
   }
   __syncthreads();  // the only workgroup barrier: the roles below never meet again
 
@@ -178,54 +195,153 @@ ffn_engine_kernel(FfnArgs a) {
     const uint32_t vz2 = (uint32_t)(lane >> 4) * kS2B + 16u * (lane & 15);
     const uint32_t base13 = (uint32_t)wg * kRows13;
     const uint32_t base2 = (uint32_t)wg * kRows2;
-    auto issue = [&](int g) __attribute__((always_inline)) {
+    // phase-1 slot: block b = rows 8 b .. 8 b + 7 of w1||w3 (8 x 2048 B contiguous, then their
+    // 8 x 512 B of words); phase-2 slot: unit u of this workgroup's 16 w2 rows (one 1 KiB piece per
+    // row, words 4 rows per piece)
+    auto issue1 = [&](int g, uint32_t b) __attribute__((always_inline)) {
       uint8_t* dst = reinterpret_cast<uint8_t*>(ring) + (g % kRing) * kSlotB;
-      if (g < NS1) {  // 8 rows x 2048 B contiguous, then their 8 x 512 B of words
-        const uint32_t r0 = base13 + 8u * g;
+      const uint32_t r0 = 8u * b;
 #pragma unroll
-        for (int p = 0; p < 16; ++p)
-          dma_lds_ring<16, kNT>(r13, v16, r0 * 2048u + 1024u * p, dst + 1024 * p);
+      for (int p = 0; p < 16; ++p)
+        dma_lds_ring<16, kNT>(r13, v16, r0 * 2048u + 1024u * p, dst + 1024 * p);
 #pragma unroll
-        for (int p = 0; p < 4; ++p)
-          dma_lds_ring<16, kNT>(rz13, v16, r0 * 512u + 1024u * p, dst + kScaleOff + 1024 * p);
-      } else {  // unit u of 16 rows: one 1 KiB piece per row, words 4 rows per piece
-        const uint32_t u = (uint32_t)(g - NS1);
-#pragma unroll
-        for (int p = 0; p < 16; ++p)
-          dma_lds_ring<16, kNT>(r2, v16, (base2 + p) * (uint32_t)kK2B + 1024u * u, dst + 1024 * p);
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-          dma_lds_ring<16, kNT>(rz2, vz2, (base2 + 4u * p) * (uint32_t)kS2B + 256u * u,
-                                dst + kScaleOff + 1024 * p);
-      }
+      for (int p = 0; p < 4; ++p)
+        dma_lds_ring<16, kNT>(rz13, v16, r0 * 512u + 1024u * p, dst + kScaleOff + 1024 * p);
     };
-    for (int g = 0; g < NSL; ++g) {
-      if (g >= kRing) {  // slot g % kRing free again (consumer of slot g - kRing done reading)
-        const unsigned long long tw = a.stamps ? now() : 0;
+    auto issue2 = [&](int g, uint32_t u) __attribute__((always_inline)) {
+      uint8_t* dst = reinterpret_cast<uint8_t*>(ring) + (g % kRing) * kSlotB;
+#pragma unroll
+      for (int p = 0; p < 16; ++p)
+        dma_lds_ring<16, kNT>(r2, v16, (base2 + p) * (uint32_t)kK2B + 1024u * u, dst + 1024 * p);
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        dma_lds_ring<16, kNT>(rz2, vz2, (base2 + 4u * p) * (uint32_t)kS2B + 256u * u,
+                              dst + kScaleOff + 1024 * p);
+    };
+    auto wait_free = [&](int g) __attribute__((always_inline)) {
+      if (g < kRing) return;  // slot g % kRing free again (consumer of slot g - kRing done)
+      const unsigned long long tw = a.stamps ? now() : 0;
+      SeamWait sw;
+      while (lds_ld(&freew[g % kRing]) != (unsigned)(g - kRing + 1)) {
+        if (sw.timed_out()) {
+          flag_decode_error(kDecodeErrSplitK);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (a.stamps) t_free += now() - tw;
+    };
+    auto publish = [&](int g) __attribute__((always_inline)) {
+      lds_st(&full[g % kRing], (unsigned)(g + 1));
+    };
+    int n1 = NS1;
+    if constexpr (DYN) {
+      // w1||w3 blocks come from a queue per blockIdx % 8 (kHeads heads of NS1 kNWG / kHeads
+      // blocks each), two blocks per ticket, taken by this workgroup's dispatcher wave into the
+      // LDS ticket ring tq: a CU whose stream runs slow takes fewer blocks, so the phase-1 finish
+      // lines up across CUs (what the all-to-all edge waits for)
+      constexpr unsigned kLimit = (unsigned)(NS1 * kNWG / kHeads);
+      const uint32_t qbase = (uint32_t)(wg % kHeads) * kLimit;
+      for (int g = 0;; ++g) {
+        const int i = g >> 1;
+        {
+          SeamWait sw;
+          while ((int)lds_ld(&tqn) <= i) {
+            if (sw.timed_out()) {
+              flag_decode_error(kDecodeErrSplitK);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        const uint32_t t = lds_ld(&tq[i % kTq]);
+        if (t >= kLimit) {  // queue empty: this workgroup's phase 1 is slots 0 .. g - 1
+          n1 = g;
+          wait_vmcnt<0>();
+          for (int k = g - kAhead > 0 ? g - kAhead : 0; k < g; ++k) publish(k);
+          lds_st(&n1w, (unsigned)g);
+          break;
+        }
+        lds_st(&ldr_g, (unsigned)(g + 1));
+        const uint32_t blockid = qbase + t + (uint32_t)(g & 1);
+        wait_free(g);
+        lds_st(&blk[g % kRing], blockid);
+        issue1(g, blockid);
+        if (g >= kAhead) {
+          wait_vmcnt<kAhead * kPieces>();
+          publish(g - kAhead);
+        }
+      }
+      stamp(a, 1, now());
+      for (int j = 0; j < NS2; ++j) {
+        const int g = n1 + j;
+        wait_free(g);
+        issue2(g, (uint32_t)j);
+        if (j >= kAhead) {
+          wait_vmcnt<kAhead * kPieces>();
+          publish(g - kAhead);
+        }
+      }
+      stamp(a, 2, now());
+      static_for<0, kAhead>([&](auto kc) __attribute__((always_inline)) {  // drain, oldest first
+        constexpr int k = kAhead - 1 - decltype(kc)::value;
+        wait_vmcnt<k * kPieces>();
+        publish(n1 + NS2 - 1 - k);
+      });
+    } else {
+      for (int g = 0; g < NSL; ++g) {
+        wait_free(g);
+        if (g < NS1) {
+          lds_st(&blk[g % kRing], base13 / 8u + (uint32_t)g);
+          issue1(g, base13 / 8u + (uint32_t)g);
+        } else {
+          issue2(g, (uint32_t)(g - NS1));
+        }
+        if (g == NS1 - 1) stamp(a, 1, now());
+        if (g >= kAhead) {  // slot g - kAhead has landed: kAhead slots' pieces may still be out
+          wait_vmcnt<kAhead * kPieces>();
+          publish(g - kAhead);
+        }
+      }
+      stamp(a, 2, now());
+      static_for<0, kAhead>([&](auto kc) __attribute__((always_inline)) {  // drain, oldest first
+        constexpr int k = kAhead - 1 - decltype(kc)::value;
+        wait_vmcnt<k * kPieces>();
+        publish(NSL - 1 - k);
+      });
+    }
+    stamp(a, 3, now());
+    stamp(a, 4, t_free);
+    return;
+  }
+
+  if (DYN && wave == kCons + 1) {
+    // ---------------------------------- dispatcher ------------------------------------------
+    // one returning agent-scope atomic per two w1||w3 blocks, at most kTqAhead tickets ahead of
+    // the loader (tickets taken early could leave another CU idle)
+    constexpr unsigned kLimit = (unsigned)(NS1 * kNWG / kHeads);
+    unsigned* head = a.ctl + kHead0 + 32 * (wg % kHeads);
+    for (int i = 0;; ++i) {
+      {
         SeamWait sw;
-        while (lds_ld(&freew[g % kRing]) != (unsigned)(g - kRing + 1)) {
+        while (2 * i > (int)lds_ld(&ldr_g) + 2 * kTqAhead) {
           if (sw.timed_out()) {
             flag_decode_error(kDecodeErrSplitK);
             break;
           }
           __builtin_amdgcn_s_sleep(1);
         }
-        if (a.stamps) t_free += now() - tw;
       }
-      issue(g);
-      if (g == NS1 - 1) stamp(a, 1, now());
-      if (g >= kAhead) {  // slot g - kAhead has landed: kAhead slots' pieces may still be out
-        wait_vmcnt<kAhead * kPieces>();
-        lds_st(&full[(g - kAhead) % kRing], (unsigned)(g - kAhead + 1));
+      unsigned t = 0;
+      if (lane == 0)
+        t = __hip_atomic_fetch_add(head, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t = __shfl(t, 0);
+      if (lane == 0) {
+        lds_st(&tq[i % kTq], t);
+        lds_st(&tqn, (unsigned)(i + 1));
       }
+      if (t >= kLimit) break;
     }
-    stamp(a, 2, now());
-    wait_vmcnt<kPieces>();
-    lds_st(&full[(NSL - 2) % kRing], (unsigned)(NSL - 1));
-    wait_vmcnt<0>();
-    lds_st(&full[(NSL - 1) % kRing], (unsigned)NSL);
-    stamp(a, 3, now());
-    stamp(a, 4, t_free);
     return;
   }
 
@@ -301,9 +417,42 @@ ffn_engine_kernel(FfnArgs a) {
 
   stamp(a, 8 + 6 * c, now());
   // ---- phase 1: w1||w3 rows -> SwiGLU granules ----
+  int n1 = NS1;
 #pragma unroll 1
-  for (int g = c; g < NS1; g += kCons) {
-    wait_full(g);
+  for (int g = c;; g += kCons) {
+    if constexpr (DYN) {  // slot g holds a block, or the loader has closed phase 1 before it
+      const unsigned long long tw = a.stamps ? now() : 0;
+      SeamWait sw;
+      bool have = false;
+      while (true) {
+        // FULL first, then the phase-1 count: the loader sets n1w before it publishes any
+        // phase-2 slot (whose FULL value g + 1 a phase-1 wait could otherwise mistake), and LDS
+        // keeps one wave's writes in order
+        const bool f = lds_ld(&full[g % kRing]) == (unsigned)(g + 1);
+        const unsigned n = lds_ld(&n1w);
+        if (n != ~0u && g >= (int)n) {
+          n1 = (int)n;
+          break;
+        }
+        if (f) {
+          have = true;
+          break;
+        }
+        if (sw.timed_out()) {
+          flag_decode_error(kDecodeErrSplitK);
+          n1 = g;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (a.stamps) t_full += now() - tw;
+      asm volatile("" ::: "memory");
+      if (!have) break;
+    } else {
+      if (g >= NS1) break;
+      wait_full(g);
+    }
+    const uint32_t blkid = lds_ld(&blk[g % kRing]);
     const uint8_t* sl = ringb + (g % kRing) * kSlotB;
     // the slot's 8 rows x 2 units into registers, then the slot is released before the
     // arithmetic: a slot is held for its landing plus one LDS pass, not for the dot products
@@ -332,7 +481,7 @@ ffn_engine_kernel(FfnArgs a) {
     if (lane < 2) {
       const uint32_t s0 = f32_to_bf16(round_bf16(a0 / (1.f + __expf(-a0))) * b0);
       const uint32_t s1 = f32_to_bf16(round_bf16(a1 / (1.f + __expf(-a1))) * b1);
-      const size_t gi = (size_t)wg * (kRows13 / 4) + 2 * g + lane;
+      const size_t gi = (size_t)2 * blkid + lane;
       __hip_atomic_store(a.pay + gi, s0 | (s1 << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -354,9 +503,9 @@ ffn_engine_kernel(FfnArgs a) {
   }
   stamp(a, 9 + 6 * c, now());
   // ---- phase 2: wait for every workgroup's SwiGLU outputs, load this consumer's units, w2 ----
-  // phase-2 slots g = NS1 + u; consumer c owns the units u with (NS1 + u) % kCons == c
+  // phase-2 slots g = n1 + u; consumer c owns the units u with (n1 + u) % kCons == c
   constexpr int kMaxU = (NS2 + kCons - 1) / kCons;
-  const int u0 = ((c - NS1) % kCons + kCons) % kCons;  // first unit of this consumer
+  const int u0 = ((c - n1) % kCons + kCons) % kCons;  // first unit of this consumer
   const int nu = u0 < NS2 ? (NS2 - u0 + kCons - 1) / kCons : 0;
   uint32_t x2[kMaxU][16];
   float sx2[kMaxU];
@@ -413,7 +562,7 @@ ffn_engine_kernel(FfnArgs a) {
 #pragma unroll
   for (int ui = 0; ui < kMaxU; ++ui) {
     if (ui < nu) {
-      const int g = NS1 + u0 + kCons * ui;
+      const int g = n1 + u0 + kCons * ui;
       wait_full(g);
       const uint8_t* sl = ringb + (g % kRing) * kSlotB;
       // computed straight from LDS: with kRing = 7 the phase-2 slots never wait for one another,
@@ -450,7 +599,11 @@ ffn_engine_kernel(FfnArgs a) {
   if (lane == 0) {  // epoch hand-over: the last workgroup out advances it for the next launch
     const unsigned prev =
         __hip_atomic_fetch_add(a.ctl + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == kNWG - 1) {
+    if (prev == kNWG - 1) {  // every workgroup is done: the queues start empty again
+      if constexpr (DYN)
+        for (int q = 0; q < kHeads; ++q)
+          __hip_atomic_store(a.ctl + kHead0 + 32 * q, 0u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(a.ctl + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(a.ctl, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -477,15 +630,22 @@ int ffn_engine_cus() {
 static unsigned long long* g_engine_stamps = nullptr;
 static int g_engine_consumers = 7;
 static int g_engine_dq = 1;
+static int g_engine_ahead = 2;
+static int g_engine_dyn = 1;
 
 // A/B knobs: consumer waves per workgroup (3: 256-thread workgroups, one consumer per SIMD
 // beside the loader's; 7: 512 threads, two per SIMD) and the nibble decode (0: shift, and, or;
-// 1: byte permutes)
-extern "C" int tao_tune_ffn_engine(int consumers, int dq) {
+// 1: byte permutes), and the loader's slots in flight beyond the last published one (1..3; 3
+// consumers run 1 / 2, dq 0 runs 2)
+extern "C" int tao_tune_ffn_engine(int consumers, int dq, int ahead, int dyn) {
+  TAO_CHECK_ARG(dyn == 0 || dyn == 1, "tune: ffn engine dyn must be 0 or 1");
+  g_engine_dyn = dyn;
   TAO_CHECK_ARG(consumers == 3 || consumers == 7, "tune: ffn engine consumers must be 3 or 7");
   TAO_CHECK_ARG(dq == 0 || dq == 1, "tune: ffn engine decode must be 0 or 1");
+  TAO_CHECK_ARG(ahead >= 1 && ahead <= 3, "tune: ffn engine slots ahead must be 1..3");
   g_engine_consumers = consumers;
   g_engine_dq = dq;
+  g_engine_ahead = ahead;
   return TAO_OK;
 }
 
@@ -523,24 +683,29 @@ extern "C" int tao_int4wo_ffn_engine_bf16(const uint16_t* h, const uint16_t* nor
   FfnArgs a{h, norm_weight, eps, w13, reinterpret_cast<const uint32_t*>(sz13), w2,
             reinterpret_cast<const uint32_t*>(sz2), out, ctl, payload, (int)inter,
             g_engine_stamps, 0x000F000Fu, 0x43004300u};
-  const int nc = g_engine_consumers, dq = g_engine_dq;
-  if (nc == 3 && dq == 0)
-    hipLaunchKernelGGL((ffn_engine_kernel<14, 7, 3, 0>), dim3(kNWG), dim3(256), 0,
-                       (hipStream_t)stream, a);
-  else if (nc == 3)
-    hipLaunchKernelGGL((ffn_engine_kernel<14, 7, 3, 1>), dim3(kNWG), dim3(256), 0,
-                       (hipStream_t)stream, a);
-  else if (dq == 0)
-    hipLaunchKernelGGL((ffn_engine_kernel<14, 7, 7, 0>), dim3(kNWG), dim3(512), 0,
-                       (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL((ffn_engine_kernel<14, 7, 7, 1>), dim3(kNWG), dim3(512), 0,
-                       (hipStream_t)stream, a);
+  const int nc = g_engine_consumers, dq = g_engine_dq, ah = g_engine_ahead;
+#define TAO_FFN_GO(NC, DQ, AH, DY)                                                             \
+  hipLaunchKernelGGL((ffn_engine_kernel<14, 7, NC, DQ, AH, DY>), dim3(kNWG),                 \
+                     dim3(64 * (NC + 1 + DY)), 0, (hipStream_t)stream, a)
+  if (g_engine_dyn) {
+    TAO_FFN_GO(7, 1, 2, true);
+  } else if (nc == 3) {
+    TAO_FFN_GO(3, 1, 2, false);
+  } else if (dq == 0) {
+    TAO_FFN_GO(7, 0, 2, false);
+  } else if (ah == 3) {
+    TAO_FFN_GO(7, 1, 3, false);
+  } else if (ah == 1) {
+    TAO_FFN_GO(7, 1, 1, false);
+  } else {
+    TAO_FFN_GO(7, 1, 2, false);
+  }
+#undef TAO_FFN_GO
   return check_launch("ffn_engine_kernel");
 }
 
-// workspace: ctl (2 KiB: epoch at word 0 = 1, done counter at 32, shard counters at 64 + 32 s,
-// all zero otherwise) + the SwiGLU payload [inter / 2] u32
+// workspace: ctl (kCtlBytes: epoch at word 0 = 1, done counter at 32, shard counters at
+// 64 + 32 s, queue heads at 320 + 32 q, all zero otherwise) + the SwiGLU payload [inter / 2] u32
 extern "C" int64_t tao_int4wo_ffn_engine_workspace_bytes(int64_t inter) {
-  return 2048 + inter / 2 * 4;
+  return tao::kCtlBytes + inter / 2 * 4;
 }

@@ -109,7 +109,7 @@ _SIGNATURES = {
                                  _p, _p, _p, _i64, _i64, _i64, _i64, ctypes.c_float, _i64, _p],
     "tao_int4wo_ffn_engine_supported": [_i64, _i64, _i64],
     "tao_debug_ffn_engine_stamps": [_p],
-    "tao_tune_ffn_engine": [_int, _int],
+    "tao_tune_ffn_engine": [_int, _int, _int, _int],
     "tao_int4wo_ffn_engine_workspace_bytes": [_i64],
     "tao_int4wo_ffn_engine_bf16": [_p, _p, ctypes.c_float, _p, _p, _p, _p, _p, _i64, _i64, _i64,
                                    _p, _p, _p],

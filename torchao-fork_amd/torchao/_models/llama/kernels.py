@@ -440,7 +440,7 @@ def int4_ffn_engine(h: torch.Tensor, norm_weight: torch.Tensor, eps: float, w13:
     base = ws.data_ptr()
     _lib.call("tao_int4wo_ffn_engine_bf16", h.data_ptr(), norm_weight.data_ptr(), float(eps),
               p13.data_ptr(), z13.data_ptr(), p2.data_ptr(), z2.data_ptr(), out.data_ptr(), dim,
-              inter, int(g13), base, base + 2048, _stream(h))
+              inter, int(g13), base, base + 4096, _stream(h))
     return out
 
 
