@@ -30,8 +30,8 @@ def main():
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--consumers", type=int, default=7)
     ap.add_argument("--dq", type=int, default=1)
-    ap.add_argument("--ahead", type=int, default=2)
-    ap.add_argument("--dyn", type=int, default=1)
+    ap.add_argument("--ahead", type=int, default=3)
+    ap.add_argument("--dyn", type=int, default=0)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     layers = []

@@ -28,7 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--configs", nargs="*", default=["7:1:2:1", "7:1:2:0", "7:1:3:0"],
+    ap.add_argument("--configs", nargs="*", default=["7:1:3:0", "7:1:2:0", "3:1:2:0", "7:0:2:0", "7:1:2:1"],
                     help="consumers:decode pairs (tao_tune_ffn_engine)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)

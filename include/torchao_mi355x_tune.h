@@ -148,8 +148,8 @@ int tao_gemm_sf_status(unsigned* bits);
 int tao_debug_ffn_engine_stamps(void* buf);
 /* A/B knobs of the decode FFN engine: consumer waves per workgroup (3 or 7, built-in 7), the
  * nibble decode (0 shift + and + or, 1 byte permutes, built-in 1), the loader's slots in flight
- * (1..3, built-in 2) and the w1||w3 block assignment (0 static rows per workgroup, 1 queues,
- * built-in 1; 1 runs 7 consumers, decode 1, 2 slots). */
+ * (1..3, built-in 3) and the w1||w3 block assignment (0 static rows per workgroup, built-in;
+ * 1 per-XCD queues fed by a dispatcher wave, which runs 7 consumers, decode 1, 2 slots). */
 int tao_tune_ffn_engine(int consumers, int dq, int ahead, int dyn);
 /* Measurement kernel (bench.py, not the product path): a pure streaming read of `bytes` (a
  * positive multiple of 8192) from `buf` (16-B aligned) with 16-B non-temporal loads; `sink` is

@@ -511,7 +511,7 @@ __global__ __launch_bounds__(64 * (kCons + 1 + DYN), 1) void ffn_engine_kernel(F
   float sx2[kMaxU];
   {
     // ONE poller per workgroup (the wave that signalled it) reads the 8 shard counters, sleeping
-    // ~0.2 us between polls; the counters only grow (kNWG / kShards arrivals per launch), so this
+    // ~0.05 us between polls; the counters only grow (kNWG / kShards arrivals per launch), so this
     // launch's are complete at (kNWG / kShards) x epoch. It then sets an LDS word the other
     // consumer waves poll (the table row's "after an LDS word it then sets").
     SeamWait sw;
@@ -527,7 +527,7 @@ __global__ __launch_bounds__(64 * (kCons + 1 + DYN), 1) void ffn_engine_kernel(F
           flag_decode_error(kDecodeErrSplitK);
           break;
         }
-        __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_s_sleep(2);
       }
       if (lane == 0) lds_st(&p2go, 1u);
     } else {
@@ -630,8 +630,8 @@ int ffn_engine_cus() {
 static unsigned long long* g_engine_stamps = nullptr;
 static int g_engine_consumers = 7;
 static int g_engine_dq = 1;
-static int g_engine_ahead = 2;
-static int g_engine_dyn = 1;
+static int g_engine_ahead = 3;
+static int g_engine_dyn = 0;
 
 // A/B knobs: consumer waves per workgroup (3: 256-thread workgroups, one consumer per SIMD
 // beside the loader's; 7: 512 threads, two per SIMD) and the nibble decode (0: shift, and, or;

@@ -305,6 +305,9 @@ def main(argv=None):
                          "one-token kernels (a different K summation order than the reference's "
                          "all-rows model(idx)[:, -1].argmax; 0 restores the all-rows path; "
                          "kernels.PREFILL_LAST_ROW; -1 = built-in, on)")
+    ap.add_argument("--ffn_engine", type=int, default=-1,
+                    help="1 / 0: decode feed-forward on the persistent LDS-DMA engine "
+                         "(kernels.DECODE_FFN_ENGINE; -1 = built-in, off)")
     ap.add_argument("--native_prefill_attn", action="store_true",
                     help="prefill attention on tao_attn_prefill_bf16 (kernels.PREFILL_ATTN = True)")
     ap.add_argument("--qkv_attn", type=int, default=-1,
@@ -333,9 +336,11 @@ def main(argv=None):
 
     if (args.head_prologue or args.sdpa_prefill or args.qkv_attn >= 0
             or args.native_prefill_attn or args.prefill_add_norm >= 0
-            or args.prefill_last_row >= 0):
+            or args.prefill_last_row >= 0 or args.ffn_engine >= 0):
         from torchao._models.llama import kernels
 
+        if args.ffn_engine >= 0:
+            kernels.DECODE_FFN_ENGINE = bool(args.ffn_engine)
         if args.prefill_last_row >= 0:
             kernels.PREFILL_LAST_ROW = bool(args.prefill_last_row)
         if args.qkv_attn >= 0:
