@@ -396,3 +396,37 @@ def test_operands_on_another_device_raise():
         torch.ops.torchao.int8_scaled_mm(xq, xs.cpu(), q8.to(DEV), s8.to(DEV), None)
     with pytest.raises(RuntimeError, match="same device"):
         torch.ops.torchao.int8_dyn_linear(x, q8, s8.to(DEV), None)
+
+
+@pytest.mark.gpu
+def test_fuse_gate_up_then_quantize_gpu():
+    """The reference FeedForward layout merged by fuse_gate_up_ and then quantize_d (int4 g32):
+    the merged model's outputs equal the unmerged quantized model's within one GEMV's
+    re-association (the merged linear quantizes to the same values; it runs one GEMV launch for
+    w1 and w3), and the merged linear dispatches to the HIP int4 op."""
+    import copy
+
+    import torch.nn.functional as F
+
+    from torchao.quantization import Int4WeightOnlyConfig, fuse_gate_up_, quantize_
+
+    class FeedForward(torch.nn.Module):
+        def __init__(self, d, h):
+            super().__init__()
+            self.w1 = torch.nn.Linear(d, h, bias=False)
+            self.w3 = torch.nn.Linear(d, h, bias=False)
+            self.w2 = torch.nn.Linear(h, d, bias=False)
+
+        def forward(self, x):
+            return self.w2(F.silu(self.w1(x)) * self.w3(x))
+
+    torch.manual_seed(1)
+    ff = FeedForward(1024, 2816).to(device="cuda", dtype=torch.bfloat16)
+    merged = copy.deepcopy(ff)
+    assert fuse_gate_up_(merged) == 1
+    quantize_(ff, Int4WeightOnlyConfig(group_size=32))
+    quantize_(merged, Int4WeightOnlyConfig(group_size=32))
+    for M in (1, 16):
+        x = torch.randn(M, 1024, device="cuda", dtype=torch.bfloat16)
+        a, b = ff(x).float(), merged(x).float()
+        assert float((a - b).norm() / a.norm()) < 1e-2

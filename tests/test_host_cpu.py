@@ -708,3 +708,40 @@ def test_single_fetch_gemm_lds_images_conflict_free():
         for r in range(64):
             assert sorted(f(r, g) for g in range(n)) == list(range(n))
             assert all(f(r, f(r, g)) == g for g in range(n))
+
+
+def test_fuse_gate_up_matches_reference_feedforward_cpu():
+    """fuse_gate_up_ (opt-in, before quantize_) on modules shaped like the reference FeedForward
+    (torchao/_models/llama/model.py:481-492): same outputs in bf16 (the merged linear computes the
+    same rows), int4 quantization of the merged weight equals quantizing w1 / w3 apart, and
+    modules without the three linears are left alone."""
+    import torch.nn.functional as F
+
+    from torchao.quantization import fuse_gate_up_
+
+    class FeedForward(torch.nn.Module):  # the reference module's structure
+        def __init__(self, d, h):
+            super().__init__()
+            self.w1 = torch.nn.Linear(d, h, bias=False)
+            self.w3 = torch.nn.Linear(d, h, bias=False)
+            self.w2 = torch.nn.Linear(h, d, bias=False)
+
+        def forward(self, x):
+            return self.w2(F.silu(self.w1(x)) * self.w3(x))
+
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(FeedForward(64, 96), torch.nn.Linear(64, 64), FeedForward(64, 32))
+    model = model.to(torch.float32)
+    x = torch.randn(3, 64)
+    ref = model(x)
+    w1, w3 = model[0].w1.weight.detach().clone(), model[0].w3.weight.detach().clone()
+    assert fuse_gate_up_(model) == 2
+    assert not hasattr(model[0], "w1") and model[0].w13.weight.shape == (192, 64)
+    assert torch.equal(model[0].w13.weight[0::2], w1) and torch.equal(model[0].w13.weight[1::2], w3)
+    torch.testing.assert_close(model(x), ref, rtol=1e-5, atol=1e-5)
+    # row-wise int4 qparams of the merged rows == those of w1 and w3 apart
+    from oracle import oracle
+
+    s13, z13 = oracle.int4_qparams(model[0].w13.weight.detach().to(torch.bfloat16), 32)
+    s1, z1 = oracle.int4_qparams(w1.to(torch.bfloat16), 32)
+    assert torch.equal(s13[0::2], s1) and torch.equal(z13[0::2], z1)

@@ -1,5 +1,6 @@
 """Quantization workflows on the MI355X weight-only linear path."""
 
+from torchao.quantization.fuse import fuse_gate_up_
 from torchao.quantization.linear_activation_quantized_tensor import (
     LinearActivationQuantizedTensor,
     to_linear_activation_quantized,
@@ -26,6 +27,7 @@ from torchao.quantization.utils import compute_error
 
 __all__ = [
     "quantize_",
+    "fuse_gate_up_",
     "Int4WeightOnlyConfig",
     "Int8WeightOnlyConfig",
     "Int8DynamicActivationInt8WeightConfig",
