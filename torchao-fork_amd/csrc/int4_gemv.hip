@@ -29,6 +29,10 @@
 // TAO_GEMV_STAMPS / TAO_NORM_DEBUG / GEMV_XPRE up to commit 1bac331; their measurements are in
 // profiles/ (r1_gemv_debug*.log, r2/r5g_gemv_stamps.jsonl, r5g_ab_gemv_*.jsonl).
 
+#ifndef TAO_GEMV_NIBPERM
+#define TAO_GEMV_NIBPERM 1
+#endif
+
 namespace tao {
 
 TAO_DECODE_ERROR_WORD(int4gemv_decode_status)
@@ -303,9 +307,17 @@ __device__ __forceinline__ void gemv_body(
         const uint32_t wd[4] = {wv[r].x, wv[r].y, wv[r].z, wv[r].w};
         float d = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j) {
+#if TAO_GEMV_NIBPERM
+          uint32_t p[4];
+          nib_pairs4_bf16(wd[j], p);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) d = dot2_bf16(xd[j][i], p[i], d);
+#else
 #pragma unroll
           for (int i = 0; i < 4; ++i) d = dot2_bf16(xd[j][i], nib_pair_bf16(wd[j], i), d);
+#endif
+        }
         acc[r][m] = fmaf(sc[r], d - sx136, fmaf(zp[r], sx, acc[r][m]));
       }
     }

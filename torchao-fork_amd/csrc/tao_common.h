@@ -125,6 +125,17 @@ __device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float acc) {
 __device__ __forceinline__ uint32_t nib_pair_bf16(uint32_t w, int i) {
   return ((w >> (4 * i)) & 0x000F000Fu) | 0x43004300u;
 }
+// All four pairs of a word, p[i] == nib_pair_bf16(w, i), by byte permutes: lo = w & 0x0F0F0F0F
+// holds q0, q4, q1, q5 in its bytes and hi = (w >> 4) & 0x0F0F0F0F holds q2, q6, q3, q7; one
+// v_perm_b32 puts two of them under 0x43 bytes ([q_a, 0x43, q_b, 0x43] = (128 + q_a, 128 + q_b)):
+// 7 VALU per 4 pairs instead of 11 (3 shifts + 4 ands + 4 ors)
+__device__ __forceinline__ void nib_pairs4_bf16(uint32_t w, uint32_t (&p)[4]) {
+  const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
+  p[0] = __builtin_amdgcn_perm(0x43434343u, lo, 0x04020400u);
+  p[1] = __builtin_amdgcn_perm(0x43434343u, hi, 0x04020400u);
+  p[2] = __builtin_amdgcn_perm(0x43434343u, lo, 0x04030401u);
+  p[3] = __builtin_amdgcn_perm(0x43434343u, hi, 0x04030401u);
+}
 
 template <typename T>
 __device__ __forceinline__ T ld_nt(const T* p) {
