@@ -29,10 +29,6 @@
 // TAO_GEMV_STAMPS / TAO_NORM_DEBUG / GEMV_XPRE up to commit 1bac331; their measurements are in
 // profiles/ (r1_gemv_debug*.log, r2/r5g_gemv_stamps.jsonl, r5g_ab_gemv_*.jsonl).
 
-#ifndef TAO_GEMV_NIBPERM
-#define TAO_GEMV_NIBPERM 1
-#endif
-
 namespace tao {
 
 TAO_DECODE_ERROR_WORD(int4gemv_decode_status)
@@ -308,15 +304,13 @@ __device__ __forceinline__ void gemv_body(
         float d = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-#if TAO_GEMV_NIBPERM
+          // byte-permute decode (tao_common.h): the same bf16 pairs in 7 VALU instead of 11;
+          // bench step 1.098 / 1.116 -> 1.074 / 1.089 ms, 4096x14336 9.3 -> 8.8 us, 28672x4096
+          // 14.8 -> 14.1 us (same-box A/B, profiles/r6k_ab_gemv_nibperm.jsonl)
           uint32_t p[4];
           nib_pairs4_bf16(wd[j], p);
 #pragma unroll
           for (int i = 0; i < 4; ++i) d = dot2_bf16(xd[j][i], p[i], d);
-#else
-#pragma unroll
-          for (int i = 0; i < 4; ++i) d = dot2_bf16(xd[j][i], nib_pair_bf16(wd[j], i), d);
-#endif
         }
         acc[r][m] = fmaf(sc[r], d - sx136, fmaf(zp[r], sx, acc[r][m]));
       }
