@@ -570,6 +570,34 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
         a, b = a.float(), b.float()
         return round(float((a - b).norm() / b.norm().clamp_min(1e-30)), 5)
 
+    def intake(path, xx, wl, zl, copies):
+        """the LDS-DMA intake floor of the single-fetch tile family at this shape
+        (tao_sf_intake_probe: the launch shape's per-workgroup bytes through its LDS ring, no
+        compute), kernel us over the same rotated weight copies"""
+        import ctypes
+        shp = (ctypes.c_int * 7)()
+        sink = torch.zeros(1024, dtype=torch.int32, device=device)
+        h = _lib.lib()
+
+        def probe(c):
+            rc = h.tao_sf_intake_probe(path, xx.data_ptr(), wl[c].data_ptr(),
+                                       zl[c].data_ptr() if zl else None, M, N, K, g,
+                                       ctypes.cast(shp, ctypes.c_void_p), sink.data_ptr(),
+                                       torch.cuda.current_stream().cuda_stream)
+            if rc != 0:
+                raise RuntimeError(h.tao_last_error().decode(errors="replace"))
+        try:
+            (pus,) = timed(probe, copies, 1)
+        except RuntimeError as e:
+            return {"unavailable": str(e)[:160]}
+        bn, S, ns, a, ld, ks, step_b = list(shp)
+        steps = K // ks
+        last = steps - a * (S - 1)
+        per_wg = step_b * max(a, last)
+        return {"us": round(pus, 2), "bn": bn, "k_slices": S, "stages": ns, "loader_waves": ld,
+                "k_step": ks, "bytes_per_wg_step": step_b, "bytes_per_wg": per_wg,
+                "GBps_per_cu": round(per_wg / (pus * 1e-6) / 1e9, 1)}
+
     out = {}
     # int8 dyn: per-token quant kernel + int8 MFMA GEMM with the fused scale epilogue
     copies = max(2, int(320e6 // (N * K)))
@@ -602,6 +630,7 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
         ref8_diff = rel(ref8(0), ours8(0))
     except Exception as e:  # the hipBLASLt int8 path is build dependent: report, never fail
         ref8_us = f"unavailable: {type(e).__name__}: {str(e)[:120]}"
+    ip8 = intake(2, xq, ws, None, copies)
     ops = 2 * M * N * K
     nbytes = N * K + N * 2 + M * K + M * 4 + M * N * 2  # int8 W + scales, int8 x + scales, bf16 y
     att = max(ops / (INT8_PEAK_TOPS * 1e12), nbytes / (HBM_PEAK_GBPS * 1e9)) * 1e6
@@ -617,6 +646,9 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
         "reference_gpu_us": round(ref8_us, 2) if isinstance(ref8_us, float) else ref8_us,
         "reference_gpu_op": "torch._int_mm (hipBLASLt int8, safe_int_mm) * x_scale -> bf16 * w_scale",
         "reference_gpu_rel_l2": ref8_diff,
+        # the single-fetch int8 tile family at this shape (config 3 itself stays on the incumbent
+        # kernel named above): its LDS-DMA intake alone, no compute
+        "intake_probe_sf_int8": ip8,
     }
     del ws
     # int4 g32 weight-only at the same M: bf16 MFMA with in-register nibble dequant
@@ -651,6 +683,9 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
             ref4_diff = rel(ref4(0), int4(0))
     except Exception as e:  # the aten op is build dependent: report, never fail
         ref4_us = f"unavailable: {type(e).__name__}: {str(e)[:120]}"
+    ip4 = intake(0, x, [w[0] for w in w4], [w[1] for w in w4], copies)
+    if "us" in ip4:
+        ip4["gemm_over_intake"] = round(us4 / ip4["us"], 3)
     nbytes4 = int4_alg_bytes(N, K, g, M)
     att4 = max(ops / (BF16_PEAK_TFLOPS * 1e12), nbytes4 / (HBM_PEAK_GBPS * 1e9)) * 1e6
     out["int4_wo"] = {
@@ -664,6 +699,9 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
         "reference_gpu_us": round(ref4_us, 2) if isinstance(ref4_us, float) else ref4_us,
         "reference_gpu_op": "aten._weight_int4pack_mm (PyTorch-ROCm)",
         "reference_gpu_rel_l2": ref4_diff,
+        # the routed launch shape's LDS-DMA intake alone (same per-workgroup bytes, ring, waits
+        # and barriers, no MFMA, no dequantisation, no seam): the floor this tile family reaches
+        "intake_probe": ip4,
     }
     del w4, wref
     torch.cuda.empty_cache()

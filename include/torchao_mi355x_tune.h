@@ -161,6 +161,16 @@ int tao_hbm_read_probe(const void* buf, int64_t bytes, void* sink, void* stream)
  * 16-B element per thread, one pass (`grid` ignored), non-temporal. Graph-capturable. */
 int tao_hbm_copy_probe(const void* src, void* dst, int64_t bytes, int grid, int mode,
                        void* stream);
+/* Measurement kernel (bench.py prefill_mfma intake ceiling, not the product path): the LDS-DMA
+ * intake of the single-fetch prefill GEMM's launch shape at (path 0 int4 / 2 int8 dyn, 64 < M <=
+ * 128, N, K): every workgroup streams exactly its tile's x, weight and (scale, zero) bytes per k
+ * step through the kernel's LDS ring, counted waits and barriers, and computes nothing. x / w / z
+ * as the GEMM's operands (z: int4 (scale, zero) words; unused for int8). shape_out[0..6] <- bn,
+ * K slices, stages, k steps per slice, loader waves, k step, bytes per workgroup per step. `sink`
+ * >= 4 KiB of device memory (never written in practice). Graph-capturable. */
+int tao_sf_intake_probe(int path, const void* x, const void* w, const void* z, int64_t M,
+                        int64_t N, int64_t K, int64_t group_size, int* shape_out, void* sink,
+                        void* stream);
 /* Number of split-K workspaces currently owned by captured graphs (each is released with its
  * graph). Diagnostic for tests; never fails. */
 int tao_graph_workspace_count(void);

@@ -654,3 +654,40 @@ def test_sf_random_shapes_all_forms_agree(sf, case):
         assert torch.equal(h1, h0) and torch.equal(y1, y0)
     if N * K <= 4096 * 4096:
         assert oracle.rel_l2(ref.cpu(), oracle.int4_linear(a.cpu(), q, s, z, 32)) < TOL_REF
+
+
+@pytest.mark.parametrize("path", [0, 2])
+def test_sf_intake_probe_runs_the_launch_shape(sf, path):
+    """bench.py's intake ceiling (tao_sf_intake_probe): the probe streams the launch shape the GEMM
+    takes at 128 x 4096 x 4096 (the int4 route: 64-column tiles, 4 K slices, 4 stages, 4 loader
+    waves; int8 dyn: the single-fetch default) and reports it; it rejects M outside one tile."""
+    import ctypes
+
+    M, N, K, g = 128, 4096, 4096, 32
+    if path == 0:
+        q, s, z, packed, sz = _int4(N, K, g, seed=5)
+        x = oracle.make_activation(M, K, seed=6).to(DEV)
+        w, zz = packed, sz
+    else:
+        x, _, w, _ = (t.to(DEV) for t in _int8(M, N, K, seed=7))
+        zz = None
+    shp = (ctypes.c_int * 7)()
+    sink = torch.zeros(1024, dtype=torch.int32, device=DEV)
+    h = _lib.lib()
+
+    def run(m):
+        return h.tao_sf_intake_probe(path, x.data_ptr(), w.data_ptr(),
+                                     zz.data_ptr() if zz is not None else None, m, N, K, g,
+                                     ctypes.cast(shp, ctypes.c_void_p), sink.data_ptr(),
+                                     torch.cuda.current_stream().cuda_stream)
+
+    assert run(M) == 0
+    torch.cuda.synchronize()
+    bn, S, ns, a, ld, ks, step_b = list(shp)
+    if path == 0:
+        assert (bn, S, ns, a, ld, ks) == (64, 4, 4, 8, 4, 128)
+        assert step_b == 128 * 256 + 64 * 64 + 64 * 16
+    else:
+        assert ks in (128, 256) and step_b == 128 * ks + bn * ks and S * a <= K // ks
+    assert int(sink.sum().item()) == 0
+    assert run(32) != 0  # one 128-row tile only

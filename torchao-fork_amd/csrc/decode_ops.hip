@@ -125,8 +125,8 @@ __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(
 // (tao_int4wo_linear_partials_f32): the linear's output is formed here as bf16(sum_z part[z]) in
 // slice order from 0 (the single-fetch reducer's order and rounding, so bit-identical to its bf16
 // output), then h = bf16(x + that), y = RMSNorm(h) as rmsnorm_rows_kernel<NP, true>.
-// SS > 0: S == SS known at compile time, so every slice's loads are issued before the first add
-// (one round trip; a runtime S loop waits once per slice). SS == 0: any S, one slice at a time.
+// SS > 0 (2, 4, 8): S == SS known at compile time, so every slice's loads are issued before the
+// first add (one round trip; a runtime S loop waits once per slice). SS == 0: any S, one at a time.
 template <int NP, int SS>
 __global__ __launch_bounds__(256) void rmsnorm_part_kernel(
     const uint16_t* __restrict__ x, const float* __restrict__ part, int S, size_t plane,
@@ -757,6 +757,7 @@ int tao_add_rmsnorm_partials_bf16(const uint16_t* x, const float* part, int64_t 
   switch (S) {                                                                                \
     case 2: launch(rmsnorm_part_kernel<NP, 2>, grid, blk, 0, st, x, part, S, plane, w, h, y, D, eps); break; \
     case 4: launch(rmsnorm_part_kernel<NP, 4>, grid, blk, 0, st, x, part, S, plane, w, h, y, D, eps); break; \
+    case 8: launch(rmsnorm_part_kernel<NP, 8>, grid, blk, 0, st, x, part, S, plane, w, h, y, D, eps); break; \
     default: launch(rmsnorm_part_kernel<NP, 0>, grid, blk, 0, st, x, part, S, plane, w, h, y, D, eps); \
   }
   if (nv <= 256) TAO_PART(1)

@@ -228,9 +228,6 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
     uint16_t* __restrict__ y, int M, int N, int K, int a_steps, typename P::Acc* __restrict__ slab,
     unsigned* __restrict__ cnt, int fenced, int S, int ntn, int seam, int cs, SfEpi ep, int xmap) {
   const int epi = ep.kind;
-#define SF_MARK(i) \
-  do {             \
-  } while (0)
   typedef typename P::Acc Acc;
   constexpr int WN = kWaves / WM;
   constexpr int RM = kBM / WM, CN = BN / WN;  // wave tile
@@ -473,7 +470,6 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < J) issue(s0 + p, p);
-  SF_MARK(1);
   const int jiss = J - (NS - 1);  // steps that issue a stage ahead
   int j = 0;
   for (; j < jiss; ++j) {
@@ -489,7 +485,6 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
   }
   }  // LDW == 0
   barrier_lgkm();  // all fragment reads done: the LDS is free for the epilogue image
-  SF_MARK(3);
   if constexpr (!kI8) {
     if (epi == 3) {  // partials out: this slice's fp32 tile, row-major, no hand-off
       if (!loader) {
@@ -621,7 +616,6 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
 #pragma unroll
         for (int b = 0; b < NT; ++b) acc[a][b] = sum[a][b];
     }
-    SF_MARK(4);
   }
 
   // ---- epilogue: bf16 tile through an LDS image, rows stored in 16-B pieces ------------------------
@@ -725,7 +719,6 @@ __global__ __launch_bounds__((kWaves + LDW) * 64) void gemm_sf_kernel(
         if (n_blk + 8 * cc + k < N) y[(size_t)m * N + n_blk + 8 * cc + k] = e[k];
     }
   }
-#undef SF_MARK
 }
 
 // ---- launch ------------------------------------------------------------------------------------
@@ -976,6 +969,23 @@ int sf_int4_epi(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, i
       return sf_dispatch_wm<SfI4, 64>(sh, stream, xb, pol, bias, y, M, N, K, sh.a_steps, slab, cnt,
                                       ep);
   }
+}
+
+// The launch shape the single-fetch GEMM takes for (path, M <= 128, N, K) -- 0 int4, 2 int8 dyn
+// -- for the LDS-DMA intake probe (probe_intake.hip): column tile, K slices, ring stages, k steps
+// per publishing slice, loader waves (0 / 4), k step, one wave along M (the 32x32x16 kernel).
+void sf_launch_shape(int path, int M, int N, int K, int* bn, int* splits, int* stages,
+                     int* a_steps, int* loaders, int* kstep, int* wm1) {
+  int ks = 256;
+  const SfShape sh = sf_shape(path, M, N, K, &ks);
+  *bn = sh.bn;
+  *splits = sh.splits;
+  *stages = sh.stages;
+  *a_steps = path == 2 && ks == 128 ? sh.a_steps * 2 : sh.a_steps;  // (in units of *kstep)
+  const bool ld = tuning().sf_loaders ? tuning().sf_loaders == 2 : sh.ld != 0;
+  *loaders = path == 0 && sh.wm != 1 && sh.bn <= 64 && ld ? 4 : 0;
+  *kstep = path == 0 ? 128 : (ks == 128 ? 128 : 256);
+  *wm1 = path == 0 && sh.wm == 1;
 }
 
 // K slices the partials-out launch of this int4 shape writes (0: not served, the 32x32x16 route)

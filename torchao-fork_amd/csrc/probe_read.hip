@@ -47,8 +47,159 @@ __global__ __launch_bounds__(256) void copy_probe_kernel(const uint4* __restrict
   }
 }
 
+// LDS-DMA intake probe of the single-fetch prefill GEMM's tile family (bench.py prefill_mfma
+// intake ceiling): each workgroup of a launch shape takes in exactly the bytes
+// its tile does per k step -- the 128 x rows of its K slice, the tile's BN weight rows, their
+// (scale, zero) words -- as 1-KiB (16 B / lane) and 256-B (4 B / lane) LDS-DMA pieces into an NS-stage
+// ring, with the kernel's counted vmcnt wait and one barrier per step, issued by 4 loader waves
+// beside 8 waves that only join the barriers (LDW) or by all 8 waves, and computes nothing. Its
+// time is the intake-bound floor of that tile on this chip (gemm_sf.hip's per-step DMA).
+// R = pieces per issuing wave per stage (compile time, for the counted wait).
+template <int NS, int R, int LDW>
+__global__ __launch_bounds__((8 + LDW) * 64) void sf_intake_probe_kernel(
+    const uint8_t* __restrict__ x, uint32_t x_bytes, uint32_t x_row, int kx,
+    const uint8_t* __restrict__ w, uint32_t w_bytes, uint32_t w_row, int kw,
+    const uint8_t* __restrict__ z, uint32_t z_bytes, uint32_t z_row, int kz, int zgs,
+    int px, int pw, int pz, int ntn, int S, int a_steps, int nsteps, uint32_t* __restrict__ sink) {
+  constexpr int DW = LDW > 0 ? LDW : 8;
+  constexpr int STAGE_MAX = 160 * 1024 / NS;
+  __shared__ uint4 lds[160 * 1024 / 16];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool issuer = LDW == 0 || wave >= 8;
+  const int dwv = LDW > 0 ? wave - 8 : wave;
+  const int bid = blockIdx.x;
+  const int nb = bid % ntn, sl = (bid / ntn) % S;
+  const int s0 = sl * a_steps, J = sl == S - 1 ? nsteps - s0 : a_steps;
+  const int stage = px * 1024 + pw * 1024 + pz * 256;
+  const Rsrc xr = make_rsrc(x, x_bytes), wr = make_rsrc(w, w_bytes), zr = make_rsrc(z, z_bytes);
+  // piece r of this wave: index i = r DW + dwv over [x pieces | w pieces | z pieces]
+  uint32_t dv[R];
+  int dd[R], dk[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = r * DW + dwv;
+    if (i < px) {  // 1024 / kx rows per piece, kx / 16 lanes per row
+      const int g = kx / 16, row = i * (1024 / kx) + lane / g;
+      dv[r] = (uint32_t)row * x_row + 16u * (uint32_t)(lane % g);
+      dd[r] = i * 1024;
+      dk[r] = 0;
+    } else if (i < px + pw) {
+      const int j = i - px, g = kw / 16, row = nb * (pw * 1024 / kw) + j * (1024 / kw) + lane / g;
+      dv[r] = (uint32_t)row * w_row + 16u * (uint32_t)(lane % g);
+      dd[r] = px * 1024 + j * 1024;
+      dk[r] = 1;
+    } else if (i < px + pw + pz) {  // 4 B per lane: 256 / kz rows per piece
+      const int j = i - px - pw, g = kz / 4, row = nb * (pz * 256 / kz) + j * (256 / kz) + lane / g;
+      dv[r] = (uint32_t)row * z_row + 4u * (uint32_t)(lane % g);
+      dd[r] = px * 1024 + pw * 1024 + j * 256;
+      dk[r] = 2;
+    } else {
+      dk[r] = 3;  // no piece (the issuing waves' share is uneven)
+    }
+  }
+  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+    uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * (stage < STAGE_MAX ? stage : STAGE_MAX);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (dk[r] == 0) dma_lds_ring<16>(xr, dv[r], (uint32_t)st * (uint32_t)kx, base + dd[r]);
+      else if (dk[r] == 1) dma_lds_ring<16, kNT>(wr, dv[r], (uint32_t)st * (uint32_t)kw, base + dd[r]);
+      else if (dk[r] == 2)
+        dma_lds_ring<4, kNT>(zr, dv[r], (uint32_t)(st * (kx / 2) / zgs) * 4u, base + dd[r]);
+      else  // keep the per-wave count of vector-memory ops at R per stage
+        dma_lds_ring<4>(xr, 0u, 0u, base);
+    }
+  };
+  if (issuer) {
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+      if (p < J) issue(s0 + p, p);
+  }
+  for (int j = 0; j < J; ++j) {
+    if (issuer) {
+      if (J - 1 - j >= NS - 2) wait_vmcnt<(NS - 2) * R>();
+      else wait_vmcnt<0>();
+    }
+    barrier_lgkm();
+    if (issuer && j + NS - 1 < J) issue(s0 + j + NS - 1, (j + NS - 1) % NS);
+  }
+  wait_vmcnt<0>();
+  barrier_lgkm();
+  if (threadIdx.x == 0) {
+    const uint32_t v = reinterpret_cast<const uint32_t*>(lds)[bid & 1023];
+    if (v == 0x9E3779B9u) sink[bid & 1023] = v;  // keeps the ring live; never taken in practice
+  }
+}
+
 }  // namespace
+
+void sf_launch_shape(int path, int M, int N, int K, int* bn, int* splits, int* stages,
+                     int* a_steps, int* loaders, int* kstep, int* wm1);
+
 }  // namespace tao
+
+// The intake probe for the single-fetch launch shape the GEMM takes at (path, M <= 128, N, K):
+// path 0 = int4 (x bf16 [M][K], w packed [N][K/2] bytes, z (scale, zero) [N][K/g] dwords), 2 =
+// int8 dyn (x int8 [M][K], w int8 [N][K], z unused). Writes the launch shape it streamed to
+// shape_out[0..6] (bn, splits, stages, a_steps, loaders, kstep, bytes per workgroup per step).
+extern "C" int tao_sf_intake_probe(int path, const void* x, const void* w, const void* z,
+                                   int64_t M, int64_t N, int64_t K, int64_t group_size,
+                                   int* shape_out, void* sink, void* stream) {
+  TAO_CHECK_ARG(path == 0 || path == 2, "intake probe: path must be 0 (int4) or 2 (int8 dyn)");
+  TAO_CHECK_ARG(x != nullptr && w != nullptr && sink != nullptr && shape_out != nullptr &&
+                    (path == 2 || z != nullptr),
+                "intake probe: null pointer");
+  TAO_CHECK_ARG(M > 64 && M <= 128 && N > 0 && K > 0 && N * K < (1LL << 32),
+                "intake probe: one 128-row tile (64 < M <= 128), N x K < 2^32");
+  TAO_CHECK_ARG(path == 2 || (group_size >= 32 && group_size <= 256 && K % group_size == 0),
+                "intake probe: bad group size %lld", (long long)group_size);
+  int bn, S, ns, a, ld, ks, wm1;
+  tao::sf_launch_shape(path, (int)M, (int)N, (int)K, &bn, &S, &ns, &a, &ld, &ks, &wm1);
+  const int kx = path == 0 ? 256 : ks, kw = path == 0 ? 64 : ks, kz = path == 0 ? 16 : 0;
+  TAO_CHECK_ARG(K % ks == 0 && N % bn == 0, "intake probe: N (%lld) / K (%lld) off the tile grid",
+                (long long)N, (long long)K);
+  const int px = 128 * kx / 1024, pw = bn * kw / 1024, pz = bn * kz / 256;
+  const int T = px + pw + pz, DW = ld ? 4 : 8, R = (T + DW - 1) / DW;
+  if (ns < 2) ns = 2;
+  if (ns > 4) ns = 4;
+  shape_out[0] = bn;
+  shape_out[1] = S;
+  shape_out[2] = ns;
+  shape_out[3] = a;
+  shape_out[4] = ld;
+  shape_out[5] = ks;
+  shape_out[6] = px * 1024 + pw * 1024 + pz * 256;
+  TAO_CHECK_ARG((int64_t)ns * shape_out[6] <= 160 * 1024, "intake probe: %d stages of %d B exceed LDS",
+                ns, shape_out[6]);
+  const int ntn = (int)(N / bn), nsteps = (int)(K / ks);
+  const uint8_t* xb = static_cast<const uint8_t*>(x);
+  const uint8_t* wb = static_cast<const uint8_t*>(w);
+  const uint8_t* zb = static_cast<const uint8_t*>(z != nullptr ? z : w);
+  const uint32_t xrow = (uint32_t)(K * (path == 0 ? 2 : 1)), wrow = (uint32_t)(path == 0 ? K / 2 : K);
+  const uint32_t zrow = path == 0 ? (uint32_t)(K / group_size * 4) : 4u;
+  const uint32_t xbytes = (uint32_t)(M * xrow), wbytes = (uint32_t)(N * wrow);
+  const uint32_t zbytes = path == 0 ? (uint32_t)(N * zrow) : 4u;
+  const int zgs = path == 0 ? (int)group_size : 32;
+  const dim3 grid((unsigned)(ntn * S));
+  hipStream_t st = tao::as_stream(stream);
+  uint32_t* sk = static_cast<uint32_t*>(sink);
+#define TAO_IP(NS_, R_, LDW_)                                                                      \
+  tao::launch(tao::sf_intake_probe_kernel<NS_, R_, LDW_>, grid, dim3((8 + LDW_) * 64), 0, st, xb, \
+              xbytes, xrow, kx, wb, wbytes, wrow, kw, zb, zbytes, zrow, kz, zgs, px, pw, pz, ntn,  \
+              S, a, nsteps, sk)
+  if (ld && R == 10 && ns == 4) TAO_IP(4, 10, 4);
+  else if (ld && R == 10 && ns == 3) TAO_IP(3, 10, 4);
+  else if (!ld && R == 5 && ns == 3) TAO_IP(3, 5, 0);
+  else if (!ld && R == 5 && ns == 2) TAO_IP(2, 5, 0);
+  else if (!ld && R == 6 && ns == 3) TAO_IP(3, 6, 0);
+  else if (!ld && R == 6 && ns == 2) TAO_IP(2, 6, 0);
+  else
+    return tao::set_error(TAO_ERR_UNSUPPORTED,
+                          "intake probe: no instance for %d pieces per wave, %d stages, loaders %d",
+                          R, ns, ld);
+#undef TAO_IP
+  return tao::check_launch("sf_intake_probe_kernel");
+}
 
 extern "C" int tao_hbm_copy_probe(const void* src, void* dst, int64_t bytes, int grid, int mode,
                                   void* stream) {
