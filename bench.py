@@ -580,7 +580,7 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
         h = _lib.lib()
 
         def probe(c):
-            rc = h.tao_sf_intake_probe(path, xx.data_ptr(), wl[c].data_ptr(),
+            rc = h.tao_sf_intake_probe(path, 0, xx.data_ptr(), wl[c].data_ptr(),
                                        zl[c].data_ptr() if zl else None, M, N, K, g,
                                        ctypes.cast(shp, ctypes.c_void_p), sink.data_ptr(),
                                        torch.cuda.current_stream().cuda_stream)

@@ -121,8 +121,9 @@ int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages, int a_ste
  * reducer (slice S-1 sums the whole tile). Thread-local; for measurement. */
 int tao_tune_gemm_sf_seam(int seam);
 /* Single-fetch GEMMs: dedicated LDS-DMA loader waves beside the compute waves (0 = built-in,
- * 1 = off, 2 = on). 32x32x16 int4 kernel: one per SIMD, bn 64 / 128, one wave per column group;
- * 16x16 kernel: 4 beside its 8 compute waves, 64-column tiles. Thread-local; for measurement. */
+ * 1 = off, 2 = on, 3 = 8 loader waves on the 16x16 int4 kernel, else as 2). 32x32x16 int4 kernel:
+ * one per SIMD, bn 64 / 128, one wave per column group; 16x16 kernel: 4 (or 8) beside its 8
+ * compute waves, 64-column tiles. Thread-local; for measurement. */
 int tao_tune_gemm_sf_loaders(int mode);
 /* Single-fetch GEMM, fixed-reducer seam: place each K slice's workgroups on their own XCDs
  * (slice z on XCDs [8z/S, 8(z+1)/S)), so each XCD's L2 takes in 1/S of x. 0 = built-in,
@@ -167,10 +168,14 @@ int tao_hbm_copy_probe(const void* src, void* dst, int64_t bytes, int grid, int 
  * step through the kernel's LDS ring, counted waits and barriers, and computes nothing. x / w / z
  * as the GEMM's operands (z: int4 (scale, zero) words; unused for int8). shape_out[0..6] <- bn,
  * K slices, stages, k steps per slice, loader waves, k step, bytes per workgroup per step. `sink`
- * >= 4 KiB of device memory (never written in practice). Graph-capturable. */
-int tao_sf_intake_probe(int path, const void* x, const void* w, const void* z, int64_t M,
-                        int64_t N, int64_t K, int64_t group_size, int* shape_out, void* sink,
-                        void* stream);
+ * >= 4 KiB of device memory (never written in practice). mode 0 is that intake; 1..3 attribute it
+ * (int4 route with loader waves only): 1 weight + (scale, zero) pieces only, 2 x pieces only,
+ * 3 every piece with x read from a private [grid][128][K] copy per workgroup, 4 every piece with
+ * the k steps of each workgroup rotated to start at step (block / 8) mod steps, 5 x pieces only,
+ * rotated. Graph-capturable. */
+int tao_sf_intake_probe(int path, int mode, const void* x, const void* w, const void* z,
+                        int64_t M, int64_t N, int64_t K, int64_t group_size, int* shape_out,
+                        void* sink, void* stream);
 /* Number of split-K workspaces currently owned by captured graphs (each is released with its
  * graph). Diagnostic for tests; never fails. */
 int tao_graph_workspace_count(void);

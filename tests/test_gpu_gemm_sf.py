@@ -676,7 +676,7 @@ def test_sf_intake_probe_runs_the_launch_shape(sf, path):
     h = _lib.lib()
 
     def run(m):
-        return h.tao_sf_intake_probe(path, x.data_ptr(), w.data_ptr(),
+        return h.tao_sf_intake_probe(path, 0, x.data_ptr(), w.data_ptr(),
                                      zz.data_ptr() if zz is not None else None, m, N, K, g,
                                      ctypes.cast(shp, ctypes.c_void_p), sink.data_ptr(),
                                      torch.cuda.current_stream().cuda_stream)

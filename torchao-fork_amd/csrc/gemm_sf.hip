@@ -734,10 +734,16 @@ struct SfShape {
   int xm = 0;  // fixed-reducer seam: each K slice's workgroups on their own XCDs (sf_xmap)
 };
 
+// loader waves of the 16x16 kernel: tao_tune_gemm_sf_loaders 1 = none, 2 = 4, 3 = 8; 0 = route
+int sf_loader_waves(const SfShape& sh) {
+  const int m = tuning().sf_loaders;
+  return m == 1 ? 0 : m == 2 ? 4 : m == 3 ? 8 : (sh.ld != 0 ? 4 : 0);
+}
+
 template <class P, int BN, int WM, int NS>
 bool sf_go(const SfShape& sh, hipStream_t stream, const uint8_t* x, const P& pol,
            const uint16_t* bias, uint16_t* y, int M, int N, int K, int a, typename P::Acc* slab,
-           unsigned* cnt, const SfEpi& ep, bool loaders) {
+           unsigned* cnt, const SfEpi& ep, int loaders) {
   constexpr int STAGE = kBM * P::kXRow + BN * P::kWRow + BN * P::kZRow;
   constexpr int NB = NS;
   if constexpr (NB * STAGE <= 160 * 1024 && (kBM * P::kXRow + BN * P::kWRow + BN * P::kZRow) > 0) {
@@ -751,8 +757,16 @@ bool sf_go(const SfShape& sh, hipStream_t stream, const uint8_t* x, const P& pol
       const int xmap = xm && !sh.seam && (sh.splits == 2 || sh.splits == 4 || sh.splits == 8) &&
                        ntn % (8 / sh.splits) == 0;
       if constexpr (BN <= 64 && T % 4 == 0 && ((kBM * P::kXRow) / 1024) % 4 == 0) {  // wider: spills
-        if (loaders) {  // 4 loader waves beside the 8 compute waves
+        if (loaders == 4) {  // 4 loader waves beside the 8 compute waves
           launch(gemm_sf_kernel<P, BN, WM, NS, 4>, grid, dim3(768), 0, stream, x, pol, bias, y, M,
+                 N, K, a, slab, cnt, sk_flags(), sh.splits, ntn, sh.seam,
+                 tuning().cnt_stride, ep, xmap);
+          return true;
+        }
+      }
+      if constexpr (BN <= 64 && T % 8 == 0 && ((kBM * P::kXRow) / 1024) % 8 == 0 && P::kABytes == 2) {
+        if (loaders == 8) {  // 8 loader waves (two per SIMD), 16 waves: <= 128 VGPRs
+          launch(gemm_sf_kernel<P, BN, WM, NS, 8>, grid, dim3(1024), 0, stream, x, pol, bias, y, M,
                  N, K, a, slab, cnt, sk_flags(), sh.splits, ntn, sh.seam,
                  tuning().cnt_stride, ep, xmap);
           return true;
@@ -775,7 +789,7 @@ int sf_dispatch_wm(const SfShape& sh, hipStream_t st, const uint8_t* x, const P&
   auto go = [&](auto wmc, auto nsc) {
     constexpr int W = decltype(wmc)::value, S_ = decltype(nsc)::value;
     ok = sf_go<P, BN, W, S_>(sh, st, x, pol, bias, y, M, N, K, a, slab, cnt, ep,
-                             tuning().sf_loaders ? tuning().sf_loaders == 2 : sh.ld != 0);
+                             sf_loader_waves(sh));
   };
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
@@ -982,8 +996,7 @@ void sf_launch_shape(int path, int M, int N, int K, int* bn, int* splits, int* s
   *splits = sh.splits;
   *stages = sh.stages;
   *a_steps = path == 2 && ks == 128 ? sh.a_steps * 2 : sh.a_steps;  // (in units of *kstep)
-  const bool ld = tuning().sf_loaders ? tuning().sf_loaders == 2 : sh.ld != 0;
-  *loaders = path == 0 && sh.wm != 1 && sh.bn <= 64 && ld ? 4 : 0;
+  *loaders = path == 0 && sh.wm != 1 && sh.bn <= 64 ? sf_loader_waves(sh) : 0;
   *kstep = path == 0 ? 128 : (ks == 128 ? 128 : 256);
   *wm1 = path == 0 && sh.wm == 1;
 }
@@ -1144,9 +1157,10 @@ extern "C" int tao_tune_gemm_sf(int mode, int bn, int wm, int splits, int stages
   return TAO_OK;
 }
 
-// Dedicated loader waves of the single-fetch kernels: 0 = built-in, 1 = off, 2 = on.
+// Dedicated loader waves of the single-fetch kernels: 0 = built-in, 1 = off, 2 = on (4 waves),
+// 3 = 8 waves (16x16 int4 kernel, 64-column tiles; elsewhere as 2).
 extern "C" int tao_tune_gemm_sf_loaders(int mode) {
-  TAO_CHECK_ARG(mode >= 0 && mode <= 2, "tune: gemm_sf_loaders must be 0, 1 or 2");
+  TAO_CHECK_ARG(mode >= 0 && mode <= 3, "tune: gemm_sf_loaders must be 0..3");
   tao::tuning().sf_loaders = mode;
   return TAO_OK;
 }

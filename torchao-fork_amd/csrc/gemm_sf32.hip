@@ -576,7 +576,7 @@ int sf32_int4(const uint16_t* x, const uint32_t* packed, const uint16_t* sz, int
   // dedicated loader waves (one per SIMD): tao_tune_gemm_sf_loaders 2 = on, 1 = off, 0 = built-in
   // (on for 128-column tiles at 3 stages: w1||w3 28672x4096 M = 128 47.4-48.5 -> 39.6 us,
   // 10240x8192 S = 2 48.9 -> 48.7; profiles/r5e_sf32_loaders.jsonl)
-  const int ldm = tuning().sf_loaders;
+  const int ldm = tuning().sf_loaders == 3 ? 2 : tuning().sf_loaders;  // (8 waves: 16x16 only)
   // (k halves + loaders, 12 waves: 70B's 10240x8192 49.4 -> 45.4 us; w1||w3 42.6 -> 44.8, so the
   // one-compute-wave form stays there: profiles/r5g_ab_kh2_loaders.jsonl)
   const bool loaders = (kh == 1 && ((ldm == 2 && (bn == 128 || bn == 64)) ||

@@ -766,6 +766,11 @@ M1Shape m1_shape(int N, int S) {
     } else if (N >= 8192) {  // one wave walks both slices of 4 rows (PAIR)
       c.occ = 4;
       c.sh = {1, N >= 16384 ? 4 : 1};
+    } else if (N >= 6144) {  // wqkv 6144x4096: one wave walks both slices of 2 rows (PAIR):
+      // 4.94 vs 5.18 us for 2 waves along K (same-process A/B after the byte-permute decode,
+      // profiles/r6p_ab_wqkv_shape.jsonl)
+      c.rpw = 2;
+      c.sh = {1, 4};
     } else {
       c.rpw = 2;
       c.sh = {2, N <= 4096 ? 1 : 4};

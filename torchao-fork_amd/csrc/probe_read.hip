@@ -54,8 +54,13 @@ __global__ __launch_bounds__(256) void copy_probe_kernel(const uint4* __restrict
 // ring, with the kernel's counted vmcnt wait and one barrier per step, issued by 4 loader waves
 // beside 8 waves that only join the barriers (LDW) or by all 8 waves, and computes nothing. Its
 // time is the intake-bound floor of that tile on this chip (gemm_sf.hip's per-step DMA).
-// R = pieces per issuing wave per stage (compile time, for the counted wait).
-template <int NS, int R, int LDW>
+// R = pieces per issuing wave per stage (compile time, for the counted wait). MODE (attribution
+// of the intake, experiments only): 0 the tile's pieces; 1 its weight and (scale, zero) pieces
+// only; 2 its x pieces only; 3 all pieces, x read from a private copy per workgroup (x holds
+// grid x 128 rows: no two workgroups request the same x lines); 4 the tile's pieces with each
+// workgroup starting its k steps at a different step (rot = (block / 8) mod steps: the workgroups
+// of one XCD that share a K slice first request different x lines); 5 x pieces only, rotated.
+template <int NS, int R, int LDW, int MODE>
 __global__ __launch_bounds__((8 + LDW) * 64) void sf_intake_probe_kernel(
     const uint8_t* __restrict__ x, uint32_t x_bytes, uint32_t x_row, int kx,
     const uint8_t* __restrict__ w, uint32_t w_bytes, uint32_t w_row, int kw,
@@ -76,11 +81,14 @@ __global__ __launch_bounds__((8 + LDW) * 64) void sf_intake_probe_kernel(
   // piece r of this wave: index i = r DW + dwv over [x pieces | w pieces | z pieces]
   uint32_t dv[R];
   int dd[R], dk[R];
+  const int xrow0 = MODE == 3 ? bid * 128 : 0;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const int i = r * DW + dwv;
+    int i = r * DW + dwv;
+    if (MODE == 1) i += px;                    // no x pieces
+    if ((MODE == 2 || MODE == 5) && i >= px) i = px + pw + pz;  // x pieces only
     if (i < px) {  // 1024 / kx rows per piece, kx / 16 lanes per row
-      const int g = kx / 16, row = i * (1024 / kx) + lane / g;
+      const int g = kx / 16, row = xrow0 + i * (1024 / kx) + lane / g;
       dv[r] = (uint32_t)row * x_row + 16u * (uint32_t)(lane % g);
       dd[r] = i * 1024;
       dk[r] = 0;
@@ -98,7 +106,9 @@ __global__ __launch_bounds__((8 + LDW) * 64) void sf_intake_probe_kernel(
       dk[r] = 3;  // no piece (the issuing waves' share is uneven)
     }
   }
-  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+  const int rot = MODE >= 4 ? (bid >> 3) % J : 0;
+  auto issue = [&](int stp, int buf) __attribute__((always_inline)) {
+    const int st = MODE >= 4 ? s0 + (stp - s0 + rot) % J : stp;
     uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * (stage < STAGE_MAX ? stage : STAGE_MAX);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -142,10 +152,11 @@ void sf_launch_shape(int path, int M, int N, int K, int* bn, int* splits, int* s
 // path 0 = int4 (x bf16 [M][K], w packed [N][K/2] bytes, z (scale, zero) [N][K/g] dwords), 2 =
 // int8 dyn (x int8 [M][K], w int8 [N][K], z unused). Writes the launch shape it streamed to
 // shape_out[0..6] (bn, splits, stages, a_steps, loaders, kstep, bytes per workgroup per step).
-extern "C" int tao_sf_intake_probe(int path, const void* x, const void* w, const void* z,
-                                   int64_t M, int64_t N, int64_t K, int64_t group_size,
-                                   int* shape_out, void* sink, void* stream) {
+extern "C" int tao_sf_intake_probe(int path, int mode, const void* x, const void* w,
+                                   const void* z, int64_t M, int64_t N, int64_t K,
+                                   int64_t group_size, int* shape_out, void* sink, void* stream) {
   TAO_CHECK_ARG(path == 0 || path == 2, "intake probe: path must be 0 (int4) or 2 (int8 dyn)");
+  TAO_CHECK_ARG(mode >= 0 && mode <= 5, "intake probe: mode (%d) must be 0..5", mode);
   TAO_CHECK_ARG(x != nullptr && w != nullptr && sink != nullptr && shape_out != nullptr &&
                     (path == 2 || z != nullptr),
                 "intake probe: null pointer");
@@ -159,7 +170,7 @@ extern "C" int tao_sf_intake_probe(int path, const void* x, const void* w, const
   TAO_CHECK_ARG(K % ks == 0 && N % bn == 0, "intake probe: N (%lld) / K (%lld) off the tile grid",
                 (long long)N, (long long)K);
   const int px = 128 * kx / 1024, pw = bn * kw / 1024, pz = bn * kz / 256;
-  const int T = px + pw + pz, DW = ld ? 4 : 8, R = (T + DW - 1) / DW;
+  const int T = px + pw + pz, DW = ld ? ld : 8, R = (T + DW - 1) / DW;
   if (ns < 2) ns = 2;
   if (ns > 4) ns = 4;
   shape_out[0] = bn;
@@ -177,22 +188,33 @@ extern "C" int tao_sf_intake_probe(int path, const void* x, const void* w, const
   const uint8_t* zb = static_cast<const uint8_t*>(z != nullptr ? z : w);
   const uint32_t xrow = (uint32_t)(K * (path == 0 ? 2 : 1)), wrow = (uint32_t)(path == 0 ? K / 2 : K);
   const uint32_t zrow = path == 0 ? (uint32_t)(K / group_size * 4) : 4u;
-  const uint32_t xbytes = (uint32_t)(M * xrow), wbytes = (uint32_t)(N * wrow);
+  const int64_t xrows = mode == 3 ? 128LL * (N / bn) * S : M;  // mode 3: a private x per workgroup
+  TAO_CHECK_ARG(xrows * xrow < (1LL << 32), "intake probe: x too large");
+  const uint32_t xbytes = (uint32_t)(xrows * xrow), wbytes = (uint32_t)(N * wrow);
   const uint32_t zbytes = path == 0 ? (uint32_t)(N * zrow) : 4u;
   const int zgs = path == 0 ? (int)group_size : 32;
   const dim3 grid((unsigned)(ntn * S));
   hipStream_t st = tao::as_stream(stream);
   uint32_t* sk = static_cast<uint32_t*>(sink);
-#define TAO_IP(NS_, R_, LDW_)                                                                      \
-  tao::launch(tao::sf_intake_probe_kernel<NS_, R_, LDW_>, grid, dim3((8 + LDW_) * 64), 0, st, xb, \
-              xbytes, xrow, kx, wb, wbytes, wrow, kw, zb, zbytes, zrow, kz, zgs, px, pw, pz, ntn,  \
-              S, a, nsteps, sk)
-  if (ld && R == 10 && ns == 4) TAO_IP(4, 10, 4);
-  else if (ld && R == 10 && ns == 3) TAO_IP(3, 10, 4);
-  else if (!ld && R == 5 && ns == 3) TAO_IP(3, 5, 0);
-  else if (!ld && R == 5 && ns == 2) TAO_IP(2, 5, 0);
-  else if (!ld && R == 6 && ns == 3) TAO_IP(3, 6, 0);
-  else if (!ld && R == 6 && ns == 2) TAO_IP(2, 6, 0);
+#define TAO_IP(NS_, R_, LDW_, MODE_)                                                               \
+  tao::launch(tao::sf_intake_probe_kernel<NS_, R_, LDW_, MODE_>, grid, dim3((8 + LDW_) * 64), 0,  \
+              st, xb, xbytes, xrow, kx, wb, wbytes, wrow, kw, zb, zbytes, zrow, kz, zgs, px, pw,   \
+              pz, ntn, S, a, nsteps, sk)
+  if (mode == 0 && ld == 8 && R == 5 && ns == 4) TAO_IP(4, 5, 8, 0);
+  else if (mode == 2 && ld == 8 && R == 5 && ns == 4) TAO_IP(4, 4, 8, 2);
+  else if (mode == 0 && ld && R == 10 && ns == 4) TAO_IP(4, 10, 4, 0);
+  else if (mode == 0 && ld && R == 10 && ns == 3) TAO_IP(3, 10, 4, 0);
+  else if (mode == 0 && !ld && R == 5 && ns == 4) TAO_IP(4, 5, 0, 0);
+  else if (mode == 2 && !ld && R == 5 && ns == 4) TAO_IP(4, 4, 0, 2);  // 32 x pieces, 8 waves
+  else if (mode == 0 && !ld && R == 5 && ns == 3) TAO_IP(3, 5, 0, 0);
+  else if (mode == 0 && !ld && R == 5 && ns == 2) TAO_IP(2, 5, 0, 0);
+  else if (mode == 0 && !ld && R == 6 && ns == 3) TAO_IP(3, 6, 0, 0);
+  else if (mode == 0 && !ld && R == 6 && ns == 2) TAO_IP(2, 6, 0, 0);
+  else if (mode == 1 && ld && R == 10 && ns == 4) TAO_IP(4, 2, 4, 1);  // 8 w / z pieces
+  else if (mode == 2 && ld && R == 10 && ns == 4) TAO_IP(4, 8, 4, 2);  // 32 x pieces
+  else if (mode == 3 && ld && R == 10 && ns == 4) TAO_IP(4, 10, 4, 3);
+  else if (mode == 4 && ld && R == 10 && ns == 4) TAO_IP(4, 10, 4, 4);
+  else if (mode == 5 && ld && R == 10 && ns == 4) TAO_IP(4, 8, 4, 5);
   else
     return tao::set_error(TAO_ERR_UNSUPPORTED,
                           "intake probe: no instance for %d pieces per wave, %d stages, loaders %d",

@@ -77,7 +77,7 @@ struct Tuning {
   int sf_seam = -1;  // single-fetch GEMM split-K seam: -1 built-in, 0 fixed reducer, 1 spread
   int sf_late_pub = 0;  // robustness test hook: slice-0 publishers add after the reducer timed out
   int sf_xmap = 0;     // fixed-reducer seam: K slices on their own XCDs (0 built-in, 1 off, 2 on)
-  int sf_loaders = 0;  // 32x32x16 int4 GEMM: dedicated LDS-DMA loader waves (0 built-in, 1 off, 2 on)
+  int sf_loaders = 0;  // single-fetch GEMMs: loader waves (0 built-in, 1 off, 2 on, 3 eight)
   int attn_prefill_nw = 0;  // prefill attention: waves per query block (0 built-in, 1, 2, 4)
   int gemv_lds = 0;  // int4 GEMV: minimum dynamic LDS per workgroup (caps residency; tao_tune_int4_lds)
 };

@@ -65,7 +65,7 @@ _SIGNATURES = {
     "tao_tune_cnt_stride": [_int],
     "tao_hbm_read_probe": [_p, _i64, _p, _p],
     "tao_hbm_copy_probe": [_p, _p, _i64, _int, _int, _p],
-    "tao_sf_intake_probe": [_int, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _p, _p],
+    "tao_sf_intake_probe": [_int, _int, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _p, _p],
     "tao_graph_workspace_count": [],
     "tao_int4_pack": [_p, _p, _i64, _i64, _p],
     "tao_int4_pack_u8": [_p, _p, _i64, _i64, _p],
