@@ -778,17 +778,23 @@ M1Shape m1_shape(int N, int S) {
   } else {  // K > 4096: waves split K (each walking its slices in pairs) while N is small
     // (profiles/r1_sweep_gemv_70b.jsonl, r1_sweep_gemv_shards.jsonl: Llama-3-70B linears and
     // their 2/4/8-way column shards)
+    // Round 6 re-sweep after the byte-permute decode (graph-timed, then same-process A/B:
+    // profiles/r6r_sweep_gemv_70b.jsonl, r6s_ab_gemv_70b.jsonl; us, old -> new shape): 57344x8192
+    // 52.4 -> 46.7, 8192^2 10.3 -> 9.0, 10240x8192 12.1 -> 11.0, 7168x8192 9.4 -> 8.7, 1024x8192
+    // 4.0 -> 3.5, 1280x8192 4.1 -> 3.9; 2048x8192, 3584x8192, 1024x28672, 8192x28672 unchanged
     c.occ = 4;
-    if (N >= 32768) {  // heads: 8 rows per wave (128256x8192 93.9 vs 99.7 µs at 4)
+    if (N >= 32768) {  // heads / fused w1||w3: 8 rows per wave (128256x8192 93.9 vs 99.7 µs at 4)
       c.rpw = 8;
-      c.sh = {4, 1};
+      c.sh = {2, 1};
     } else if (N <= 2560 && S <= 4) {
       c.rpw = 2;
-      c.sh = {2, 1};
+      c.sh = {N <= 1536 ? 4 : 2, 1};
     } else if (N <= 2048) {  // few rows, long K: more waves along K (1024x28672 5.7 vs 9.0 µs)
       c.sh = {N <= 1024 ? 8 : 4, 1};
-    } else {
+    } else if (N <= 4096 || S > 4) {
       c.sh = {N <= 4096 ? 2 : (S >= 8 ? 1 : 4), 1};
+    } else {  // K = 8192, N > 4096: one wave walks the row's 4 slices (two PAIR steps)
+      c.sh = N >= 10240 && N < 16384 ? GemvShape{2, 2} : GemvShape{1, 1};
     }
   }
   const int trpw = tao::tuning().rpw;
