@@ -74,7 +74,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E, spec (MI355X_MICROARCH.md chip table)
-PMC_FILE = os.path.join(ROOT, "profiles", "r6a_pmc_fetch_bench.json")  # --pmc-file overrides
+PMC_FILE = os.path.join(ROOT, "profiles", "r6u_pmc_fetch_bench.json")  # --pmc-file overrides
 
 LLAMA3_8B = dict(dim=4096, n_layer=32, n_head=32, n_kv_head=8, head_dim=128,
                  intermediate=14336, vocab=128256)
@@ -446,7 +446,7 @@ def config2_shapes(device, g=32, copies=32, reps=20):
 
 
 INT8WO_SHAPES = ((4096, 4096), (6144, 4096), (14336, 4096), (4096, 14336))
-PMC_INT8WO_FILE = os.path.join(ROOT, "profiles", "r6a_pmc_fetch_int8wo.json")
+PMC_INT8WO_FILE = os.path.join(ROOT, "profiles", "r6u_pmc_fetch_int8wo.json")
 
 
 def int8wo_alg_bytes(N, K, M=1):

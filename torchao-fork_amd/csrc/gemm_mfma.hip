@@ -25,9 +25,6 @@
 
 #include "tao_common.h"
 
-// Experiment switch (experiments/gemm_debug.sh builds variants; 0 in the product):
-// 1 = no x global loads, 2 = no weight global loads, 3 = no x LDS traffic, 4 = no step barrier,
-// 5 = no global loads at all.
 // Experiment switch: ring depth override (experiments/gemm_depth.sh; 0 = the policy below).
 #ifndef TAO_GEMM_DEPTH
 #define TAO_GEMM_DEPTH 0

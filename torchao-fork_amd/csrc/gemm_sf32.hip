@@ -42,9 +42,7 @@
 #ifndef TAO_SF32_IL
 #define TAO_SF32_IL 1
 #endif
-// Timing-only build (experiments/sf32_steps.py; never the shipped library): s_memtime (shader
-// clock) of every wave of workgroups 0..7 at each k step: step top, own DMAs landed, barrier
-// passed, MFMAs issued; and the s_memrealtime / s_memtime pair at entry and exit.
+// A-fragment buffers of the compute waves (1 or 2; measured the same: r5g_ab_sf32_abuf.jsonl)
 #ifndef TAO_SF32_ABUF
 #define TAO_SF32_ABUF 2
 #endif
