@@ -97,13 +97,13 @@ def test_swiglu_epilogue(norm, I, K):
 
 
 @pytest.mark.parametrize("norm", [False, True])
-@pytest.mark.parametrize("H,Hkv,pos", [(32, 8, 17), (4, 4, 0), (8, 2, 63)])
+@pytest.mark.parametrize("H,Hkv,pos", [(32, 8, 17), (4, 4, 0), (8, 2, 63), (64, 8, 5)])
 def test_rope_kv_epilogue(norm, H, Hkv, pos):
     from torchao._models.llama import kernels
     from torchao._models.llama.model import ModelArgs, _rope_freqs
 
     D, T = 128, 64
-    K = 1024 if H < 32 else 4096
+    K = 1024 if H < 32 else 8192 if H == 64 else 4096  # (64, 8): Llama-3-70B's wqkv 10240x8192
     N = (H + 2 * Hkv) * D
     lin, parts = _int4_linear(N, K, seed=3)
     cfg = ModelArgs(n_layer=1, n_head=H, n_local_heads=Hkv, dim=H * D, rope_base=500000)

@@ -841,6 +841,15 @@ M1Shape pro_shape(int N, int K) {
   if (tao::tuning().rpw == 0) c.rpw = N < 16384 ? 2 : 4;
   if (tao::tuning().wk == 0) c.sh.wk = 1;
   if (tao::tuning().g == 0) c.sh.g = 4;
+  // Round 6, after the byte-permute decode (same-process A/B, profiles/r6z_ab_decode_shape.jsonl):
+  // Llama-3-70B's wqkv + RoPE (10240x8192) 15.1 -> 13.9 us on 4 rows per wave and 2 waves along
+  // K; its w1||w3 and every Llama-3-8B shape keep the whole-row shape above
+  if (K > 4096 && N > 8192 && N < 16384 && tao::tuning().rpw == 0 && tao::tuning().wk == 0 &&
+      tao::tuning().g == 0) {
+    c.rpw = 4;
+    c.sh.wk = 2;
+    c.sh.g = 2;
+  }
   // enough threads to hold x in the prologue: K <= 8 * NPT * threads, NPT <= kMaxNormPT
   const int wk = c.sh.wk < S ? c.sh.wk : S;
   while (64 * wk * c.sh.g * 8 * kMaxNormPT < K && wk * c.sh.g * 2 <= 8) c.sh.g *= 2;
