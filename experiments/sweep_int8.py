@@ -2,7 +2,9 @@
 int8 weight-only (bf16 x) and the fused int8 x int8 one-token linear (int8_dyn_linear).
 Weights rotated past the Infinity Cache, one dispatch-event timing per launch (KernelTimer),
 median; every config's output is checked against the default (int8 dyn: bit-exact).
-python experiments/sweep_int8.py [NxK ...]"""
+--graph: time by the wall time per launch of back-to-back launches replayed from one HIP graph
+(sweep_gemv.graph_us), as bench.py's int8wo_m1 block does.
+python experiments/sweep_int8.py [--graph] [NxK ...]"""
 
 import json
 import os
@@ -20,7 +22,12 @@ SHAPES = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 409
 
 
 def main():
-    shapes = SHAPES if len(sys.argv) < 2 else [tuple(map(int, a.split("x"))) for a in sys.argv[1:]]
+    args = [a for a in sys.argv[1:] if a != "--graph"]
+    use_graph = "--graph" in sys.argv[1:]
+    if use_graph:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from sweep_gemv import graph_us
+    shapes = SHAPES if not args else [tuple(map(int, a.split("x"))) for a in args]
     for N, K in shapes:
         S = (K // 16 + 63) // 64
         copies = max(3, min(48, int(400e6 // (N * K))))
@@ -48,10 +55,13 @@ def main():
                         for c in range(copies):
                             fn(ws[c])
                         torch.cuda.synchronize()
-                        with _lib.KernelTimer(reps) as kt:
-                            for i in range(reps):
-                                fn(ws[i % copies])
-                        us = statistics.median(kt.durations_ms[2:]) * 1e3
+                        if use_graph:
+                            us = graph_us(lambda: [fn(ws[i % copies]) for i in range(reps)], reps)
+                        else:
+                            with _lib.KernelTimer(reps) as kt:
+                                for i in range(reps):
+                                    fn(ws[i % copies])
+                            us = statistics.median(kt.durations_ms[2:]) * 1e3
                         nbytes = N * K + 2 * N + 2 * K + 2 * N
                         rec = {"path": name, "N": N, "K": K, "rpw": rpw, "wk": wk, "g": g,
                                "us": round(us, 3), "GBps": round(nbytes / us / 1e3, 1),
