@@ -598,6 +598,17 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
                 "k_step": ks, "bytes_per_wg_step": step_b, "bytes_per_wg": per_wg,
                 "GBps_per_cu": round(per_wg / (pus * 1e-6) / 1e9, 1)}
 
+    # the floor any launch shows by these events on this box: a one-workgroup 8-KiB read
+    # (tao_hbm_read_probe), so each GEMM's roofline can also be read against attainable + floor
+    fl_buf = torch.zeros(8192, dtype=torch.uint8, device=device)
+    fl_sink = torch.zeros(1024, dtype=torch.int32, device=device)
+
+    def empty_launch(c):
+        _lib.call("tao_hbm_read_probe", fl_buf.data_ptr(), 8192, fl_sink.data_ptr(),
+                  torch.cuda.current_stream().cuda_stream)
+
+    (floor_us,) = timed(empty_launch, 1, 1)
+
     out = {}
     # int8 dyn: per-token quant kernel + int8 MFMA GEMM with the fused scale epilogue
     copies = max(2, int(320e6 // (N * K)))
@@ -642,6 +653,8 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
         "mfma_frac": round(ops / (gemm_us * 1e-6) / 1e12 / INT8_PEAK_TOPS, 4),
         "GBps": round(nbytes / (gemm_us * 1e-6) / 1e9, 1),
         "attainable_us": round(att, 2), "roofline_frac": round(att / gemm_us, 4),
+        "launch_floor_us": round(floor_us, 2),
+        "roofline_frac_with_launch_floor": round((att + floor_us) / gemm_us, 4),
         "graph_us": round(ours8_graph_us, 2) if ours8_graph_us else None,
         "reference_gpu_us": round(ref8_us, 2) if isinstance(ref8_us, float) else ref8_us,
         "reference_gpu_op": "torch._int_mm (hipBLASLt int8, safe_int_mm) * x_scale -> bf16 * w_scale",
@@ -695,6 +708,8 @@ def prefill_mfma(device, M=128, N=4096, K=4096, g=32, reps=40):
         "TFLOPS": round(ops / (us4 * 1e-6) / 1e12, 1),
         "mfma_frac": round(ops / (us4 * 1e-6) / 1e12 / BF16_PEAK_TFLOPS, 4),
         "attainable_us": round(att4, 2), "roofline_frac": round(att4 / us4, 4),
+        "launch_floor_us": round(floor_us, 2),
+        "roofline_frac_with_launch_floor": round((att4 + floor_us) / us4, 4),
         "graph_us": round(ours4_graph_us, 2) if ours4_graph_us else None,
         "reference_gpu_us": round(ref4_us, 2) if isinstance(ref4_us, float) else ref4_us,
         "reference_gpu_op": "aten._weight_int4pack_mm (PyTorch-ROCm)",
