@@ -1,7 +1,7 @@
 #!/bin/bash
 # Variant builds for A/B timing: each NAME=SRC:DEFINES links csrc/SRC built with DEFINES (in place
 # of its shipped object) into experiments/build/libvar_NAME.so. CPU-side step.
-#   bash experiments/variant.sh addloop=decode_ops:-DTAO_ADDNORM_LOOP=1
+#   bash experiments/variant.sh il=gemm_sf:-DTAO_SF_IL=1
 set -e
 cd "$(dirname "$0")/.."
 B=experiments/build
