@@ -11,8 +11,8 @@
 //     (16 B of nibbles per lane) + one 256-B (scale, zero) load at group size 32;
 //   * a wave owns RPW rows and one slice at a time; a workgroup is G row-groups x Wk waves along
 //     K (Wk = min(slices, 8)); slices beyond Wk are looped;
-//   * per lane: D = sum x*(128+q) via v_dot2c_f32_bf16 on magic-number bf16 pairs
-//     (one v_and_or_b32 per 2 weights), Sx = sum x, then s*(D - 136 Sx) + z*Sx per 32-k chunk —
+//   * per lane: D = sum x*(128+q) via v_dot2c_f32_bf16 on magic-number bf16 pairs (formed by
+//     byte permutes: 7 VALU per 8 weights), Sx = sum x, then s*(D - 136 Sx) + z*Sx per 32-k chunk —
 //     every 32-k chunk lies in exactly one quantisation group because g in {32..256};
 //   * cross-lane: reduce-scatter over the RPW*M partials (V/2 + V/4 + ... shuffles), then a
 //     butterfly over the remaining lanes; cross-wave: LDS, one wave finishes and writes y.
